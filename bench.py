@@ -1,0 +1,294 @@
+"""Benchmark: batched ShippingEnv step on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n ENVS_PER_GPU]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+A "step" is one se_step launch over all envs of the GPU (one pass of the hot
+path over one batch). Workload for `value`: BASELINE config 3 — N = 2^20 envs
+per GPU, full step (moves, cargo pickup/delivery, rewards), the reference's 5
+default ports, synthetic agent actions (90 % move, 5 % take cargo, 3 % take
+fuel, 2 % select; Philox-generated, resident in HBM before timing). Config 4
+(64 random ports, auto-reset with ballot-compacted done list and per-block
+episode-return reduction, RCCL all-reduce of the stats) is measured in the same
+run and reported under "config4". Weak scaling: every rank owns 2^20 envs with
+global ids rank*2^20 + i.
+
+Rank 0 prints ONE JSON line on stdout; progress goes to stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+# algorithmic bytes per env-step for this build's field widths (DESIGN.md "Roofline"):
+#   state x,y,origin,dest u8 + cargo i32 + fuel f64 = 16 B, read and written;
+#   action i32 4 B read; reward f32 4 B, done u8 1 B, err i8 1 B written.
+BYTES_STEP = 16 + 16 + 4 + 4 + 1 + 1  # 42
+BYTES_STEP_AUTO = BYTES_STEP + 4 + 4 + 4 + 4  # + ep_return f32 and ep_len i32, read and written
+# the survey's canonical widths (x, y, origin, dest, cargo i32; fuel f64): 66 / 82 B
+CANONICAL_STEP, CANONICAL_STEP_AUTO = 66, 82
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=1000)
+    p.add_argument("--warmup", type=int, default=50)
+    p.add_argument("--n", type=int, default=1 << 20, help="envs per GPU")
+    p.add_argument("--seed", type=int, default=2026)
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-config4", action="store_true")
+    p.add_argument("--large-n", type=int, default=1 << 24,
+                   help="extra HBM-resident run (working set beyond the 256 MiB MALL); 0 = skip")
+    return p.parse_args()
+
+
+class Dist:
+    def __init__(self, want):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != want:
+            raise SystemExit(f"--gpus {want} but WORLD_SIZE={self.world}")
+        torch.cuda.set_device(self.local)
+        self.dev = torch.device("cuda", self.local)
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("nccl", device_id=self.dev)
+            self.pg = dist
+
+    def barrier(self):
+        if self.pg:
+            self.pg.barrier()
+
+    def max(self, v):
+        if not self.pg:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=self.dev)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_(self, t):
+        if self.pg:
+            self.pg.all_reduce(t)
+        return t
+
+    def close(self):
+        if self.pg:
+            self.pg.destroy_process_group()
+
+
+def make_actions(env, steps):
+    acts = torch.empty((steps, env.n), dtype=torch.int32, device=env.device)
+    for t in range(steps):
+        env.gen_actions(t, out=acts[t])
+    return acts
+
+
+def timed_loop(env, acts, first, steps, dist):
+    """Back-to-back launches; barrier + synchronize on both sides; max over ranks."""
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        env.step(acts[first + k])
+    torch.cuda.synchronize()
+    dist.barrier()
+    return dist.max(time.perf_counter() - t0)
+
+
+def kernel_time(env, acts, first, steps):
+    """Average step-kernel duration from HIP events recorded around each launch on
+    the stream the kernel is launched on (torch's current stream)."""
+    stream = torch.cuda.current_stream(env.device)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    torch.cuda.synchronize()
+    for k in range(steps):
+        ev[k][0].record(stream)
+        env.step(acts[first + (k % (acts.shape[0] - first))])
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    ms = np.array([a.elapsed_time(b) for a, b in ev])
+    return float(ms.mean()), float(np.median(ms))
+
+
+def run_config(n, ports, auto, args, dist, label):
+    from shippingenv_amd.vec import VecEnv
+
+    env = VecEnv(n, seed=args.seed, ports=ports, env_id_base=dist.rank * n, device=dist.dev,
+                 auto_reset=auto)
+    total = args.warmup + args.steps
+    log(f"[{label}] rank {dist.rank}: n={n} P={env.P} auto_reset={auto}; generating {total} action rows")
+    acts = make_actions(env, total)
+    env.reset()
+    for k in range(args.warmup):
+        env.step(acts[k])
+    torch.cuda.synchronize()
+    if auto:
+        env.clear_stats()
+    elapsed = timed_loop(env, acts, args.warmup, args.steps, dist)
+    stats = None
+    if auto:
+        # episode-return aggregation across GPUs: one RCCL all-reduce of 3 doubles
+        s = env.episode_stats().clone()
+        dist.sum_(s)
+        stats = s.cpu().tolist()
+    k_ms_mean, k_ms_med = kernel_time(env, acts, args.warmup, min(args.steps, 500))
+    env.close()
+    del acts
+    torch.cuda.empty_cache()
+    return elapsed, k_ms_mean, k_ms_med, stats
+
+
+def roofline(bytes_per_step, n, k_ms, canonical):
+    achieved = bytes_per_step * n / (k_ms * 1e-3) / 1e9
+    return {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBPS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBPS, 4),
+        "traffic": None,
+        "bytes_per_env_step": bytes_per_step,
+        "canonical_bytes_per_env_step": canonical,
+        "canonical_achieved": round(canonical * n / (k_ms * 1e-3) / 1e9, 1),
+        "kernel_ms": round(k_ms, 5),
+    }
+
+
+def pmc_traffic():
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("step_kernel_bytes_per_launch"), os.path.relpath(path, ROOT)
+
+
+def cpu_baseline(n_workload, ports_seed, budget_s):
+    """The C restatement (oracle, Philox mode, 1 thread) on a bounded sample of the
+    same workload: 2^16 of the envs, as many whole steps as fit the budget."""
+    from oracle import oracle as O
+    from shippingenv_amd.maps import builtin_water
+    from shippingenv_amd.vec import DEFAULT_PORTS, draw_port_stocks
+
+    n = min(n_workload, 1 << 16)
+    water = builtin_water()
+    pf, pc = draw_port_stocks(5, ports_seed)
+    world = O.OracleWorld(water, [p[0] for p in DEFAULT_PORTS], [p[1] for p in DEFAULT_PORTS], pf, pc)
+    st = O.OracleState(n)
+    O.reset(world, st, seed=ports_seed, epoch=0)
+    acts = [O.gen_actions(n, 5, ports_seed, 0, t) for t in range(64)]
+    steps, spent, t = 0, 0.0, 0
+    while spent < budget_s:
+        t0 = time.perf_counter()
+        O.step(world, st, actions=acts[t % 64], seed=ports_seed, t=t)
+        spent += time.perf_counter() - t0
+        steps += 1
+        t += 1
+    return {
+        "value": round(n * steps / spent, 1),
+        "unit": "env-steps/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"oracle/shipenv_oracle.c (Philox mode, same action mix) on {n} envs x {steps} "
+                  f"steps ({spent:.1f} s, 1 thread); reference Python measured in the build "
+                  "container: 1.0-1.2e5 env-steps/s on 1 core (BASELINE.md)",
+    }
+
+
+def main():
+    args = parse()
+    dist = Dist(args.gpus)
+    from shippingenv_amd.maps import builtin_water
+    from shippingenv_amd.vec import random_water_ports
+
+    n = args.n
+    el3, k3, k3_med, _ = run_config(n, None, False, args, dist, "config3")
+    value = n * dist.world * args.steps / el3
+    out = {
+        "metric": "env-steps/sec at N=2^20 parallel envs per GPU (config 3: full step, 5 default ports)",
+        "value": round(value, 1),
+        "unit": "env-steps/s",
+        "n_gpus": dist.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el3 / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64+int (fuel/reward f64, positions/cargo int)",
+        "data": "synthetic (Philox agent actions resident in HBM; reference map and ports)",
+        "config": {
+            "workload": "BASELINE configs[2]: N=2^20 envs/GPU, full step, default 5 ports",
+            "envs_per_gpu": n,
+            "global_envs": n * dist.world,
+            "ports": 5,
+            "parallelism": f"env-shard dp{dist.world} (no data-path collective)",
+        },
+        "roofline": roofline(BYTES_STEP, n, k3, CANONICAL_STEP),
+    }
+    out["roofline"]["kernel_ms_median"] = round(k3_med, 5)
+    traffic, src = pmc_traffic()
+    if traffic:
+        out["roofline"]["traffic"] = traffic
+        out["roofline"]["traffic_source"] = src
+
+    if not args.no_config4:
+        ports64 = random_water_ports(builtin_water(), 64, seed=3)
+        el4, k4, _, stats = run_config(n, ports64, True, args, dist, "config4")
+        out["config4"] = {
+            "workload": "BASELINE configs[3]: N=2^20 envs/GPU, 64 random ports, auto-reset, "
+                        "ballot-compacted done list, per-block return reduction, RCCL all-reduce",
+            "value": round(n * dist.world * args.steps / el4, 1),
+            "ms_per_step": round(el4 / args.steps * 1e3, 5),
+            "roofline": roofline(BYTES_STEP_AUTO, n, k4, CANONICAL_STEP_AUTO),
+            "episodes": stats[1],
+            "mean_return": stats[0] / stats[1] if stats and stats[1] else None,
+            "mean_len": stats[2] / stats[1] if stats and stats[1] else None,
+        }
+
+    if args.large_n and dist.world == 1:
+        small = argparse.Namespace(**vars(args))
+        small.steps, small.warmup = 100, 5
+        el, k, _, _ = run_config(args.large_n, None, False, small, dist, "large-n")
+        out["large_n"] = {
+            "envs": args.large_n,
+            "note": "working set beyond the 256 MiB Infinity Cache: traffic reaches HBM",
+            "value": round(args.large_n * small.steps / el, 1),
+            "roofline": roofline(BYTES_STEP, args.large_n, k, CANONICAL_STEP),
+        }
+
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
+        log("[cpu] timing the C restatement")
+        out["cpu_baseline"] = cpu_baseline(n, args.seed, args.cpu_seconds)
+
+    if dist.rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,175 @@
+/* shipenv.h — C-ABI of libshipenv_hip.so, the MI355X-native batched ShippingEnv step.
+ *
+ * The reference has no FFI: its "operator API" is the Python class
+ * shipping.Environment (/root/reference/shipping/environment.py:28-376). Each
+ * entry point below replaces one method of that class for N environments at
+ * once; the Python mirror shippingenv_amd/shipping/environment.py binds them
+ * through ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - Every function returns 0 on success or a negative SE_E* status; the text of
+ *    the last failure on the calling thread is se_last_error().
+ *  - All N-sized buffers are DEVICE pointers owned by the caller (e.g. torch
+ *    tensors' data_ptr()); the library never frees them. They must be 16-byte
+ *    aligned. The library owns only its staged map/ports copies and scratch.
+ *  - Launching calls take a hipStream_t as void* (NULL = the null stream), are
+ *    asynchronous on it and never synchronise the host.
+ *  - Per-environment failures are not API errors: they are reported per env in
+ *    err[i] (SE_ERR_*), exactly where the reference raises an exception; such an
+ *    env's state is left untouched with reward 0 and done 0.
+ */
+#ifndef SHIPENV_H
+#define SHIPENV_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SHIPENV_ABI_VERSION 1
+
+/* API status codes */
+#define SE_OK 0
+#define SE_EINVAL (-1)  /* bad argument */
+#define SE_EHIP (-2)    /* HIP runtime error */
+#define SE_ESTATE (-3)  /* call out of order (e.g. step before bind) */
+
+/* Per-environment error classes; the Python mirror re-raises the reference's
+ * exception type and message for each (shipping/environment.py line). */
+#define SE_ERR_OK 0
+#define SE_ERR_OOB 1            /* ValueError("Move is out of range")                       :284 */
+#define SE_ERR_SAME_PORT 2      /* Exception("Destination port must be different ...")      :267 */
+#define SE_ERR_PORT_RANGE 3     /* IndexError("Port index is out of range")                 :269 */
+#define SE_ERR_NOT_AT_PORT 4    /* Exception("Not currently at port")                  :343, :352 */
+#define SE_ERR_AMOUNT 5         /* ValueError("Invalid fuel amount")                   :346, :355 */
+#define SE_ERR_NO_DEST 6        /* Exception("Cannot move without destination port")        :276 */
+#define SE_ERR_BAD_CATEGORY 7   /* ValueError("Action category unknown")                    :374 */
+#define SE_ERR_NO_PORTS 8       /* Exception("No ports available")                          :360 */
+#define SE_ERR_BAD_INDEX 9      /* IndexError("list index out of range"), utils/preprocessing.py:127 */
+
+/* se_create flags */
+#define SE_FLAG_AUTO_RESET 1u   /* reset an env inside se_step right after it reports done */
+
+#define SE_NONE 255             /* origin/dest "None" in the u8 index fields */
+#define SE_MAX_PORTS 254
+#define SE_MAX_SIDE 256         /* H, W <= 256 (positions are u8) */
+
+typedef struct se_env se_env;
+
+/* Done-list entry written by the auto-reset path (wave-ballot compaction). */
+typedef struct se_done_rec {
+    int32_t env;         /* local env index */
+    float ep_return;     /* return of the finished episode */
+    int32_t ep_len;      /* its length in step calls */
+    int32_t step;        /* the step counter value of the step that finished it */
+} se_done_rec;
+
+/* Per-env SoA state, one entry per environment, all device pointers (16-B aligned).
+ * ep_return, ep_len, done_recs and done_count may be NULL unless SE_FLAG_AUTO_RESET. */
+typedef struct se_state {
+    uint8_t* x;         /* ship_position[0], row of np_game      (environment.py:37,:241,:297) */
+    uint8_t* y;         /* ship_position[1], column of np_game */
+    double* fuel;       /* self.fuel, f64 like the reference (int 200 - sum of np.float64)  :39 */
+    int32_t* cargo;     /* self.cargo                                                      :38 */
+    uint8_t* origin;    /* self.origin_port_index, SE_NONE = None                          :40 */
+    uint8_t* dest;      /* self.destination_port_index, SE_NONE = None                     :41 */
+    float* reward;      /* step() reward, the reference's f64 value rounded once to f32    :376 */
+    uint8_t* done;      /* step() done                                                     :376 */
+    int8_t* err;        /* SE_ERR_* per env */
+    float* ep_return;   /* running episode return (auto-reset) */
+    int32_t* ep_len;    /* running episode length in step calls (auto-reset) */
+    struct se_done_rec* done_recs; /* auto-reset done list, capacity 2*n records */
+    int32_t* done_count;           /* auto-reset done counters, 3 entries, zeroed by se_bind */
+} se_state;
+
+/* One replayed MOVE's variates (the draws the reference made through `random`,
+ * SURVEY.md Appendix A); used by se_step_replay only. 48 bytes. */
+typedef struct se_tape {
+    double u_fuel;       /* random() behind uniform(-0.1, 0.1)                  :104 */
+    double u_gate;       /* random() of the cargo-loss gate                       :320 */
+    double u_type;       /* random() loss type (read only if the gate fires)      :177 */
+    double beta;         /* betavariate(2, 2) (read only for a partial loss)      :195 */
+    int32_t arrive_dest; /* accepted randint at arrival                          :333 */
+    int32_t pad;
+} se_tape;
+
+/* Environment.__init__ + _initialize_map + add_port (environment.py:29-65).
+ * water: H*W bytes row-major [x*W + y], 0 = GROUND, nonzero = not ground (the
+ * thresholded map of :45-55). Ports are stamped non-ground like add_port (:65).
+ * port_fuel / port_cargo: the stocks add_port drew (:63-64). P may be 0.
+ * env_id_base: global id of env 0 (rank * n for sharded runs): the Philox key
+ * (seed, env_id_base + i) makes results shard-invariant. */
+int se_create(se_env** out, int device, int64_t n, int64_t env_id_base, int32_t H, int32_t W,
+              const uint8_t* water, int32_t P, const int32_t* port_x, const int32_t* port_y,
+              const int32_t* port_fuel, const int32_t* port_cargo, uint64_t seed, uint32_t flags);
+
+/* Replace the ports table (add_port / remove_port / attribute assignment); host arrays. */
+int se_set_ports(se_env* env, int32_t P, const int32_t* port_x, const int32_t* port_y,
+                 const int32_t* port_fuel, const int32_t* port_cargo);
+
+/* Bind the caller-owned SoA buffers (n entries each). */
+int se_bind(se_env* env, const se_state* state);
+
+/* reset() (environment.py:227-243) for every env with mask[i] != 0 (mask NULL = all):
+ * cargo 0, fuel 200, origin ~ U{0..P-1}, dest ~ U{others}, ship at the origin port.
+ * Draws: Philox(seed, env) at counter (reset epoch, slot 5); the epoch advances per call. */
+int se_reset(se_env* env, const uint8_t* mask, void* stream);
+
+/* reset() with given origin/dest per env (device int32 arrays): replays a
+ * recorded reset, or restores a state. */
+int se_reset_to(se_env* env, const uint8_t* mask, const int32_t* origin, const int32_t* dest,
+                void* stream);
+
+/* step() for all envs with actions in the agent-index encoding of
+ * utils/preprocessing.py:111-137 (a < 4 move N,E,S,W; < 4+P select; < 4+P+50
+ * take cargo; else take fuel). Draws from Philox(seed, env) at counter
+ * (step counter, slot); the step counter advances by one per call. */
+int se_step(se_env* env, const int32_t* actions, void* stream);
+
+/* step() with the reference's typed action [ActionType, value] (environment.py:359-376):
+ * type 1..4 (shipping/type.py:1-5); MOVE value = (a, b) any integers; others value = a. */
+int se_step_typed(se_env* env, const int32_t* type, const int32_t* a, const int32_t* b,
+                  void* stream);
+
+/* step() with typed actions whose variates come from tape[i] (replay of recorded
+ * reference draws). The step counter does not advance. */
+int se_step_replay(se_env* env, const int32_t* type, const int32_t* a, const int32_t* b,
+                   const se_tape* tape, void* stream);
+
+/* utils.preprocessing.preprocess_state rows (:25-62) as f32, row stride ld >= 6+4P:
+ * [x, y, fuel, fuel ("cargo" is self.fuel, environment.py:206), origin, dest, (px,py,pfuel,pcargo)*P],
+ * None -> -1. */
+int se_observe(se_env* env, float* obs, int64_t ld, void* stream);
+
+/* DQN is_valid_action (agents/dqn.py:125-175) for every agent index a < 4+P+250,
+ * packed MSB-first per row (numpy.packbits order), row stride ceil((4+P+250)/8) bytes. */
+int se_valid_mask(se_env* env, uint8_t* bits, void* stream);
+
+/* Synthetic agent: fills actions[i] from Philox(seed, env) at (t, slot 6) with the
+ * bench mix (90% move, 5% take cargo U{1..20}, 3% take fuel U{1..20}, 2% select). */
+int se_gen_actions(se_env* env, int32_t* actions, uint32_t t, void* stream);
+
+/* Episode statistics accumulated by the auto-reset path since the last clear:
+ * out[0] = sum of returns, out[1] = episodes, out[2] = sum of lengths (device
+ * double[3]). Deterministic: per-block partials are summed in a fixed order. */
+int se_episode_stats(se_env* env, double* out, void* stream);
+int se_clear_stats(se_env* env, void* stream);
+
+/* Where the most recent se_step (auto-reset) wrote its done list: records
+ * done_recs[rec_offset ...] and their number in done_count[count_index]. The
+ * list stays intact while the following step runs; the step after it reuses it. */
+int se_done_list(se_env* env, int64_t* rec_offset, int32_t* count_index);
+
+/* Step counter / reset epoch (checkpoint-resume; shard replay). */
+int se_get_counters(se_env* env, uint64_t* step, uint64_t* epoch);
+int se_set_counters(se_env* env, uint64_t step, uint64_t epoch);
+
+int se_destroy(se_env* env);
+const char* se_last_error(void);
+int se_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,456 @@
+/* shipenv_oracle.c — CPU restatement of the reference hot path (TEST INFRASTRUCTURE).
+ *
+ * Header: shipenv_oracle.h. Built by oracle/Makefile with -O2 -ffp-contract=off
+ * (the reference's arithmetic is unfused IEEE f64: CPython floats and np.sqrt).
+ *
+ * Parity: pinned. The replay mode reproduces every record of
+ * tests/golden/{tape,states}_seed*.npz (generated from the reference itself by
+ * tests/golden/make_golden.py) bit for bit; tests/test_oracle_golden.py checks it.
+ * The Philox mode is the production RNG contract, which the HIP
+ * kernel must match bit for bit; its distributional equivalence to the
+ * reference's MT19937 draws is argued in DESIGN.md.
+ */
+#include "shipenv_oracle.h"
+
+#include <math.h>
+#include <stddef.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ constants */
+/* shipping/environment.py:8-26 */
+#define INITIAL_FUEL 200
+#define MAX_CARGO_CAPACITY 50
+#define R_CARGO_DELIVER 2
+#define R_REACH_DESTINATION 10
+#define R_CLOSER 2
+#define R_TAKE 0.05
+#define P_OUT_OF_FUEL (-10)
+#define P_GROUND (-5)
+#define P_WATER (-1)
+#define P_CARGO_LOSS (-3)
+#define P_FARTHER (-2)
+#define P_USE_FUEL (-0.0001)
+
+/* shipping/type.py:1-5 */
+enum { MOVE_SHIP = 1, SELECT_PORT = 2, TAKE_FUEL = 3, TAKE_CARGO = 4 };
+
+/* error classes (include/shipenv.h SE_ERR_*) */
+enum {
+    E_OK = 0, E_OOB = 1, E_SAME_PORT = 2, E_PORT_RANGE = 3, E_NOT_AT_PORT = 4, E_AMOUNT = 5,
+    E_NO_DEST = 6, E_BAD_CATEGORY = 7, E_NO_PORTS = 8, E_BAD_INDEX = 9
+};
+
+/* Philox counter slots (DESIGN.md "RNG contract") */
+enum { SLOT_MOVE = 0, SLOT_LOSS = 1, SLOT_BETA = 2, SLOT_ARRIVE = 3, SLOT_RESET = 4,
+       SLOT_EXPLICIT_RESET = 5, SLOT_ACTION = 6 };
+
+/* ------------------------------------------------------------------ Philox4x32-10 */
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n1 = (uint32_t)p1;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        uint32_t n3 = (uint32_t)p0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+static void draw4(uint64_t seed, int64_t env, uint32_t t, uint32_t slot, uint32_t out[4]) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t ctr[4] = {(uint32_t)(uint64_t)env, (uint32_t)((uint64_t)env >> 32), t, slot};
+    orc_philox4x32_10(ctr, key, out);
+}
+
+/* CPython random_random(): (a>>5, b>>6) -> 53-bit double in [0, 1) */
+static double u53(uint32_t a, uint32_t b) {
+    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+static int32_t uniform_int(uint32_t r, int32_t m) { return (int32_t)(((uint64_t)r * (uint32_t)m) >> 32); }
+
+/* a port index uniform over the P-1 ports other than `other` */
+static int32_t pick_other(uint32_t r, int32_t P, int32_t other) {
+    int32_t k = uniform_int(r, P - 1);
+    return k + (k >= other);
+}
+
+static double med3(double a, double b, double c) {
+    double lo = a < b ? a : b, hi = a < b ? b : a;
+    return c < lo ? lo : (c > hi ? hi : c);
+}
+
+/* ------------------------------------------------------------------ draw source */
+typedef struct {
+    const orc_tape* tape; /* replay if non-NULL */
+    uint64_t seed;
+    int64_t env;
+    uint32_t t;
+} source;
+
+/* u_fuel and u_gate: environment.py:104 (uniform) and :320 (random), always both */
+static void src_move(const source* s, double* u_fuel, double* u_gate) {
+    if (s->tape) {
+        *u_fuel = s->tape->u_fuel;
+        *u_gate = s->tape->u_gate;
+        return;
+    }
+    uint32_t o[4];
+    draw4(s->seed, s->env, s->t, SLOT_MOVE, o);
+    *u_fuel = u53(o[0], o[1]);
+    *u_gate = u53(o[2], o[3]);
+}
+
+static double src_loss_type(const source* s) { /* environment.py:177 */
+    if (s->tape) return s->tape->u_type;
+    uint32_t o[4];
+    draw4(s->seed, s->env, s->t, SLOT_LOSS, o);
+    return u53(o[0], o[1]);
+}
+
+static double src_beta(const source* s) { /* environment.py:195, betavariate(2, 2) */
+    if (s->tape) return s->tape->beta;
+    uint32_t a[4], b[4];
+    draw4(s->seed, s->env, s->t, SLOT_LOSS, a);
+    draw4(s->seed, s->env, s->t, SLOT_BETA, b);
+    return med3(u53(a[2], a[3]), u53(b[0], b[1]), u53(b[2], b[3]));
+}
+
+static int32_t src_arrive(const source* s, int32_t P, int32_t origin) { /* :333-335 */
+    if (s->tape) return s->tape->arrive_dest;
+    uint32_t o[4];
+    draw4(s->seed, s->env, s->t, SLOT_ARRIVE, o);
+    return pick_other(o[0], P, origin);
+}
+
+/* ------------------------------------------------------------------ one env */
+typedef struct {
+    int32_t x, y;
+    double fuel;
+    int32_t cargo, origin, dest;
+} ship;
+
+static int ground_at(const orc_world* w, int32_t x, int32_t y) {
+    return w->nonground[(size_t)x * w->W + y] == 0; /* np_game[x, y] == Entity.GROUND, :293 */
+}
+
+/* _is_within_map, :77-101 (x against size[0], y against size[1]) */
+static int within(const orc_world* w, int64_t x, int64_t y) {
+    return 0 <= x && x < w->H && 0 <= y && y < w->W;
+}
+
+/* _get_current_port_idx, :145-153: first port equal to the ship position */
+static int32_t current_port(const orc_world* w, const ship* s) {
+    for (int32_t i = 0; i < w->P; ++i)
+        if (w->port_x[i] == s->x && w->port_y[i] == s->y) return i;
+    return -1;
+}
+
+/* _move_ship, :273-339 */
+static int move_ship(const orc_world* w, ship* s, int64_t mx, int64_t my, const source* src,
+                     double* reward, int32_t* done) {
+    if (s->dest < 0) return E_NO_DEST; /* :276 */
+    double r = 0.0;
+    int32_t d = 0;
+    int64_t nx = s->x + mx, ny = s->y + my; /* :280-282 */
+    if (!within(w, nx, ny)) return E_OOB; /* :284, no draw consumed */
+
+    double u_fuel, u_gate;
+    src_move(src, &u_fuel, &u_gate);
+    /* _calculate_fuel_cost :103-104 -> util.calculate_euclidean_distance (util.py:3-4):
+     * np.sqrt of the integer sum of squares, times (1 + uniform(-0.1, 0.1)) */
+    double dist = sqrt((double)(mx * mx + my * my));
+    double uni = -0.1 + 0.2 * u_fuel; /* CPython uniform: a + (b - a) * random() */
+    double cost = dist * (1.0 + uni);
+    if (s->fuel < cost) { /* :288-290 */
+        r += P_OUT_OF_FUEL;
+        d = 1;
+    }
+    int32_t ox = s->x, oy = s->y;
+    if (ground_at(w, (int32_t)nx, (int32_t)ny)) { /* :293-294 */
+        r += P_GROUND;
+    } else { /* :296-300, the ship moves even when it just ran out of fuel */
+        s->x = (int32_t)nx;
+        s->y = (int32_t)ny;
+        s->fuel -= cost;
+        r += P_USE_FUEL;
+        r += P_WATER;
+    }
+    /* :307-315: distance of the old and the ATTEMPTED cell to the destination */
+    int32_t px = w->port_x[s->dest], py = w->port_y[s->dest];
+    double prev = sqrt((double)((int64_t)(ox - px) * (ox - px) + (int64_t)(oy - py) * (oy - py)));
+    double next = sqrt((double)((nx - px) * (nx - px) + (ny - py) * (ny - py)));
+    if (prev - next > 0) r += R_CLOSER;
+    else r += P_FARTHER;
+    /* :318-323: loss gate normalize(cargo, 50, 0) = cargo / 50 (util.py:6-8) */
+    double likelihood = (double)s->cargo / (double)MAX_CARGO_CAPACITY;
+    if (u_gate <= likelihood) {
+        /* _calculate_cargo_loss :169-200: the loss-type draw happens first, always */
+        double lt = src_loss_type(src);
+        int32_t loss;
+        if (s->cargo == 0) loss = 0;
+        else if (lt < 0.1) loss = 0;
+        else if (lt > 0.9) loss = s->cargo;
+        else loss = (int32_t)(src_beta(src) * (double)s->cargo); /* int() truncation */
+        s->cargo -= loss;
+        r += (double)(loss * P_CARGO_LOSS);
+    }
+    /* :325-337 arrival (also while blocked, if the ship already sits on dest) */
+    if (s->x == w->port_x[s->dest] && s->y == w->port_y[s->dest]) {
+        int32_t drop = s->cargo;
+        s->cargo = 0;
+        r += (double)(drop * R_CARGO_DELIVER);
+        s->origin = s->dest;
+        s->dest = src_arrive(src, w->P, s->origin);
+        r += R_REACH_DESTINATION;
+    }
+    *reward = r;
+    *done = d;
+    return E_OK;
+}
+
+/* step, :359-376, with the typed action [category, value] */
+static int step_typed(const orc_world* w, ship* s, int32_t type, int32_t a, int32_t b,
+                      const source* src, double* reward, int32_t* done) {
+    *reward = 0.0;
+    *done = 0;
+    if (w->P == 0) return E_NO_PORTS; /* :360 */
+    switch (type) {
+    case SELECT_PORT: /* _select_port :265-271 */
+        if (!(0 <= a && a < w->P)) return E_PORT_RANGE;
+        if (s->origin == a) return E_SAME_PORT;
+        s->dest = a;
+        return E_OK;
+    case TAKE_CARGO: { /* _take_cargo :341-348 */
+        int32_t idx = current_port(w, s);
+        if (idx < 0) return E_NOT_AT_PORT;
+        if (!(0 < a && a <= w->port_cargo[idx])) return E_AMOUNT;
+        s->cargo += a;
+        *reward = R_TAKE;
+        return E_OK;
+    }
+    case TAKE_FUEL: { /* _take_fuel :350-357 */
+        int32_t idx = current_port(w, s);
+        if (idx < 0) return E_NOT_AT_PORT;
+        if (!(0 < a && a <= w->port_fuel[idx])) return E_AMOUNT;
+        s->fuel += (double)a;
+        *reward = R_TAKE;
+        return E_OK;
+    }
+    case MOVE_SHIP:
+        return move_ship(w, s, a, b, src, reward, done);
+    default:
+        return E_BAD_CATEGORY; /* :373-374 */
+    }
+}
+
+/* utils/preprocessing.py:111-137 map_action_to_env_action (Python list indexing:
+ * moves[-4..-1] wrap, anything below raises IndexError) */
+static int decode_agent(int32_t P, int32_t act, int32_t* type, int32_t* a, int32_t* b) {
+    static const int32_t mx[4] = {0, -1, 0, 1}; /* N, E, S, W (:126, shipping/type.py:8-16) */
+    static const int32_t my[4] = {-1, 0, 1, 0};
+    if (act < 4) {
+        if (act < -4) return E_BAD_INDEX;
+        int32_t k = act < 0 ? act + 4 : act;
+        *type = MOVE_SHIP;
+        *a = mx[k];
+        *b = my[k];
+    } else if (act < 4 + P) {
+        *type = SELECT_PORT;
+        *a = act - 4;
+    } else if (act < 4 + P + MAX_CARGO_CAPACITY) {
+        *type = TAKE_CARGO;
+        *a = act - (4 + P);
+    } else {
+        *type = TAKE_FUEL;
+        *a = act - (4 + P + MAX_CARGO_CAPACITY);
+    }
+    return E_OK;
+}
+
+static void load(ship* s, int64_t i, const int32_t* x, const int32_t* y, const double* fuel,
+                 const int32_t* cargo, const int32_t* origin, const int32_t* dest) {
+    s->x = x[i]; s->y = y[i]; s->fuel = fuel[i];
+    s->cargo = cargo[i]; s->origin = origin[i]; s->dest = dest[i];
+}
+
+static void store(const ship* s, int64_t i, int32_t* x, int32_t* y, double* fuel, int32_t* cargo,
+                  int32_t* origin, int32_t* dest) {
+    x[i] = s->x; y[i] = s->y; fuel[i] = s->fuel;
+    cargo[i] = s->cargo; origin[i] = s->origin; dest[i] = s->dest;
+}
+
+int orc_step_batch(const orc_world* w, int64_t n, int act_mode, const int32_t* act_type,
+                   const int32_t* act_a, const int32_t* act_b, const orc_tape* tape, uint64_t seed,
+                   int64_t env_id_base, uint32_t t, int32_t* x, int32_t* y, double* fuel,
+                   int32_t* cargo, int32_t* origin, int32_t* dest, double* reward, int32_t* done,
+                   int32_t* err) {
+    for (int64_t i = 0; i < n; ++i) {
+        ship s;
+        load(&s, i, x, y, fuel, cargo, origin, dest);
+        source src = {tape ? tape + i : NULL, seed, env_id_base + i, t};
+        int32_t ty = 0, a = 0, b = 0;
+        int e;
+        double r = 0.0;
+        int32_t d = 0;
+        if (act_mode == 0) {
+            /* the decode runs before env.step (agents/dqn.py:286-287), so its
+             * IndexError wins over "No ports available" */
+            e = decode_agent(w->P, act_a[i], &ty, &a, &b);
+        } else {
+            ty = act_type[i]; a = act_a[i]; b = act_b[i];
+            e = E_OK;
+        }
+        if (e == E_OK) {
+            ship t2 = s;
+            e = step_typed(w, &t2, ty, a, b, &src, &r, &d);
+            if (e == E_OK) s = t2; /* an exception leaves the state as it was */
+        }
+        if (e != E_OK) {
+            r = 0.0;
+            d = 0;
+        }
+        store(&s, i, x, y, fuel, cargo, origin, dest);
+        reward[i] = r;
+        done[i] = d;
+        err[i] = e;
+    }
+    return 0;
+}
+
+/* reset :227-243 with Philox slot `slot` of counter word t */
+static void reset_philox(const orc_world* w, ship* s, uint64_t seed, int64_t env, uint32_t t,
+                         uint32_t slot) {
+    uint32_t o[4];
+    draw4(seed, env, t, slot, o);
+    s->origin = uniform_int(o[0], w->P);
+    s->dest = pick_other(o[1], w->P, s->origin);
+    s->cargo = 0;
+    s->fuel = INITIAL_FUEL;
+    s->x = w->port_x[s->origin];
+    s->y = w->port_y[s->origin];
+}
+
+int orc_reset_batch(const orc_world* w, int64_t n, const uint8_t* mask, const int32_t* origin_in,
+                    const int32_t* dest_in, uint64_t seed, int64_t env_id_base, uint32_t epoch,
+                    int32_t* x, int32_t* y, double* fuel, int32_t* cargo, int32_t* origin,
+                    int32_t* dest) {
+    if (w->P < 2) return -1; /* the reference's dest != origin loop never ends for P < 2 */
+    for (int64_t i = 0; i < n; ++i) {
+        if (mask && !mask[i]) continue;
+        ship s;
+        if (origin_in) {
+            s.origin = origin_in[i];
+            s.dest = dest_in[i];
+            s.cargo = 0;
+            s.fuel = INITIAL_FUEL;
+            s.x = w->port_x[s.origin];
+            s.y = w->port_y[s.origin];
+        } else {
+            reset_philox(w, &s, seed, env_id_base + i, epoch, SLOT_EXPLICIT_RESET);
+        }
+        store(&s, i, x, y, fuel, cargo, origin, dest);
+    }
+    return 0;
+}
+
+int orc_step_batch_autoreset(const orc_world* w, int64_t n, const int32_t* actions, uint64_t seed,
+                             int64_t env_id_base, uint32_t t, int32_t* x, int32_t* y, double* fuel,
+                             int32_t* cargo, int32_t* origin, int32_t* dest, float* ep_return,
+                             int32_t* ep_len, double* reward, int32_t* done, int32_t* err,
+                             double* stats) {
+    if (w->P < 2) return -1;
+    orc_step_batch(w, n, 0, NULL, actions, NULL, NULL, seed, env_id_base, t, x, y, fuel, cargo,
+                   origin, dest, reward, done, err);
+    for (int64_t i = 0; i < n; ++i) {
+        float rf = (float)reward[i];
+        ep_return[i] += rf;
+        ep_len[i] += 1;
+        if (done[i]) {
+            stats[0] += (double)ep_return[i];
+            stats[1] += 1.0;
+            stats[2] += (double)ep_len[i];
+            ship s;
+            reset_philox(w, &s, seed, env_id_base + i, t, SLOT_RESET);
+            store(&s, i, x, y, fuel, cargo, origin, dest);
+            ep_return[i] = 0.0f;
+            ep_len[i] = 0;
+        }
+    }
+    return 0;
+}
+
+int orc_observe(const orc_world* w, int64_t n, const int32_t* x, const int32_t* y,
+                const double* fuel, const int32_t* origin, const int32_t* dest, float* obs) {
+    const int64_t ld = 6 + 4 * (int64_t)w->P;
+    for (int64_t i = 0; i < n; ++i) {
+        float* row = obs + i * ld;
+        row[0] = (float)x[i];
+        row[1] = (float)y[i];
+        row[2] = (float)fuel[i];
+        row[3] = (float)fuel[i]; /* "cargo": self.fuel, shipping/environment.py:206 */
+        row[4] = (float)origin[i]; /* None -> -1, utils/preprocessing.py:42-45 */
+        row[5] = (float)dest[i];
+        for (int32_t p = 0; p < w->P; ++p) {
+            row[6 + 4 * p + 0] = (float)w->port_x[p];
+            row[6 + 4 * p + 1] = (float)w->port_y[p];
+            row[6 + 4 * p + 2] = (float)w->port_fuel[p];
+            row[6 + 4 * p + 3] = (float)w->port_cargo[p];
+        }
+    }
+    return 0;
+}
+
+int orc_valid_mask(const orc_world* w, int64_t n, const int32_t* x, const int32_t* y,
+                   const int32_t* origin, uint8_t* bits) {
+    const int32_t P = w->P, A = 4 + P + 50 + 200;
+    const int64_t stride = (A + 7) / 8;
+    memset(bits, 0, (size_t)(n * stride));
+    for (int64_t i = 0; i < n; ++i) {
+        ship s = {x[i], y[i], 0.0, 0, origin[i], 0};
+        int32_t cur = current_port(w, &s);
+        for (int32_t a = 0; a < A; ++a) {
+            int v;
+            if (a < 4) v = 1;
+            else if (a < 4 + P) { /* must sit on that port and it must not be the origin */
+                int32_t p = a - 4;
+                v = !(origin[i] >= 0 && p == origin[i]) && w->port_x[p] == x[i] &&
+                    w->port_y[p] == y[i];
+            } else if (a < 4 + P + 50) {
+                int32_t amt = a - (4 + P);
+                v = cur >= 0 && 0 < amt && amt <= w->port_cargo[cur];
+            } else {
+                int32_t amt = a - (4 + P + 50);
+                v = cur >= 0 && 0 < amt && amt <= w->port_fuel[cur];
+            }
+            if (v) bits[i * stride + a / 8] |= (uint8_t)(0x80u >> (a % 8));
+        }
+    }
+    return 0;
+}
+
+/* Bench action mix: 90 % move (uniform direction),
+ * 5 % TAKE_CARGO U{1..20}, 3 % TAKE_FUEL U{1..20}, 2 % SELECT U{0..P-1}. */
+int orc_gen_actions(int64_t n, int32_t P, uint64_t seed, int64_t env_id_base, uint32_t t,
+                    int32_t* actions) {
+    for (int64_t i = 0; i < n; ++i) {
+        uint32_t o[4];
+        draw4(seed, env_id_base + i, t, SLOT_ACTION, o);
+        int32_t c = uniform_int(o[0], 100);
+        int32_t a;
+        if (c < 90) a = (int32_t)(o[1] & 3u);
+        else if (c < 95) a = 4 + P + 1 + uniform_int(o[1], 20);
+        else if (c < 98) a = 4 + P + 50 + 1 + uniform_int(o[1], 20);
+        else a = 4 + uniform_int(o[2], P);
+        actions[i] = a;
+    }
+    return 0;
+}

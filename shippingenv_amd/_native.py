@@ -1,0 +1,111 @@
+"""ctypes binding of libshipenv_hip.so (the C-ABI of include/shipenv.h).
+
+There is no fallback: if the gfx950 library is missing or fails to load,
+``lib()`` raises ``NativeLibraryError``. The library is built in-tree by
+``__graft_entry__.build()`` (or ``python -m shippingenv_amd.build``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_lib", "libshipenv_hip.so")
+ABI_VERSION = 1
+
+SE_FLAG_AUTO_RESET = 1
+SE_NONE = 255
+
+# per-env error classes (include/shipenv.h SE_ERR_*)
+ERR_OK, ERR_OOB, ERR_SAME_PORT, ERR_PORT_RANGE, ERR_NOT_AT_PORT = 0, 1, 2, 3, 4
+ERR_AMOUNT, ERR_NO_DEST, ERR_BAD_CATEGORY, ERR_NO_PORTS, ERR_BAD_INDEX = 5, 6, 7, 8, 9
+
+# every symbol include/shipenv.h declares
+EXPORTS = (
+    "se_create", "se_set_ports", "se_bind", "se_reset", "se_reset_to", "se_step",
+    "se_step_typed", "se_step_replay", "se_observe", "se_valid_mask", "se_gen_actions",
+    "se_episode_stats", "se_clear_stats", "se_done_list", "se_get_counters", "se_set_counters",
+    "se_destroy", "se_last_error", "se_abi_version",
+)
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class ShipEnvError(RuntimeError):
+    """A negative status from the C-ABI (API misuse or a HIP failure)."""
+
+
+class SeState(C.Structure):
+    _fields_ = [(name, C.c_void_p) for name in (
+        "x", "y", "fuel", "cargo", "origin", "dest", "reward", "done", "err", "ep_return",
+        "ep_len", "done_recs", "done_count")]
+
+
+class SeDoneRec(C.Structure):
+    _fields_ = [("env", C.c_int32), ("ep_return", C.c_float), ("ep_len", C.c_int32),
+                ("step", C.c_int32)]
+
+
+_LIB = None
+
+
+def _declare(lib):
+    P, i32, i64, u32, u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
+    sig = {
+        "se_create": [C.POINTER(P), C.c_int, i64, i64, i32, i32, P, i32, P, P, P, P, u64, u32],
+        "se_set_ports": [P, i32, P, P, P, P],
+        "se_bind": [P, C.POINTER(SeState)],
+        "se_reset": [P, P, P],
+        "se_reset_to": [P, P, P, P, P],
+        "se_step": [P, P, P],
+        "se_step_typed": [P, P, P, P, P],
+        "se_step_replay": [P, P, P, P, P, P],
+        "se_observe": [P, P, i64, P],
+        "se_valid_mask": [P, P, P],
+        "se_gen_actions": [P, P, u32, P],
+        "se_episode_stats": [P, P, P],
+        "se_clear_stats": [P, P],
+        "se_done_list": [P, C.POINTER(i64), C.POINTER(i32)],
+        "se_get_counters": [P, C.POINTER(u64), C.POINTER(u64)],
+        "se_set_counters": [P, u64, u64],
+        "se_destroy": [P],
+        "se_last_error": [],
+        "se_abi_version": [],
+    }
+    for name, args in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = C.c_int
+    lib.se_last_error.restype = C.c_char_p
+
+
+def lib():
+    """Load the gfx950 library (once). Raises NativeLibraryError if it is unusable."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    try:
+        handle = C.CDLL(LIB_PATH)
+    except OSError as e:
+        raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+    missing = [s for s in EXPORTS if not hasattr(handle, s)]
+    if missing:
+        raise NativeLibraryError(f"{LIB_PATH} lacks symbols {missing}")
+    _declare(handle)
+    if handle.se_abi_version() != ABI_VERSION:
+        raise NativeLibraryError("ABI version mismatch; rebuild the library")
+    _LIB = handle
+    return _LIB
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().se_last_error().decode(errors="replace")
+        raise ShipEnvError(f"shipenv status {rc}: {msg}")
+    return rc

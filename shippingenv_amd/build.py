@@ -1,0 +1,54 @@
+"""Build the gfx950 library in-tree: shippingenv_amd/_lib/libshipenv_hip.so.
+
+    python -m shippingenv_amd.build
+
+hipcc only (no torch extension machinery): the library is a plain C-ABI shared
+object. -ffp-contract=off keeps the reference's unfused f64 arithmetic.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "csrc", "shipenv.hip")
+DEPS = [SRC, os.path.join(HERE, "csrc", "philox.h"), os.path.join(ROOT, "include", "shipenv.h")]
+OUT = os.path.join(HERE, "_lib", "libshipenv_hip.so")
+ARCH = os.environ.get("SHIPENV_OFFLOAD_ARCH", "gfx950")
+
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+         "-Wall", "-Wextra", f"--offload-arch={ARCH}"]
+
+
+def hipcc():
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm is required to build libshipenv_hip.so)")
+
+
+def up_to_date():
+    if not os.path.exists(OUT):
+        return False
+    t = os.path.getmtime(OUT)
+    return all(os.path.getmtime(d) <= t for d in DEPS)
+
+
+def build(force=False, verbose=True):
+    if not force and up_to_date():
+        return OUT
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    tmp = OUT + ".tmp"
+    cmd = [hipcc()] + FLAGS + ["-o", tmp, SRC]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,72 @@
+// philox.h — device-side counter-based RNG for the step kernels (gfx950).
+//
+// Philox4x32-10 (Salmon et al., SC'11; constants of Random123's philox4x32),
+// keyed by the 64-bit seed and indexed by (global env id, step counter, slot):
+// no RNG state lives in HBM. The draw conventions below are the "RNG contract"
+// of DESIGN.md; oracle/shipenv_oracle.c states the same contract independently
+// on the CPU, and tests compare the two bit for bit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace shipenv {
+
+enum Slot : uint32_t {
+    kSlotMove = 0,           // u_fuel (words 0,1), u_gate (words 2,3)
+    kSlotLoss = 1,           // u_type (0,1), first beta uniform (2,3)
+    kSlotBeta = 2,           // second and third beta uniforms
+    kSlotArrive = 3,         // word 0 -> new destination != origin
+    kSlotReset = 4,          // auto-reset inside step t: word 0 origin, word 1 dest
+    kSlotExplicitReset = 5,  // se_reset with the reset epoch in the t word
+    kSlotAction = 6,         // synthetic bench agent
+};
+
+struct U4 {
+    uint32_t v[4];
+};
+
+__device__ __forceinline__ U4 philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                       uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0;
+        c1 = lo1;
+        c2 = n2;
+        c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return U4{{c0, c1, c2, c3}};
+}
+
+// (seed, env, t, slot) -> 4 words
+struct Key {
+    uint32_t k0, k1;  // seed
+    uint32_t e0, e1;  // global env id
+};
+
+__device__ __forceinline__ U4 draw(const Key& k, uint32_t t, uint32_t slot) {
+    return philox10(k.e0, k.e1, t, slot, k.k0, k.k1);
+}
+
+// CPython's 53-bit random(): (a >> 5) * 2^26 + (b >> 6), scaled by 2^-53.
+// Exact in f64 (both products are exact), so contraction cannot change it.
+__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
+    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+// integer uniform on [0, m): high word of r * m (bias < m / 2^32)
+__device__ __forceinline__ int32_t uniform_int(uint32_t r, uint32_t m) {
+    return (int32_t)__umulhi(r, m);
+}
+
+// port index uniform over the P-1 ports other than `other`
+__device__ __forceinline__ int32_t pick_other(uint32_t r, int32_t P, int32_t other) {
+    const int32_t k = uniform_int(r, (uint32_t)(P - 1));
+    return k + (k >= other ? 1 : 0);
+}
+
+}  // namespace shipenv

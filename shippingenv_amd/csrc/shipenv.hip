@@ -1,0 +1,1075 @@
+// shipenv.hip — MI355X (gfx950) batched ShippingEnv: step / reset / observe kernels
+// and the C-ABI of include/shipenv.h.
+//
+// What one step does per environment is shipping/environment.py:359-376 (step)
+// and :273-339 (_move_ship) of the reference; DESIGN.md walks through the
+// mapping. The shape of the work is what drives the design:
+//   * the path is HBM-streaming integer/f64 work, ~0 useful FLOPs: no MFMA;
+//   * state is SoA with narrow fields (u8 positions/indices, i32 cargo,
+//     f64 fuel) so each field of 4 consecutive envs is one 4-/16-byte lane
+//     access: every wave instruction is a fully coalesced 256 B - 1 KiB access;
+//   * the static world (ground bitmap, port bitmap, ports table) is staged once
+//     per workgroup into LDS; the per-env map lookups are LDS reads;
+//   * RNG is counter-based Philox keyed by (seed, global env id): 0 bytes of RNG
+//     state in HBM and shard-invariant results;
+//   * auto-reset compacts finished envs into a done list with one wave ballot
+//     prefix and one atomic per wave, and reduces episode statistics per
+//     workgroup into a fixed slab (deterministic sums, no float atomics).
+//
+// Built with -ffp-contract=off: the reference's f64 arithmetic (CPython float,
+// np.sqrt) is unfused, and an FMA in -0.1 + 0.2*u changes fuel bits.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/shipenv.h"
+#include "philox.h"
+
+using namespace shipenv;
+
+namespace {
+
+constexpr int kBlock = 256;       // 4 waves
+constexpr int kEnvsPerThread = 4; // one 4-byte / 16-byte lane access per field
+constexpr int kMaxBlocks = 2048;  // 256 CUs x 8; grid-stride beyond
+
+// reference constants, shipping/environment.py:8-26
+constexpr double kFuelInit = 200.0;
+constexpr double kMaxCargo = 50.0;
+
+// ------------------------------------------------------------------ world image
+// One device buffer of 32-bit words, staged as-is into LDS:
+//   [0, words)            ground bitmap   (bit = 1: np_game[x, y] == GROUND)
+//   [words, 2*words)      port bitmap     (bit = 1: some port sits on the cell)
+//   [2w, 2w+P)            port position   (x | y << 8)
+//   [2w+P, 2w+2P)         port fuel stock
+//   [2w+2P, 2w+3P)        port cargo stock
+struct WorldDims {
+    int32_t H, W, P, words;
+    __host__ __device__ int total() const { return 2 * words + 3 * P; }
+};
+
+struct LdsWorld {
+    const uint32_t* ground;
+    const uint32_t* portbit;
+    const uint32_t* pos;
+    const int32_t* pfuel;
+    const int32_t* pcargo;
+    int32_t H, W, P;
+
+    __device__ bool is_ground(int x, int y) const {
+        const uint32_t c = (uint32_t)(x * W + y);
+        return (ground[c >> 5] >> (c & 31)) & 1u;
+    }
+    // _get_current_port_idx (:145-153): first port on the ship's cell, -1 if none
+    __device__ int port_at(int x, int y) const {
+        const uint32_t c = (uint32_t)(x * W + y);
+        if (!((portbit[c >> 5] >> (c & 31)) & 1u)) return -1;
+        const uint32_t key = (uint32_t)x | ((uint32_t)y << 8);
+        for (int i = 0; i < P; ++i)
+            if (pos[i] == key) return i;
+        return -1;
+    }
+    __device__ int px(int i) const { return (int)(pos[i] & 0xffu); }
+    __device__ int py(int i) const { return (int)((pos[i] >> 8) & 0xffu); }
+};
+
+__device__ __forceinline__ LdsWorld stage_world(const uint32_t* __restrict__ g, WorldDims d,
+                                                uint32_t* lds) {
+    const int total = d.total();
+    for (int i = threadIdx.x; i < total; i += blockDim.x) lds[i] = g[i];
+    __syncthreads();
+    LdsWorld w;
+    w.ground = lds;
+    w.portbit = lds + d.words;
+    w.pos = lds + 2 * d.words;
+    w.pfuel = (const int32_t*)(lds + 2 * d.words + d.P);
+    w.pcargo = (const int32_t*)(lds + 2 * d.words + 2 * d.P);
+    w.H = d.H;
+    w.W = d.W;
+    w.P = d.P;
+    return w;
+}
+
+// ------------------------------------------------------------------ one env
+struct Ship {
+    int x, y;
+    double fuel;
+    int cargo, origin, dest;  // origin/dest: SE_NONE = None
+};
+
+// Variates of one MOVE: Philox (production) or a replay tape.
+template <bool kReplay>
+struct Draws;
+
+template <>
+struct Draws<false> {
+    Key key;
+    uint32_t t;
+    __device__ void move(double& u_fuel, double& u_gate) const {
+        const U4 o = draw(key, t, kSlotMove);
+        u_fuel = u53(o.v[0], o.v[1]);
+        u_gate = u53(o.v[2], o.v[3]);
+    }
+    __device__ double loss_type() const {
+        const U4 o = draw(key, t, kSlotLoss);
+        return u53(o.v[0], o.v[1]);
+    }
+    // Beta(2, 2) as the median of three uniforms (exact in distribution)
+    __device__ double beta() const {
+        const U4 a = draw(key, t, kSlotLoss), b = draw(key, t, kSlotBeta);
+        const double u1 = u53(a.v[2], a.v[3]), u2 = u53(b.v[0], b.v[1]), u3 = u53(b.v[2], b.v[3]);
+        return fmax(fmin(u1, u2), fmin(fmax(u1, u2), u3));
+    }
+    __device__ int arrive(int P, int origin) const {
+        const U4 o = draw(key, t, kSlotArrive);
+        return pick_other(o.v[0], P, origin);
+    }
+};
+
+template <>
+struct Draws<true> {
+    const se_tape* rec;
+    __device__ void move(double& u_fuel, double& u_gate) const {
+        u_fuel = rec->u_fuel;
+        u_gate = rec->u_gate;
+    }
+    __device__ double loss_type() const { return rec->u_type; }
+    __device__ double beta() const { return rec->beta; }
+    __device__ int arrive(int, int) const { return rec->arrive_dest; }
+};
+
+// sqrt of a non-negative integer, correctly rounded (np.sqrt on the int sum of
+// squares, shipping/util.py:4). Unit moves take the exact fast path.
+__device__ __forceinline__ double int_sqrt_rn(int64_t v) {
+    return v == 1 ? 1.0 : __dsqrt_rn((double)v);
+}
+
+// _move_ship (:273-339). Returns SE_ERR_*; on error s is untouched.
+template <bool kReplay>
+__device__ __forceinline__ int move_ship(const LdsWorld& w, Ship& s, int64_t mx, int64_t my,
+                                         const Draws<kReplay>& dr, double& reward, int& done) {
+    if (s.dest == SE_NONE) return SE_ERR_NO_DEST;  // :276
+    const int64_t nx = s.x + mx, ny = s.y + my;
+    if (nx < 0 || nx >= w.H || ny < 0 || ny >= w.W) return SE_ERR_OOB;  // :284, before any draw
+
+    double u_fuel, u_gate;
+    dr.move(u_fuel, u_gate);
+    // fuel cost (:103-104): dist * (1 + uniform(-0.1, 0.1)), uniform = -0.1 + 0.2*u, unfused
+    const double cost = int_sqrt_rn(mx * mx + my * my) * (1.0 + (-0.1 + 0.2 * u_fuel));
+    double r = 0.0;
+    int d = 0;
+    if (s.fuel < cost) {  // :288-290
+        r += -10.0;
+        d = 1;
+    }
+    const int ox = s.x, oy = s.y;
+    if (w.is_ground((int)nx, (int)ny)) {  // :293-294: blocked, but still "arrives" below if on dest
+        r += -5.0;
+    } else {  // :296-300
+        s.x = (int)nx;
+        s.y = (int)ny;
+        s.fuel -= cost;
+        r += -0.0001;
+        r += -1.0;
+    }
+    // :307-315 closer/farther, old cell vs ATTEMPTED cell. sqrt is monotone and the
+    // squared distances are small integers, so comparing them is exact.
+    const int px = w.px(s.dest), py = w.py(s.dest);
+    const int64_t d_old = (int64_t)(ox - px) * (ox - px) + (int64_t)(oy - py) * (oy - py);
+    const int64_t d_new = (nx - px) * (nx - px) + (ny - py) * (ny - py);
+    r += d_old > d_new ? 2.0 : -2.0;
+    // :318-323 cargo-loss gate: random() <= cargo / 50
+    if (u_gate <= (double)s.cargo / kMaxCargo) {
+        const double lt = dr.loss_type();  // drawn first, even with no cargo (:177)
+        int loss = 0;
+        if (s.cargo != 0 && lt >= 0.1) loss = lt > 0.9 ? s.cargo : (int)(dr.beta() * (double)s.cargo);
+        s.cargo -= loss;
+        r += (double)(-3 * loss);
+    }
+    // :325-337 arrival at the destination port
+    if (s.x == px && s.y == py) {
+        r += (double)(2 * s.cargo);
+        s.cargo = 0;
+        s.origin = s.dest;
+        s.dest = dr.arrive(w.P, s.origin);
+        r += 10.0;
+    }
+    reward = r;
+    done = d;
+    return SE_ERR_OK;
+}
+
+// step (:359-376) with a typed action. On error the state is untouched.
+template <bool kReplay>
+__device__ __forceinline__ int step_typed(const LdsWorld& w, Ship& s, int type, int a, int b,
+                                          const Draws<kReplay>& dr, double& reward, int& done) {
+    reward = 0.0;
+    done = 0;
+    if (w.P == 0) return SE_ERR_NO_PORTS;  // :360
+    switch (type) {
+    case 2:  // SELECT_PORT, _select_port :265-271
+        if (a < 0 || a >= w.P) return SE_ERR_PORT_RANGE;
+        if (s.origin == a) return SE_ERR_SAME_PORT;
+        s.dest = a;
+        return SE_ERR_OK;
+    case 4:    // TAKE_CARGO, _take_cargo :341-348
+    case 3: {  // TAKE_FUEL, _take_fuel :350-357
+        const int idx = w.port_at(s.x, s.y);
+        if (idx < 0) return SE_ERR_NOT_AT_PORT;
+        const int stock = type == 4 ? w.pcargo[idx] : w.pfuel[idx];
+        if (a <= 0 || a > stock) return SE_ERR_AMOUNT;
+        if (type == 4) s.cargo += a;
+        else s.fuel += (double)a;
+        reward = 0.05;
+        return SE_ERR_OK;
+    }
+    case 1: {  // MOVE_SHIP
+        Ship t = s;
+        const int e = move_ship<kReplay>(w, t, a, b, dr, reward, done);
+        if (e == SE_ERR_OK) s = t;
+        return e;
+    }
+    default:
+        return SE_ERR_BAD_CATEGORY;  // :373-374
+    }
+}
+
+// utils/preprocessing.py:111-137 (moves N, E, S, W; Python wraps -4..-1)
+__device__ __forceinline__ int decode_agent(int P, int act, int& type, int& a, int& b) {
+    if (act < 4) {
+        if (act < -4) return SE_ERR_BAD_INDEX;
+        const int k = act & 3;  // -4..-1 -> 0..3
+        type = 1;
+        a = k == 1 ? -1 : (k == 3 ? 1 : 0);  // EAST = (-1, 0), WEST = (1, 0)
+        b = k == 0 ? -1 : (k == 2 ? 1 : 0);  // NORTH = (0, -1), SOUTH = (0, 1)
+        return SE_ERR_OK;
+    }
+    if (act < 4 + P) {
+        type = 2;
+        a = act - 4;
+    } else if (act < 4 + P + 50) {
+        type = 4;
+        a = act - (4 + P);
+    } else {
+        type = 3;
+        a = act - (4 + P + 50);
+    }
+    b = 0;
+    return SE_ERR_OK;
+}
+
+// reset (:227-243) from two Philox words
+__device__ __forceinline__ void reset_ship(const LdsWorld& w, Ship& s, uint32_t r0, uint32_t r1) {
+    s.origin = uniform_int(r0, (uint32_t)w.P);
+    s.dest = pick_other(r1, w.P, s.origin);
+    s.cargo = 0;
+    s.fuel = kFuelInit;
+    s.x = w.px(s.origin);
+    s.y = w.py(s.origin);
+}
+
+__device__ __forceinline__ Key env_key(uint64_t seed, int64_t env) {
+    Key k;
+    k.k0 = (uint32_t)seed;
+    k.k1 = (uint32_t)(seed >> 32);
+    k.e0 = (uint32_t)(uint64_t)env;
+    k.e1 = (uint32_t)((uint64_t)env >> 32);
+    return k;
+}
+
+__device__ __forceinline__ uint32_t lane_id() {
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+// number of set bits of `mask` below this lane
+__device__ __forceinline__ uint32_t count_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// ------------------------------------------------------------------ step kernel
+struct StepArgs {
+    const uint32_t* world;
+    WorldDims dims;
+    int64_t n;
+    int64_t env_base;
+    uint64_t seed;
+    uint32_t t;
+    se_state st;
+    const int32_t* act;   // agent index (kTyped = false) or type (kTyped = true)
+    const int32_t* act_a;
+    const int32_t* act_b;
+    const se_tape* tape;
+    se_done_rec* done_recs;  // this step's done list
+    int32_t* done_count;     // this step's counter
+    int32_t* next_count;     // zeroed for the next step
+    double* slab;            // per-block {sum_ret, n_eps, sum_len, pad}
+};
+
+template <typename T>
+__device__ __forceinline__ void ld4(const T* __restrict__ p, int64_t base, bool full, int64_t n,
+                                    T (&v)[4]) {
+    if (full) {
+        if constexpr (sizeof(T) == 1) {
+            const uint32_t w = *reinterpret_cast<const uint32_t*>(p + base);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (T)((w >> (8 * j)) & 0xffu);
+        } else if constexpr (sizeof(T) == 4) {
+            const uint4 w = *reinterpret_cast<const uint4*>(p + base);
+            v[0] = __builtin_bit_cast(T, w.x);
+            v[1] = __builtin_bit_cast(T, w.y);
+            v[2] = __builtin_bit_cast(T, w.z);
+            v[3] = __builtin_bit_cast(T, w.w);
+        } else {
+            const double2 a = *reinterpret_cast<const double2*>(p + base);
+            const double2 b = *reinterpret_cast<const double2*>(p + base + 2);
+            v[0] = a.x;
+            v[1] = a.y;
+            v[2] = b.x;
+            v[3] = b.y;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = base + j < n ? p[base + j] : T(0);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void st4(T* __restrict__ p, int64_t base, bool full, int64_t n,
+                                    const T (&v)[4]) {
+    if (full) {
+        if constexpr (sizeof(T) == 1) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w |= (uint32_t)(uint8_t)v[j] << (8 * j);
+            *reinterpret_cast<uint32_t*>(p + base) = w;
+        } else if constexpr (sizeof(T) == 4) {
+            uint4 w;
+            w.x = __builtin_bit_cast(uint32_t, v[0]);
+            w.y = __builtin_bit_cast(uint32_t, v[1]);
+            w.z = __builtin_bit_cast(uint32_t, v[2]);
+            w.w = __builtin_bit_cast(uint32_t, v[3]);
+            *reinterpret_cast<uint4*>(p + base) = w;
+        } else {
+            *reinterpret_cast<double2*>(p + base) = make_double2(v[0], v[1]);
+            *reinterpret_cast<double2*>(p + base + 2) = make_double2(v[2], v[3]);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (base + j < n) p[base + j] = v[j];
+    }
+}
+
+template <bool kTyped, bool kReplay, bool kAuto>
+__global__ __launch_bounds__(kBlock) void step_kernel(StepArgs A) {
+    extern __shared__ uint32_t lds[];
+    __shared__ double red[kBlock / 64][3];
+    const LdsWorld w = stage_world(A.world, A.dims, lds);
+    const se_state& S = A.st;
+    const int64_t groups = (A.n + kEnvsPerThread - 1) / kEnvsPerThread;
+
+    double blk_ret = 0.0, blk_eps = 0.0, blk_len = 0.0;
+    if (kAuto && blockIdx.x == 0 && threadIdx.x == 0) *A.next_count = 0;
+
+    for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < groups;
+         g += (int64_t)gridDim.x * kBlock) {
+        const int64_t base = g * kEnvsPerThread;
+        const bool full = base + kEnvsPerThread <= A.n;
+
+        uint8_t x[4], y[4], org[4], dst[4];
+        double fuel[4];
+        int32_t cargo[4], act[4], aa[4], ab[4];
+        ld4(S.x, base, full, A.n, x);
+        ld4(S.y, base, full, A.n, y);
+        ld4(S.origin, base, full, A.n, org);
+        ld4(S.dest, base, full, A.n, dst);
+        ld4(S.fuel, base, full, A.n, fuel);
+        ld4(S.cargo, base, full, A.n, cargo);
+        ld4(A.act, base, full, A.n, act);
+        if (kTyped) {
+            ld4(A.act_a, base, full, A.n, aa);
+            ld4(A.act_b, base, full, A.n, ab);
+        }
+        float ep_ret[4];
+        int32_t ep_len[4];
+        if (kAuto) {
+            ld4(S.ep_return, base, full, A.n, ep_ret);
+            ld4(S.ep_len, base, full, A.n, ep_len);
+        }
+
+        float rew[4];
+        uint8_t dn[4];
+        int8_t er[4];
+        int ndone = 0;
+        bool fin[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t i = base + j;
+            Ship s{x[j], y[j], fuel[j], cargo[j], org[j], dst[j]};
+            double r = 0.0;
+            int d = 0, e;
+            int ty, a, b;
+            if (kTyped) {
+                ty = act[j];
+                a = aa[j];
+                b = ab[j];
+                e = SE_ERR_OK;
+            } else {
+                e = decode_agent(w.P, act[j], ty, a, b);
+            }
+            const Key key = env_key(A.seed, A.env_base + i);
+            if (e == SE_ERR_OK && i < A.n) {
+                if constexpr (kReplay) {
+                    Draws<true> dr{A.tape + i};
+                    e = step_typed<true>(w, s, ty, a, b, dr, r, d);
+                } else {
+                    Draws<false> dr{key, A.t};
+                    e = step_typed<false>(w, s, ty, a, b, dr, r, d);
+                }
+            }
+            if (e != SE_ERR_OK) {
+                r = 0.0;
+                d = 0;
+            }
+            rew[j] = (float)r;  // one rounding of the reference's f64 reward
+            dn[j] = (uint8_t)d;
+            er[j] = (int8_t)e;
+            fin[j] = false;
+            if (kAuto && i < A.n) {
+                ep_ret[j] += rew[j];
+                ep_len[j] += 1;
+                if (d) {
+                    fin[j] = true;
+                    ++ndone;
+                    blk_ret += (double)ep_ret[j];
+                    blk_eps += 1.0;
+                    blk_len += (double)ep_len[j];
+                }
+            }
+            if (kAuto && fin[j]) {
+                const U4 o = draw(key, A.t, kSlotReset);
+                reset_ship(w, s, o.v[0], o.v[1]);
+            }
+            x[j] = (uint8_t)s.x;
+            y[j] = (uint8_t)s.y;
+            fuel[j] = s.fuel;
+            cargo[j] = s.cargo;
+            org[j] = (uint8_t)s.origin;
+            dst[j] = (uint8_t)s.dest;
+        }
+
+        if (kAuto) {
+            // done-list compaction: wave-exclusive prefix of per-lane counts (0..4)
+            // from three ballots, one atomic per wave.
+            const uint64_t b0 = __ballot(ndone & 1), b1 = __ballot(ndone & 2), b2 = __ballot(ndone & 4);
+            const uint32_t total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+            if (total) {
+                const uint32_t below = count_below(b0) + 2 * count_below(b1) + 4 * count_below(b2);
+                const uint64_t active = __ballot(1);
+                const uint32_t leader = (uint32_t)__ffsll((long long)active) - 1;
+                int32_t slot = 0;
+                if (lane_id() == leader) slot = atomicAdd(A.done_count, (int32_t)total);
+                slot = __shfl(slot, (int)leader) + (int32_t)below;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (fin[j]) {
+                        se_done_rec rec;
+                        rec.env = (int32_t)(base + j);
+                        rec.ep_return = ep_ret[j];
+                        rec.ep_len = ep_len[j];
+                        rec.step = (int32_t)A.t;
+                        A.done_recs[slot++] = rec;
+                        ep_ret[j] = 0.0f;
+                        ep_len[j] = 0;
+                    }
+                }
+            }
+            st4(S.ep_return, base, full, A.n, ep_ret);
+            st4(S.ep_len, base, full, A.n, ep_len);
+        }
+        st4(S.x, base, full, A.n, x);
+        st4(S.y, base, full, A.n, y);
+        st4(S.origin, base, full, A.n, org);
+        st4(S.dest, base, full, A.n, dst);
+        st4(S.fuel, base, full, A.n, fuel);
+        st4(S.cargo, base, full, A.n, cargo);
+        st4(S.reward, base, full, A.n, rew);
+        st4(S.done, base, full, A.n, dn);
+        st4(S.err, base, full, A.n, er);
+    }
+
+    if (kAuto) {
+        // per-block statistics: fixed-order wave butterfly, then waves in order
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            blk_ret += __shfl_xor(blk_ret, off);
+            blk_eps += __shfl_xor(blk_eps, off);
+            blk_len += __shfl_xor(blk_len, off);
+        }
+        const int wave = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0) {
+            red[wave][0] = blk_ret;
+            red[wave][1] = blk_eps;
+            red[wave][2] = blk_len;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double a = 0.0, b = 0.0, c = 0.0;
+            for (int k = 0; k < kBlock / 64; ++k) {
+                a += red[k][0];
+                b += red[k][1];
+                c += red[k][2];
+            }
+            if (b != 0.0) {
+                double* s = A.slab + 4 * blockIdx.x;
+                s[0] += a;
+                s[1] += b;
+                s[2] += c;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ reset kernel
+struct ResetArgs {
+    const uint32_t* world;
+    WorldDims dims;
+    int64_t n, env_base;
+    uint64_t seed;
+    uint32_t epoch;
+    se_state st;
+    const uint8_t* mask;
+    const int32_t* origin_in;  // explicit values (se_reset_to) or NULL
+    const int32_t* dest_in;
+};
+
+__global__ __launch_bounds__(kBlock) void reset_kernel(ResetArgs A) {
+    extern __shared__ uint32_t lds[];
+    const LdsWorld w = stage_world(A.world, A.dims, lds);
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < A.n;
+         i += (int64_t)gridDim.x * kBlock) {
+        if (A.mask && !A.mask[i]) continue;
+        Ship s;
+        if (A.origin_in) {
+            s.origin = A.origin_in[i];
+            s.dest = A.dest_in[i];
+            s.cargo = 0;
+            s.fuel = kFuelInit;
+            s.x = w.px(s.origin);
+            s.y = w.py(s.origin);
+        } else {
+            const U4 o = draw(env_key(A.seed, A.env_base + i), A.epoch, kSlotExplicitReset);
+            reset_ship(w, s, o.v[0], o.v[1]);
+        }
+        A.st.x[i] = (uint8_t)s.x;
+        A.st.y[i] = (uint8_t)s.y;
+        A.st.fuel[i] = s.fuel;
+        A.st.cargo[i] = s.cargo;
+        A.st.origin[i] = (uint8_t)s.origin;
+        A.st.dest[i] = (uint8_t)s.dest;
+        if (A.st.ep_return) A.st.ep_return[i] = 0.0f;
+        if (A.st.ep_len) A.st.ep_len[i] = 0;
+        A.st.done[i] = 0;
+        A.st.err[i] = 0;
+        A.st.reward[i] = 0.0f;
+    }
+}
+
+// ------------------------------------------------------------------ observation
+// preprocess_state rows (utils/preprocessing.py:25-62): one thread per output
+// element so the f32 row writes are coalesced; the port block comes from LDS.
+struct ObsArgs {
+    const uint32_t* world;
+    WorldDims dims;
+    int64_t n, ld;
+    se_state st;
+    float* obs;
+};
+
+__global__ __launch_bounds__(kBlock) void observe_kernel(ObsArgs A) {
+    extern __shared__ uint32_t lds[];
+    const LdsWorld w = stage_world(A.world, A.dims, lds);
+    const int64_t width = 6 + 4 * (int64_t)w.P;
+    const int64_t total = A.n * width;
+    for (int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x; k < total;
+         k += (int64_t)gridDim.x * kBlock) {
+        const int64_t i = k / width;
+        const int c = (int)(k - i * width);
+        float v;
+        if (c < 6) {
+            switch (c) {
+            case 0: v = (float)A.st.x[i]; break;
+            case 1: v = (float)A.st.y[i]; break;
+            case 2:
+            case 3: v = (float)A.st.fuel[i]; break;  // "cargo" is self.fuel (environment.py:206)
+            case 4: v = A.st.origin[i] == SE_NONE ? -1.0f : (float)A.st.origin[i]; break;
+            default: v = A.st.dest[i] == SE_NONE ? -1.0f : (float)A.st.dest[i]; break;
+            }
+        } else {
+            const int p = (c - 6) >> 2, f = (c - 6) & 3;
+            v = f == 0 ? (float)w.px(p) : f == 1 ? (float)w.py(p) : f == 2 ? (float)w.pfuel[p] : (float)w.pcargo[p];
+        }
+        A.obs[i * A.ld + c] = v;
+    }
+}
+
+// ------------------------------------------------------------------ DQN validity mask
+// agents/dqn.py:125-175, one thread per output byte (8 agent indices).
+struct MaskArgs {
+    const uint32_t* world;
+    WorldDims dims;
+    int64_t n;
+    int32_t stride;
+    se_state st;
+    uint8_t* bits;
+};
+
+__global__ __launch_bounds__(kBlock) void valid_mask_kernel(MaskArgs A) {
+    extern __shared__ uint32_t lds[];
+    const LdsWorld w = stage_world(A.world, A.dims, lds);
+    const int P = w.P, nact = 4 + P + 250;
+    const int64_t total = A.n * A.stride;
+    for (int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x; k < total;
+         k += (int64_t)gridDim.x * kBlock) {
+        const int64_t i = k / A.stride;
+        const int byte = (int)(k - i * A.stride);
+        const int x = A.st.x[i], y = A.st.y[i];
+        const int origin = A.st.origin[i] == SE_NONE ? -1 : A.st.origin[i];
+        const int cur = w.port_at(x, y);
+        uint32_t out = 0;
+        for (int bit = 0; bit < 8; ++bit) {
+            const int a = byte * 8 + bit;
+            bool v;
+            if (a >= nact) v = false;
+            else if (a < 4) v = true;
+            else if (a < 4 + P) {
+                const int p = a - 4;
+                v = p != origin && w.px(p) == x && w.py(p) == y;
+            } else if (a < 4 + P + 50) {
+                const int amt = a - (4 + P);
+                v = cur >= 0 && amt > 0 && amt <= w.pcargo[cur];
+            } else {
+                const int amt = a - (4 + P + 50);
+                v = cur >= 0 && amt > 0 && amt <= w.pfuel[cur];
+            }
+            out |= (uint32_t)v << (7 - bit);
+        }
+        A.bits[k] = (uint8_t)out;
+    }
+}
+
+// ------------------------------------------------------------------ synthetic agent
+__global__ __launch_bounds__(kBlock) void gen_actions_kernel(int64_t n, int64_t env_base,
+                                                             uint64_t seed, uint32_t t, int32_t P,
+                                                             int32_t* __restrict__ out) {
+    const int64_t groups = (n + 3) / 4;
+    for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < groups;
+         g += (int64_t)gridDim.x * kBlock) {
+        const int64_t base = g * 4;
+        int32_t v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const U4 o = draw(env_key(seed, env_base + base + j), t, kSlotAction);
+            const int32_t c = uniform_int(o.v[0], 100);
+            int32_t a;
+            if (c < 90) a = (int32_t)(o.v[1] & 3u);
+            else if (c < 95) a = 4 + P + 1 + uniform_int(o.v[1], 20);
+            else if (c < 98) a = 4 + P + 50 + 1 + uniform_int(o.v[1], 20);
+            else a = 4 + uniform_int(o.v[2], (uint32_t)P);
+            v[j] = a;
+        }
+        st4(out, base, base + 4 <= n, n, v);
+    }
+}
+
+// ------------------------------------------------------------------ stats reduce
+__global__ __launch_bounds__(64) void stats_kernel(const double* __restrict__ slab, int blocks,
+                                                   double* __restrict__ out) {
+    double a = 0.0, b = 0.0, c = 0.0;
+    for (int i = threadIdx.x; i < blocks; i += 64) {
+        a += slab[4 * i];
+        b += slab[4 * i + 1];
+        c += slab[4 * i + 2];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off);
+        b += __shfl_xor(b, off);
+        c += __shfl_xor(c, off);
+    }
+    if (threadIdx.x == 0) {
+        out[0] = a;
+        out[1] = b;
+        out[2] = c;
+    }
+}
+
+}  // namespace
+
+// ====================================================================== host side
+struct se_env {
+    int device = 0;
+    int64_t n = 0, env_base = 0;
+    WorldDims dims{};
+    uint64_t seed = 0;
+    uint32_t flags = 0;
+    uint64_t step_t = 0, epoch = 0;
+    std::vector<uint8_t> water;  // H*W, 0 = ground
+    uint32_t* d_world = nullptr;
+    int world_cap = 0;  // words allocated
+    se_state st{};
+    bool bound = false;
+    double* d_slab = nullptr;       // [grid][4]
+    int grid = 0;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return fail(SE_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));        \
+    } while (0)
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+int grid_for(int64_t items) {
+    int64_t b = (items + kBlock - 1) / kBlock;
+    if (b < 1) b = 1;
+    if (b > kMaxBlocks) b = kMaxBlocks;
+    return (int)b;
+}
+
+size_t lds_bytes(const se_env* env) { return (size_t)env->dims.total() * 4; }
+
+int upload_world(se_env* env, int32_t P, const int32_t* px, const int32_t* py, const int32_t* pf,
+                 const int32_t* pc) {
+    if (P < 0 || P > SE_MAX_PORTS) return fail(SE_EINVAL, "P must be in [0, 254]");
+    const int H = env->dims.H, W = env->dims.W;
+    for (int i = 0; i < P; ++i) {
+        if (px[i] < 0 || px[i] >= H || py[i] < 0 || py[i] >= W)
+            return fail(SE_EINVAL, "Coordinates not within map");  // add_port, environment.py:59-60
+        if (pf[i] < 0 || pc[i] < 0) return fail(SE_EINVAL, "port stocks must be >= 0");
+    }
+    const int words = (H * W + 31) / 32;
+    WorldDims d{H, W, P, words};
+    std::vector<uint32_t> img((size_t)d.total(), 0u);
+    std::vector<uint8_t> nonground(env->water);
+    for (int i = 0; i < P; ++i) nonground[(size_t)px[i] * W + py[i]] = 1;  // Entity.PORT (:65)
+    for (int c = 0; c < H * W; ++c)
+        if (!nonground[c]) img[c >> 5] |= 1u << (c & 31);
+    for (int i = 0; i < P; ++i) {
+        const int c = px[i] * W + py[i];
+        img[words + (c >> 5)] |= 1u << (c & 31);
+        img[2 * words + i] = (uint32_t)px[i] | ((uint32_t)py[i] << 8);
+        img[2 * words + P + i] = (uint32_t)pf[i];
+        img[2 * words + 2 * P + i] = (uint32_t)pc[i];
+    }
+    if (d.total() > env->world_cap) {
+        if (env->d_world) HIP_TRY(hipFree(env->d_world));
+        env->d_world = nullptr;
+        HIP_TRY(hipMalloc(&env->d_world, (size_t)d.total() * 4));
+        env->world_cap = d.total();
+    }
+    HIP_TRY(hipMemcpy(env->d_world, img.data(), (size_t)d.total() * 4, hipMemcpyHostToDevice));
+    env->dims = d;
+    return SE_OK;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+int check_ready(se_env* env) {
+    if (!env) return fail(SE_EINVAL, "null env");
+    if (!env->bound) return fail(SE_ESTATE, "se_bind has not been called");
+    return SE_OK;
+}
+
+int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const int32_t* a,
+                const int32_t* b, const se_tape* tape, void* stream) {
+    int rc = check_ready(env);
+    if (rc) return rc;
+    if (!act || (typed && (!a || !b)) || (replay && !tape))
+        return fail(SE_EINVAL, "null action/tape pointer");
+    if (!aligned16(act) || (typed && (!aligned16(a) || !aligned16(b))))
+        return fail(SE_EINVAL, "action buffers must be 16-byte aligned");
+    const bool autoreset = (env->flags & SE_FLAG_AUTO_RESET) && !replay;
+    if (autoreset && env->dims.P < 2) return fail(SE_EINVAL, "auto-reset needs at least two ports");
+    DeviceGuard g(env->device);
+    StepArgs A{};
+    A.world = env->d_world;
+    A.dims = env->dims;
+    A.n = env->n;
+    A.env_base = env->env_base;
+    A.seed = env->seed;
+    A.t = (uint32_t)env->step_t;
+    A.st = env->st;
+    A.act = act;
+    A.act_a = a;
+    A.act_b = b;
+    A.tape = tape;
+    // records double-buffered, counters over three slots: the list of step t-1
+    // stays readable while step t runs (step t zeroes the counter of step t+1).
+    if (autoreset) {
+        A.done_recs = env->st.done_recs + (size_t)(env->step_t & 1u) * (size_t)env->n;
+        A.done_count = env->st.done_count + (int)(env->step_t % 3u);
+        A.next_count = env->st.done_count + (int)((env->step_t + 1u) % 3u);
+    }
+    A.slab = env->d_slab;
+    const hipStream_t s = (hipStream_t)stream;
+    const size_t lds = lds_bytes(env);
+    const int grid = env->grid;
+    if (env->n > 0) {
+        if (!typed && !autoreset) step_kernel<false, false, false><<<grid, kBlock, lds, s>>>(A);
+        else if (!typed && autoreset) step_kernel<false, false, true><<<grid, kBlock, lds, s>>>(A);
+        else if (typed && replay) step_kernel<true, true, false><<<grid, kBlock, lds, s>>>(A);
+        else if (typed && !autoreset) step_kernel<true, false, false><<<grid, kBlock, lds, s>>>(A);
+        else step_kernel<true, false, true><<<grid, kBlock, lds, s>>>(A);
+        HIP_TRY(hipGetLastError());
+    }
+    if (!replay) env->step_t += 1;
+    return SE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int se_abi_version(void) { return SHIPENV_ABI_VERSION; }
+
+const char* se_last_error(void) { return g_err.c_str(); }
+
+int se_create(se_env** out, int device, int64_t n, int64_t env_id_base, int32_t H, int32_t W,
+              const uint8_t* water, int32_t P, const int32_t* port_x, const int32_t* port_y,
+              const int32_t* port_fuel, const int32_t* port_cargo, uint64_t seed, uint32_t flags) {
+    if (!out) return fail(SE_EINVAL, "null out");
+    *out = nullptr;
+    if (n < 0) return fail(SE_EINVAL, "n must be >= 0");
+    if (H < 1 || W < 1 || H > SE_MAX_SIDE || W > SE_MAX_SIDE)
+        return fail(SE_EINVAL, "map sides must be in [1, 256]");
+    if (!water) return fail(SE_EINVAL, "null water map");
+    if (P > 0 && (!port_x || !port_y || !port_fuel || !port_cargo))
+        return fail(SE_EINVAL, "null port arrays");
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(SE_EINVAL, "bad device ordinal");
+    DeviceGuard g(device);
+    se_env* env = new se_env();
+    env->device = device;
+    env->n = n;
+    env->env_base = env_id_base;
+    env->seed = seed;
+    env->flags = flags;
+    env->dims.H = H;
+    env->dims.W = W;
+    env->water.assign(water, water + (size_t)H * W);
+    for (auto& v : env->water) v = v ? 1 : 0;
+    int rc = upload_world(env, P, port_x, port_y, port_fuel, port_cargo);
+    if (rc) {
+        se_destroy(env);
+        return rc;
+    }
+    env->grid = grid_for((n + kEnvsPerThread - 1) / kEnvsPerThread);
+    hipError_t e = hipMalloc(&env->d_slab, (size_t)env->grid * 4 * sizeof(double));
+    if (e == hipSuccess) e = hipMemset(env->d_slab, 0, (size_t)env->grid * 4 * sizeof(double));
+    if (e != hipSuccess) {
+        se_destroy(env);
+        return fail(SE_EHIP, std::string("se_create allocation: ") + hipGetErrorString(e));
+    }
+    *out = env;
+    return SE_OK;
+}
+
+int se_set_ports(se_env* env, int32_t P, const int32_t* port_x, const int32_t* port_y,
+                 const int32_t* port_fuel, const int32_t* port_cargo) {
+    if (!env) return fail(SE_EINVAL, "null env");
+    if (P > 0 && (!port_x || !port_y || !port_fuel || !port_cargo))
+        return fail(SE_EINVAL, "null port arrays");
+    DeviceGuard g(env->device);
+    HIP_TRY(hipDeviceSynchronize());  // the old image may still be read by queued work
+    return upload_world(env, P, port_x, port_y, port_fuel, port_cargo);
+}
+
+int se_bind(se_env* env, const se_state* st) {
+    if (!env || !st) return fail(SE_EINVAL, "null argument");
+    const void* req[] = {st->x, st->y, st->fuel, st->cargo, st->origin, st->dest,
+                         st->reward, st->done, st->err};
+    for (const void* p : req) {
+        if (!p && env->n > 0) return fail(SE_EINVAL, "null state buffer");
+        if (!aligned16(p)) return fail(SE_EINVAL, "state buffers must be 16-byte aligned");
+    }
+    if (env->flags & SE_FLAG_AUTO_RESET) {
+        if (!st->ep_return || !st->ep_len || !st->done_recs || !st->done_count)
+            return fail(SE_EINVAL, "auto-reset needs ep_return, ep_len, done_recs and done_count");
+        if (!aligned16(st->ep_return) || !aligned16(st->ep_len) || !aligned16(st->done_recs))
+            return fail(SE_EINVAL, "state buffers must be 16-byte aligned");
+        DeviceGuard g(env->device);
+        HIP_TRY(hipMemset(st->done_count, 0, 3 * sizeof(int32_t)));
+    }
+    env->st = *st;
+    env->bound = true;
+    return SE_OK;
+}
+
+int se_reset(se_env* env, const uint8_t* mask, void* stream) {
+    int rc = check_ready(env);
+    if (rc) return rc;
+    if (env->dims.P < 2) return fail(SE_EINVAL, "reset needs at least two ports");
+    DeviceGuard g(env->device);
+    ResetArgs A{env->d_world, env->dims, env->n, env->env_base, env->seed,
+                (uint32_t)env->epoch, env->st, mask, nullptr, nullptr};
+    if (env->n > 0) {
+        reset_kernel<<<grid_for(env->n), kBlock, lds_bytes(env), (hipStream_t)stream>>>(A);
+        HIP_TRY(hipGetLastError());
+    }
+    env->epoch += 1;
+    return SE_OK;
+}
+
+int se_reset_to(se_env* env, const uint8_t* mask, const int32_t* origin, const int32_t* dest,
+                void* stream) {
+    int rc = check_ready(env);
+    if (rc) return rc;
+    if (!origin || !dest) return fail(SE_EINVAL, "null origin/dest");
+    DeviceGuard g(env->device);
+    ResetArgs A{env->d_world, env->dims, env->n, env->env_base, env->seed,
+                (uint32_t)env->epoch, env->st, mask, origin, dest};
+    if (env->n > 0) {
+        reset_kernel<<<grid_for(env->n), kBlock, lds_bytes(env), (hipStream_t)stream>>>(A);
+        HIP_TRY(hipGetLastError());
+    }
+    return SE_OK;
+}
+
+int se_step(se_env* env, const int32_t* actions, void* stream) {
+    return launch_step(env, false, false, actions, nullptr, nullptr, nullptr, stream);
+}
+
+int se_step_typed(se_env* env, const int32_t* type, const int32_t* a, const int32_t* b,
+                  void* stream) {
+    return launch_step(env, true, false, type, a, b, nullptr, stream);
+}
+
+int se_step_replay(se_env* env, const int32_t* type, const int32_t* a, const int32_t* b,
+                   const se_tape* tape, void* stream) {
+    return launch_step(env, true, true, type, a, b, tape, stream);
+}
+
+int se_observe(se_env* env, float* obs, int64_t ld, void* stream) {
+    int rc = check_ready(env);
+    if (rc) return rc;
+    if (!obs || ld < 6 + 4 * (int64_t)env->dims.P) return fail(SE_EINVAL, "bad obs buffer / ld");
+    DeviceGuard g(env->device);
+    ObsArgs A{env->d_world, env->dims, env->n, ld, env->st, obs};
+    const int64_t total = env->n * (6 + 4 * (int64_t)env->dims.P);
+    if (total > 0) {
+        observe_kernel<<<grid_for(total), kBlock, lds_bytes(env), (hipStream_t)stream>>>(A);
+        HIP_TRY(hipGetLastError());
+    }
+    return SE_OK;
+}
+
+int se_valid_mask(se_env* env, uint8_t* bits, void* stream) {
+    int rc = check_ready(env);
+    if (rc) return rc;
+    if (!bits) return fail(SE_EINVAL, "null bits");
+    DeviceGuard g(env->device);
+    const int32_t stride = (4 + env->dims.P + 250 + 7) / 8;
+    MaskArgs A{env->d_world, env->dims, env->n, stride, env->st, bits};
+    const int64_t total = env->n * stride;
+    if (total > 0) {
+        valid_mask_kernel<<<grid_for(total), kBlock, lds_bytes(env), (hipStream_t)stream>>>(A);
+        HIP_TRY(hipGetLastError());
+    }
+    return SE_OK;
+}
+
+int se_gen_actions(se_env* env, int32_t* actions, uint32_t t, void* stream) {
+    if (!env || !actions) return fail(SE_EINVAL, "null argument");
+    if (!aligned16(actions)) return fail(SE_EINVAL, "actions must be 16-byte aligned");
+    if (env->dims.P < 1) return fail(SE_EINVAL, "the synthetic agent needs ports");
+    DeviceGuard g(env->device);
+    if (env->n > 0) {
+        gen_actions_kernel<<<grid_for((env->n + 3) / 4), kBlock, 0, (hipStream_t)stream>>>(
+            env->n, env->env_base, env->seed, t, env->dims.P, actions);
+        HIP_TRY(hipGetLastError());
+    }
+    return SE_OK;
+}
+
+int se_episode_stats(se_env* env, double* out, void* stream) {
+    if (!env || !out) return fail(SE_EINVAL, "null argument");
+    DeviceGuard g(env->device);
+    stats_kernel<<<1, 64, 0, (hipStream_t)stream>>>(env->d_slab, env->grid, out);
+    HIP_TRY(hipGetLastError());
+    return SE_OK;
+}
+
+int se_clear_stats(se_env* env, void* stream) {
+    if (!env) return fail(SE_EINVAL, "null env");
+    DeviceGuard g(env->device);
+    HIP_TRY(hipMemsetAsync(env->d_slab, 0, (size_t)env->grid * 4 * sizeof(double),
+                           (hipStream_t)stream));
+    return SE_OK;
+}
+
+int se_done_list(se_env* env, int64_t* rec_offset, int32_t* count_index) {
+    if (!env || !rec_offset || !count_index) return fail(SE_EINVAL, "null argument");
+    if (!(env->flags & SE_FLAG_AUTO_RESET)) return fail(SE_ESTATE, "no done list without auto-reset");
+    if (env->step_t == 0) return fail(SE_ESTATE, "no step has run");
+    const uint64_t t = env->step_t - 1;
+    *rec_offset = (int64_t)(t & 1u) * env->n;
+    *count_index = (int32_t)(t % 3u);
+    return SE_OK;
+}
+
+int se_get_counters(se_env* env, uint64_t* step, uint64_t* epoch) {
+    if (!env) return fail(SE_EINVAL, "null env");
+    if (step) *step = env->step_t;
+    if (epoch) *epoch = env->epoch;
+    return SE_OK;
+}
+
+int se_set_counters(se_env* env, uint64_t step, uint64_t epoch) {
+    if (!env) return fail(SE_EINVAL, "null env");
+    DeviceGuard g(env->device);
+    HIP_TRY(hipDeviceSynchronize());
+    if (env->bound && env->st.done_count) HIP_TRY(hipMemset(env->st.done_count, 0, 3 * sizeof(int32_t)));
+    env->step_t = step;
+    env->epoch = epoch;
+    return SE_OK;
+}
+
+int se_destroy(se_env* env) {
+    if (!env) return SE_OK;
+    DeviceGuard g(env->device);
+    if (env->d_world) (void)hipFree(env->d_world);
+    if (env->d_slab) (void)hipFree(env->d_slab);
+    delete env;
+    return SE_OK;
+}
+
+}  // extern "C"

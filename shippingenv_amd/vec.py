@@ -1,0 +1,243 @@
+"""VecEnv: N ShippingEnv environments stepped together on one MI355X.
+
+The batched form of shipping.Environment (shipping/environment.py:28-376).
+State lives in HBM as SoA torch tensors owned by this object and bound once
+to the native handle (include/shipenv.h, se_bind); every call launches on the
+current torch stream and returns without synchronising the host.
+
+Field widths (DESIGN.md "Data layout"): x, y, origin, dest u8 (origin/dest
+255 = None), fuel f64, cargo i32, reward f32, done u8, err i8.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import random as _random
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .maps import builtin_water
+
+DEFAULT_PORTS = [[41, 40], [60, 22], [78, 29], [49, 72], [62, 72]]  # utils/constants.py:57-63
+
+TAPE_DTYPE = np.dtype(
+    [("u_fuel", "<f8"), ("u_gate", "<f8"), ("u_type", "<f8"), ("beta", "<f8"),
+     ("arrive_dest", "<i4"), ("pad", "<i4")]
+)  # se_tape
+
+
+def draw_port_stocks(n_ports, seed):
+    """add_port's stocks (environment.py:63-64): randint(5, 20) for fuel, then cargo, per port."""
+    rng = _random.Random(seed)
+    fuel, cargo = [], []
+    for _ in range(n_ports):
+        fuel.append(rng.randint(5, 20))
+        cargo.append(rng.randint(5, 20))
+    return fuel, cargo
+
+
+def random_water_ports(water, n_ports, seed):
+    """n distinct water cells, seeded (config 4's 64 random ports)."""
+    rng = np.random.default_rng(seed)
+    cells = np.argwhere(np.asarray(water) != 0)
+    pick = rng.choice(len(cells), size=n_ports, replace=False)
+    return [[int(a), int(b)] for a, b in cells[np.sort(pick)]]
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _i32(a):
+    return np.ascontiguousarray(a, np.int32)
+
+
+class VecEnv:
+    def __init__(self, n, *, water=None, ports=None, port_fuel=None, port_cargo=None, seed=0,
+                 env_id_base=0, device=None, auto_reset=False, stock_seed=None):
+        if not torch.cuda.is_available():
+            raise N.NativeLibraryError("VecEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
+        lib = N.lib()
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None \
+            else torch.device(device)
+        self.n = int(n)
+        self.seed = int(seed)
+        self.env_id_base = int(env_id_base)
+        self.auto_reset = bool(auto_reset)
+        self.water = np.ascontiguousarray(builtin_water() if water is None else water, np.uint8)
+        self.H, self.W = self.water.shape
+        ports = DEFAULT_PORTS if ports is None else ports
+        if port_fuel is None or port_cargo is None:
+            f, c = draw_port_stocks(len(ports), self.seed if stock_seed is None else stock_seed)
+            port_fuel = f if port_fuel is None else port_fuel
+            port_cargo = c if port_cargo is None else port_cargo
+        self.port_x = _i32([p[0] for p in ports])
+        self.port_y = _i32([p[1] for p in ports])
+        self.port_fuel = _i32(port_fuel)
+        self.port_cargo = _i32(port_cargo)
+        self.P = len(self.port_x)
+
+        kw = dict(device=self.device)
+        n = self.n
+        self.x = torch.zeros(n, dtype=torch.uint8, **kw)
+        self.y = torch.zeros(n, dtype=torch.uint8, **kw)
+        self.fuel = torch.zeros(n, dtype=torch.float64, **kw)
+        self.cargo = torch.zeros(n, dtype=torch.int32, **kw)
+        self.origin = torch.full((n,), N.SE_NONE, dtype=torch.uint8, **kw)
+        self.dest = torch.full((n,), N.SE_NONE, dtype=torch.uint8, **kw)
+        self.reward = torch.zeros(n, dtype=torch.float32, **kw)
+        self.done = torch.zeros(n, dtype=torch.uint8, **kw)
+        self.err = torch.zeros(n, dtype=torch.int8, **kw)
+        self.ep_return = torch.zeros(n, dtype=torch.float32, **kw)
+        self.ep_len = torch.zeros(n, dtype=torch.int32, **kw)
+        # done list (auto-reset): 2n records {env, ep_return bits, ep_len, step} + 3 counters
+        nrec = 2 * n if self.auto_reset else 0
+        self.done_recs = torch.zeros((max(nrec, 1), 4), dtype=torch.int32, **kw)
+        self.done_count = torch.zeros(4, dtype=torch.int32, **kw)
+
+        self._h = C.c_void_p()
+        flags = N.SE_FLAG_AUTO_RESET if self.auto_reset else 0
+        with torch.cuda.device(self.device):
+            N.check(lib.se_create(C.byref(self._h), self.device.index, n, self.env_id_base,
+                                  self.H, self.W, self.water.ctypes.data_as(C.c_void_p), self.P,
+                                  self.port_x.ctypes.data_as(C.c_void_p),
+                                  self.port_y.ctypes.data_as(C.c_void_p),
+                                  self.port_fuel.ctypes.data_as(C.c_void_p),
+                                  self.port_cargo.ctypes.data_as(C.c_void_p), self.seed, flags))
+        self._state = N.SeState(*[t.data_ptr() for t in (
+            self.x, self.y, self.fuel, self.cargo, self.origin, self.dest, self.reward,
+            self.done, self.err, self.ep_return, self.ep_len, self.done_recs, self.done_count)])
+        N.check(lib.se_bind(self._h, C.byref(self._state)))
+        self._stats = torch.zeros(3, dtype=torch.float64, **kw)
+
+    # ------------------------------------------------------------------ helpers
+    @property
+    def action_space_size(self):
+        """utils/preprocessing.py:93-108: 4 moves + P ports + 50 cargo + 200 fuel amounts."""
+        return 4 + self.P + 50 + 200
+
+    @property
+    def obs_size(self):
+        return 6 + 4 * self.P
+
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _dev(self, t, dtype):
+        if not isinstance(t, torch.Tensor):
+            t = torch.as_tensor(np.asarray(t), device=self.device)
+        t = t.to(device=self.device, dtype=dtype)
+        if not t.is_contiguous() or t.data_ptr() % 16:
+            t = t.contiguous().clone()
+        if t.numel() != self.n:
+            raise ValueError(f"expected {self.n} entries, got {t.numel()}")
+        return t
+
+    # ------------------------------------------------------------------ API
+    def set_ports(self, ports, port_fuel, port_cargo):
+        self.port_x = _i32([p[0] for p in ports])
+        self.port_y = _i32([p[1] for p in ports])
+        self.port_fuel = _i32(port_fuel)
+        self.port_cargo = _i32(port_cargo)
+        self.P = len(self.port_x)
+        N.check(N.lib().se_set_ports(self._h, self.P, self.port_x.ctypes.data_as(C.c_void_p),
+                                     self.port_y.ctypes.data_as(C.c_void_p),
+                                     self.port_fuel.ctypes.data_as(C.c_void_p),
+                                     self.port_cargo.ctypes.data_as(C.c_void_p)))
+
+    def reset(self, mask=None):
+        """reset() (environment.py:227-243) of every env, or of those with mask != 0."""
+        m = None if mask is None else self._dev(mask, torch.uint8)
+        N.check(N.lib().se_reset(self._h, _ptr(m), self._stream()))
+        self._keep = m
+
+    def reset_to(self, origin, dest, mask=None):
+        o, d = self._dev(origin, torch.int32), self._dev(dest, torch.int32)
+        m = None if mask is None else self._dev(mask, torch.uint8)
+        N.check(N.lib().se_reset_to(self._h, _ptr(m), _ptr(o), _ptr(d), self._stream()))
+        self._keep = (o, d, m)
+
+    def step(self, actions):
+        """step() with int32 actions in the agent-index encoding; returns (reward, done, err)."""
+        a = self._dev(actions, torch.int32)
+        N.check(N.lib().se_step(self._h, _ptr(a), self._stream()))
+        self._keep = a
+        return self.reward, self.done, self.err
+
+    def step_typed(self, act_type, a, b):
+        t, aa, bb = (self._dev(v, torch.int32) for v in (act_type, a, b))
+        N.check(N.lib().se_step_typed(self._h, _ptr(t), _ptr(aa), _ptr(bb), self._stream()))
+        self._keep = (t, aa, bb)
+        return self.reward, self.done, self.err
+
+    def step_replay(self, act_type, a, b, tape):
+        """step() with recorded variates; tape: numpy structured array of TAPE_DTYPE (n,)."""
+        t, aa, bb = (self._dev(v, torch.int32) for v in (act_type, a, b))
+        tape = np.ascontiguousarray(tape, TAPE_DTYPE)
+        if len(tape) != self.n:
+            raise ValueError("tape length != n")
+        tp = torch.from_numpy(tape.view(np.uint8).reshape(-1).copy()).to(self.device)
+        N.check(N.lib().se_step_replay(self._h, _ptr(t), _ptr(aa), _ptr(bb), _ptr(tp),
+                                       self._stream()))
+        self._keep = (t, aa, bb, tp)
+        return self.reward, self.done, self.err
+
+    def observe(self, out=None):
+        """preprocess_state rows (utils/preprocessing.py:25-62) as f32 [n, 6+4P]."""
+        if out is None:
+            out = torch.empty((self.n, self.obs_size), dtype=torch.float32, device=self.device)
+        N.check(N.lib().se_observe(self._h, _ptr(out), out.stride(0), self._stream()))
+        return out
+
+    def valid_mask(self, out=None):
+        """DQN is_valid_action bits (agents/dqn.py:125-175), packed MSB-first per row."""
+        stride = (self.action_space_size + 7) // 8
+        if out is None:
+            out = torch.empty((self.n, stride), dtype=torch.uint8, device=self.device)
+        N.check(N.lib().se_valid_mask(self._h, _ptr(out), self._stream()))
+        return out
+
+    def gen_actions(self, t, out=None):
+        """The bench's synthetic agent (config 3/4 action mix) for step index t."""
+        if out is None:
+            out = torch.empty(self.n, dtype=torch.int32, device=self.device)
+        N.check(N.lib().se_gen_actions(self._h, _ptr(out), int(t) & 0xFFFFFFFF, self._stream()))
+        return out
+
+    def episode_stats(self):
+        """Device f64[3] {sum of returns, episodes, sum of lengths} since the last clear."""
+        N.check(N.lib().se_episode_stats(self._h, _ptr(self._stats), self._stream()))
+        return self._stats
+
+    def clear_stats(self):
+        N.check(N.lib().se_clear_stats(self._h, self._stream()))
+
+    def done_list(self):
+        """Episodes finished by the last step (auto-reset): (env, ep_return, ep_len, step)."""
+        off, idx = C.c_int64(), C.c_int32()
+        N.check(N.lib().se_done_list(self._h, C.byref(off), C.byref(idx)))
+        k = int(self.done_count[idx.value].item())
+        raw = self.done_recs[off.value: off.value + k].clone()
+        return raw[:, 0], raw[:, 1].view(torch.float32), raw[:, 2], raw[:, 3]
+
+    @property
+    def counters(self):
+        s, e = C.c_uint64(), C.c_uint64()
+        N.check(N.lib().se_get_counters(self._h, C.byref(s), C.byref(e)))
+        return s.value, e.value
+
+    def set_counters(self, step, epoch):
+        N.check(N.lib().se_set_counters(self._h, int(step), int(epoch)))
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            torch.cuda.synchronize(self.device)
+            N.lib().se_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass

@@ -1,0 +1,334 @@
+"""Parity of the HIP path (through the C-ABI) with the reference and the oracle.
+
+* replay: every golden record (the reference's own steps, resets and errors)
+  through se_step_replay / se_reset_to -> bit-exact state, reward == f32(ref),
+  done, err;
+* Philox: the kernel and the oracle on the same seed and actions, bit-exact
+  (config 2 move-only, config 3 mix, config 4 auto-reset with 64 ports);
+* full size (N = 2^20): invariants plus a sampled exact check per env id.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden_files, load_golden
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("x", "y", "fuel", "cargo", "origin", "dest")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from shippingenv_amd import build
+
+    build.build(verbose=False)
+
+
+def VecEnv(*a, **k):
+    from shippingenv_amd.vec import VecEnv as V
+
+    return V(*a, **k)
+
+
+def set_state(env, z, sel, prefix="pre_"):
+    for f in FIELDS:
+        v = z[prefix + f][sel]
+        if f in ("origin", "dest"):
+            v = np.where(v < 0, 255, v)
+        t = getattr(env, f)
+        t.copy_(torch.from_numpy(np.ascontiguousarray(v).astype(t.cpu().numpy().dtype)))
+
+
+def get_state(env):
+    torch.cuda.synchronize()
+    out = {}
+    for f in FIELDS:
+        v = getattr(env, f).cpu().numpy()
+        if f in ("origin", "dest"):
+            v = np.where(v == 255, -1, v.astype(np.int32))
+        elif f != "fuel":
+            v = v.astype(np.int32)
+        out[f] = v
+    return out
+
+
+def assert_state(got, want, what):
+    for f in FIELDS:
+        if f == "fuel":
+            np.testing.assert_array_equal(got[f].view(np.int64), np.asarray(want[f]).view(np.int64),
+                                          err_msg=f"{what}: fuel bits")
+        else:
+            np.testing.assert_array_equal(got[f], want[f], err_msg=f"{what}: {f}")
+
+
+def tape_of(z, sel):
+    from shippingenv_amd.vec import TAPE_DTYPE
+
+    tape = np.zeros(len(sel), TAPE_DTYPE)
+    for f in ("u_fuel", "u_gate", "u_type", "beta", "arrive_dest"):
+        tape[f] = z[f][sel]
+    return tape
+
+
+def env_for(z, n, water, with_ports=True, **kw):
+    sl = slice(None) if with_ports else slice(0, 0)
+    ports = [[int(a), int(b)] for a, b in zip(z["port_x"][sl], z["port_y"][sl])]
+    return VecEnv(n, water=water, ports=ports, port_fuel=z["port_fuel"][sl],
+                  port_cargo=z["port_cargo"][sl], **kw)
+
+
+# ---------------------------------------------------------------- replay parity
+@pytest.mark.parametrize("path", golden_files(), ids=os.path.basename)
+def test_replay_matches_reference(path, water):
+    z = load_golden(path)
+    for kind, with_ports in ((0, True), (2, False)):
+        sel = np.nonzero(z["kind"] == kind)[0]
+        if not len(sel):
+            continue
+        env = env_for(z, len(sel), water, with_ports)
+        set_state(env, z, sel)
+        reward, done, err = env.step_replay(z["act_type"][sel], z["act_a"][sel], z["act_b"][sel],
+                                            tape_of(z, sel))
+        got = get_state(env)
+        want = {f: z["post_" + f][sel] for f in FIELDS}
+        assert_state(got, want, os.path.basename(path))
+        np.testing.assert_array_equal(reward.cpu().numpy(), z["reward"][sel].astype(np.float32))
+        np.testing.assert_array_equal(done.cpu().numpy().astype(np.int32), z["done"][sel])
+        np.testing.assert_array_equal(err.cpu().numpy().astype(np.int32), z["err"][sel])
+        # the north-star tolerance, stated: reward within 1e-6 (relative) of the f64 value
+        np.testing.assert_allclose(reward.cpu().numpy().astype(np.float64), z["reward"][sel],
+                                   rtol=1e-6, atol=1e-6)
+        env.close()
+
+
+@pytest.mark.parametrize("path", golden_files("tape"), ids=os.path.basename)
+def test_replay_resets_match_reference(path, water):
+    z = load_golden(path)
+    sel = np.nonzero(z["kind"] == 1)[0]
+    env = env_for(z, len(sel), water)
+    env.reset_to(z["reset_origin"][sel], z["reset_dest"][sel])
+    assert_state(get_state(env), {f: z["post_" + f][sel] for f in FIELDS}, "reset")
+    env.close()
+
+
+@pytest.mark.parametrize("path", golden_files("tape")[:3], ids=os.path.basename)
+def test_replay_episode_chain_n1(path, water):
+    """One env walks the whole recorded trajectory from its own outputs (N = 1:
+    the scalar tail path of the kernel)."""
+    z = load_golden(path)
+    env = env_for(z, 1, water)
+    tapes = tape_of(z, np.arange(len(z["kind"])))
+    for i in range(len(z["kind"])):
+        if z["kind"][i] == 1:
+            env.reset_to(z["reset_origin"][i:i + 1], z["reset_dest"][i:i + 1])
+        else:
+            r, d, e = env.step_replay(z["act_type"][i:i + 1], z["act_a"][i:i + 1],
+                                      z["act_b"][i:i + 1], tapes[i:i + 1])
+            assert int(e.item()) == z["err"][i] and int(d.item()) == z["done"][i], i
+            assert r.item() == np.float32(z["reward"][i]), i
+        if i % 97 == 0 or i == len(z["kind"]) - 1:
+            assert_state(get_state(env), {f: z["post_" + f][i:i + 1] for f in FIELDS}, f"rec {i}")
+    env.close()
+
+
+# ---------------------------------------------------------------- Philox parity vs oracle
+def _oracle_pair(O, env):
+    world = O.OracleWorld(env.water, env.port_x, env.port_y, env.port_fuel, env.port_cargo)
+    st = O.OracleState(env.n)
+    return world, st
+
+
+def _assert_vs_oracle(env, st, what):
+    got = get_state(env)
+    want = {f: getattr(st, f) for f in FIELDS}
+    assert_state(got, want, what)
+
+
+@pytest.mark.parametrize("n", [4096, 4099])
+def test_config2_move_only_vs_oracle(oracle_mod, n):
+    """Config 2: N=4096, move-only actions, 1000 steps, bit-exact x, y, fuel bits,
+    cargo, done (and reward == f32 of the oracle's f64) on every step."""
+    O = oracle_mod
+    seed = 1234
+    env = VecEnv(n, seed=seed)
+    world, st = _oracle_pair(O, env)
+    env.reset()
+    O.reset(world, st, seed=seed, epoch=0)
+    _assert_vs_oracle(env, st, "reset")
+    rng = np.random.default_rng(0)
+    for t in range(1000):
+        acts = rng.integers(0, 4, size=n).astype(np.int32)
+        r, d, e = env.step(acts)
+        O.step(world, st, actions=acts, seed=seed, t=t)
+        if t % 50 == 0 or t == 999:
+            _assert_vs_oracle(env, st, f"t={t}")
+        np.testing.assert_array_equal(r.cpu().numpy(), st.reward.astype(np.float32))
+        np.testing.assert_array_equal(d.cpu().numpy().astype(np.int32), st.done)
+        np.testing.assert_array_equal(e.cpu().numpy().astype(np.int32), st.err)
+    assert st.done.sum() > 0  # fuel ran out somewhere
+    env.close()
+
+
+def test_config3_full_mix_vs_oracle(oracle_mod):
+    O = oracle_mod
+    seed, n = 77, 8192
+    env = VecEnv(n, seed=seed)
+    world, st = _oracle_pair(O, env)
+    env.reset()
+    O.reset(world, st, seed=seed, epoch=0)
+    seen_err = set()
+    for t in range(400):
+        acts = env.gen_actions(t)
+        ref = O.gen_actions(n, env.P, seed, 0, t)
+        np.testing.assert_array_equal(acts.cpu().numpy(), ref)
+        r, d, e = env.step(acts)
+        O.step(world, st, actions=ref, seed=seed, t=t)
+        np.testing.assert_array_equal(r.cpu().numpy(), st.reward.astype(np.float32))
+        np.testing.assert_array_equal(e.cpu().numpy().astype(np.int32), st.err)
+        seen_err |= set(np.unique(st.err).tolist())
+        if t % 40 == 0:
+            _assert_vs_oracle(env, st, f"t={t}")
+    _assert_vs_oracle(env, st, "end")
+    assert {0, 2, 4, 5}.issubset(seen_err)
+    env.close()
+
+
+def test_config4_autoreset_64_ports_vs_oracle(oracle_mod, water):
+    from shippingenv_amd.vec import random_water_ports
+
+    O = oracle_mod
+    seed, n = 4242, 8192
+    ports = random_water_ports(water, 64, seed=3)
+    env = VecEnv(n, seed=seed, ports=ports, auto_reset=True)
+    world, st = _oracle_pair(O, env)
+    env.reset()
+    O.reset(world, st, seed=seed, epoch=0)
+    stats = np.zeros(3)
+    total_done = 0
+    for t in range(600):
+        acts = env.gen_actions(t)
+        ref = O.gen_actions(n, env.P, seed, 0, t)
+        env.step(acts)
+        O.step_autoreset(world, st, ref, seed=seed, t=t, stats=stats)
+        np.testing.assert_array_equal(env.reward.cpu().numpy(), st.reward.astype(np.float32))
+        np.testing.assert_array_equal(env.done.cpu().numpy().astype(np.int32), st.done)
+        ids, ret, length, step = env.done_list()
+        want = np.nonzero(st.done)[0]
+        order = np.argsort(ids.cpu().numpy())
+        np.testing.assert_array_equal(ids.cpu().numpy()[order], want)
+        assert (step.cpu().numpy() == t).all()
+        total_done += len(want)
+        if t % 60 == 0:
+            _assert_vs_oracle(env, st, f"t={t}")
+            np.testing.assert_array_equal(env.ep_return.cpu().numpy(), st.ep_return)
+            np.testing.assert_array_equal(env.ep_len.cpu().numpy(), st.ep_len)
+    got = env.episode_stats().cpu().numpy()
+    assert total_done > 0 and got[1] == stats[1] == total_done
+    assert got[2] == stats[2]
+    np.testing.assert_allclose(got[0], stats[0], rtol=1e-12)  # summation order differs
+    env.close()
+
+
+def test_observe_and_valid_mask_vs_oracle(oracle_mod):
+    O = oracle_mod
+    seed, n = 5, 3001
+    env = VecEnv(n, seed=seed)
+    world, st = _oracle_pair(O, env)
+    env.reset()
+    O.reset(world, st, seed=seed, epoch=0)
+    for t in range(30):
+        env.step(env.gen_actions(t))
+        O.step(world, st, actions=O.gen_actions(n, env.P, seed, 0, t), seed=seed, t=t)
+    obs = env.observe().cpu().numpy()
+    np.testing.assert_array_equal(obs, O.observe(world, st))
+    np.testing.assert_array_equal(env.valid_mask().cpu().numpy(), O.valid_mask(world, st))
+    env.close()
+
+
+def test_observe_and_valid_mask_vs_golden(water):
+    z = load_golden(os.path.join(GOLDEN, "tape_seed0.npz"))
+    k = len(z["valid_bits"])
+    env = env_for(z, k, water)
+    set_state(env, z, np.arange(k), prefix="post_")
+    np.testing.assert_array_equal(env.valid_mask().cpu().numpy(), z["valid_bits"])
+    obs = env.observe().cpu().numpy()
+    np.testing.assert_array_equal(obs[:, :6], z["obs6"][:k].astype(np.float32))
+    env.close()
+
+
+def test_fuel_cost_sqrt_is_correctly_rounded(oracle_mod):
+    """Typed moves (dx, dy) from (0, 0) over the whole grid: fuel bits use
+    np.sqrt of every reachable squared distance (shipping/util.py:4)."""
+    O = oracle_mod
+    dx, dy = np.meshgrid(np.arange(100), np.arange(100), indexing="ij")
+    n = dx.size
+    env = VecEnv(n, seed=9, water=np.ones((100, 100), np.uint8))
+    world, st = _oracle_pair(O, env)
+    env.reset()
+    O.reset(world, st, seed=9, epoch=0)
+    for f in ("x", "y"):
+        getattr(env, f).zero_()
+        getattr(st, f)[:] = 0
+    ty = np.ones(n, np.int32)
+    env.step_typed(ty, dx.ravel(), dy.ravel())
+    O.step(world, st, act_type=ty, act_a=dx.ravel(), act_b=dy.ravel(), seed=9, t=0)
+    _assert_vs_oracle(env, st, "sqrt")
+    env.close()
+
+
+# ---------------------------------------------------------------- full size
+def test_full_size_invariants_and_sampled_exactness(oracle_mod):
+    """N = 2^20 (BASELINE config 3): every ship on a non-ground cell, indices in
+    range, and 2048 sampled env ids bit-exact against the oracle run with the
+    same global id (shard invariance of the Philox key)."""
+    O = oracle_mod
+    n, seed, T = 1 << 20, 2024, 40
+    env = VecEnv(n, seed=seed)
+    env.reset()
+    rng = np.random.default_rng(1)
+    ids = np.sort(rng.choice(n, 2048, replace=False))
+    world = O.OracleWorld(env.water, env.port_x, env.port_y, env.port_fuel, env.port_cargo)
+    sts = [O.OracleState(1) for _ in ids]
+    for st, i in zip(sts, ids):
+        O.reset(world, st, seed=seed, env_id_base=int(i), epoch=0)
+    for t in range(T):
+        acts = env.gen_actions(t)
+        env.step(acts)
+        a_host = acts.cpu().numpy()
+        for st, i in zip(sts, ids):
+            O.step(world, st, actions=a_host[i:i + 1], seed=seed, env_id_base=int(i), t=t)
+    got = get_state(env)
+    nonground = world.nonground.astype(bool)
+    assert nonground[got["x"], got["y"]].all()
+    assert (got["origin"] >= 0).all() and (got["origin"] < env.P).all()
+    assert (got["dest"] >= 0).all() and (got["dest"] < env.P).all() and (got["dest"] != got["origin"]).all()
+    for f in FIELDS:
+        want = np.concatenate([getattr(st, f) for st in sts])
+        if f == "fuel":
+            np.testing.assert_array_equal(got[f][ids].view(np.int64), want.view(np.int64))
+        else:
+            np.testing.assert_array_equal(got[f][ids], want, err_msg=f)
+    env.close()
+
+
+def test_shard_invariance(oracle_mod):
+    """Envs [k, k+m) of one big VecEnv == a VecEnv of m envs with env_id_base=k."""
+    n, k, m, seed = 20000, 12345, 4000, 31
+    big = VecEnv(n, seed=seed)
+    part = VecEnv(m, seed=seed, env_id_base=k)
+    big.reset()
+    # resets are keyed by env id too: the shard's reset equals the slice of the big one
+    part.reset()
+    for t in range(60):
+        big.step(big.gen_actions(t))
+        part.step(part.gen_actions(t))
+    a, b = get_state(big), get_state(part)
+    for f in FIELDS:
+        np.testing.assert_array_equal(a[f][k:k + m], b[f], err_msg=f)
+    big.close()
+    part.close()

@@ -1,0 +1,76 @@
+"""The C-ABI library loads, exports every symbol include/shipenv.h declares, and
+reports API misuse as a status (no compute: runs without a GPU)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def header_symbols():
+    text = open(os.path.join(ROOT, "include", "shipenv.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(se_\w+)\s*\(", text, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from shippingenv_amd import _native, build
+
+    build.build(verbose=False)
+    return _native.lib()
+
+
+def test_exports_every_declared_symbol(lib):
+    from shippingenv_amd import _native
+
+    syms = header_symbols()
+    assert len(syms) >= 19
+    assert sorted(_native.EXPORTS) == syms
+    for s in syms:
+        assert hasattr(lib, s), s
+
+
+def test_abi_version(lib):
+    assert lib.se_abi_version() == 1
+
+
+def test_library_is_gfx950():
+    from shippingenv_amd import _native
+
+    blob = open(_native.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_misuse_is_a_status_not_a_crash(lib):
+    from shippingenv_amd import _native
+
+    h = C.c_void_p()
+    water = (C.c_uint8 * 4)(1, 1, 1, 1)
+    # bad map side -> SE_EINVAL before touching the device
+    rc = lib.se_create(C.byref(h), 0, 16, 0, 0, 2, water, 0, None, None, None, None, 0, 0)
+    assert rc == -1 and b"map sides" in lib.se_last_error()
+    assert lib.se_step(None, None, None) == -1
+    assert lib.se_destroy(None) == 0
+    with pytest.raises(_native.ShipEnvError):
+        _native.check(lib.se_bind(None, None))
+
+
+def test_product_path_has_no_fallback(monkeypatch, tmp_path):
+    """A missing library raises instead of silently stepping on the CPU."""
+    from shippingenv_amd import _native
+
+    monkeypatch.setattr(_native, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(_native, "_LIB", None)
+    with pytest.raises(_native.NativeLibraryError):
+        _native.lib()
+
+
+def test_product_does_not_import_oracle():
+    pkg = os.path.join(ROOT, "shippingenv_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".h", ".cpp")):
+                text = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in re.sub(r"#.*|//.*", "", text).replace("oracles", ""), f
