@@ -43,15 +43,18 @@ constexpr double kFuelInit = 200.0;
 constexpr double kMaxCargo = 50.0;
 
 // ------------------------------------------------------------------ world image
-// One device buffer of 32-bit words, staged as-is into LDS:
-//   [0, words)            ground bitmap   (bit = 1: np_game[x, y] == GROUND)
-//   [words, 2*words)      port bitmap     (bit = 1: some port sits on the cell)
-//   [2w, 2w+P)            port position   (x | y << 8)
-//   [2w+P, 2w+2P)         port fuel stock
-//   [2w+2P, 2w+3P)        port cargo stock
+// One device buffer of 32-bit words, staged as-is into LDS by every workgroup:
+//   [0, words)              ground bitmap  (bit = 1: np_game[x, y] == GROUND)
+//   [words, 2*words)        port bitmap    (bit = 1: some port sits on the cell)
+//   [2w, 2w+P)              port position  (x | y << 8)
+//   [2w+P, 2w+2P)           port fuel stock
+//   [2w+2P, 2w+3P)          port cargo stock
+//   [frac, frac+2*50)       f64 table fl(c / 50) for c in [0, 50) (8-byte aligned)
+// For the 100x100 map with 5 ports that is 2.9 KB.
 struct WorldDims {
     int32_t H, W, P, words;
-    __host__ __device__ int total() const { return 2 * words + 3 * P; }
+    __host__ __device__ int frac() const { return (2 * words + 3 * P + 1) & ~1; }
+    __host__ __device__ int total() const { return frac() + 2 * 50; }
 };
 
 struct LdsWorld {
@@ -60,6 +63,7 @@ struct LdsWorld {
     const uint32_t* pos;
     const int32_t* pfuel;
     const int32_t* pcargo;
+    const double* frac;
     int32_t H, W, P;
 
     __device__ bool is_ground(int x, int y) const {
@@ -77,6 +81,8 @@ struct LdsWorld {
     }
     __device__ int px(int i) const { return (int)(pos[i] & 0xffu); }
     __device__ int py(int i) const { return (int)((pos[i] >> 8) & 0xffu); }
+    // normalize(cargo, 50, 0) (util.py:6-8), only read for 0 < cargo < 50
+    __device__ double likelihood(int cargo) const { return frac[cargo]; }
 };
 
 __device__ __forceinline__ LdsWorld stage_world(const uint32_t* __restrict__ g, WorldDims d,
@@ -90,6 +96,7 @@ __device__ __forceinline__ LdsWorld stage_world(const uint32_t* __restrict__ g, 
     w.pos = lds + 2 * d.words;
     w.pfuel = (const int32_t*)(lds + 2 * d.words + d.P);
     w.pcargo = (const int32_t*)(lds + 2 * d.words + 2 * d.P);
+    w.frac = (const double*)(lds + d.frac());
     w.H = d.H;
     w.W = d.W;
     w.P = d.P;
@@ -103,28 +110,34 @@ struct Ship {
     int cargo, origin, dest;  // origin/dest: SE_NONE = None
 };
 
-// Variates of one MOVE: Philox (production) or a replay tape.
+__device__ __forceinline__ Key env_key(uint64_t seed, int64_t env) {
+    Key k;
+    k.k0 = (uint32_t)seed;
+    k.k1 = (uint32_t)(seed >> 32);
+    k.e0 = (uint32_t)(uint64_t)env;
+    k.e1 = (uint32_t)((uint64_t)env >> 32);
+    return k;
+}
+
+// The rare draws of one MOVE (loss type, beta, arrival): Philox or a replay tape.
+// The common pair (u_fuel, u_gate) is drawn up front for a whole group.
 template <bool kReplay>
-struct Draws;
+struct RareDraws;
 
 template <>
-struct Draws<false> {
+struct RareDraws<false> {
     Key key;
     uint32_t t;
-    __device__ void move(double& u_fuel, double& u_gate) const {
-        const U4 o = draw(key, t, kSlotMove);
-        u_fuel = u53(o.v[0], o.v[1]);
-        u_gate = u53(o.v[2], o.v[3]);
-    }
-    __device__ double loss_type() const {
-        const U4 o = draw(key, t, kSlotLoss);
-        return u53(o.v[0], o.v[1]);
-    }
-    // Beta(2, 2) as the median of three uniforms (exact in distribution)
-    __device__ double beta() const {
-        const U4 a = draw(key, t, kSlotLoss), b = draw(key, t, kSlotBeta);
-        const double u1 = u53(a.v[2], a.v[3]), u2 = u53(b.v[0], b.v[1]), u3 = u53(b.v[2], b.v[3]);
-        return fmax(fmin(u1, u2), fmin(fmax(u1, u2), u3));
+    // u_type from words 0,1 of slot LOSS; Beta(2,2) = median of three uniforms
+    // (words 2,3 of LOSS and 0..3 of BETA) — exact in distribution.
+    __device__ void loss(double& u_type, double& beta) const {
+        const U4 a = draw(key, t, kSlotLoss);
+        u_type = u53(a.v[0], a.v[1]);
+        if (u_type >= 0.1 && u_type <= 0.9) {
+            const U4 b = draw(key, t, kSlotBeta);
+            const double u1 = u53(a.v[2], a.v[3]), u2 = u53(b.v[0], b.v[1]), u3 = u53(b.v[2], b.v[3]);
+            beta = fmax(fmin(u1, u2), fmin(fmax(u1, u2), u3));
+        }
     }
     __device__ int arrive(int P, int origin) const {
         const U4 o = draw(key, t, kSlotArrive);
@@ -133,14 +146,12 @@ struct Draws<false> {
 };
 
 template <>
-struct Draws<true> {
+struct RareDraws<true> {
     const se_tape* rec;
-    __device__ void move(double& u_fuel, double& u_gate) const {
-        u_fuel = rec->u_fuel;
-        u_gate = rec->u_gate;
+    __device__ void loss(double& u_type, double& beta) const {
+        u_type = rec->u_type;
+        beta = rec->beta;
     }
-    __device__ double loss_type() const { return rec->u_type; }
-    __device__ double beta() const { return rec->beta; }
     __device__ int arrive(int, int) const { return rec->arrive_dest; }
 };
 
@@ -150,118 +161,88 @@ __device__ __forceinline__ double int_sqrt_rn(int64_t v) {
     return v == 1 ? 1.0 : __dsqrt_rn((double)v);
 }
 
-// _move_ship (:273-339). Returns SE_ERR_*; on error s is untouched.
-template <bool kReplay>
-__device__ __forceinline__ int move_ship(const LdsWorld& w, Ship& s, int64_t mx, int64_t my,
-                                         const Draws<kReplay>& dr, double& reward, int& done) {
-    if (s.dest == SE_NONE) return SE_ERR_NO_DEST;  // :276
-    const int64_t nx = s.x + mx, ny = s.y + my;
-    if (nx < 0 || nx >= w.H || ny < 0 || ny >= w.W) return SE_ERR_OOB;  // :284, before any draw
-
-    double u_fuel, u_gate;
-    dr.move(u_fuel, u_gate);
-    // fuel cost (:103-104): dist * (1 + uniform(-0.1, 0.1)), uniform = -0.1 + 0.2*u, unfused
-    const double cost = int_sqrt_rn(mx * mx + my * my) * (1.0 + (-0.1 + 0.2 * u_fuel));
-    double r = 0.0;
-    int d = 0;
-    if (s.fuel < cost) {  // :288-290
-        r += -10.0;
-        d = 1;
-    }
-    const int ox = s.x, oy = s.y;
-    if (w.is_ground((int)nx, (int)ny)) {  // :293-294: blocked, but still "arrives" below if on dest
-        r += -5.0;
-    } else {  // :296-300
-        s.x = (int)nx;
-        s.y = (int)ny;
-        s.fuel -= cost;
-        r += -0.0001;
-        r += -1.0;
-    }
-    // :307-315 closer/farther, old cell vs ATTEMPTED cell. sqrt is monotone and the
-    // squared distances are small integers, so comparing them is exact.
-    const int px = w.px(s.dest), py = w.py(s.dest);
-    const int64_t d_old = (int64_t)(ox - px) * (ox - px) + (int64_t)(oy - py) * (oy - py);
-    const int64_t d_new = (nx - px) * (nx - px) + (ny - py) * (ny - py);
-    r += d_old > d_new ? 2.0 : -2.0;
-    // :318-323 cargo-loss gate: random() <= cargo / 50
-    if (u_gate <= (double)s.cargo / kMaxCargo) {
-        const double lt = dr.loss_type();  // drawn first, even with no cargo (:177)
-        int loss = 0;
-        if (s.cargo != 0 && lt >= 0.1) loss = lt > 0.9 ? s.cargo : (int)(dr.beta() * (double)s.cargo);
-        s.cargo -= loss;
-        r += (double)(-3 * loss);
-    }
-    // :325-337 arrival at the destination port
-    if (s.x == px && s.y == py) {
-        r += (double)(2 * s.cargo);
-        s.cargo = 0;
-        s.origin = s.dest;
-        s.dest = dr.arrive(w.P, s.origin);
-        r += 10.0;
-    }
-    reward = r;
-    done = d;
-    return SE_ERR_OK;
+// utils/preprocessing.py:111-137 (moves N, E, S, W; Python wraps -4..-1)
+__device__ __forceinline__ int decode_agent(int P, int act, int& type, int& a, int& b) {
+    const int k = act & 3;  // -4..-1 -> 0..3 like Python's negative list index
+    const bool move = act < 4;
+    type = move ? 1 : (act < 4 + P ? 2 : (act < 4 + P + 50 ? 4 : 3));
+    const int val = act - (type == 2 ? 4 : (type == 4 ? 4 + P : 4 + P + 50));
+    a = move ? (k == 1 ? -1 : (k == 3 ? 1 : 0)) : val;  // EAST = (-1, 0), WEST = (1, 0)
+    b = move ? (k == 0 ? -1 : (k == 2 ? 1 : 0)) : 0;    // NORTH = (0, -1), SOUTH = (0, 1)
+    return act < -4 ? SE_ERR_BAD_INDEX : SE_ERR_OK;
 }
 
-// step (:359-376) with a typed action. On error the state is untouched.
-template <bool kReplay>
-__device__ __forceinline__ int step_typed(const LdsWorld& w, Ship& s, int type, int a, int b,
-                                          const Draws<kReplay>& dr, double& reward, int& done) {
+// One env's step (:359-376) given its action and its common draws. Returns
+// SE_ERR_*; the state is only written on success, so an error leaves it as it was.
+template <bool kUnitMoves, bool kReplay>
+__device__ __forceinline__ int env_step(const LdsWorld& w, Ship& s, int type, int a, int b,
+                                        double u_fuel, double u_gate,
+                                        const RareDraws<kReplay>& rare, double& reward, int& done) {
     reward = 0.0;
     done = 0;
     if (w.P == 0) return SE_ERR_NO_PORTS;  // :360
-    switch (type) {
-    case 2:  // SELECT_PORT, _select_port :265-271
+    if (type == 1) {                        // _move_ship (:273-339)
+        if (s.dest == SE_NONE) return SE_ERR_NO_DEST;  // :276
+        const int64_t nx = (int64_t)s.x + a, ny = (int64_t)s.y + b;
+        if (nx < 0 || nx >= w.H || ny < 0 || ny >= w.W) return SE_ERR_OOB;  // :284
+        // fuel cost (:103-104): dist * (1 + uniform(-0.1, 0.1)), uniform = -0.1 + 0.2*u, unfused
+        const double dist = kUnitMoves ? 1.0 : int_sqrt_rn((int64_t)a * a + (int64_t)b * b);
+        const double cost = dist * (1.0 + (-0.1 + 0.2 * u_fuel));
+        const bool out_of_fuel = s.fuel < cost;  // :288-290
+        const double r0 = out_of_fuel ? -10.0 : 0.0;
+        const bool ground = w.is_ground((int)nx, (int)ny);  // :293
+        // :294 blocked (-5) or :296-300 moved (-0.0001 then -1), in the reference's add order
+        double r = ground ? r0 + -5.0 : (r0 + -0.0001) + -1.0;
+        const int ox = s.x, oy = s.y;
+        if (!ground) {
+            s.x = (int)nx;
+            s.y = (int)ny;
+            s.fuel = s.fuel - cost;
+        }
+        // :307-315 old cell vs ATTEMPTED cell; sqrt is monotone and the squared
+        // distances are small integers, so comparing them is exact
+        const int px = w.px(s.dest), py = w.py(s.dest);
+        const int64_t d_old = (int64_t)(ox - px) * (ox - px) + (int64_t)(oy - py) * (oy - py);
+        const int64_t d_new = (nx - px) * (nx - px) + (ny - py) * (ny - py);
+        r += d_old > d_new ? 2.0 : -2.0;
+        // :318-323 the gate random() <= cargo/50. With no cargo a firing gate has no
+        // effect (loss 0, :180-181); from 50 on it always fires (random() < 1).
+        const bool gate = s.cargo >= 50 || (s.cargo > 0 && u_gate <= w.likelihood(s.cargo));
+        if (gate) {
+            double lt, beta = 0.0;
+            rare.loss(lt, beta);
+            const int loss = lt < 0.1 ? 0 : (lt > 0.9 ? s.cargo : (int)(beta * (double)s.cargo));
+            s.cargo -= loss;
+            r += (double)(-3 * loss);
+        }
+        if (s.x == px && s.y == py) {  // :325-337 arrival
+            r += (double)(2 * s.cargo);
+            s.cargo = 0;
+            s.origin = s.dest;
+            s.dest = rare.arrive(w.P, s.origin);
+            r += 10.0;
+        }
+        reward = r;
+        done = out_of_fuel ? 1 : 0;
+        return SE_ERR_OK;
+    }
+    if (type == 2) {  // _select_port (:265-271)
         if (a < 0 || a >= w.P) return SE_ERR_PORT_RANGE;
         if (s.origin == a) return SE_ERR_SAME_PORT;
         s.dest = a;
         return SE_ERR_OK;
-    case 4:    // TAKE_CARGO, _take_cargo :341-348
-    case 3: {  // TAKE_FUEL, _take_fuel :350-357
+    }
+    if (type == 3 || type == 4) {  // _take_fuel (:350-357) / _take_cargo (:341-348)
         const int idx = w.port_at(s.x, s.y);
         if (idx < 0) return SE_ERR_NOT_AT_PORT;
         const int stock = type == 4 ? w.pcargo[idx] : w.pfuel[idx];
         if (a <= 0 || a > stock) return SE_ERR_AMOUNT;
         if (type == 4) s.cargo += a;
-        else s.fuel += (double)a;
+        else s.fuel = s.fuel + (double)a;
         reward = 0.05;
         return SE_ERR_OK;
     }
-    case 1: {  // MOVE_SHIP
-        Ship t = s;
-        const int e = move_ship<kReplay>(w, t, a, b, dr, reward, done);
-        if (e == SE_ERR_OK) s = t;
-        return e;
-    }
-    default:
-        return SE_ERR_BAD_CATEGORY;  // :373-374
-    }
-}
-
-// utils/preprocessing.py:111-137 (moves N, E, S, W; Python wraps -4..-1)
-__device__ __forceinline__ int decode_agent(int P, int act, int& type, int& a, int& b) {
-    if (act < 4) {
-        if (act < -4) return SE_ERR_BAD_INDEX;
-        const int k = act & 3;  // -4..-1 -> 0..3
-        type = 1;
-        a = k == 1 ? -1 : (k == 3 ? 1 : 0);  // EAST = (-1, 0), WEST = (1, 0)
-        b = k == 0 ? -1 : (k == 2 ? 1 : 0);  // NORTH = (0, -1), SOUTH = (0, 1)
-        return SE_ERR_OK;
-    }
-    if (act < 4 + P) {
-        type = 2;
-        a = act - 4;
-    } else if (act < 4 + P + 50) {
-        type = 4;
-        a = act - (4 + P);
-    } else {
-        type = 3;
-        a = act - (4 + P + 50);
-    }
-    b = 0;
-    return SE_ERR_OK;
+    return SE_ERR_BAD_CATEGORY;  // :373-374
 }
 
 // reset (:227-243) from two Philox words
@@ -272,15 +253,6 @@ __device__ __forceinline__ void reset_ship(const LdsWorld& w, Ship& s, uint32_t 
     s.fuel = kFuelInit;
     s.x = w.px(s.origin);
     s.y = w.py(s.origin);
-}
-
-__device__ __forceinline__ Key env_key(uint64_t seed, int64_t env) {
-    Key k;
-    k.k0 = (uint32_t)seed;
-    k.k1 = (uint32_t)(seed >> 32);
-    k.e0 = (uint32_t)(uint64_t)env;
-    k.e1 = (uint32_t)((uint64_t)env >> 32);
-    return k;
 }
 
 __device__ __forceinline__ uint32_t lane_id() {
@@ -315,11 +287,7 @@ template <typename T>
 __device__ __forceinline__ void ld4(const T* __restrict__ p, int64_t base, bool full, int64_t n,
                                     T (&v)[4]) {
     if (full) {
-        if constexpr (sizeof(T) == 1) {
-            const uint32_t w = *reinterpret_cast<const uint32_t*>(p + base);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = (T)((w >> (8 * j)) & 0xffu);
-        } else if constexpr (sizeof(T) == 4) {
+        if constexpr (sizeof(T) == 4) {
             const uint4 w = *reinterpret_cast<const uint4*>(p + base);
             v[0] = __builtin_bit_cast(T, w.x);
             v[1] = __builtin_bit_cast(T, w.y);
@@ -339,16 +307,33 @@ __device__ __forceinline__ void ld4(const T* __restrict__ p, int64_t base, bool 
     }
 }
 
+// 4 u8 fields of consecutive envs as one packed word
+__device__ __forceinline__ uint32_t ld4u8(const uint8_t* __restrict__ p, int64_t base, bool full,
+                                          int64_t n) {
+    if (full) return *reinterpret_cast<const uint32_t*>(p + base);
+    uint32_t w = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (base + j < n) w |= (uint32_t)p[base + j] << (8 * j);
+    return w;
+}
+
+__device__ __forceinline__ void st4u8(uint8_t* __restrict__ p, int64_t base, bool full, int64_t n,
+                                      uint32_t w) {
+    if (full) {
+        *reinterpret_cast<uint32_t*>(p + base) = w;
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (base + j < n) p[base + j] = (uint8_t)(w >> (8 * j));
+}
+
 template <typename T>
 __device__ __forceinline__ void st4(T* __restrict__ p, int64_t base, bool full, int64_t n,
                                     const T (&v)[4]) {
     if (full) {
-        if constexpr (sizeof(T) == 1) {
-            uint32_t w = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) w |= (uint32_t)(uint8_t)v[j] << (8 * j);
-            *reinterpret_cast<uint32_t*>(p + base) = w;
-        } else if constexpr (sizeof(T) == 4) {
+        if constexpr (sizeof(T) == 4) {
             uint4 w;
             w.x = __builtin_bit_cast(uint32_t, v[0]);
             w.y = __builtin_bit_cast(uint32_t, v[1]);
@@ -366,102 +351,135 @@ __device__ __forceinline__ void st4(T* __restrict__ p, int64_t base, bool full, 
     }
 }
 
-template <bool kTyped, bool kReplay, bool kAuto>
-__global__ __launch_bounds__(kBlock) void step_kernel(StepArgs A) {
-    extern __shared__ uint32_t lds[];
-    __shared__ double red[kBlock / 64][3];
-    const LdsWorld w = stage_world(A.world, A.dims, lds);
-    const se_state& S = A.st;
-    const int64_t groups = (A.n + kEnvsPerThread - 1) / kEnvsPerThread;
+__device__ __forceinline__ int byte_of(uint32_t w, int j) { return (int)((w >> (8 * j)) & 0xffu); }
 
-    double blk_ret = 0.0, blk_eps = 0.0, blk_len = 0.0;
-    if (kAuto && blockIdx.x == 0 && threadIdx.x == 0) *A.next_count = 0;
+// The raw inputs of 4 consecutive envs (one lane access per field).
+template <bool kTyped, bool kAuto>
+struct Group {
+    uint32_t x, y, org, dst;  // packed u8 x4
+    int32_t cargo[4];
+    double fuel[4];
+    int32_t act[4], aa[4], ab[4];
+    float ep_ret[4];
+    int32_t ep_len[4];
 
-    for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < groups;
-         g += (int64_t)gridDim.x * kBlock) {
-        const int64_t base = g * kEnvsPerThread;
-        const bool full = base + kEnvsPerThread <= A.n;
-
-        uint8_t x[4], y[4], org[4], dst[4];
-        double fuel[4];
-        int32_t cargo[4], act[4], aa[4], ab[4];
-        ld4(S.x, base, full, A.n, x);
-        ld4(S.y, base, full, A.n, y);
-        ld4(S.origin, base, full, A.n, org);
-        ld4(S.dest, base, full, A.n, dst);
-        ld4(S.fuel, base, full, A.n, fuel);
+    __device__ __forceinline__ void load(const StepArgs& A, int64_t base, bool full) {
+        const se_state& S = A.st;
+        x = ld4u8(S.x, base, full, A.n);
+        y = ld4u8(S.y, base, full, A.n);
+        org = ld4u8(S.origin, base, full, A.n);
+        dst = ld4u8(S.dest, base, full, A.n);
         ld4(S.cargo, base, full, A.n, cargo);
+        ld4(S.fuel, base, full, A.n, fuel);
         ld4(A.act, base, full, A.n, act);
         if (kTyped) {
             ld4(A.act_a, base, full, A.n, aa);
             ld4(A.act_b, base, full, A.n, ab);
         }
-        float ep_ret[4];
-        int32_t ep_len[4];
         if (kAuto) {
             ld4(S.ep_return, base, full, A.n, ep_ret);
             ld4(S.ep_len, base, full, A.n, ep_len);
         }
+    }
+};
 
+// One thread steps 4 consecutive envs per grid-stride iteration. The first
+// group's loads are issued before the world is staged into LDS, and each
+// iteration prefetches the next group before computing the current one.
+template <bool kTyped, bool kReplay, bool kAuto>
+__global__ __launch_bounds__(kBlock) void step_kernel(StepArgs A) {
+    extern __shared__ uint32_t lds[];
+    __shared__ double red[kBlock / 64][3];
+    const se_state& S = A.st;
+    const int64_t groups = (A.n + kEnvsPerThread - 1) / kEnvsPerThread;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+
+    Group<kTyped, kAuto> cur;
+    if (g < groups) cur.load(A, g * kEnvsPerThread, g * kEnvsPerThread + kEnvsPerThread <= A.n);
+    const LdsWorld w = stage_world(A.world, A.dims, lds);
+
+    double blk_ret = 0.0, blk_eps = 0.0, blk_len = 0.0;
+    if (kAuto && blockIdx.x == 0 && threadIdx.x == 0) *A.next_count = 0;
+
+    for (; g < groups; g += stride) {
+        const int64_t base = g * kEnvsPerThread;
+        const bool full = base + kEnvsPerThread <= A.n;
+        Group<kTyped, kAuto> nxt;
+        const int64_t gn = g + stride;
+        if (gn < groups) nxt.load(A, gn * kEnvsPerThread, gn * kEnvsPerThread + kEnvsPerThread <= A.n);
+
+        // decode, then the common draws of all 4 envs (independent Philox chains)
+        int ty[4], va[4], vb[4], er[4];
+        double u_fuel[4], u_gate[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (kTyped) {
+                ty[j] = cur.act[j];
+                va[j] = cur.aa[j];
+                vb[j] = cur.ab[j];
+                er[j] = SE_ERR_OK;
+            } else {
+                er[j] = decode_agent(w.P, cur.act[j], ty[j], va[j], vb[j]);
+            }
+            if constexpr (kReplay) {
+                const bool in = base + j < A.n;
+                u_fuel[j] = in ? A.tape[base + j].u_fuel : 0.0;
+                u_gate[j] = in ? A.tape[base + j].u_gate : 0.0;
+            } else {
+                const U4 o = draw(env_key(A.seed, A.env_base + base + j), A.t, kSlotMove);
+                u_fuel[j] = u53(o.v[0], o.v[1]);
+                u_gate[j] = u53(o.v[2], o.v[3]);
+            }
+        }
+
+        uint32_t ox = 0, oy = 0, oorg = 0, odst = 0, dn4 = 0, er4 = 0;
         float rew[4];
-        uint8_t dn[4];
-        int8_t er[4];
         int ndone = 0;
         bool fin[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int64_t i = base + j;
-            Ship s{x[j], y[j], fuel[j], cargo[j], org[j], dst[j]};
+            Ship s{byte_of(cur.x, j), byte_of(cur.y, j), cur.fuel[j], cur.cargo[j],
+                   byte_of(cur.org, j), byte_of(cur.dst, j)};
             double r = 0.0;
-            int d = 0, e;
-            int ty, a, b;
-            if (kTyped) {
-                ty = act[j];
-                a = aa[j];
-                b = ab[j];
-                e = SE_ERR_OK;
-            } else {
-                e = decode_agent(w.P, act[j], ty, a, b);
-            }
-            const Key key = env_key(A.seed, A.env_base + i);
-            if (e == SE_ERR_OK && i < A.n) {
-                if constexpr (kReplay) {
-                    Draws<true> dr{A.tape + i};
-                    e = step_typed<true>(w, s, ty, a, b, dr, r, d);
-                } else {
-                    Draws<false> dr{key, A.t};
-                    e = step_typed<false>(w, s, ty, a, b, dr, r, d);
+            int d = 0, e = er[j];
+            if (kReplay) {
+                if (e == SE_ERR_OK && i < A.n) {
+                    RareDraws<true> rare{A.tape + i};
+                    e = env_step<false, true>(w, s, ty[j], va[j], vb[j], u_fuel[j], u_gate[j], rare, r, d);
                 }
+            } else if (e == SE_ERR_OK) {
+                RareDraws<false> rare{env_key(A.seed, A.env_base + i), A.t};
+                e = env_step<!kTyped, false>(w, s, ty[j], va[j], vb[j], u_fuel[j], u_gate[j], rare, r, d);
             }
             if (e != SE_ERR_OK) {
                 r = 0.0;
                 d = 0;
             }
             rew[j] = (float)r;  // one rounding of the reference's f64 reward
-            dn[j] = (uint8_t)d;
-            er[j] = (int8_t)e;
             fin[j] = false;
             if (kAuto && i < A.n) {
-                ep_ret[j] += rew[j];
-                ep_len[j] += 1;
+                cur.ep_ret[j] += rew[j];
+                cur.ep_len[j] += 1;
                 if (d) {
                     fin[j] = true;
                     ++ndone;
-                    blk_ret += (double)ep_ret[j];
+                    blk_ret += (double)cur.ep_ret[j];
                     blk_eps += 1.0;
-                    blk_len += (double)ep_len[j];
+                    blk_len += (double)cur.ep_len[j];
+                    const U4 o = draw(env_key(A.seed, A.env_base + i), A.t, kSlotReset);
+                    reset_ship(w, s, o.v[0], o.v[1]);
                 }
             }
-            if (kAuto && fin[j]) {
-                const U4 o = draw(key, A.t, kSlotReset);
-                reset_ship(w, s, o.v[0], o.v[1]);
-            }
-            x[j] = (uint8_t)s.x;
-            y[j] = (uint8_t)s.y;
-            fuel[j] = s.fuel;
-            cargo[j] = s.cargo;
-            org[j] = (uint8_t)s.origin;
-            dst[j] = (uint8_t)s.dest;
+            ox |= (uint32_t)(s.x & 0xff) << (8 * j);
+            oy |= (uint32_t)(s.y & 0xff) << (8 * j);
+            oorg |= (uint32_t)(s.origin & 0xff) << (8 * j);
+            odst |= (uint32_t)(s.dest & 0xff) << (8 * j);
+            dn4 |= (uint32_t)d << (8 * j);
+            er4 |= (uint32_t)(e & 0xff) << (8 * j);
+            cur.fuel[j] = s.fuel;
+            cur.cargo[j] = s.cargo;
         }
 
         if (kAuto) {
@@ -481,27 +499,28 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs A) {
                     if (fin[j]) {
                         se_done_rec rec;
                         rec.env = (int32_t)(base + j);
-                        rec.ep_return = ep_ret[j];
-                        rec.ep_len = ep_len[j];
+                        rec.ep_return = cur.ep_ret[j];
+                        rec.ep_len = cur.ep_len[j];
                         rec.step = (int32_t)A.t;
                         A.done_recs[slot++] = rec;
-                        ep_ret[j] = 0.0f;
-                        ep_len[j] = 0;
+                        cur.ep_ret[j] = 0.0f;
+                        cur.ep_len[j] = 0;
                     }
                 }
             }
-            st4(S.ep_return, base, full, A.n, ep_ret);
-            st4(S.ep_len, base, full, A.n, ep_len);
+            st4(S.ep_return, base, full, A.n, cur.ep_ret);
+            st4(S.ep_len, base, full, A.n, cur.ep_len);
         }
-        st4(S.x, base, full, A.n, x);
-        st4(S.y, base, full, A.n, y);
-        st4(S.origin, base, full, A.n, org);
-        st4(S.dest, base, full, A.n, dst);
-        st4(S.fuel, base, full, A.n, fuel);
-        st4(S.cargo, base, full, A.n, cargo);
+        st4u8(S.x, base, full, A.n, ox);
+        st4u8(S.y, base, full, A.n, oy);
+        st4u8(S.origin, base, full, A.n, oorg);
+        st4u8(S.dest, base, full, A.n, odst);
+        st4(S.fuel, base, full, A.n, cur.fuel);
+        st4(S.cargo, base, full, A.n, cur.cargo);
         st4(S.reward, base, full, A.n, rew);
-        st4(S.done, base, full, A.n, dn);
-        st4(S.err, base, full, A.n, er);
+        st4u8(S.done, base, full, A.n, dn4);
+        st4u8(reinterpret_cast<uint8_t*>(S.err), base, full, A.n, er4);
+        cur = nxt;
     }
 
     if (kAuto) {
@@ -527,10 +546,10 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs A) {
                 c += red[k][2];
             }
             if (b != 0.0) {
-                double* s = A.slab + 4 * blockIdx.x;
-                s[0] += a;
-                s[1] += b;
-                s[2] += c;
+                double* sl = A.slab + 4 * blockIdx.x;
+                sl[0] += a;
+                sl[1] += b;
+                sl[2] += c;
             }
         }
     }
@@ -788,6 +807,12 @@ int upload_world(se_env* env, int32_t P, const int32_t* px, const int32_t* py, c
         img[2 * words + i] = (uint32_t)px[i] | ((uint32_t)py[i] << 8);
         img[2 * words + P + i] = (uint32_t)pf[i];
         img[2 * words + 2 * P + i] = (uint32_t)pc[i];
+    }
+    // normalize(cargo, 50, 0) = cargo / 50 (util.py:6-8): Python's int / int true
+    // division is the correctly rounded quotient, which IEEE f64 division gives here.
+    for (int c = 0; c < 50; ++c) {
+        const double q = (double)c / kMaxCargo;
+        memcpy(&img[d.frac() + 2 * c], &q, sizeof q);
     }
     if (d.total() > env->world_cap) {
         if (env->d_world) HIP_TRY(hipFree(env->d_world));
