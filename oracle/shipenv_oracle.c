@@ -41,8 +41,8 @@ enum {
 };
 
 /* Philox counter slots (DESIGN.md "RNG contract") */
-enum { SLOT_MOVE = 0, SLOT_LOSS = 1, SLOT_BETA = 2, SLOT_ARRIVE = 3, SLOT_RESET = 4,
-       SLOT_EXPLICIT_RESET = 5, SLOT_ACTION = 6 };
+enum { SLOT_FUEL = 0, SLOT_LOSS = 1, SLOT_BETA = 2, SLOT_ARRIVE = 3, SLOT_RESET = 4,
+       SLOT_EXPLICIT_RESET = 5, SLOT_ACTION = 6, SLOT_GATE = 7 };
 
 /* ------------------------------------------------------------------ Philox4x32-10 */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
@@ -96,17 +96,24 @@ typedef struct {
     uint32_t t;
 } source;
 
-/* u_fuel and u_gate: environment.py:104 (uniform) and :320 (random), always both */
+/* u_fuel and u_gate: environment.py:104 (uniform) and :320 (random), always both.
+ * Philox: the four envs 4k..4k+3 share one block at counter (k, t, FUEL) and one at
+ * (k, t, GATE); env 4k+j takes word j as a 32-bit uniform u = w * 2^-32. */
+static double u32(uint32_t w) { return (double)w * (1.0 / 4294967296.0); }
+
 static void src_move(const source* s, double* u_fuel, double* u_gate) {
     if (s->tape) {
         *u_fuel = s->tape->u_fuel;
         *u_gate = s->tape->u_gate;
         return;
     }
-    uint32_t o[4];
-    draw4(s->seed, s->env, s->t, SLOT_MOVE, o);
-    *u_fuel = u53(o[0], o[1]);
-    *u_gate = u53(o[2], o[3]);
+    uint32_t f[4], g[4];
+    const int64_t quad = (int64_t)((uint64_t)s->env >> 2);
+    const int lane = (int)(s->env & 3);
+    draw4(s->seed, quad, s->t, SLOT_FUEL, f);
+    draw4(s->seed, quad, s->t, SLOT_GATE, g);
+    *u_fuel = u32(f[lane]);
+    *u_gate = u32(g[lane]);
 }
 
 static double src_loss_type(const source* s) { /* environment.py:177 */

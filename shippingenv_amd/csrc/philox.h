@@ -12,13 +12,14 @@
 namespace shipenv {
 
 enum Slot : uint32_t {
-    kSlotMove = 0,           // u_fuel (words 0,1), u_gate (words 2,3)
+    kSlotFuel = 0,           // counter env word = env / 4: word j = u_fuel of env 4k+j (32-bit)
     kSlotLoss = 1,           // u_type (0,1), first beta uniform (2,3)
     kSlotBeta = 2,           // second and third beta uniforms
     kSlotArrive = 3,         // word 0 -> new destination != origin
     kSlotReset = 4,          // auto-reset inside step t: word 0 origin, word 1 dest
     kSlotExplicitReset = 5,  // se_reset with the reset epoch in the t word
     kSlotAction = 6,         // synthetic bench agent
+    kSlotGate = 7,           // counter env word = env / 4: word j = u_gate of env 4k+j (32-bit)
 };
 
 struct U4 {
