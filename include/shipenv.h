@@ -47,6 +47,15 @@ extern "C" {
 #define SE_ERR_BAD_CATEGORY 7   /* ValueError("Action category unknown")                    :374 */
 #define SE_ERR_NO_PORTS 8       /* Exception("No ports available")                          :360 */
 #define SE_ERR_BAD_INDEX 9      /* IndexError("list index out of range"), utils/preprocessing.py:127 */
+#define SE_ERR_NEED_DRAW 10     /* replay only: the step needs a variate the tape lacks (no effect) */
+
+/* se_tape.used bits written by se_step_replay: the reference draws the step consumed */
+#define SE_USED_FUEL_GATE 1     /* uniform() for the fuel cost (:104) and the gate random() (:320) */
+#define SE_USED_LOSS_TYPE 2     /* random() loss type (:177) */
+#define SE_USED_BETA 4          /* betavariate(2, 2) (:195) */
+#define SE_USED_ARRIVE 8        /* randint redraw of the destination (:333-335) */
+#define SE_USED_MOVED 16        /* not a draw: the ship moved onto a non-ground cell (:296-300),
+                                   so fuel became an np.float64 and the reward a float */
 
 /* se_create flags */
 #define SE_FLAG_AUTO_RESET 1u   /* reset an env inside se_step right after it reports done */
@@ -81,17 +90,21 @@ typedef struct se_state {
     int32_t* ep_len;    /* running episode length in step calls (auto-reset) */
     struct se_done_rec* done_recs; /* auto-reset done list, capacity 2*n records */
     int32_t* done_count;           /* auto-reset done counters, 3 entries, zeroed by se_bind */
+    double* reward64;              /* optional (NULL): the reference's f64 reward, unrounded */
 } se_state;
 
 /* One replayed MOVE's variates (the draws the reference made through `random`,
- * SURVEY.md Appendix A); used by se_step_replay only. 48 bytes. */
+ * SURVEY.md Appendix A); used by se_step_replay only. 48 bytes. A variate the
+ * step needs but the record lacks (NaN, or arrive_dest < 0) yields
+ * SE_ERR_NEED_DRAW and no state change: a caller holding the reference's RNG
+ * draws exactly that next variate and steps again (shipping.Environment does). */
 typedef struct se_tape {
     double u_fuel;       /* random() behind uniform(-0.1, 0.1)                  :104 */
     double u_gate;       /* random() of the cargo-loss gate                       :320 */
     double u_type;       /* random() loss type (read only if the gate fires)      :177 */
     double beta;         /* betavariate(2, 2) (read only for a partial loss)      :195 */
     int32_t arrive_dest; /* accepted randint at arrival                          :333 */
-    int32_t pad;
+    int32_t used;        /* out: SE_USED_* bits of the draws the step consumed */
 } se_tape;
 
 /* Environment.__init__ + _initialize_map + add_port (environment.py:29-65).
@@ -133,9 +146,9 @@ int se_step_typed(se_env* env, const int32_t* type, const int32_t* a, const int3
                   void* stream);
 
 /* step() with typed actions whose variates come from tape[i] (replay of recorded
- * reference draws). The step counter does not advance. */
+ * reference draws); writes tape[i].used. The step counter does not advance. */
 int se_step_replay(se_env* env, const int32_t* type, const int32_t* a, const int32_t* b,
-                   const se_tape* tape, void* stream);
+                   se_tape* tape, void* stream);
 
 /* utils.preprocessing.preprocess_state rows (:25-62) as f32, row stride ld >= 6+4P:
  * [x, y, fuel, fuel ("cargo" is self.fuel, environment.py:206), origin, dest, (px,py,pfuel,pcargo)*P],

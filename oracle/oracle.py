@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(HERE, "liboracle_shipenv.so")
 
 TAPE_DTYPE = np.dtype(
     [("u_fuel", "<f8"), ("u_gate", "<f8"), ("u_type", "<f8"), ("beta", "<f8"),
-     ("arrive_dest", "<i4"), ("pad", "<i4")]
+     ("arrive_dest", "<i4"), ("used", "<i4")]
 )
 
 

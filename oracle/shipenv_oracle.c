@@ -37,8 +37,10 @@ enum { MOVE_SHIP = 1, SELECT_PORT = 2, TAKE_FUEL = 3, TAKE_CARGO = 4 };
 /* error classes (include/shipenv.h SE_ERR_*) */
 enum {
     E_OK = 0, E_OOB = 1, E_SAME_PORT = 2, E_PORT_RANGE = 3, E_NOT_AT_PORT = 4, E_AMOUNT = 5,
-    E_NO_DEST = 6, E_BAD_CATEGORY = 7, E_NO_PORTS = 8, E_BAD_INDEX = 9
+    E_NO_DEST = 6, E_BAD_CATEGORY = 7, E_NO_PORTS = 8, E_BAD_INDEX = 9, E_NEED_DRAW = 10
 };
+/* tape.used bits (include/shipenv.h SE_USED_*) */
+enum { U_FUEL_GATE = 1, U_LOSS_TYPE = 2, U_BETA = 4, U_ARRIVE = 8 };
 
 /* Philox counter slots (DESIGN.md "RNG contract") */
 enum { SLOT_FUEL = 0, SLOT_LOSS = 1, SLOT_BETA = 2, SLOT_ARRIVE = 3, SLOT_RESET = 4,
@@ -94,6 +96,8 @@ typedef struct {
     uint64_t seed;
     int64_t env;
     uint32_t t;
+    int32_t used;         /* U_* bits of the draws consumed */
+    int need;             /* replay: a consumed draw is missing from the tape */
 } source;
 
 /* u_fuel and u_gate: environment.py:104 (uniform) and :320 (random), always both.
@@ -101,10 +105,12 @@ typedef struct {
  * (k, t, GATE); env 4k+j takes word j as a 32-bit uniform u = w * 2^-32. */
 static double u32(uint32_t w) { return (double)w * (1.0 / 4294967296.0); }
 
-static void src_move(const source* s, double* u_fuel, double* u_gate) {
+static void src_move(source* s, double* u_fuel, double* u_gate) {
+    s->used |= U_FUEL_GATE;
     if (s->tape) {
         *u_fuel = s->tape->u_fuel;
         *u_gate = s->tape->u_gate;
+        s->need |= isnan(*u_fuel) || isnan(*u_gate);
         return;
     }
     uint32_t f[4], g[4];
@@ -116,23 +122,35 @@ static void src_move(const source* s, double* u_fuel, double* u_gate) {
     *u_gate = u32(g[lane]);
 }
 
-static double src_loss_type(const source* s) { /* environment.py:177 */
-    if (s->tape) return s->tape->u_type;
+static double src_loss_type(source* s) { /* environment.py:177 */
+    s->used |= U_LOSS_TYPE;
+    if (s->tape) {
+        s->need |= isnan(s->tape->u_type);
+        return s->tape->u_type;
+    }
     uint32_t o[4];
     draw4(s->seed, s->env, s->t, SLOT_LOSS, o);
     return u53(o[0], o[1]);
 }
 
-static double src_beta(const source* s) { /* environment.py:195, betavariate(2, 2) */
-    if (s->tape) return s->tape->beta;
+static double src_beta(source* s) { /* environment.py:195, betavariate(2, 2) */
+    s->used |= U_BETA;
+    if (s->tape) {
+        s->need |= isnan(s->tape->beta);
+        return s->tape->beta;
+    }
     uint32_t a[4], b[4];
     draw4(s->seed, s->env, s->t, SLOT_LOSS, a);
     draw4(s->seed, s->env, s->t, SLOT_BETA, b);
     return med3(u53(a[2], a[3]), u53(b[0], b[1]), u53(b[2], b[3]));
 }
 
-static int32_t src_arrive(const source* s, int32_t P, int32_t origin) { /* :333-335 */
-    if (s->tape) return s->tape->arrive_dest;
+static int32_t src_arrive(source* s, int32_t P, int32_t origin) { /* :333-335 */
+    s->used |= U_ARRIVE;
+    if (s->tape) {
+        s->need |= s->tape->arrive_dest < 0;
+        return s->tape->arrive_dest;
+    }
     uint32_t o[4];
     draw4(s->seed, s->env, s->t, SLOT_ARRIVE, o);
     return pick_other(o[0], P, origin);
@@ -162,7 +180,7 @@ static int32_t current_port(const orc_world* w, const ship* s) {
 }
 
 /* _move_ship, :273-339 */
-static int move_ship(const orc_world* w, ship* s, int64_t mx, int64_t my, const source* src,
+static int move_ship(const orc_world* w, ship* s, int64_t mx, int64_t my, source* src,
                      double* reward, int32_t* done) {
     if (s->dest < 0) return E_NO_DEST; /* :276 */
     double r = 0.0;
@@ -185,6 +203,7 @@ static int move_ship(const orc_world* w, ship* s, int64_t mx, int64_t my, const 
     if (ground_at(w, (int32_t)nx, (int32_t)ny)) { /* :293-294 */
         r += P_GROUND;
     } else { /* :296-300, the ship moves even when it just ran out of fuel */
+        src->used |= 16; /* SE_USED_MOVED: fuel becomes an np.float64, the reward a float */
         s->x = (int32_t)nx;
         s->y = (int32_t)ny;
         s->fuel -= cost;
@@ -226,7 +245,7 @@ static int move_ship(const orc_world* w, ship* s, int64_t mx, int64_t my, const 
 
 /* step, :359-376, with the typed action [category, value] */
 static int step_typed(const orc_world* w, ship* s, int32_t type, int32_t a, int32_t b,
-                      const source* src, double* reward, int32_t* done) {
+                      source* src, double* reward, int32_t* done) {
     *reward = 0.0;
     *done = 0;
     if (w->P == 0) return E_NO_PORTS; /* :360 */
@@ -252,8 +271,10 @@ static int step_typed(const orc_world* w, ship* s, int32_t type, int32_t a, int3
         *reward = R_TAKE;
         return E_OK;
     }
-    case MOVE_SHIP:
-        return move_ship(w, s, a, b, src, reward, done);
+    case MOVE_SHIP: {
+        int e = move_ship(w, s, a, b, src, reward, done);
+        return (e == E_OK && src->need) ? E_NEED_DRAW : e;
+    }
     default:
         return E_BAD_CATEGORY; /* :373-374 */
     }
@@ -303,7 +324,7 @@ int orc_step_batch(const orc_world* w, int64_t n, int act_mode, const int32_t* a
     for (int64_t i = 0; i < n; ++i) {
         ship s;
         load(&s, i, x, y, fuel, cargo, origin, dest);
-        source src = {tape ? tape + i : NULL, seed, env_id_base + i, t};
+        source src = {tape ? tape + i : NULL, seed, env_id_base + i, t, 0, 0};
         int32_t ty = 0, a = 0, b = 0;
         int e;
         double r = 0.0;
@@ -325,6 +346,7 @@ int orc_step_batch(const orc_world* w, int64_t n, int act_mode, const int32_t* a
             r = 0.0;
             d = 0;
         }
+        if (tape) ((orc_tape*)tape)[i].pad = e == E_NEED_DRAW ? src.used : (e == E_OK ? src.used : 0);
         store(&s, i, x, y, fuel, cargo, origin, dest);
         reward[i] = r;
         done[i] = d;

@@ -19,6 +19,10 @@ SE_NONE = 255
 # per-env error classes (include/shipenv.h SE_ERR_*)
 ERR_OK, ERR_OOB, ERR_SAME_PORT, ERR_PORT_RANGE, ERR_NOT_AT_PORT = 0, 1, 2, 3, 4
 ERR_AMOUNT, ERR_NO_DEST, ERR_BAD_CATEGORY, ERR_NO_PORTS, ERR_BAD_INDEX = 5, 6, 7, 8, 9
+ERR_NEED_DRAW = 10
+
+# se_tape.used bits
+USED_FUEL_GATE, USED_LOSS_TYPE, USED_BETA, USED_ARRIVE, USED_MOVED = 1, 2, 4, 8, 16
 
 # every symbol include/shipenv.h declares
 EXPORTS = (
@@ -40,7 +44,7 @@ class ShipEnvError(RuntimeError):
 class SeState(C.Structure):
     _fields_ = [(name, C.c_void_p) for name in (
         "x", "y", "fuel", "cargo", "origin", "dest", "reward", "done", "err", "ep_return",
-        "ep_len", "done_recs", "done_count")]
+        "ep_len", "done_recs", "done_count", "reward64")]
 
 
 class SeDoneRec(C.Structure):

@@ -44,6 +44,10 @@ constexpr int kEnvsPerThread = 4; // one 4-byte / 16-byte lane access per field
 constexpr int kMaxBlocks = 2048;  // 256 CUs x 8; grid-stride beyond
 constexpr int kStepBlocks = 2048; // step kernel default cap (SHIPENV_STEP_BLOCKS overrides)
 
+// se_tape.used bits (replay): which of the reference's draws this step consumed
+constexpr uint32_t kUsedFuelGate = SE_USED_FUEL_GATE, kUsedLossType = SE_USED_LOSS_TYPE,
+                   kUsedBeta = SE_USED_BETA, kUsedArrive = SE_USED_ARRIVE, kUsedMoved = SE_USED_MOVED;
+
 // reference constants, shipping/environment.py:8-26
 constexpr double kFuelInit = 200.0;
 constexpr double kMaxCargo = 50.0;
@@ -143,16 +147,16 @@ template <>
 struct Draws<false> {
     Key key;
     uint32_t t;
-    // u_type from words 0,1 of slot LOSS; Beta(2,2) = median of three uniforms
-    // (words 2,3 of LOSS and 0..3 of BETA) — exact in distribution.
-    __device__ void loss(double& u_type, double& beta) const {
+    __device__ double loss_type() const {  // words 0,1 of slot LOSS
         const U4 a = draw(key, t, kSlotLoss);
-        u_type = u53(a.v[0], a.v[1]);
-        if (u_type >= 0.1 && u_type <= 0.9) {
-            const U4 b = draw(key, t, kSlotBeta);
-            const double u1 = u53(a.v[2], a.v[3]), u2 = u53(b.v[0], b.v[1]), u3 = u53(b.v[2], b.v[3]);
-            beta = fmax(fmin(u1, u2), fmin(fmax(u1, u2), u3));
-        }
+        return u53(a.v[0], a.v[1]);
+    }
+    // Beta(2,2) as the median of three uniforms (words 2,3 of LOSS and 0..3 of
+    // BETA) — exact in distribution, a fixed number of draws.
+    __device__ double beta() const {
+        const U4 a = draw(key, t, kSlotLoss), b = draw(key, t, kSlotBeta);
+        const double u1 = u53(a.v[2], a.v[3]), u2 = u53(b.v[0], b.v[1]), u3 = u53(b.v[2], b.v[3]);
+        return fmax(fmin(u1, u2), fmin(fmax(u1, u2), u3));
     }
     __device__ int arrive(int P, int origin) const {
         const U4 o = draw(key, t, kSlotArrive);
@@ -160,13 +164,13 @@ struct Draws<false> {
     }
 };
 
+// Replay: the variates the reference drew through `random`. A missing one (NaN,
+// or arrive_dest < 0) makes the step report SE_ERR_NEED_DRAW without effect.
 template <>
 struct Draws<true> {
     const se_tape* rec;
-    __device__ void loss(double& u_type, double& beta) const {
-        u_type = rec->u_type;
-        beta = rec->beta;
-    }
+    __device__ double loss_type() const { return rec->u_type; }
+    __device__ double beta() const { return rec->beta; }
     __device__ int arrive(int, int) const { return rec->arrive_dest; }
 };
 
@@ -195,7 +199,8 @@ __device__ __forceinline__ bool needs_gate(const LdsWorld& w, const Ship& s, int
 template <bool kUnitMoves, bool kReplay>
 __device__ __forceinline__ int env_step(const LdsWorld& w, Ship& s, int e_in, int type, int a, int b,
                                         double u_fuel, double u_gate,
-                                        const Draws<kReplay>& dr, double& reward, int& done) {
+                                        const Draws<kReplay>& dr, double& reward, int& done,
+                                        uint32_t& used) {
     // --- MOVE (_move_ship :273-339)
     const bool no_dest = s.dest == SE_NONE;                                      // :276
     const bool big = !kUnitMoves && (a < -256 || a > 256 || b < -256 || b > 256);  // surely OOB
@@ -240,22 +245,42 @@ __device__ __forceinline__ int env_step(const LdsWorld& w, Ship& s, int e_in, in
     const bool do_move = ok && type == 1;
 
     int cargo_m = s.cargo, origin_m = s.origin, dest_m = s.dest;
-    // :318-323 the gate random() <= cargo/50 (u_gate only meaningful for 0 < cargo < 50)
+    bool need = false;  // replay only: a variate the reference drew here is missing
+    used = do_move ? (kUsedFuelGate | (ground ? 0u : kUsedMoved)) : 0u;
+    if (kReplay) need = do_move && (u_fuel != u_fuel || u_gate != u_gate);
+    // :318-323 the gate random() <= cargo/50. Production skips the cargo-0 case (a
+    // firing gate then loses nothing, :180-181); replay keeps it, because the
+    // reference still draws the loss type there (:177) and replay tracks every draw.
+    // From cargo 50 on it always fires (random() < 1 <= cargo/50).
     const int ci = (s.cargo > 0 && s.cargo < 50) ? s.cargo : 0;
-    const bool fires = s.cargo >= 50 || (s.cargo > 0 && u_gate <= w.likelihood(ci));
+    const bool fires = s.cargo >= 50 || ((kReplay || s.cargo > 0) && u_gate <= w.likelihood(ci));
     if (do_move && fires) {  // _calculate_cargo_loss :169-200
-        double lt, beta = 0.0;
-        dr.loss(lt, beta);
+        used |= kUsedLossType;
+        const double lt = dr.loss_type();
+        const bool partial = cargo_m != 0 && lt >= 0.1 && lt <= 0.9;  // :180, :184, :188
+        double beta = 0.0;
+        if (partial) {
+            used |= kUsedBeta;
+            beta = dr.beta();
+        }
+        if (kReplay) need = need || lt != lt || (partial && beta != beta);
         const int loss = lt < 0.1 ? 0 : (lt > 0.9 ? cargo_m : (int)(beta * (double)cargo_m));
         cargo_m -= loss;
         rm += (double)(-3 * loss);
     }
     if (do_move && mx == px && my == py) {  // :325-337 arrival
+        used |= kUsedArrive;
         rm += (double)(2 * cargo_m);
         cargo_m = 0;
         origin_m = dest_m;
         dest_m = dr.arrive(w.P, origin_m);
+        if (kReplay) need = need || dest_m < 0;
         rm += 10.0;
+    }
+    if (kReplay && need) {  // ask the caller for the next variate; change nothing
+        reward = 0.0;
+        done = 0;
+        return SE_ERR_NEED_DRAW;
     }
 
     const bool take_fuel = ok && type == 3, take_cargo = ok && type == 4;
@@ -312,7 +337,7 @@ struct StepArgs {
     const int32_t* act;   // agent index (kTyped = false) or type (kTyped = true)
     const int32_t* act_a;
     const int32_t* act_b;
-    const se_tape* tape;
+    se_tape* tape;           // replay: variates in, used flags out
     se_done_rec* done_recs;  // this step's done list
     int32_t* done_count;     // this step's counter
     int32_t* next_count;     // zeroed for the next step
@@ -523,14 +548,17 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
             r = ug[j] + (double)va + (double)vb;
         } else
 #endif
+        uint32_t used = 0;
         if constexpr (kReplay) {
             const Draws<true> dr{A.tape + (live ? i : 0)};
-            e = env_step<false, true>(w, s, e, ty, va, vb, uf[j], ug[j], dr, r, d);
+            e = env_step<false, true>(w, s, e, ty, va, vb, uf[j], ug[j], dr, r, d, used);
+            if (live) A.tape[i].used = (int32_t)used;
         } else {
             const Draws<false> dr{key, A.t};
-            e = env_step<!kTyped, false>(w, s, e, ty, va, vb, uf[j], ug[j], dr, r, d);
+            e = env_step<!kTyped, false>(w, s, e, ty, va, vb, uf[j], ug[j], dr, r, d, used);
         }
         rw[j] = (float)r;  // one rounding of the reference's f64 reward
+        if (kReplay && live && S.reward64) S.reward64[i] = r;
         if (kAuto && live) {
             epr[j] += rw[j];
             epl[j] += 1;
@@ -943,7 +971,7 @@ int check_ready(se_env* env) {
 }
 
 int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const int32_t* a,
-                const int32_t* b, const se_tape* tape, void* stream) {
+                const int32_t* b, se_tape* tape, void* stream) {
     int rc = check_ready(env);
     if (rc) return rc;
     if (!act || (typed && (!a || !b)) || (replay && !tape))
@@ -1110,7 +1138,7 @@ int se_step_typed(se_env* env, const int32_t* type, const int32_t* a, const int3
 }
 
 int se_step_replay(se_env* env, const int32_t* type, const int32_t* a, const int32_t* b,
-                   const se_tape* tape, void* stream) {
+                   se_tape* tape, void* stream) {
     return launch_step(env, true, true, type, a, b, tape, stream);
 }
 

@@ -1,0 +1,133 @@
+"""One environment on the GPU behind shipping.Environment.
+
+The compat class keeps the reference's attributes on the host (agents read and
+assign them directly) and runs every state transition through the step kernel:
+se_step_replay on a one-env handle whose SoA buffers, action and tape all live
+in one 256-byte device block, so a step is one H2D copy, one launch and one D2H
+copy on the current stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import _native as N
+
+# byte offsets inside the I/O block (each field 16-byte aligned for se_bind)
+_X, _Y, _ORG, _DST, _DONE, _ERR = 0, 16, 32, 48, 64, 80
+_FUEL, _CARGO, _REW, _REW64 = 96, 112, 128, 144
+_TYPE, _A, _B, _TAPE = 160, 176, 192, 208
+_SIZE = 256
+_I32_MIN, _I32_MAX = -(2 ** 31), 2 ** 31 - 1
+
+
+@dataclass
+class StepResult:
+    x: int
+    y: int
+    fuel: float
+    cargo: int
+    origin: int  # -1 = None
+    dest: int  # -1 = None
+    reward: float  # the reference's f64 reward
+    done: bool
+    err: int
+    used: int  # SE_USED_* bits
+
+
+def _clamp32(v):
+    return _I32_MIN if v < _I32_MIN else (_I32_MAX if v > _I32_MAX else v)
+
+
+class DeviceStepper:
+    def __init__(self, water, port_x, port_y, port_fuel, port_cargo, device=None):
+        if not torch.cuda.is_available():
+            raise N.NativeLibraryError("shipping.Environment steps on a ROCm GPU; none is visible")
+        lib = N.lib()
+        self.dev = torch.device("cuda", torch.cuda.current_device()) if device is None \
+            else torch.device(device)
+        self.io = torch.zeros(_SIZE, dtype=torch.uint8, device=self.dev)
+        self.host = torch.zeros(_SIZE, dtype=torch.uint8).pin_memory()
+        self.h = self.host.numpy()
+        water = np.ascontiguousarray(water, np.uint8)
+        H, W = water.shape
+        self._h = C.c_void_p()
+        px, py, pf, pc = (np.ascontiguousarray(v, np.int32) for v in (port_x, port_y, port_fuel, port_cargo))
+        with torch.cuda.device(self.dev):
+            N.check(lib.se_create(C.byref(self._h), self.dev.index, 1, 0, H, W,
+                                  water.ctypes.data_as(C.c_void_p), len(px),
+                                  px.ctypes.data_as(C.c_void_p), py.ctypes.data_as(C.c_void_p),
+                                  pf.ctypes.data_as(C.c_void_p), pc.ctypes.data_as(C.c_void_p), 0, 0))
+        b = self.io.data_ptr()
+        self._state = N.SeState(b + _X, b + _Y, b + _FUEL, b + _CARGO, b + _ORG, b + _DST,
+                                b + _REW, b + _DONE, b + _ERR, None, None, None, None, b + _REW64)
+        N.check(lib.se_bind(self._h, C.byref(self._state)))
+        self._base = b
+        self._f64 = self.h.view(np.float64)
+        self._i32 = self.h.view(np.int32)
+
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def _put_state(self, x, y, fuel, cargo, origin, dest):
+        h = self.h
+        h[_X], h[_Y] = x, y
+        h[_ORG] = N.SE_NONE if origin is None else origin
+        h[_DST] = N.SE_NONE if dest is None else dest
+        self._f64[_FUEL // 8] = fuel
+        self._i32[_CARGO // 4] = cargo
+
+    def _get(self, err, used):
+        h = self.h
+        org, dst = int(h[_ORG]), int(h[_DST])
+        return StepResult(int(h[_X]), int(h[_Y]), float(self._f64[_FUEL // 8]),
+                          int(self._i32[_CARGO // 4]), -1 if org == N.SE_NONE else org,
+                          -1 if dst == N.SE_NONE else dst, float(self._f64[_REW64 // 8]),
+                          bool(h[_DONE]), err, used)
+
+    def set_world(self, water, port_x, port_y, port_fuel, port_cargo):
+        """Replace map and ports (a new handle: the map size may change)."""
+        self.close()
+        self.__init__(water, port_x, port_y, port_fuel, port_cargo, self.dev)
+
+    def step(self, x, y, fuel, cargo, origin, dest, act_type, a, b, tape):
+        """tape: (u_fuel, u_gate, u_type, beta, arrive_dest), NaN / -1 where not drawn."""
+        self._put_state(x, y, fuel, cargo, origin, dest)
+        i32 = self._i32
+        i32[_TYPE // 4], i32[_A // 4], i32[_B // 4] = act_type, _clamp32(a), _clamp32(b)
+        f = self._f64
+        t0 = _TAPE // 8
+        f[t0], f[t0 + 1], f[t0 + 2], f[t0 + 3] = tape[0], tape[1], tape[2], tape[3]
+        i32[_TAPE // 4 + 8], i32[_TAPE // 4 + 9] = tape[4], 0
+        self._f64[_REW64 // 8] = 0.0
+        self.io.copy_(self.host, non_blocking=True)
+        b_ = self._base
+        N.check(N.lib().se_step_replay(self._h, C.c_void_p(b_ + _TYPE), C.c_void_p(b_ + _A),
+                                       C.c_void_p(b_ + _B), C.c_void_p(b_ + _TAPE), self._stream()))
+        self.host.copy_(self.io)  # synchronises the stream
+        return self._get(int(self.h[_ERR].astype(np.int8)), int(i32[_TAPE // 4 + 9]))
+
+    def reset_to(self, origin, dest):
+        i32 = self._i32
+        i32[_TYPE // 4], i32[_A // 4] = origin, dest
+        self.io.copy_(self.host, non_blocking=True)
+        b_ = self._base
+        N.check(N.lib().se_reset_to(self._h, None, C.c_void_p(b_ + _TYPE), C.c_void_p(b_ + _A),
+                                    self._stream()))
+        self.host.copy_(self.io)
+        return self._get(0, 0)
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            torch.cuda.synchronize(self.dev)
+            N.lib().se_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass

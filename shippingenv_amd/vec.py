@@ -23,7 +23,7 @@ DEFAULT_PORTS = [[41, 40], [60, 22], [78, 29], [49, 72], [62, 72]]  # utils/cons
 
 TAPE_DTYPE = np.dtype(
     [("u_fuel", "<f8"), ("u_gate", "<f8"), ("u_type", "<f8"), ("beta", "<f8"),
-     ("arrive_dest", "<i4"), ("pad", "<i4")]
+     ("arrive_dest", "<i4"), ("used", "<i4")]
 )  # se_tape
 
 
@@ -107,7 +107,7 @@ class VecEnv:
                                   self.port_cargo.ctypes.data_as(C.c_void_p), self.seed, flags))
         self._state = N.SeState(*[t.data_ptr() for t in (
             self.x, self.y, self.fuel, self.cargo, self.origin, self.dest, self.reward,
-            self.done, self.err, self.ep_return, self.ep_len, self.done_recs, self.done_count)])
+            self.done, self.err, self.ep_return, self.ep_len, self.done_recs, self.done_count)] + [None])
         N.check(lib.se_bind(self._h, C.byref(self._state)))
         self._stats = torch.zeros(3, dtype=torch.float64, **kw)
 

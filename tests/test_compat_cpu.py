@@ -1,0 +1,57 @@
+"""Host logic of the drop-in shipping.Environment against the reference's own
+seeded traces, with the step kernel replaced by the oracle (no GPU here)."""
+import sys
+
+import pytest
+
+from compat_replay import load_script, replay
+
+
+@pytest.fixture()
+def oracle_backend(oracle_mod):
+    from shippingenv_amd.shipping import environment
+    from oracle_stepper import OracleStepper
+
+    environment._set_stepper_factory(OracleStepper)
+    yield
+    environment._set_stepper_factory(None)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_seeded_trace_matches_reference(oracle_backend, seed):
+    assert replay(load_script(seed)) > 600
+
+
+def test_dropin_package_resolves(monkeypatch):
+    import os
+
+    from conftest import ROOT
+
+    monkeypatch.syspath_prepend(os.path.join(ROOT, "shippingenv_amd", "dropin"))
+    for m in [m for m in sys.modules if m == "shipping" or m.startswith("shipping.")]:
+        monkeypatch.delitem(sys.modules, m)
+    import shipping
+    from shipping import Environment, ShipMove, environment
+
+    assert Environment is environment.Environment
+    assert environment.ActionType.MOVE_SHIP == 1 and ShipMove.EAST == (-1, 0)
+    import shipping.environment as se
+
+    assert se is environment
+
+
+def test_no_gpu_means_no_silent_fallback(monkeypatch):
+    from shippingenv_amd import _native
+    from shippingenv_amd.maps import BUILTIN_MAP
+    from shippingenv_amd.shipping import Environment, environment
+
+    environment._set_stepper_factory(None)
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    env = Environment(BUILTIN_MAP)
+    env.add_port([41, 40])
+    env.add_port([60, 22])
+    with pytest.raises(_native.NativeLibraryError):
+        env.reset()
