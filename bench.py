@@ -19,12 +19,10 @@ from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import sys
 import time
 
-import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -61,21 +59,18 @@ def parse():
 
 
 class Dist:
+    """torch.distributed glue (shippingenv_amd.dist): barrier, max over ranks, stats all-reduce."""
+
     def __init__(self, want):
-        self.world = int(os.environ.get("WORLD_SIZE", "1"))
-        self.rank = int(os.environ.get("RANK", "0"))
-        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        from shippingenv_amd import dist as D
+
+        self.D = D
+        self.rank, self.world, self.local, self.dev = D.init_from_env()
         if self.world != want:
             raise SystemExit(f"--gpus {want} but WORLD_SIZE={self.world}")
-        torch.cuda.set_device(self.local)
-        self.dev = torch.device("cuda", self.local)
-        self.pg = None
-        if self.world > 1:
-            import torch.distributed as dist
+        import torch.distributed as tdist
 
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("nccl", device_id=self.dev)
-            self.pg = dist
+        self.pg = tdist if self.world > 1 else None
 
     def barrier(self):
         if self.pg:
@@ -87,11 +82,6 @@ class Dist:
         t = torch.tensor([v], dtype=torch.float64, device=self.dev)
         self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
         return float(t.item())
-
-    def sum_(self, t):
-        if self.pg:
-            self.pg.all_reduce(t)
-        return t
 
     def close(self):
         if self.pg:
@@ -105,32 +95,28 @@ def make_actions(env, steps):
     return acts
 
 
-def timed_loop(env, acts, first, steps, dist):
-    """Back-to-back launches; barrier + synchronize on both sides; max over ranks."""
+def timed_loop(env, acts, first, steps, dist, reduce_every=0):
+    """K back-to-back launches bracketed by barrier + synchronize on both sides; wall
+    time is the max over ranks. HIP events recorded on the launch stream around the
+    same region give the GPU time per launch (roofline.kernel_ms)."""
+    stream = torch.cuda.current_stream(env.device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    stats = torch.zeros(3, dtype=torch.float64, device=env.device)
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    e0.record(stream)
     for k in range(steps):
         env.step(acts[first + k])
+        if reduce_every and (k + 1) % reduce_every == 0:
+            # episode-return aggregation over the GPUs (RCCL all-reduce of 3 doubles)
+            stats.copy_(env.episode_stats())
+            dist.D.reduce_episode_stats(stats)
+    e1.record(stream)
     torch.cuda.synchronize()
     dist.barrier()
-    return dist.max(time.perf_counter() - t0)
-
-
-def kernel_time(env, acts, first, steps):
-    """Average step-kernel duration from HIP events recorded around each launch on
-    the stream the kernel is launched on (torch's current stream)."""
-    stream = torch.cuda.current_stream(env.device)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps)]
-    torch.cuda.synchronize()
-    for k in range(steps):
-        ev[k][0].record(stream)
-        env.step(acts[first + (k % (acts.shape[0] - first))])
-        ev[k][1].record(stream)
-    torch.cuda.synchronize()
-    ms = np.array([a.elapsed_time(b) for a, b in ev])
-    return float(ms.mean()), float(np.median(ms))
+    wall = dist.max(time.perf_counter() - t0)
+    return wall, e0.elapsed_time(e1) / steps
 
 
 def run_config(n, ports, auto, args, dist, label):
@@ -147,18 +133,17 @@ def run_config(n, ports, auto, args, dist, label):
     torch.cuda.synchronize()
     if auto:
         env.clear_stats()
-    elapsed = timed_loop(env, acts, args.warmup, args.steps, dist)
+    wall, k_ms = timed_loop(env, acts, args.warmup, args.steps, dist,
+                            reduce_every=100 if auto else 0)
     stats = None
     if auto:
-        # episode-return aggregation across GPUs: one RCCL all-reduce of 3 doubles
         s = env.episode_stats().clone()
-        dist.sum_(s)
+        dist.D.reduce_episode_stats(s)
         stats = s.cpu().tolist()
-    k_ms_mean, k_ms_med = kernel_time(env, acts, args.warmup, min(args.steps, 500))
     env.close()
     del acts
     torch.cuda.empty_cache()
-    return elapsed, k_ms_mean, k_ms_med, stats
+    return wall, k_ms, stats
 
 
 def roofline(bytes_per_step, n, k_ms, canonical):
@@ -226,7 +211,7 @@ def main():
     from shippingenv_amd.vec import random_water_ports
 
     n = args.n
-    el3, k3, k3_med, _ = run_config(n, None, False, args, dist, "config3")
+    el3, k3, _ = run_config(n, None, False, args, dist, "config3")
     value = n * dist.world * args.steps / el3
     out = {
         "metric": "env-steps/sec at N=2^20 parallel envs per GPU (config 3: full step, 5 default ports)",
@@ -250,7 +235,6 @@ def main():
         },
         "roofline": roofline(BYTES_STEP, n, k3, CANONICAL_STEP),
     }
-    out["roofline"]["kernel_ms_median"] = round(k3_med, 5)
     traffic, src = pmc_traffic()
     if traffic:
         out["roofline"]["traffic"] = traffic
@@ -258,10 +242,11 @@ def main():
 
     if not args.no_config4:
         ports64 = random_water_ports(builtin_water(), 64, seed=3)
-        el4, k4, _, stats = run_config(n, ports64, True, args, dist, "config4")
+        el4, k4, stats = run_config(n, ports64, True, args, dist, "config4")
         out["config4"] = {
             "workload": "BASELINE configs[3]: N=2^20 envs/GPU, 64 random ports, auto-reset, "
-                        "ballot-compacted done list, per-block return reduction, RCCL all-reduce",
+                        "ballot-compacted done list, per-block return reduction, RCCL all-reduce "
+                        "of the stats every 100 steps (inside the timed region)",
             "value": round(n * dist.world * args.steps / el4, 1),
             "ms_per_step": round(el4 / args.steps * 1e3, 5),
             "roofline": roofline(BYTES_STEP_AUTO, n, k4, CANONICAL_STEP_AUTO),
@@ -273,7 +258,7 @@ def main():
     if args.large_n and dist.world == 1:
         small = argparse.Namespace(**vars(args))
         small.steps, small.warmup = 100, 5
-        el, k, _, _ = run_config(args.large_n, None, False, small, dist, "large-n")
+        el, k, _ = run_config(args.large_n, None, False, small, dist, "large-n")
         out["large_n"] = {
             "envs": args.large_n,
             "note": "working set beyond the 256 MiB Infinity Cache: traffic reaches HBM",

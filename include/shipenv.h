@@ -88,8 +88,9 @@ typedef struct se_state {
     int8_t* err;        /* SE_ERR_* per env */
     float* ep_return;   /* running episode return (auto-reset) */
     int32_t* ep_len;    /* running episode length in step calls (auto-reset) */
-    struct se_done_rec* done_recs; /* auto-reset done list, capacity 2*n records */
-    int32_t* done_count;           /* auto-reset done counters, 3 entries, zeroed by se_bind */
+    struct se_done_rec* done_recs; /* auto-reset done lists: 2 * segments * seg_stride records
+                                      (se_done_layout), double-buffered by step parity */
+    int32_t* done_count;           /* auto-reset per-segment counts: 2 * segments entries */
     double* reward64;              /* optional (NULL): the reference's f64 reward, unrounded */
 } se_state;
 
@@ -169,10 +170,17 @@ int se_gen_actions(se_env* env, int32_t* actions, uint32_t t, void* stream);
 int se_episode_stats(se_env* env, double* out, void* stream);
 int se_clear_stats(se_env* env, void* stream);
 
-/* Where the most recent se_step (auto-reset) wrote its done list: records
- * done_recs[rec_offset ...] and their number in done_count[count_index]. The
- * list stays intact while the following step runs; the step after it reuses it. */
-int se_done_list(se_env* env, int64_t* rec_offset, int32_t* count_index);
+/* Done lists (auto-reset). Every workgroup of the step kernel writes the envs it
+ * finished, in env order, into its own segment; no global atomics, so the list is
+ * deterministic. se_done_layout gives the segment stride and count the done_recs /
+ * done_count buffers must be sized for (2 * segments * seg_stride records,
+ * 2 * segments counts). se_done_list gives where the most recent step wrote
+ * (record offset of its buffer, offset of its counts); that list stays intact
+ * while the following step runs. se_done_compact copies it contiguously
+ * (out: up to n records, out_count: 1 int) on the stream. */
+int se_done_layout(se_env* env, int64_t* seg_stride, int32_t* segments);
+int se_done_list(se_env* env, int64_t* rec_offset, int64_t* count_offset);
+int se_done_compact(se_env* env, se_done_rec* out, int32_t* out_count, void* stream);
 
 /* Step counter / reset epoch (checkpoint-resume; shard replay). */
 int se_get_counters(se_env* env, uint64_t* step, uint64_t* epoch);

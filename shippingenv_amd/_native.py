@@ -28,7 +28,8 @@ USED_FUEL_GATE, USED_LOSS_TYPE, USED_BETA, USED_ARRIVE, USED_MOVED = 1, 2, 4, 8,
 EXPORTS = (
     "se_create", "se_set_ports", "se_bind", "se_reset", "se_reset_to", "se_step",
     "se_step_typed", "se_step_replay", "se_observe", "se_valid_mask", "se_gen_actions",
-    "se_episode_stats", "se_clear_stats", "se_done_list", "se_get_counters", "se_set_counters",
+    "se_episode_stats", "se_clear_stats", "se_done_layout", "se_done_list", "se_done_compact",
+    "se_get_counters", "se_set_counters",
     "se_destroy", "se_last_error", "se_abi_version",
 )
 
@@ -71,7 +72,9 @@ def _declare(lib):
         "se_gen_actions": [P, P, u32, P],
         "se_episode_stats": [P, P, P],
         "se_clear_stats": [P, P],
-        "se_done_list": [P, C.POINTER(i64), C.POINTER(i32)],
+        "se_done_layout": [P, C.POINTER(i64), C.POINTER(i32)],
+        "se_done_list": [P, C.POINTER(i64), C.POINTER(i64)],
+        "se_done_compact": [P, P, P, P],
         "se_get_counters": [P, C.POINTER(u64), C.POINTER(u64)],
         "se_set_counters": [P, u64, u64],
         "se_destroy": [P],

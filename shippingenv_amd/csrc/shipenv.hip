@@ -338,9 +338,10 @@ struct StepArgs {
     const int32_t* act_a;
     const int32_t* act_b;
     se_tape* tape;           // replay: variates in, used flags out
-    se_done_rec* done_recs;  // this step's done list
-    int32_t* done_count;     // this step's counter
-    int32_t* next_count;     // zeroed for the next step
+    se_done_rec* done_recs;  // this step's done list: per-block segments of `seg` records
+    int32_t* done_count;     // this step's per-block record counts
+    int64_t seg;             // segment stride (records) of one workgroup
+    int64_t iters;           // groups per thread (each workgroup owns iters * 256 groups)
     double* slab;            // per-block {sum_ret, n_eps, sum_len, pad}
 };
 
@@ -462,9 +463,17 @@ __device__ __forceinline__ double u32(uint32_t w) { return (double)w * (1.0 / 42
 // Step the 4 envs of one group (base = 4k). u_fuel / u_gate of env 4k+j are word j
 // of the quad's FUEL / GATE Philox blocks; the GATE block is only drawn when some
 // env of the group can observe its gate.
+// Finished episodes of one group (auto-reset): bit j of `mask` for env base+j.
+struct Finished {
+    uint32_t mask = 0;
+    float ret[4];
+    int32_t len[4];
+};
+
 template <bool kTyped, bool kReplay, bool kAuto, bool kFull>
 __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
-                                           Group<kTyped, kAuto>& G, int64_t base, BlockStats& bs) {
+                                           Group<kTyped, kAuto>& G, int64_t base, BlockStats& bs,
+                                           Finished& F) {
     const se_state& S = A.st;
     const int64_t n = A.n;
     int32_t act[4] = {G.a0, G.a1, G.a2, G.a3};
@@ -583,22 +592,11 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
     }
 
     if constexpr (kAuto) {
-        // done-list compaction: wave-exclusive prefix of per-lane counts (0..4)
-        // from three ballots, one atomic per wave.
-        const int ndone = __popc(fin);
-        const uint64_t b0 = __ballot(ndone & 1), b1 = __ballot(ndone & 2), b2 = __ballot(ndone & 4);
-        const uint32_t total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
-        if (total) {
-            const uint32_t below = count_below(b0) + 2 * count_below(b1) + 4 * count_below(b2);
-            const uint64_t active = __ballot(1);
-            const uint32_t leader = (uint32_t)__ffsll((long long)active) - 1;
-            int32_t slot = 0;
-            if (lane_id() == leader) slot = atomicAdd(A.done_count, (int32_t)total);
-            slot = __shfl(slot, (int)leader) + (int32_t)below;
-            const int32_t t = (int32_t)A.t;
+        F.mask = fin;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if ((fin >> j) & 1u) A.done_recs[slot++] = se_done_rec{(int32_t)(base + j), epr[j], epl[j], t};
+        for (int j = 0; j < 4; ++j) {
+            F.ret[j] = epr[j];
+            F.len[j] = epl[j];
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -619,35 +617,76 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
     st4u8<kFull>(reinterpret_cast<uint8_t*>(S.err), base, n, ee);
 }
 
-// One thread steps 4 consecutive envs per grid-stride iteration; a full group's
-// fields are single 4- or 16-byte lane accesses. The first group's loads are
-// issued before the world is staged into LDS so the staging hides under them.
-// The last n % 4 envs (if any) are stepped by thread 0 of block 0.
+// Done-list compaction of one grid-stride iteration (auto-reset), no global
+// atomics: a wave-exclusive prefix of the per-lane counts (0..4) from three
+// ballots, a block prefix over the 4 wave totals in LDS, and the records go to
+// this workgroup's own segment of the list in env order (deterministic).
+// All threads of the block call it (it holds two barriers).
+__device__ __forceinline__ void block_compact(const StepArgs& A, const Finished& F, int64_t base,
+                                              int32_t* wtot, int32_t& running, bool last) {
+    const int nd = __popc(F.mask);
+    const uint64_t b0 = __ballot(nd & 1), b1 = __ballot(nd & 2), b2 = __ballot(nd & 4);
+    const uint32_t wave_total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) wtot[wave] = (int32_t)wave_total;
+    if (!__syncthreads_or(nd)) return;  // nothing finished in the block: no second barrier
+    int32_t before = 0, block_total = 0;
+#pragma unroll
+    for (int k = 0; k < kBlock / 64; ++k) {
+        const int32_t v = wtot[k];
+        before += k < wave ? v : 0;
+        block_total += v;
+    }
+    if (nd) {
+        int64_t slot = (int64_t)blockIdx.x * A.seg + running + before +
+                       (int32_t)(count_below(b0) + 2 * count_below(b1) + 4 * count_below(b2));
+        const int32_t t = (int32_t)A.t;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if ((F.mask >> j) & 1u) A.done_recs[slot++] = se_done_rec{(int32_t)(base + j), F.ret[j], F.len[j], t};
+    }
+    running += block_total;
+    if (!last) __syncthreads();  // wtot is rewritten by the next iteration
+}
+
+// Workgroup b owns the contiguous groups [b*iters*256, (b+1)*iters*256) (a group is
+// 4 consecutive envs, one thread per group per iteration), so its done-list
+// segment follows env order and the concatenated segments are globally sorted.
+// A full group's fields are single 4- or 16-byte lane accesses; the one partial
+// group at the end (n % 4 envs) is stepped in place by its owner with guarded
+// scalar accesses. The first group's loads are issued before the world is staged
+// into LDS so the staging hides under them; each iteration loads the next group
+// before storing the current one. The trip count is uniform over the block (the
+// auto-reset compaction holds barriers).
 template <bool kTyped, bool kReplay, bool kAuto>
 __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs A) {
     extern __shared__ uint32_t lds[];
     __shared__ double red[kBlock / 64][3];
-    const int64_t full = A.n >> 2;
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    __shared__ int32_t wtot[kBlock / 64];
+    const int64_t full = A.n >> 2, groups = (A.n + 3) >> 2;
+    const int64_t first = (int64_t)blockIdx.x * A.iters * kBlock + threadIdx.x;
 
     Group<kTyped, kAuto> G;
-    if (g < full) G.template load<true>(A, g * 4);
+    if (first < full) G.template load<true>(A, first * 4);
     const LdsWorld w = stage_world(A.world, A.dims, lds);
-    if (kAuto && blockIdx.x == 0 && threadIdx.x == 0) *A.next_count = 0;
 
     BlockStats bs;
-    while (g < full) {
-        step_group<kTyped, kReplay, kAuto, true>(A, w, G, g * 4, bs);
-        g += stride;
-        if (g < full) G.template load<true>(A, g * 4);
-    }
-    if ((A.n & 3) && blockIdx.x == 0 && threadIdx.x == 0) {
-        G.template load<false>(A, full * 4);
-        step_group<kTyped, kReplay, kAuto, false>(A, w, G, full * 4, bs);
+    int32_t running = 0;  // this block's done records so far (block-uniform)
+    for (int64_t k = 0; k < A.iters; ++k) {
+        const int64_t g = first + k * kBlock;
+        Finished F;
+        if (g < full) {
+            step_group<kTyped, kReplay, kAuto, true>(A, w, G, g * 4, bs, F);
+            if (k + 1 < A.iters && g + kBlock < full) G.template load<true>(A, (g + kBlock) * 4);
+        } else if (g < groups) {  // the partial last group
+            G.template load<false>(A, g * 4);
+            step_group<kTyped, kReplay, kAuto, false>(A, w, G, g * 4, bs, F);
+        }
+        if constexpr (kAuto) block_compact(A, F, g * 4, wtot, running, k + 1 == A.iters);
     }
 
     if (kAuto) {
+        if (threadIdx.x == 0) A.done_count[blockIdx.x] = running;
         // per-block statistics: fixed-order wave butterfly, then waves in order
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
@@ -677,6 +716,26 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs A) {
             }
         }
     }
+}
+
+// Contiguous copy of the last step's per-block done lists (se_done_compact): block
+// b sums the counts before it (grid <= 2048 entries) and copies its segment.
+__global__ __launch_bounds__(kBlock) void done_compact_kernel(const se_done_rec* __restrict__ recs,
+                                                              const int32_t* __restrict__ counts,
+                                                              int64_t seg, se_done_rec* __restrict__ out,
+                                                              int32_t* __restrict__ out_count) {
+    __shared__ int32_t part[kBlock];
+    int32_t acc = 0;
+    for (int i = threadIdx.x; i < (int)blockIdx.x; i += kBlock) acc += counts[i];
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    for (int off = kBlock / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) part[threadIdx.x] += part[threadIdx.x + off];
+        __syncthreads();
+    }
+    const int32_t start = part[0], cnt = counts[blockIdx.x];
+    for (int i = threadIdx.x; i < cnt; i += kBlock) out[start + i] = recs[(int64_t)blockIdx.x * seg + i];
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *out_count = start + cnt;
 }
 
 // ------------------------------------------------------------------ reset kernel
@@ -858,6 +917,8 @@ struct se_env {
     uint64_t step_t = 0, epoch = 0;
     std::vector<uint8_t> water;  // H*W, 0 = ground
     uint32_t* d_world = nullptr;
+    int64_t seg = 0;    // done-list segment stride (records per workgroup)
+    int64_t iters = 1;  // groups per thread of the step kernel
     int world_cap = 0;  // words allocated
     se_state st{};
     bool bound = false;
@@ -993,13 +1054,15 @@ int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const 
     A.act_a = a;
     A.act_b = b;
     A.tape = tape;
-    // records double-buffered, counters over three slots: the list of step t-1
-    // stays readable while step t runs (step t zeroes the counter of step t+1).
+    // done lists double-buffered by step parity: the list of step t-1 stays
+    // readable while step t runs; every block rewrites its own count each step.
     if (autoreset) {
-        A.done_recs = env->st.done_recs + (size_t)(env->step_t & 1u) * (size_t)env->n;
-        A.done_count = env->st.done_count + (int)(env->step_t % 3u);
-        A.next_count = env->st.done_count + (int)((env->step_t + 1u) % 3u);
+        const size_t par = (size_t)(env->step_t & 1u);
+        A.done_recs = env->st.done_recs + par * (size_t)env->grid * (size_t)env->seg;
+        A.done_count = env->st.done_count + par * (size_t)env->grid;
     }
+    A.seg = env->seg;
+    A.iters = env->iters;
     A.slab = env->d_slab;
     const hipStream_t s = (hipStream_t)stream;
     const size_t lds = lds_bytes(env);
@@ -1056,7 +1119,14 @@ int se_create(se_env** out, int device, int64_t n, int64_t env_id_base, int32_t 
         se_destroy(env);
         return rc;
     }
-    env->grid = grid_for((n + kEnvsPerThread - 1) / kEnvsPerThread, step_block_cap());
+    {
+        // workgroup b owns iters * 256 consecutive groups of 4 envs
+        const int64_t groups = (n + kEnvsPerThread - 1) / kEnvsPerThread;
+        const int64_t cap = step_block_cap();
+        env->iters = groups > 0 ? (groups + cap * kBlock - 1) / (cap * kBlock) : 1;
+        env->grid = (int)(groups > 0 ? (groups + env->iters * kBlock - 1) / (env->iters * kBlock) : 1);
+        env->seg = env->iters * kBlock * kEnvsPerThread;
+    }
     hipError_t e = hipMalloc(&env->d_slab, (size_t)env->grid * 4 * sizeof(double));
     if (e == hipSuccess) e = hipMemset(env->d_slab, 0, (size_t)env->grid * 4 * sizeof(double));
     if (e != hipSuccess) {
@@ -1091,7 +1161,7 @@ int se_bind(se_env* env, const se_state* st) {
         if (!aligned16(st->ep_return) || !aligned16(st->ep_len) || !aligned16(st->done_recs))
             return fail(SE_EINVAL, "state buffers must be 16-byte aligned");
         DeviceGuard g(env->device);
-        HIP_TRY(hipMemset(st->done_count, 0, 3 * sizeof(int32_t)));
+        HIP_TRY(hipMemset(st->done_count, 0, 2 * (size_t)env->grid * sizeof(int32_t)));
     }
     env->st = *st;
     env->bound = true;
@@ -1200,13 +1270,32 @@ int se_clear_stats(se_env* env, void* stream) {
     return SE_OK;
 }
 
-int se_done_list(se_env* env, int64_t* rec_offset, int32_t* count_index) {
-    if (!env || !rec_offset || !count_index) return fail(SE_EINVAL, "null argument");
+int se_done_layout(se_env* env, int64_t* seg_stride, int32_t* segments) {
+    if (!env) return fail(SE_EINVAL, "null env");
+    if (seg_stride) *seg_stride = env->seg;
+    if (segments) *segments = env->grid;
+    return SE_OK;
+}
+
+int se_done_list(se_env* env, int64_t* rec_offset, int64_t* count_offset) {
+    if (!env || !rec_offset || !count_offset) return fail(SE_EINVAL, "null argument");
     if (!(env->flags & SE_FLAG_AUTO_RESET)) return fail(SE_ESTATE, "no done list without auto-reset");
     if (env->step_t == 0) return fail(SE_ESTATE, "no step has run");
-    const uint64_t t = env->step_t - 1;
-    *rec_offset = (int64_t)(t & 1u) * env->n;
-    *count_index = (int32_t)(t % 3u);
+    const int64_t par = (int64_t)((env->step_t - 1) & 1u);
+    *rec_offset = par * (int64_t)env->grid * env->seg;
+    *count_offset = par * (int64_t)env->grid;
+    return SE_OK;
+}
+
+int se_done_compact(se_env* env, se_done_rec* out, int32_t* out_count, void* stream) {
+    int64_t ro = 0, co = 0;
+    int rc = se_done_list(env, &ro, &co);
+    if (rc) return rc;
+    if (!out || !out_count) return fail(SE_EINVAL, "null output");
+    DeviceGuard g(env->device);
+    done_compact_kernel<<<env->grid, kBlock, 0, (hipStream_t)stream>>>(
+        env->st.done_recs + ro, env->st.done_count + co, env->seg, out, out_count);
+    HIP_TRY(hipGetLastError());
     return SE_OK;
 }
 
@@ -1221,7 +1310,8 @@ int se_set_counters(se_env* env, uint64_t step, uint64_t epoch) {
     if (!env) return fail(SE_EINVAL, "null env");
     DeviceGuard g(env->device);
     HIP_TRY(hipDeviceSynchronize());
-    if (env->bound && env->st.done_count) HIP_TRY(hipMemset(env->st.done_count, 0, 3 * sizeof(int32_t)));
+    if (env->bound && env->st.done_count)
+        HIP_TRY(hipMemset(env->st.done_count, 0, 2 * (size_t)env->grid * sizeof(int32_t)));
     env->step_t = step;
     env->epoch = epoch;
     return SE_OK;

@@ -91,11 +91,6 @@ class VecEnv:
         self.err = torch.zeros(n, dtype=torch.int8, **kw)
         self.ep_return = torch.zeros(n, dtype=torch.float32, **kw)
         self.ep_len = torch.zeros(n, dtype=torch.int32, **kw)
-        # done list (auto-reset): 2n records {env, ep_return bits, ep_len, step} + 3 counters
-        nrec = 2 * n if self.auto_reset else 0
-        self.done_recs = torch.zeros((max(nrec, 1), 4), dtype=torch.int32, **kw)
-        self.done_count = torch.zeros(4, dtype=torch.int32, **kw)
-
         self._h = C.c_void_p()
         flags = N.SE_FLAG_AUTO_RESET if self.auto_reset else 0
         with torch.cuda.device(self.device):
@@ -105,6 +100,15 @@ class VecEnv:
                                   self.port_y.ctypes.data_as(C.c_void_p),
                                   self.port_fuel.ctypes.data_as(C.c_void_p),
                                   self.port_cargo.ctypes.data_as(C.c_void_p), self.seed, flags))
+        # done lists (auto-reset): per-workgroup segments, double-buffered
+        # (include/shipenv.h se_done_layout); records are {env, ep_return bits, ep_len, step}
+        seg, nseg = C.c_int64(), C.c_int32()
+        N.check(lib.se_done_layout(self._h, C.byref(seg), C.byref(nseg)))
+        self.done_seg, self.done_segments = seg.value, nseg.value
+        nrec = 2 * self.done_seg * self.done_segments if self.auto_reset else 1
+        self.done_recs = torch.zeros((nrec, 4), dtype=torch.int32, **kw)
+        self.done_count = torch.zeros(max(2 * self.done_segments, 4), dtype=torch.int32, **kw)
+        self._done_out = None
         self._state = N.SeState(*[t.data_ptr() for t in (
             self.x, self.y, self.fuel, self.cargo, self.origin, self.dest, self.reward,
             self.done, self.err, self.ep_return, self.ep_len, self.done_recs, self.done_count)] + [None])
@@ -214,11 +218,15 @@ class VecEnv:
         N.check(N.lib().se_clear_stats(self._h, self._stream()))
 
     def done_list(self):
-        """Episodes finished by the last step (auto-reset): (env, ep_return, ep_len, step)."""
-        off, idx = C.c_int64(), C.c_int32()
-        N.check(N.lib().se_done_list(self._h, C.byref(off), C.byref(idx)))
-        k = int(self.done_count[idx.value].item())
-        raw = self.done_recs[off.value: off.value + k].clone()
+        """Episodes finished by the last step (auto-reset), in env order:
+        (env, ep_return, ep_len, step) tensors."""
+        if self._done_out is None:
+            self._done_out = torch.empty((self.n + 4, 4), dtype=torch.int32, device=self.device)
+            self._done_cnt = torch.empty(1, dtype=torch.int32, device=self.device)
+        N.check(N.lib().se_done_compact(self._h, _ptr(self._done_out), _ptr(self._done_cnt),
+                                        self._stream()))
+        k = int(self._done_cnt.item())
+        raw = self._done_out[:k].clone()
         return raw[:, 0], raw[:, 1].view(torch.float32), raw[:, 2], raw[:, 3]
 
     @property

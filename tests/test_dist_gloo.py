@@ -1,0 +1,91 @@
+"""The N>1 path on CPU: two gloo ranks each step their shard of global env ids
+(the oracle stands in for the kernel here) and all-reduce the episode stats;
+the result equals one process stepping all ids. Ports and seeds as config 4."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+N, T, SEED = 4096, 300, 77
+
+
+def _world_setup(water):
+    from shippingenv_amd.vec import draw_port_stocks, random_water_ports
+
+    ports = random_water_ports(water, 64, seed=3)
+    pf, pc = draw_port_stocks(64, SEED)
+    return ports, pf, pc
+
+
+def _run_shard(first, count, water):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+
+    ports, pf, pc = _world_setup(water)
+    world = O.OracleWorld(water, [p[0] for p in ports], [p[1] for p in ports], pf, pc)
+    st = O.OracleState(count)
+    O.reset(world, st, seed=SEED, env_id_base=first, epoch=0)
+    stats = np.zeros(3)
+    for t in range(T):
+        acts = O.gen_actions(count, 64, SEED, first, t)
+        O.step_autoreset(world, st, acts, seed=SEED, env_id_base=first, t=t, stats=stats)
+    return stats, st
+
+
+def _worker(rank, world_size, port, water, out):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world_size), LOCAL_RANK=str(rank))
+    from shippingenv_amd import dist as D
+
+    r, w, _, dev = D.init_from_env(backend="gloo")
+    assert (r, w) == (rank, world_size)
+    first, count = D.shard_bounds(N, w, r)
+    stats, st = _run_shard(first, count, water)
+    t = torch.tensor(stats, dtype=torch.float64)
+    D.reduce_episode_stats(t)
+    out[rank] = (t.tolist(), first, st.x.tolist()[:64], st.fuel.tolist()[:64])
+    torch.distributed.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_rank_gloo_matches_single_process(water):
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    mp.start_processes(_worker, args=(2, _free_port(), water, out), nprocs=2, join=True,
+                       start_method="spawn")
+    whole, st_all = _run_shard(0, N, water)
+    for rank in range(2):
+        red, first, x, fuel = out[rank]
+        assert red[1] == whole[1] and red[2] == whole[2]  # episodes, lengths: exact
+        np.testing.assert_allclose(red[0], whole[0], rtol=1e-12)  # f64 sum order differs
+        # the shard's envs are the same global ids as in the single-process run
+        np.testing.assert_array_equal(x, st_all.x[first:first + 64])
+        np.testing.assert_array_equal(np.asarray(fuel).view(np.int64),
+                                      st_all.fuel[first:first + 64].view(np.int64))
+    assert whole[1] > 0
+
+
+def test_shard_bounds_rules():
+    from shippingenv_amd.dist import shard_bounds
+
+    assert shard_bounds(1 << 20, 8, 3) == (3 << 17, 1 << 17)
+    with pytest.raises(ValueError):
+        shard_bounds(4096 + 4, 2, 0)

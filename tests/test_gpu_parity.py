@@ -219,8 +219,8 @@ def test_config4_autoreset_64_ports_vs_oracle(oracle_mod, water):
         np.testing.assert_array_equal(env.done.cpu().numpy().astype(np.int32), st.done)
         ids, ret, length, step = env.done_list()
         want = np.nonzero(st.done)[0]
-        order = np.argsort(ids.cpu().numpy())
-        np.testing.assert_array_equal(ids.cpu().numpy()[order], want)
+        # per-workgroup segments in env order: the list is deterministic and sorted
+        np.testing.assert_array_equal(ids.cpu().numpy(), want)
         assert (step.cpu().numpy() == t).all()
         total_done += len(want)
         if t % 60 == 0:
@@ -332,3 +332,32 @@ def test_shard_invariance(oracle_mod):
         np.testing.assert_array_equal(a[f][k:k + m], b[f], err_msg=f)
     big.close()
     part.close()
+
+
+def test_done_list_full_size_segments():
+    """N = 2^20 + 3 (tail group) with auto-reset: the compacted done list of every
+    step lists exactly the envs that reported done, in env order, with the
+    returns / lengths the stats slab accumulates."""
+    from shippingenv_amd.vec import random_water_ports
+
+    from conftest import golden_water
+
+    n = (1 << 20) + 3
+    env = VecEnv(n, seed=11, ports=random_water_ports(golden_water(), 64, seed=3), auto_reset=True)
+    env.reset()
+    tot_ret, tot_eps, tot_len = 0.0, 0, 0
+    for t in range(320):
+        env.step(env.gen_actions(t))
+        if t >= 180:
+            ids, ret, length, step = env.done_list()
+            want = torch.nonzero(env.done).flatten().to(torch.int32)
+            assert torch.equal(ids, want)
+            assert bool((step == t).all())
+            tot_ret += float(ret.double().sum())
+            tot_eps += len(ids)
+            tot_len += int(length.long().sum())
+    assert tot_eps > 1000
+    got = env.episode_stats().cpu().numpy()
+    assert got[1] == tot_eps and got[2] == tot_len
+    np.testing.assert_allclose(got[0], tot_ret, rtol=1e-9)
+    env.close()
