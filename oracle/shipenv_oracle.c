@@ -42,9 +42,12 @@ enum {
 /* tape.used bits (include/shipenv.h SE_USED_*) */
 enum { U_FUEL_GATE = 1, U_LOSS_TYPE = 2, U_BETA = 4, U_ARRIVE = 8 };
 
-/* Philox counter slots (DESIGN.md "RNG contract") */
-enum { SLOT_FUEL = 0, SLOT_LOSS = 1, SLOT_BETA = 2, SLOT_ARRIVE = 3, SLOT_RESET = 4,
-       SLOT_EXPLICIT_RESET = 5, SLOT_ACTION = 6, SLOT_GATE = 7 };
+/* Philox counter slots (DESIGN.md "RNG contract", v4). Every draw of a step is a
+ * quad block: counter (k, t, slot) for envs 4k..4k+3, word j for env 4k+j. The
+ * explicit reset and the synthetic agent draw one block per env. */
+enum { SLOT_FUEL = 0, SLOT_LOSS = 1, SLOT_BETA1 = 2, SLOT_ARRIVE = 3, SLOT_RESET = 4,
+       SLOT_EXPLICIT_RESET = 5, SLOT_ACTION = 6, SLOT_GATE = 7, SLOT_BETA2 = 8, SLOT_BETA3 = 9,
+       SLOT_RESET_DEST = 10 };
 
 /* ------------------------------------------------------------------ Philox4x32-10 */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
@@ -72,11 +75,6 @@ static void draw4(uint64_t seed, int64_t env, uint32_t t, uint32_t slot, uint32_
     orc_philox4x32_10(ctr, key, out);
 }
 
-/* CPython random_random(): (a>>5, b>>6) -> 53-bit double in [0, 1) */
-static double u53(uint32_t a, uint32_t b) {
-    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
-}
-
 static int32_t uniform_int(uint32_t r, int32_t m) { return (int32_t)(((uint64_t)r * (uint32_t)m) >> 32); }
 
 /* a port index uniform over the P-1 ports other than `other` */
@@ -100,11 +98,17 @@ typedef struct {
     int need;             /* replay: a consumed draw is missing from the tape */
 } source;
 
-/* u_fuel and u_gate: environment.py:104 (uniform) and :320 (random), always both.
- * Philox: the four envs 4k..4k+3 share one block at counter (k, t, FUEL) and one at
- * (k, t, GATE); env 4k+j takes word j as a 32-bit uniform u = w * 2^-32. */
+/* Philox: env e takes word e & 3 of the block at counter (e >> 2, t, slot) as a
+ * 32-bit value; uniforms are u = w * 2^-32. */
 static double u32(uint32_t w) { return (double)w * (1.0 / 4294967296.0); }
 
+static uint32_t quad_word(uint64_t seed, int64_t env, uint32_t t, uint32_t slot) {
+    uint32_t o[4];
+    draw4(seed, (int64_t)((uint64_t)env >> 2), t, slot, o);
+    return o[env & 3];
+}
+
+/* u_fuel and u_gate: environment.py:104 (uniform) and :320 (random), always both */
 static void src_move(source* s, double* u_fuel, double* u_gate) {
     s->used |= U_FUEL_GATE;
     if (s->tape) {
@@ -113,13 +117,8 @@ static void src_move(source* s, double* u_fuel, double* u_gate) {
         s->need |= isnan(*u_fuel) || isnan(*u_gate);
         return;
     }
-    uint32_t f[4], g[4];
-    const int64_t quad = (int64_t)((uint64_t)s->env >> 2);
-    const int lane = (int)(s->env & 3);
-    draw4(s->seed, quad, s->t, SLOT_FUEL, f);
-    draw4(s->seed, quad, s->t, SLOT_GATE, g);
-    *u_fuel = u32(f[lane]);
-    *u_gate = u32(g[lane]);
+    *u_fuel = u32(quad_word(s->seed, s->env, s->t, SLOT_FUEL));
+    *u_gate = u32(quad_word(s->seed, s->env, s->t, SLOT_GATE));
 }
 
 static double src_loss_type(source* s) { /* environment.py:177 */
@@ -128,21 +127,20 @@ static double src_loss_type(source* s) { /* environment.py:177 */
         s->need |= isnan(s->tape->u_type);
         return s->tape->u_type;
     }
-    uint32_t o[4];
-    draw4(s->seed, s->env, s->t, SLOT_LOSS, o);
-    return u53(o[0], o[1]);
+    return u32(quad_word(s->seed, s->env, s->t, SLOT_LOSS));
 }
 
-static double src_beta(source* s) { /* environment.py:195, betavariate(2, 2) */
+/* environment.py:195, betavariate(2, 2): the median of three uniforms has the
+ * Beta(2, 2) law exactly */
+static double src_beta(source* s) {
     s->used |= U_BETA;
     if (s->tape) {
         s->need |= isnan(s->tape->beta);
         return s->tape->beta;
     }
-    uint32_t a[4], b[4];
-    draw4(s->seed, s->env, s->t, SLOT_LOSS, a);
-    draw4(s->seed, s->env, s->t, SLOT_BETA, b);
-    return med3(u53(a[2], a[3]), u53(b[0], b[1]), u53(b[2], b[3]));
+    return med3(u32(quad_word(s->seed, s->env, s->t, SLOT_BETA1)),
+                u32(quad_word(s->seed, s->env, s->t, SLOT_BETA2)),
+                u32(quad_word(s->seed, s->env, s->t, SLOT_BETA3)));
 }
 
 static int32_t src_arrive(source* s, int32_t P, int32_t origin) { /* :333-335 */
@@ -151,9 +149,7 @@ static int32_t src_arrive(source* s, int32_t P, int32_t origin) { /* :333-335 */
         s->need |= s->tape->arrive_dest < 0;
         return s->tape->arrive_dest;
     }
-    uint32_t o[4];
-    draw4(s->seed, s->env, s->t, SLOT_ARRIVE, o);
-    return pick_other(o[0], P, origin);
+    return pick_other(quad_word(s->seed, s->env, s->t, SLOT_ARRIVE), P, origin);
 }
 
 /* ------------------------------------------------------------------ one env */
@@ -355,13 +351,10 @@ int orc_step_batch(const orc_world* w, int64_t n, int act_mode, const int32_t* a
     return 0;
 }
 
-/* reset :227-243 with Philox slot `slot` of counter word t */
-static void reset_philox(const orc_world* w, ship* s, uint64_t seed, int64_t env, uint32_t t,
-                         uint32_t slot) {
-    uint32_t o[4];
-    draw4(seed, env, t, slot, o);
-    s->origin = uniform_int(o[0], w->P);
-    s->dest = pick_other(o[1], w->P, s->origin);
+/* reset :227-243 from an origin word and a destination word */
+static void reset_words(const orc_world* w, ship* s, uint32_t r_origin, uint32_t r_dest) {
+    s->origin = uniform_int(r_origin, w->P);
+    s->dest = pick_other(r_dest, w->P, s->origin);
     s->cargo = 0;
     s->fuel = INITIAL_FUEL;
     s->x = w->port_x[s->origin];
@@ -384,7 +377,9 @@ int orc_reset_batch(const orc_world* w, int64_t n, const uint8_t* mask, const in
             s.x = w->port_x[s.origin];
             s.y = w->port_y[s.origin];
         } else {
-            reset_philox(w, &s, seed, env_id_base + i, epoch, SLOT_EXPLICIT_RESET);
+            uint32_t o[4]; /* one block per env, epoch in the t word */
+            draw4(seed, env_id_base + i, epoch, SLOT_EXPLICIT_RESET, o);
+            reset_words(w, &s, o[0], o[1]);
         }
         store(&s, i, x, y, fuel, cargo, origin, dest);
     }
@@ -408,7 +403,8 @@ int orc_step_batch_autoreset(const orc_world* w, int64_t n, const int32_t* actio
             stats[1] += 1.0;
             stats[2] += (double)ep_len[i];
             ship s;
-            reset_philox(w, &s, seed, env_id_base + i, t, SLOT_RESET);
+            const int64_t e = env_id_base + i; /* quad blocks RESET and RESET_DEST */
+            reset_words(w, &s, quad_word(seed, e, t, SLOT_RESET), quad_word(seed, e, t, SLOT_RESET_DEST));
             store(&s, i, x, y, fuel, cargo, origin, dest);
             ep_return[i] = 0.0f;
             ep_len[i] = 0;

@@ -11,15 +11,21 @@
 
 namespace shipenv {
 
+// Step draws are quad blocks: counter env word = env / 4, word j for env 4k+j, each
+// word a 32-bit uniform u = w * 2^-32 (or an integer draw). The reset kernel and the
+// synthetic agent draw one block per env.
 enum Slot : uint32_t {
-    kSlotFuel = 0,           // counter env word = env / 4: word j = u_fuel of env 4k+j (32-bit)
-    kSlotLoss = 1,           // u_type (0,1), first beta uniform (2,3)
-    kSlotBeta = 2,           // second and third beta uniforms
-    kSlotArrive = 3,         // word 0 -> new destination != origin
-    kSlotReset = 4,          // auto-reset inside step t: word 0 origin, word 1 dest
-    kSlotExplicitReset = 5,  // se_reset with the reset epoch in the t word
-    kSlotAction = 6,         // synthetic bench agent
-    kSlotGate = 7,           // counter env word = env / 4: word j = u_gate of env 4k+j (32-bit)
+    kSlotFuel = 0,           // u_fuel (fuel-cost noise, every step)
+    kSlotLoss = 1,           // u_type (loss type) when the gate fired
+    kSlotBeta1 = 2,          // first of three Beta(2,2) uniforms (partial loss)
+    kSlotArrive = 3,         // new destination != origin on arrival
+    kSlotReset = 4,          // auto-reset inside step t: origin
+    kSlotExplicitReset = 5,  // se_reset, per env, epoch in the t word: words 0 origin, 1 dest
+    kSlotAction = 6,         // synthetic bench agent, per env
+    kSlotGate = 7,           // u_gate (cargo-loss gate)
+    kSlotBeta2 = 8,
+    kSlotBeta3 = 9,
+    kSlotResetDest = 10,     // auto-reset inside step t: destination
 };
 
 struct U4 {
@@ -30,12 +36,17 @@ struct U4 {
 // separate mul_hi / mul_lo pair; the key schedule is wave-uniform (scalar).
 __device__ __forceinline__ U4 philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                        uint32_t k0, uint32_t k1) {
+    // The key is opaque here, so each block recomputes its 18 scalar key adds
+    // instead of the compiler hoisting every block's schedule out of the step
+    // loop: ~20 live SGPRs per block spilled to VGPR lanes (v_readlane + s_nop).
+    asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        // three-way xor in one v_bitop3_b32 (truth table 0x96, gfx950)
+        const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
+        const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
         c1 = (uint32_t)p1;
         c3 = (uint32_t)p0;
         c0 = n0;
@@ -54,12 +65,6 @@ struct Key {
 
 __device__ __forceinline__ U4 draw(const Key& k, uint32_t t, uint32_t slot) {
     return philox10(k.e0, k.e1, t, slot, k.k0, k.k1);
-}
-
-// CPython's 53-bit random(): (a >> 5) * 2^26 + (b >> 6), scaled by 2^-53.
-// Exact in f64 (both products are exact), so contraction cannot change it.
-__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
-    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
 }
 
 // integer uniform on [0, m): high word of r * m (bias < m / 2^32)

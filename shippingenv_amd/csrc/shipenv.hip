@@ -20,6 +20,7 @@
 // np.sqrt) is unfused, and an FMA in -0.1 + 0.2*u changes fuel bits.
 #include <hip/hip_runtime.h>
 
+#include <math.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -32,7 +33,7 @@
 #include "philox.h"
 
 #ifndef SHIPENV_ABLATE
-#define SHIPENV_ABLATE 0  // 0 = the product; 1, 2 = timing-only ablations (tools/ablate.py)
+#define SHIPENV_ABLATE 0  // 0 = the product; 1 = timing-only memory-traffic build (tools/ablate.sh)
 #endif
 
 using namespace shipenv;
@@ -63,13 +64,19 @@ constexpr double kMaxCargo = 50.0;
 //   [+P+1)          rank -> port: the FIRST port on the rank-th occupied cell
 //                   (_get_current_port_idx returns the first match, :150-152)
 //   [frac, +100)    f64 table fl(c / 50) for c in [0, 50) (8-byte aligned)
-// For the 100x100 map with 5 ports that is 4.2 KB.
+//   [gate, +50)     u32 table floor(fl(c / 50) * 2^32): the gate on a Philox word
+//   [rtab, +20)     f64 step rewards before cargo loss / arrival (8-byte aligned):
+//                   [0, 8) a move, index out_of_fuel*4 + ground*2 + closer, summed in
+//                   the reference's order (:288-315); [8] a take (0.05); [9] else 0
+// For the 100x100 map with 5 ports that is 4.5 KB.
 struct WorldDims {
     int32_t H, W, P, words;
     __host__ __device__ int pos() const { return 3 * words; }
     __host__ __device__ int rank2port() const { return 3 * words + 3 * P; }
     __host__ __device__ int frac() const { return (rank2port() + P + 1 + 1) & ~1; }
-    __host__ __device__ int total() const { return frac() + 2 * 50; }
+    __host__ __device__ int gate() const { return frac() + 2 * 50; }
+    __host__ __device__ int rtab() const { return (gate() + 50 + 1) & ~1; }
+    __host__ __device__ int total() const { return rtab() + 2 * 10; }
 };
 
 struct LdsWorld {
@@ -81,6 +88,8 @@ struct LdsWorld {
     const int32_t* pcargo;
     const int32_t* rank2port;
     const double* frac;
+    const uint32_t* gate_thr;
+    const double* rtab;
     int32_t H, W, P;
 
     __device__ bool is_ground(int x, int y) const {
@@ -88,12 +97,15 @@ struct LdsWorld {
         return (ground[c >> 5] >> (c & 31)) & 1u;
     }
     // _get_current_port_idx (:145-153): first port on the ship's cell, -1 if none.
-    // O(1): rank of the cell among occupied cells -> first port index.
+    // O(1): rank of the cell among occupied cells -> first port index. The rank is
+    // at most P (rank2port has P + 1 entries), so the read is unconditional: no
+    // branch (and exec mask) around it.
     __device__ int port_at(int x, int y) const {
         const uint32_t c = (uint32_t)(x * W + y);
         const uint32_t word = portbit[c >> 5], bit = c & 31;
         const int rank = (int)prefix[c >> 5] + __popc(word & ((1u << bit) - 1u));
-        return ((word >> bit) & 1u) ? rank2port[rank] : -1;
+        const int first = rank2port[rank];
+        return ((word >> bit) & 1u) ? first : -1;
     }
     __device__ int px(int i) const { return (int)(pos[i] & 0xffu); }
     __device__ int py(int i) const { return (int)((pos[i] >> 8) & 0xffu); }
@@ -115,6 +127,8 @@ __device__ __forceinline__ LdsWorld stage_world(const uint32_t* __restrict__ g, 
     w.pcargo = (const int32_t*)(lds + d.pos() + 2 * d.P);
     w.rank2port = (const int32_t*)(lds + d.rank2port());
     w.frac = (const double*)(lds + d.frac());
+    w.gate_thr = lds + d.gate();
+    w.rtab = (const double*)(lds + d.rtab());
     w.H = d.H;
     w.W = d.W;
     w.P = d.P;
@@ -137,42 +151,16 @@ __device__ __forceinline__ Key env_key(uint64_t seed, int64_t env) {
     return k;
 }
 
-// The rare per-env draws of one MOVE (loss type, beta, arrival redraw): Philox
-// (production) or a replay tape. u_fuel / u_gate come from the quad blocks drawn
-// for a whole group of 4 envs.
-template <bool kReplay>
-struct Draws;
+// 32-bit uniform in [0, 1): u = w * 2^-32 (exact in f64)
+__device__ __forceinline__ double u32(uint32_t w) { return (double)w * (1.0 / 4294967296.0); }
 
-template <>
-struct Draws<false> {
-    Key key;
-    uint32_t t;
-    __device__ double loss_type() const {  // words 0,1 of slot LOSS
-        const U4 a = draw(key, t, kSlotLoss);
-        return u53(a.v[0], a.v[1]);
-    }
-    // Beta(2,2) as the median of three uniforms (words 2,3 of LOSS and 0..3 of
-    // BETA) — exact in distribution, a fixed number of draws.
-    __device__ double beta() const {
-        const U4 a = draw(key, t, kSlotLoss), b = draw(key, t, kSlotBeta);
-        const double u1 = u53(a.v[2], a.v[3]), u2 = u53(b.v[0], b.v[1]), u3 = u53(b.v[2], b.v[3]);
-        return fmax(fmin(u1, u2), fmin(fmax(u1, u2), u3));
-    }
-    __device__ int arrive(int P, int origin) const {
-        const U4 o = draw(key, t, kSlotArrive);
-        return pick_other(o.v[0], P, origin);
-    }
-};
-
-// Replay: the variates the reference drew through `random`. A missing one (NaN,
-// or arrive_dest < 0) makes the step report SE_ERR_NEED_DRAW without effect.
-template <>
-struct Draws<true> {
-    const se_tape* rec;
-    __device__ double loss_type() const { return rec->u_type; }
-    __device__ double beta() const { return rec->beta; }
-    __device__ int arrive(int, int) const { return rec->arrive_dest; }
-};
+// Loss type on the LOSS word w (u = w * 2^-32, :180-188): u < 0.1 <=> w < kTypeLo,
+// u > 0.9 <=> w > kTypeHi. Both products by 2^32 are exact and not integers.
+constexpr uint32_t kTypeLo = (uint32_t)(0.1 * 4294967296.0) + 1u;  // 429496730
+constexpr uint32_t kTypeHi = (uint32_t)(0.9 * 4294967296.0);       // 3865470566
+static_assert(0.1 * 4294967296.0 != (double)(uint32_t)(0.1 * 4294967296.0), "bound is an integer");
+static_assert(0.9 * 4294967296.0 != (double)(uint32_t)(0.9 * 4294967296.0), "bound is an integer");
+enum LossKind : int { kLossNone = 0, kLossPartial = 1, kLossTotal = 2 };
 
 // sqrt of a non-negative integer, correctly rounded (np.sqrt on the int sum of
 // squares, shipping/util.py:4). Unit moves take the exact fast path.
@@ -186,123 +174,145 @@ template <bool kUnitMoves>
 __device__ __forceinline__ bool needs_gate(const LdsWorld& w, const Ship& s, int type, int a, int b) {
     if (kUnitMoves) {
         const int nx = s.x + a, ny = s.y + b;
-        return type == 1 && s.dest != SE_NONE && (unsigned)nx < (unsigned)w.H &&
-               (unsigned)ny < (unsigned)w.W && s.cargo > 0 && s.cargo < 50;
+        return (type == 1) & (s.dest != SE_NONE) & ((unsigned)nx < (unsigned)w.H) &
+               ((unsigned)ny < (unsigned)w.W) & (s.cargo > 0) & (s.cargo < 50);
     }
-    return type == 1 && s.cargo > 0 && s.cargo < 50;  // typed form: draw whenever possible
+    return (type == 1) & (s.cargo > 0) & (s.cargo < 50);  // typed form: draw whenever possible
 }
 
-// One env's step (:359-376) for a typed action (shipping/type.py:1-5), written as
-// selects over the three action families so a wave runs one straight path; only
-// cargo loss and arrival branch. Returns SE_ERR_*; an error leaves s untouched
-// (the reference raises before mutating: :284 before :287, :266-269, :342-346).
+// One env's step between its two halves.
+struct Pending {
+    double r;     // reward so far, in the reference's add order
+    int e;        // SE_ERR_*
+    bool mv;      // a MOVE that passed its checks (:276-284)
+    bool moved;   // ... and left its cell (not blocked by ground, :293-300)
+    bool fires;   // the cargo-loss gate fired (:318-323)
+    bool arrive;  // the move ends on the destination port (:325)
+    bool dead;    // out of fuel: the step returns done (:288-290)
+};
+
+// First half of one env's step (:359-376) for a typed action (shipping/type.py:1-5):
+// everything that needs no optional draw, as selects over the three action
+// families so a wave runs one straight path. On return `s` holds the state after
+// the move / select / take; env_finish applies cargo loss and arrival. An error
+// leaves s untouched (the reference raises before mutating: :284 before :287,
+// :266-269, :342-346). The gate (:318-323, random() <= cargo/50) tests the tape's
+// f64 u_gate in replay and the Philox word gw in production: w <= floor(fl(c/50)
+// * 2^32) is the same test on u = w * 2^-32. Production skips the cargo-0 case (a
+// firing gate then loses nothing, :180-181); replay keeps it because the reference
+// still draws the loss type there (:177) and replay tracks every draw. From cargo
+// 50 on the gate always fires (random() < 1 <= cargo/50).
 template <bool kUnitMoves, bool kReplay>
-__device__ __forceinline__ int env_step(const LdsWorld& w, Ship& s, int e_in, int type, int a, int b,
-                                        double u_fuel, double u_gate,
-                                        const Draws<kReplay>& dr, double& reward, int& done,
-                                        uint32_t& used) {
+__device__ __forceinline__ Pending env_begin(const LdsWorld& w, Ship& s, int e_in, int type, int a,
+                                             int b, double u_fuel, double u_gate, uint32_t gw) {
     // --- MOVE (_move_ship :273-339)
     const bool no_dest = s.dest == SE_NONE;                                      // :276
-    const bool big = !kUnitMoves && (a < -256 || a > 256 || b < -256 || b > 256);  // surely OOB
+    const bool big = !kUnitMoves & ((a < -256) | (a > 256) | (b < -256) | (b > 256));  // surely OOB
     const int nx = s.x + (big ? 0 : a), ny = s.y + (big ? 0 : b);
-    const bool oob = big || (unsigned)nx >= (unsigned)w.H || (unsigned)ny >= (unsigned)w.W;  // :284
-    const bool mv_ok = !no_dest && !oob;
+    const bool oob = big | ((unsigned)nx >= (unsigned)w.H) | ((unsigned)ny >= (unsigned)w.W);  // :284
+    const bool mv_ok = !no_dest & !oob;
     const int cx = mv_ok ? nx : s.x, cy = mv_ok ? ny : s.y;  // in-range cell for the lookups
     // fuel cost (:103-104): dist * (1 + uniform(-0.1, 0.1)), uniform = -0.1 + 0.2*u, unfused
     const double scale = 1.0 + (-0.1 + 0.2 * u_fuel);
     const double cost = kUnitMoves ? scale : int_sqrt_rn(big ? 1 : a * a + b * b) * scale;
     const bool out_of_fuel = s.fuel < cost;  // :288-290
-    const double r0 = out_of_fuel ? -10.0 : 0.0;
-    const bool ground = w.is_ground(cx, cy);  // :293
-    // :294 blocked (-5) or :296-300 moved (-0.0001 then -1), in the reference's add order
-    double rm = ground ? r0 + -5.0 : (r0 + -0.0001) + -1.0;
+    const bool ground = w.is_ground(cx, cy);  // :293: blocked (-5) or moved (-0.0001 then -1)
     const int mx = ground ? s.x : cx, my = ground ? s.y : cy;
-    const double fuel_m = ground ? s.fuel : s.fuel - cost;
     // :307-315 old cell vs ATTEMPTED cell; sqrt is monotone and the squared
     // distances are small integers, so comparing them is exact
     const int dcl = no_dest ? 0 : s.dest;
     const int px = w.px(dcl), py = w.py(dcl);
     const int d_old = (s.x - px) * (s.x - px) + (s.y - py) * (s.y - py);
     const int d_new = (cx - px) * (cx - px) + (cy - py) * (cy - py);
-    rm += d_old > d_new ? 2.0 : -2.0;
+    const bool closer = d_old > d_new;
 
     // --- SELECT_PORT (_select_port :265-271)
-    const int e_sel = (a < 0 || a >= w.P) ? SE_ERR_PORT_RANGE
-                                          : (s.origin == a ? SE_ERR_SAME_PORT : SE_ERR_OK);
+    const int e_same = s.origin == a ? SE_ERR_SAME_PORT : SE_ERR_OK;
+    const int e_sel = ((a < 0) | (a >= w.P)) ? SE_ERR_PORT_RANGE : e_same;
     // --- TAKE_FUEL / TAKE_CARGO (:341-357)
     const int idx = w.port_at(s.x, s.y);
     const int sidx = idx < 0 ? 0 : idx;
-    const int stock = type == 4 ? w.pcargo[sidx] : w.pfuel[sidx];
-    const int e_take = idx < 0 ? SE_ERR_NOT_AT_PORT : ((a <= 0 || a > stock) ? SE_ERR_AMOUNT : SE_ERR_OK);
+    const int cstock = w.pcargo[sidx], fstock = w.pfuel[sidx];
+    const int stock = type == 4 ? cstock : fstock;
+    const int e_amount = ((a <= 0) | (a > stock)) ? SE_ERR_AMOUNT : SE_ERR_OK;
+    const int e_take = idx < 0 ? SE_ERR_NOT_AT_PORT : e_amount;
+    const int e_oob = oob ? SE_ERR_OOB : SE_ERR_OK;
+    const int e_move = no_dest ? SE_ERR_NO_DEST : e_oob;
 
-    const int e = e_in != SE_ERR_OK ? e_in  // the decode runs before env.step (agents/dqn.py:286-287)
-                : w.P == 0 ? SE_ERR_NO_PORTS  // :360
-                : type == 1 ? (no_dest ? SE_ERR_NO_DEST : (oob ? SE_ERR_OOB : SE_ERR_OK))
-                : type == 2 ? e_sel
-                : (type == 3 || type == 4) ? e_take
-                : SE_ERR_BAD_CATEGORY;  // :373-374
-    const bool ok = e == SE_ERR_OK;
-    const bool do_move = ok && type == 1;
+    // Every ternary below has named values as arms: clang emits a nested or
+    // computing arm as control flow, which becomes a divergent branch.
+    const int e4 = ((type == 3) | (type == 4)) ? e_take : SE_ERR_BAD_CATEGORY;  // :373-374
+    const int e3 = type == 2 ? e_sel : e4;
+    const int e2 = type == 1 ? e_move : e3;
+    const int e1 = w.P == 0 ? SE_ERR_NO_PORTS : e2;  // :360
+    Pending p;
+    p.e = e_in != SE_ERR_OK ? e_in : e1;  // the decode runs before env.step (agents/dqn.py:286-287)
+    const bool ok = p.e == SE_ERR_OK;
+    const bool do_move = ok & (type == 1);
 
-    int cargo_m = s.cargo, origin_m = s.origin, dest_m = s.dest;
-    bool need = false;  // replay only: a variate the reference drew here is missing
-    used = do_move ? (kUsedFuelGate | (ground ? 0u : kUsedMoved)) : 0u;
-    if (kReplay) need = do_move && (u_fuel != u_fuel || u_gate != u_gate);
-    // :318-323 the gate random() <= cargo/50. Production skips the cargo-0 case (a
-    // firing gate then loses nothing, :180-181); replay keeps it, because the
-    // reference still draws the loss type there (:177) and replay tracks every draw.
-    // From cargo 50 on it always fires (random() < 1 <= cargo/50).
-    const int ci = (s.cargo > 0 && s.cargo < 50) ? s.cargo : 0;
-    const bool fires = s.cargo >= 50 || ((kReplay || s.cargo > 0) && u_gate <= w.likelihood(ci));
-    if (do_move && fires) {  // _calculate_cargo_loss :169-200
-        used |= kUsedLossType;
-        const double lt = dr.loss_type();
-        const bool partial = cargo_m != 0 && lt >= 0.1 && lt <= 0.9;  // :180, :184, :188
-        double beta = 0.0;
-        if (partial) {
-            used |= kUsedBeta;
-            beta = dr.beta();
-        }
-        if (kReplay) need = need || lt != lt || (partial && beta != beta);
-        const int loss = lt < 0.1 ? 0 : (lt > 0.9 ? cargo_m : (int)(beta * (double)cargo_m));
-        cargo_m -= loss;
-        rm += (double)(-3 * loss);
-    }
-    if (do_move && mx == px && my == py) {  // :325-337 arrival
-        used |= kUsedArrive;
-        rm += (double)(2 * cargo_m);
-        cargo_m = 0;
-        origin_m = dest_m;
-        dest_m = dr.arrive(w.P, origin_m);
-        if (kReplay) need = need || dest_m < 0;
-        rm += 10.0;
-    }
-    if (kReplay && need) {  // ask the caller for the next variate; change nothing
-        reward = 0.0;
-        done = 0;
-        return SE_ERR_NEED_DRAW;
+    const int ci = ((s.cargo > 0) & (s.cargo < 50)) ? s.cargo : 0;
+    bool fires;
+    if constexpr (kReplay) {
+        const double lk = w.likelihood(ci);
+        fires = (s.cargo >= 50) | (u_gate <= lk);
+    } else {
+        const uint32_t thr = w.gate_thr[ci];
+        fires = (s.cargo >= 50) | ((s.cargo > 0) & (gw <= thr));
     }
 
-    const bool take_fuel = ok && type == 3, take_cargo = ok && type == 4;
+    p.mv = do_move;
+    p.moved = do_move & !ground;
+    p.fires = do_move & fires;
+    p.arrive = do_move & (mx == px) & (my == py);
+    p.dead = do_move & out_of_fuel;
+    const bool take_fuel = ok & (type == 3), take_cargo = ok & (type == 4);
+    // reward before loss / arrival from the table the host summed in the reference's order
+    const int r_move = ((int)out_of_fuel << 2) | ((int)ground << 1) | (int)closer;
+    const int r_other = (take_fuel | take_cargo) ? 8 : 9;
+    p.r = w.rtab[do_move ? r_move : r_other];
     s.x = do_move ? mx : s.x;
     s.y = do_move ? my : s.y;
-    s.fuel = do_move ? fuel_m : (take_fuel ? s.fuel + (double)a : s.fuel);
-    s.cargo = do_move ? cargo_m : (take_cargo ? s.cargo + a : s.cargo);
-    s.origin = do_move ? origin_m : s.origin;
-    s.dest = do_move ? dest_m : ((ok && type == 2) ? a : s.dest);
-    reward = do_move ? rm : ((take_fuel || take_cargo) ? 0.05 : 0.0);
-    done = (do_move && out_of_fuel) ? 1 : 0;
-    return e;
+    const double burnt = s.fuel - cost, filled = s.fuel + (double)a;
+    const double fuel_mv = (do_move & !ground) ? burnt : s.fuel;  // moves and takes exclude
+    s.fuel = take_fuel ? filled : fuel_mv;
+    const int loaded = s.cargo + a;
+    s.cargo = take_cargo ? loaded : s.cargo;
+    s.dest = (ok & (type == 2)) ? a : s.dest;
+    return p;
 }
 
-// utils/preprocessing.py:111-137 (moves N, E, S, W; Python wraps -4..-1)
+// Second half: cargo loss (_calculate_cargo_loss :169-200) of kind none / partial
+// (int(beta * cargo), :195-197) / total, then arrival (:325-337) with the redrawn
+// destination. Selects only.
+__device__ __forceinline__ void env_finish(Ship& s, Pending& p, int kind, double beta, int new_dest) {
+    const int part = (int)(beta * (double)s.cargo);
+    const int some = kind == kLossTotal ? s.cargo : part;
+    const int loss = kind == kLossNone ? 0 : some;
+    const double rl = p.r + (double)(-3 * loss);
+    const int kept = s.cargo - loss;
+    p.r = p.fires ? rl : p.r;
+    s.cargo = p.fires ? kept : s.cargo;
+    const double ra = (p.r + (double)(2 * s.cargo)) + 10.0;
+    p.r = p.arrive ? ra : p.r;
+    s.cargo = p.arrive ? 0 : s.cargo;
+    const int dest = s.dest;
+    s.dest = p.arrive ? new_dest : dest;
+    s.origin = p.arrive ? dest : s.origin;
+}
+
+// utils/preprocessing.py:111-137 (moves N, E, S, W; Python wraps -4..-1), in
+// integer arithmetic: the compiler turns nested ternaries into divergent branches.
+//   act < 4: MOVE k = act & 3, N (0,-1) E (-1,0) S (0,1) W (1,0)
+//   [4, 4+P): SELECT_PORT act-4   [4+P, 54+P): TAKE_CARGO   [54+P, ...): TAKE_FUEL
 __device__ __forceinline__ int decode_agent(int P, int act, int& type, int& a, int& b) {
     const int k = act & 3;  // -4..-1 -> 0..3 like Python's negative list index
-    const bool move = act < 4;
-    type = move ? 1 : (act < 4 + P ? 2 : (act < 4 + P + 50 ? 4 : 3));
-    const int val = act - (type == 2 ? 4 : (type == 4 ? 4 + P : 4 + P + 50));
-    a = move ? (k == 1 ? -1 : (k == 3 ? 1 : 0)) : val;  // EAST = (-1, 0), WEST = (1, 0)
-    b = move ? (k == 0 ? -1 : (k == 2 ? 1 : 0)) : 0;    // NORTH = (0, -1), SOUTH = (0, 1)
+    const int move = act < 4, sel = act < 4 + P, cargo = act < 54 + P;
+    type = move ? 1 : 3 + cargo - 2 * sel;
+    const int val = act - 4 - (1 - sel) * P - (1 - cargo) * 50;
+    const int odd = k & 1;
+    const int dx = odd * (k - 2);   // EAST = (-1, 0), WEST = (1, 0)
+    a = move ? dx : val;
+    b = move * (1 - odd) * (k - 1);  // NORTH = (0, -1), SOUTH = (0, 1)
     return act < -4 ? SE_ERR_BAD_INDEX : SE_ERR_OK;
 }
 
@@ -316,9 +326,6 @@ __device__ __forceinline__ void reset_ship(const LdsWorld& w, Ship& s, uint32_t 
     s.y = w.py(s.origin);
 }
 
-__device__ __forceinline__ uint32_t lane_id() {
-    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-}
 // number of set bits of `mask` below this lane
 __device__ __forceinline__ uint32_t count_below(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
@@ -330,7 +337,7 @@ struct StepArgs {
     const uint32_t* world;
     WorldDims dims;
     int64_t n;
-    int64_t env_base;  // multiple of 4 (a quad of envs shares its fuel / gate blocks)
+    int64_t env_base;  // multiple of 4 (a quad of envs shares its draw blocks)
     uint64_t seed;
     uint32_t t;
     se_state st;
@@ -345,124 +352,159 @@ struct StepArgs {
     double* slab;            // per-block {sum_ret, n_eps, sum_len, pad}
 };
 
-// 4 consecutive elements: one 16-byte lane access (kFull) or guarded scalars (tail)
-template <bool kFull, typename T>
-__device__ __forceinline__ void ld4(const T* __restrict__ p, int64_t base, int64_t n, T& v0, T& v1,
-                                    T& v2, T& v3) {
-    if constexpr (kFull) {
-        if constexpr (sizeof(T) == 4) {
-            const uint4 w = *reinterpret_cast<const uint4*>(p + base);
-            v0 = __builtin_bit_cast(T, w.x);
-            v1 = __builtin_bit_cast(T, w.y);
-            v2 = __builtin_bit_cast(T, w.z);
-            v3 = __builtin_bit_cast(T, w.w);
-        } else {
-            const double2 a = *reinterpret_cast<const double2*>(p + base);
-            const double2 b = *reinterpret_cast<const double2*>(p + base + 2);
-            v0 = a.x;
-            v1 = a.y;
-            v2 = b.x;
-            v3 = b.y;
-        }
+// Field access for the 4 envs of one group. Full groups: the pointer advanced to
+// the block-uniform first group g0 stays scalar and the lane offset is
+// loop-invariant, so no per-access 64-bit address arithmetic runs on the VALU; each
+// field is one 4-byte (u8 x4), 16-byte (32-bit x4) or 2 x 16-byte (f64 x4) lane
+// access. The partial last group uses guarded scalar accesses at env index base.
+template <typename T>
+__device__ __forceinline__ T* slab_of(T* p, int64_t g0) {
+    return p + g0 * 4;
+}
+
+template <typename T>
+__device__ __forceinline__ void ld4_full(const T* __restrict__ p, int64_t g0, T (&v)[4]) {
+    if constexpr (sizeof(T) == 4) {
+        const uint4 w = reinterpret_cast<const uint4*>(slab_of(p, g0))[threadIdx.x];
+        v[0] = __builtin_bit_cast(T, w.x);
+        v[1] = __builtin_bit_cast(T, w.y);
+        v[2] = __builtin_bit_cast(T, w.z);
+        v[3] = __builtin_bit_cast(T, w.w);
     } else {
-        v0 = base + 0 < n ? p[base + 0] : T(0);
-        v1 = base + 1 < n ? p[base + 1] : T(0);
-        v2 = base + 2 < n ? p[base + 2] : T(0);
-        v3 = base + 3 < n ? p[base + 3] : T(0);
+        const double2* q = reinterpret_cast<const double2*>(slab_of(p, g0)) + 2 * threadIdx.x;
+        const double2 a = q[0], b = q[1];
+        v[0] = a.x;
+        v[1] = a.y;
+        v[2] = b.x;
+        v[3] = b.y;
     }
 }
 
-template <bool kFull, typename T>
-__device__ __forceinline__ void st4(T* __restrict__ p, int64_t base, int64_t n, T v0, T v1, T v2,
-                                    T v3) {
-    if constexpr (kFull) {
-        if constexpr (sizeof(T) == 4) {
-            uint4 w;
-            w.x = __builtin_bit_cast(uint32_t, v0);
-            w.y = __builtin_bit_cast(uint32_t, v1);
-            w.z = __builtin_bit_cast(uint32_t, v2);
-            w.w = __builtin_bit_cast(uint32_t, v3);
-            *reinterpret_cast<uint4*>(p + base) = w;
-        } else {
-            *reinterpret_cast<double2*>(p + base) = make_double2(v0, v1);
-            *reinterpret_cast<double2*>(p + base + 2) = make_double2(v2, v3);
-        }
+template <typename T>
+__device__ __forceinline__ void st4_full(T* __restrict__ p, int64_t g0, const T (&v)[4]) {
+    if constexpr (sizeof(T) == 4) {
+        uint4 w;
+        w.x = __builtin_bit_cast(uint32_t, v[0]);
+        w.y = __builtin_bit_cast(uint32_t, v[1]);
+        w.z = __builtin_bit_cast(uint32_t, v[2]);
+        w.w = __builtin_bit_cast(uint32_t, v[3]);
+        reinterpret_cast<uint4*>(slab_of(p, g0))[threadIdx.x] = w;
     } else {
-        if (base + 0 < n) p[base + 0] = v0;
-        if (base + 1 < n) p[base + 1] = v1;
-        if (base + 2 < n) p[base + 2] = v2;
-        if (base + 3 < n) p[base + 3] = v3;
+        double2* q = reinterpret_cast<double2*>(slab_of(p, g0)) + 2 * threadIdx.x;
+        q[0] = make_double2(v[0], v[1]);
+        q[1] = make_double2(v[2], v[3]);
     }
 }
 
-// 4 u8 fields of consecutive envs as one packed word
-template <bool kFull>
-__device__ __forceinline__ uint32_t ld4u8(const uint8_t* __restrict__ p, int64_t base, int64_t n) {
-    if constexpr (kFull) {
-        return *reinterpret_cast<const uint32_t*>(p + base);
-    } else {
-        uint32_t w = 0;
-        for (int j = 0; j < 4; ++j)
-            if (base + j < n) w |= (uint32_t)p[base + j] << (8 * j);
-        return w;
-    }
+template <typename T>
+__device__ __forceinline__ void ld4_tail(const T* __restrict__ p, int64_t base, int64_t n, T (&v)[4]) {
+    for (int j = 0; j < 4; ++j) v[j] = base + j < n ? p[base + j] : T(0);
 }
 
-template <bool kFull>
-__device__ __forceinline__ void st4u8(uint8_t* __restrict__ p, int64_t base, int64_t n, uint32_t w) {
-    if constexpr (kFull) {
-        *reinterpret_cast<uint32_t*>(p + base) = w;
-    } else {
-        for (int j = 0; j < 4; ++j)
-            if (base + j < n) p[base + j] = (uint8_t)(w >> (8 * j));
-    }
+template <typename T>
+__device__ __forceinline__ void st4_tail(T* __restrict__ p, int64_t base, int64_t n, const T (&v)[4]) {
+    for (int j = 0; j < 4; ++j)
+        if (base + j < n) p[base + j] = v[j];
+}
+
+__device__ __forceinline__ uint32_t ld4u8_full(const uint8_t* __restrict__ p, int64_t g0) {
+    return reinterpret_cast<const uint32_t*>(slab_of(p, g0))[threadIdx.x];
+}
+__device__ __forceinline__ void st4u8_full(uint8_t* __restrict__ p, int64_t g0, uint32_t w) {
+    reinterpret_cast<uint32_t*>(slab_of(p, g0))[threadIdx.x] = w;
+}
+__device__ __forceinline__ uint32_t ld4u8_tail(const uint8_t* __restrict__ p, int64_t base, int64_t n) {
+    uint32_t w = 0;
+    for (int j = 0; j < 4; ++j)
+        if (base + j < n) w |= (uint32_t)p[base + j] << (8 * j);
+    return w;
+}
+__device__ __forceinline__ void st4u8_tail(uint8_t* __restrict__ p, int64_t base, int64_t n, uint32_t w) {
+    for (int j = 0; j < 4; ++j)
+        if (base + j < n) p[base + j] = (uint8_t)(w >> (8 * j));
 }
 
 __device__ __forceinline__ int byte_of(uint32_t w, int j) { return (int)((w >> (8 * j)) & 0xffu); }
 
-// The inputs of 4 consecutive envs (one lane access per field when kFull).
+// Where one group's fields live: g0 (block-uniform) for a full group, whose envs
+// are 4 * (g0 + threadIdx.x) + j; base = the group's first env in both cases.
+template <bool kFull>
+struct At {
+    int64_t g0, base, n;
+};
+
+// The inputs of the 4 envs of one group.
 template <bool kTyped, bool kAuto>
 struct Group {
     uint32_t x, y, org, dst;  // packed u8 x4
-    int32_t c0, c1, c2, c3;   // cargo
-    double f0, f1, f2, f3;    // fuel
-    int32_t a0, a1, a2, a3;   // agent index / action type
-    int32_t p0, p1, p2, p3;   // typed: value a
-    int32_t q0, q1, q2, q3;   // typed: value b
-    float e0, e1, e2, e3;     // ep_return
-    int32_t l0, l1, l2, l3;   // ep_len
+    int32_t c[4];             // cargo
+    double f[4];              // fuel
+    int32_t a[4];             // agent index / action type
+    int32_t p[4], q[4];       // typed: values a, b
+    float e[4];               // ep_return
+    int32_t l[4];             // ep_len
 
     template <bool kFull>
-    __device__ __forceinline__ void load(const StepArgs& A, int64_t base) {
+    __device__ __forceinline__ void load(const StepArgs& A, At<kFull> at) {
         const se_state& S = A.st;
-        x = ld4u8<kFull>(S.x, base, A.n);
-        y = ld4u8<kFull>(S.y, base, A.n);
-        org = ld4u8<kFull>(S.origin, base, A.n);
-        dst = ld4u8<kFull>(S.dest, base, A.n);
-        ld4<kFull>(S.cargo, base, A.n, c0, c1, c2, c3);
-        ld4<kFull>(S.fuel, base, A.n, f0, f1, f2, f3);
-        ld4<kFull>(A.act, base, A.n, a0, a1, a2, a3);
-        if (kTyped) {
-            ld4<kFull>(A.act_a, base, A.n, p0, p1, p2, p3);
-            ld4<kFull>(A.act_b, base, A.n, q0, q1, q2, q3);
-        }
-        if (kAuto) {
-            ld4<kFull>(S.ep_return, base, A.n, e0, e1, e2, e3);
-            ld4<kFull>(S.ep_len, base, A.n, l0, l1, l2, l3);
+        if constexpr (kFull) {
+            x = ld4u8_full(S.x, at.g0);
+            y = ld4u8_full(S.y, at.g0);
+            org = ld4u8_full(S.origin, at.g0);
+            dst = ld4u8_full(S.dest, at.g0);
+            ld4_full(S.cargo, at.g0, c);
+            ld4_full(S.fuel, at.g0, f);
+            ld4_full(A.act, at.g0, a);
+            if (kTyped) {
+                ld4_full(A.act_a, at.g0, p);
+                ld4_full(A.act_b, at.g0, q);
+            }
+        } else {
+            x = ld4u8_tail(S.x, at.base, at.n);
+            y = ld4u8_tail(S.y, at.base, at.n);
+            org = ld4u8_tail(S.origin, at.base, at.n);
+            dst = ld4u8_tail(S.dest, at.base, at.n);
+            ld4_tail(S.cargo, at.base, at.n, c);
+            ld4_tail(S.fuel, at.base, at.n, f);
+            ld4_tail(A.act, at.base, at.n, a);
+            if (kTyped) {
+                ld4_tail(A.act_a, at.base, at.n, p);
+                ld4_tail(A.act_b, at.base, at.n, q);
+            }
+            if (kAuto) {
+                ld4_tail(S.ep_return, at.base, at.n, e);
+                ld4_tail(S.ep_len, at.base, at.n, l);
+            }
         }
     }
+    // episode counters of a full group: loaded late (step_group), they would
+    // otherwise hold 8 registers across the whole step
+    __device__ __forceinline__ void load_episode(const StepArgs& A, At<true> at) {
+        ld4_full(A.st.ep_return, at.g0, e);
+        ld4_full(A.st.ep_len, at.g0, l);
+    }
+    __device__ __forceinline__ void load_episode(const StepArgs&, At<false>) {}  // loaded with the rest
 };
 
+template <bool kFull, typename T>
+__device__ __forceinline__ void store4(T* p, At<kFull> at, const T (&v)[4]) {
+    if constexpr (kFull) st4_full(p, at.g0, v);
+    else st4_tail(p, at.base, at.n, v);
+}
+template <bool kFull>
+__device__ __forceinline__ void store4u8(uint8_t* p, At<kFull> at, uint32_t w) {
+    if constexpr (kFull) st4u8_full(p, at.g0, w);
+    else st4u8_tail(p, at.base, at.n, w);
+}
+
+// Per-thread episode statistics of the finished episodes. Counts are integers:
+// summed as doubles they were exact anyway, and they hold two fewer registers.
 struct BlockStats {
-    double ret = 0.0, eps = 0.0, len = 0.0;
+    double ret = 0.0;
+    int32_t eps = 0;
+    int64_t len = 0;
 };
 
-// 32-bit uniform in [0, 1): u = w * 2^-32 (exact in f64)
-__device__ __forceinline__ double u32(uint32_t w) { return (double)w * (1.0 / 4294967296.0); }
-
-// Step the 4 envs of one group (base = 4k). u_fuel / u_gate of env 4k+j are word j
-// of the quad's FUEL / GATE Philox blocks; the GATE block is only drawn when some
-// env of the group can observe its gate.
 // Finished episodes of one group (auto-reset): bit j of `mask` for env base+j.
 struct Finished {
     uint32_t mask = 0;
@@ -470,151 +512,247 @@ struct Finished {
     int32_t len[4];
 };
 
+// x, y, fuel, done, err of a group's 4 envs: final once the first half has run
+// (cargo loss and arrival change none of them).
+template <bool kFull>
+__device__ __forceinline__ void store_moved(const se_state& S, At<kFull> at, const Ship (&s)[4],
+                                            const Pending (&p)[4]) {
+    uint32_t ox = 0, oy = 0, dn = 0, ee = 0;
+    double fuel[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t sh = 8u * (uint32_t)j;
+        ox |= (uint32_t)(s[j].x & 0xff) << sh;
+        oy |= (uint32_t)(s[j].y & 0xff) << sh;
+        dn |= (uint32_t)p[j].dead << sh;
+        ee |= (uint32_t)(p[j].e & 0xff) << sh;
+        fuel[j] = s[j].fuel;
+    }
+    store4u8(S.x, at, ox);
+    store4u8(S.y, at, oy);
+    store4(S.fuel, at, fuel);
+    store4u8(S.done, at, dn);
+    store4u8(reinterpret_cast<uint8_t*>(S.err), at, ee);
+}
+
+// cargo, origin, dest, reward (+ the episode counters): final after the second half.
+template <bool kAuto, bool kFull>
+__device__ __forceinline__ void store_rest(const se_state& S, At<kFull> at, const Ship (&s)[4],
+                                           const float (&rw)[4], const float (&epr)[4],
+                                           const int32_t (&epl)[4]) {
+    uint32_t oo = 0, od = 0;
+    int32_t cargo[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t sh = 8u * (uint32_t)j;
+        oo |= (uint32_t)(s[j].origin & 0xff) << sh;
+        od |= (uint32_t)(s[j].dest & 0xff) << sh;
+        cargo[j] = s[j].cargo;
+    }
+    store4u8(S.origin, at, oo);
+    store4u8(S.dest, at, od);
+    store4(S.cargo, at, cargo);
+    store4(S.reward, at, rw);
+    if constexpr (kAuto) {
+        store4(S.ep_return, at, epr);
+        store4(S.ep_len, at, epl);
+    }
+}
+
+// Step the 4 envs 4k..4k+3 of one group (base = 4k). Production draws are Philox
+// quad blocks at counter (k, t, slot): word j belongs to env 4k+j (RNG contract,
+// DESIGN.md). Each block is drawn only when some env of the quad consumes it, so
+// the draws are lane-uniform branches instead of a branch per env and draw:
+//   FUEL   every step           GATE    a move with 0 < cargo < 50
+//   LOSS   the gate fired       BETA1-3 a partial loss (Beta(2,2) = median of 3)
+//   ARRIVE an arrival           RESET, RESET_DEST  an auto-reset
+// Replay takes every variate from the env's tape record instead.
+// Registers: x, y, fuel, done and err are stored as soon as the first half has
+// run (and auto-reset has replaced the finished envs' positions), so only cargo,
+// origin, dest and the reward stay live across the loss / arrival blocks.
 template <bool kTyped, bool kReplay, bool kAuto, bool kFull>
 __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
-                                           Group<kTyped, kAuto>& G, int64_t base, BlockStats& bs,
+                                           Group<kTyped, kAuto>& G, At<kFull> at, BlockStats& bs,
                                            Finished& F) {
     const se_state& S = A.st;
-    const int64_t n = A.n;
-    int32_t act[4] = {G.a0, G.a1, G.a2, G.a3};
-    int32_t pa[4] = {G.p0, G.p1, G.p2, G.p3};
-    int32_t qb[4] = {G.q0, G.q1, G.q2, G.q3};
-    int32_t cargo[4] = {G.c0, G.c1, G.c2, G.c3};
-    double fuel[4] = {G.f0, G.f1, G.f2, G.f3};
-    float epr[4] = {G.e0, G.e1, G.e2, G.e3};
-    int32_t epl[4] = {G.l0, G.l1, G.l2, G.l3};
-
-    // pass 1 (registers only): can any env of the group observe its gate draw?
-    bool gate_needed = false;
+    const int64_t n = A.n, base = at.base;
+    int ty[4], va[4], vb[4], er[4];
+    Ship s[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        int ty, va, vb, er = SE_ERR_OK;
         if (kTyped) {
-            ty = act[j];
-            va = pa[j];
-            vb = qb[j];
+            ty[j] = G.a[j];
+            va[j] = G.p[j];
+            vb[j] = G.q[j];
+            er[j] = SE_ERR_OK;
         } else {
-            er = decode_agent(w.P, act[j], ty, va, vb);
+            er[j] = decode_agent(w.P, G.a[j], ty[j], va[j], vb[j]);
         }
-        const Ship s{byte_of(G.x, j), byte_of(G.y, j), 0.0, cargo[j], 0, byte_of(G.dst, j)};
-        gate_needed |= er == SE_ERR_OK && needs_gate<!kTyped>(w, s, ty, va, vb);
+        s[j] = Ship{byte_of(G.x, j), byte_of(G.y, j), G.f[j], G.c[j], byte_of(G.org, j), byte_of(G.dst, j)};
     }
+    const Key qk = env_key(A.seed, (A.env_base + base) >> 2);
+    const uint32_t t = A.t;
+    Pending p[4];
 
-    double uf[4], ug[4];
-    if constexpr (kReplay) {
+#if SHIPENV_ABLATE  // timing-only build (tools/ablate.sh): memory traffic, no logic or draws
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const bool in = kFull || base + j < n;
-            uf[j] = in ? A.tape[base + j].u_fuel : 0.0;
-            ug[j] = in ? A.tape[base + j].u_gate : 0.0;
-        }
-    } else {
-        const int64_t quad = (A.env_base + base) >> 2;
-        const Key qk = env_key(A.seed, quad);
-#if SHIPENV_ABLATE == 1 || SHIPENV_ABLATE == 3  // timing-only builds: a trivial hash, no Philox
-        const uint32_t h = (uint32_t)base * 0x9E3779B9u ^ A.t;
-        const U4 fb = U4{{h, h * 3u, h ^ 0x55u, h + 7u}};
-        const U4 gb = fb;
-        (void)qk;
-        (void)gate_needed;
+    for (int j = 0; j < 4; ++j) {
+        s[j].x ^= ty[j] & 1;
+        s[j].fuel -= (double)va[j];
+        s[j].cargo += vb[j];
+        p[j] = Pending{(double)vb[j], er[j], false, false, false, false, false};
+    }
+    (void)qk;
+    (void)t;
+    (void)bs;
+    (void)F;
+    store_moved(S, at, s, p);
+    float rw[4], epr[4];
+    int32_t epl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        rw[j] = (float)p[j].r;
+        epr[j] = kAuto ? G.e[j] + rw[j] : 0.0f;
+        epl[j] = kAuto ? G.l[j] + 1 : 0;
+    }
+    store_rest<kAuto>(S, at, s, rw, epr, epl);
 #else
-        const U4 fb = draw(qk, A.t, kSlotFuel);
-        U4 gb = U4{{0u, 0u, 0u, 0u}};
-        if (gate_needed) gb = draw(qk, A.t, kSlotGate);
-#endif
+    if constexpr (kReplay) {
+        // one env at a time; a missing variate (NEED_DRAW) leaves its env untouched
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            uf[j] = u32(fb.v[j]);
-            ug[j] = u32(gb.v[j]);
-        }
-    }
-
-    // pass 2: step the 4 envs (unrolled: measured ~5 % faster than a rolled loop
-    // despite the higher register count, tools/ablate.sh)
-    uint32_t ox = 0, oy = 0, oo = 0, od = 0, dn = 0, ee = 0, fin = 0;
-    float rw[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int64_t i = base + j;
-        const bool live = kFull || i < n;
-        Ship s{byte_of(G.x, j), byte_of(G.y, j), fuel[j], cargo[j], byte_of(G.org, j),
-               byte_of(G.dst, j)};
-        int ty, va, vb, e = SE_ERR_OK;
-        if (kTyped) {
-            ty = act[j];
-            va = pa[j];
-            vb = qb[j];
-        } else {
-            e = decode_agent(w.P, act[j], ty, va, vb);
-        }
-        double r = 0.0;
-        int d = 0;
-        const Key key = env_key(A.seed, A.env_base + i);
-#if SHIPENV_ABLATE >= 2  // timing-only builds: no game logic (memory traffic kept)
-        if (true) {
-            s.x ^= ty & 1;
-            s.fuel -= uf[j];
-            r = ug[j] + (double)va + (double)vb;
-        } else
-#endif
-        uint32_t used = 0;
-        if constexpr (kReplay) {
-            const Draws<true> dr{A.tape + (live ? i : 0)};
-            e = env_step<false, true>(w, s, e, ty, va, vb, uf[j], ug[j], dr, r, d, used);
-            if (live) A.tape[i].used = (int32_t)used;
-        } else {
-            const Draws<false> dr{key, A.t};
-            e = env_step<!kTyped, false>(w, s, e, ty, va, vb, uf[j], ug[j], dr, r, d, used);
-        }
-        rw[j] = (float)r;  // one rounding of the reference's f64 reward
-        if (kReplay && live && S.reward64) S.reward64[i] = r;
-        if (kAuto && live) {
-            epr[j] += rw[j];
-            epl[j] += 1;
-            if (d) {
-                fin |= 1u << j;
-                bs.ret += (double)epr[j];
-                bs.eps += 1.0;
-                bs.len += (double)epl[j];
-                const U4 o = draw(key, A.t, kSlotReset);
-                reset_ship(w, s, o.v[0], o.v[1]);
+            const int64_t i = base + j;
+            const bool live = kFull || i < n;
+            se_tape* tp = A.tape + (live ? i : 0);
+            const Ship s0 = s[j];
+            const double uf = live ? tp->u_fuel : 0.0, ug = live ? tp->u_gate : 0.0;
+            p[j] = env_begin<false, true>(w, s[j], er[j], ty[j], va[j], vb[j], uf, ug, 0u);
+            uint32_t used = p[j].mv ? (kUsedFuelGate | (p[j].moved ? kUsedMoved : 0u)) : 0u;
+            bool need = p[j].mv && (uf != uf || ug != ug);
+            int kind = kLossNone, nd = 0;
+            double beta = 0.0;
+            if (p[j].fires) {
+                used |= kUsedLossType;
+                const double lt = tp->u_type;
+                const bool partial = s[j].cargo != 0 && lt >= 0.1 && lt <= 0.9;
+                if (partial) {
+                    used |= kUsedBeta;
+                    beta = tp->beta;
+                }
+                need = need || lt != lt || (partial && beta != beta);
+                kind = lt < 0.1 ? kLossNone : (lt > 0.9 ? kLossTotal : kLossPartial);
+            }
+            if (p[j].arrive) {
+                used |= kUsedArrive;
+                nd = tp->arrive_dest;
+                need = need || nd < 0;
+            }
+            env_finish(s[j], p[j], kind, beta, nd);
+            if (need) {  // ask the caller for the next variate; change nothing
+                s[j] = s0;
+                p[j].r = 0.0;
+                p[j].dead = false;
+                p[j].e = SE_ERR_NEED_DRAW;
+            }
+            if (live) {
+                tp->used = (int32_t)used;
+                if (S.reward64) S.reward64[i] = p[j].r;
             }
         }
-        fuel[j] = s.fuel;
-        cargo[j] = s.cargo;
-        const uint32_t sh = 8u * (uint32_t)j;
-        ox |= (uint32_t)(s.x & 0xff) << sh;
-        oy |= (uint32_t)(s.y & 0xff) << sh;
-        oo |= (uint32_t)(s.origin & 0xff) << sh;
-        od |= (uint32_t)(s.dest & 0xff) << sh;
-        dn |= (uint32_t)d << sh;
-        ee |= (uint32_t)(e & 0xff) << sh;
-    }
+        store_moved(S, at, s, p);
+        float rw[4], none[4] = {0.f, 0.f, 0.f, 0.f};
+        int32_t zero[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rw[j] = (float)p[j].r;
+        store_rest<false>(S, at, s, rw, none, zero);
+        (void)bs;
+        (void)F;
+    } else {
+        bool gate_needed = false;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            gate_needed |= (er[j] == SE_ERR_OK) & needs_gate<!kTyped>(w, s[j], ty[j], va[j], vb[j]);
+        const U4 fb = draw(qk, t, kSlotFuel);
+        U4 gb{{0u, 0u, 0u, 0u}};
+        if (gate_needed) gb = draw(qk, t, kSlotGate);
+        uint32_t fire = 0, arrive = 0, fin = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            p[j] = env_begin<!kTyped, false>(w, s[j], er[j], ty[j], va[j], vb[j], u32(fb.v[j]), 0.0, gb.v[j]);
+            fire |= (uint32_t)p[j].fires << j;
+            arrive |= (uint32_t)p[j].arrive << j;
+            fin |= (uint32_t)((kFull || base + j < n) & p[j].dead) << j;
+        }
+        // auto-reset (:227-243) of the envs that ran out of fuel, from the quad's
+        // RESET blocks: their position and fuel now, cargo / origin / dest after the
+        // second half (whose reward the finished episode still collects)
+        uint32_t reset_o = 0, reset_d = 0;  // reset origin / dest bytes of the 4 envs
+        if constexpr (kAuto) {
+            if (fin) {
+                const U4 o = draw(qk, t, kSlotReset), d = draw(qk, t, kSlotResetDest);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    Ship r;
+                    reset_ship(w, r, o.v[j], d.v[j]);
+                    reset_o |= (uint32_t)r.origin << (8 * j);
+                    reset_d |= (uint32_t)r.dest << (8 * j);
+                    const bool f = (fin >> j) & 1u;
+                    s[j].x = f ? r.x : s[j].x;
+                    s[j].y = f ? r.y : s[j].y;
+                    s[j].fuel = f ? r.fuel : s[j].fuel;
+                }
+            }
+            G.load_episode(A, at);
+        }
+        store_moved(S, at, s, p);
 
-    if constexpr (kAuto) {
-        F.mask = fin;
+        U4 lb{{0u, 0u, 0u, 0u}}, b1 = lb, b2 = lb, b3 = lb, ab = lb;
+        if (fire) lb = draw(qk, t, kSlotLoss);
+        int kind[4];
+        uint32_t partial = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            F.ret[j] = epr[j];
-            F.len[j] = epl[j];
+            const int total = lb.v[j] > kTypeHi ? kLossTotal : kLossPartial;
+            kind[j] = lb.v[j] < kTypeLo ? kLossNone : total;
+            partial |= (uint32_t)(p[j].fires & (kind[j] == kLossPartial)) << j;
         }
+        if (partial) {
+            b1 = draw(qk, t, kSlotBeta1);
+            b2 = draw(qk, t, kSlotBeta2);
+            b3 = draw(qk, t, kSlotBeta3);
+        }
+        if (arrive) ab = draw(qk, t, kSlotArrive);
+        float rw[4], epr[4];
+        int32_t epl[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            epr[j] = ((fin >> j) & 1u) ? 0.0f : epr[j];
-            epl[j] = ((fin >> j) & 1u) ? 0 : epl[j];
+            // median of the three words, then one exact conversion (monotone)
+            const uint32_t lo = min(b1.v[j], b2.v[j]), hi = max(b1.v[j], b2.v[j]);
+            const double beta = u32(max(lo, min(hi, b3.v[j])));  // v_med3_u32
+            env_finish(s[j], p[j], kind[j], beta, pick_other(ab.v[j], w.P, s[j].dest));
+            rw[j] = (float)p[j].r;  // one rounding of the reference's f64 reward
+            epr[j] = 0.0f;
+            epl[j] = 0;
+            if constexpr (kAuto) {
+                const bool f = (fin >> j) & 1u;
+                F.ret[j] = G.e[j] + rw[j];
+                F.len[j] = G.l[j] + 1;
+                if (f) {
+                    bs.ret += (double)F.ret[j];
+                    bs.eps += 1;
+                    bs.len += F.len[j];
+                }
+                epr[j] = f ? 0.0f : F.ret[j];
+                epl[j] = f ? 0 : F.len[j];
+                s[j].cargo = f ? 0 : s[j].cargo;
+                s[j].origin = f ? byte_of(reset_o, j) : s[j].origin;
+                s[j].dest = f ? byte_of(reset_d, j) : s[j].dest;
+            }
         }
-        st4<kFull>(S.ep_return, base, n, epr[0], epr[1], epr[2], epr[3]);
-        st4<kFull>(S.ep_len, base, n, epl[0], epl[1], epl[2], epl[3]);
+        if constexpr (kAuto) F.mask = fin;
+        store_rest<kAuto>(S, at, s, rw, epr, epl);
     }
-    st4u8<kFull>(S.x, base, n, ox);
-    st4u8<kFull>(S.y, base, n, oy);
-    st4u8<kFull>(S.origin, base, n, oo);
-    st4u8<kFull>(S.dest, base, n, od);
-    st4<kFull>(S.fuel, base, n, fuel[0], fuel[1], fuel[2], fuel[3]);
-    st4<kFull>(S.cargo, base, n, cargo[0], cargo[1], cargo[2], cargo[3]);
-    st4<kFull>(S.reward, base, n, rw[0], rw[1], rw[2], rw[3]);
-    st4u8<kFull>(S.done, base, n, dn);
-    st4u8<kFull>(reinterpret_cast<uint8_t*>(S.err), base, n, ee);
+#endif
 }
 
 // Done-list compaction of one grid-stride iteration (auto-reset), no global
@@ -652,35 +790,32 @@ __device__ __forceinline__ void block_compact(const StepArgs& A, const Finished&
 // Workgroup b owns the contiguous groups [b*iters*256, (b+1)*iters*256) (a group is
 // 4 consecutive envs, one thread per group per iteration), so its done-list
 // segment follows env order and the concatenated segments are globally sorted.
-// A full group's fields are single 4- or 16-byte lane accesses; the one partial
-// group at the end (n % 4 envs) is stepped in place by its owner with guarded
-// scalar accesses. The first group's loads are issued before the world is staged
-// into LDS so the staging hides under them; each iteration loads the next group
-// before storing the current one. The trip count is uniform over the block (the
-// auto-reset compaction holds barriers).
+// Every field of a group is one 4- or 16-byte lane access. The partial last group
+// (n % 4 envs) is left to step_tail_kernel, so this loop carries no guarded scalar
+// path. The first group's loads are issued before the world is staged into LDS so
+// the staging hides under them; each iteration loads the next group before storing
+// the current one. The trip count is uniform over the block (the auto-reset
+// compaction holds barriers).
 template <bool kTyped, bool kReplay, bool kAuto>
-__global__ __launch_bounds__(kBlock) void step_kernel(StepArgs A) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void step_kernel(StepArgs A) {
     extern __shared__ uint32_t lds[];
     __shared__ double red[kBlock / 64][3];
     __shared__ int32_t wtot[kBlock / 64];
-    const int64_t full = A.n >> 2, groups = (A.n + 3) >> 2;
-    const int64_t first = (int64_t)blockIdx.x * A.iters * kBlock + threadIdx.x;
+    const int64_t full = A.n >> 2;
+    const int64_t first = (int64_t)blockIdx.x * A.iters * kBlock;  // block-uniform first group
 
     Group<kTyped, kAuto> G;
-    if (first < full) G.template load<true>(A, first * 4);
+    if (first + threadIdx.x < full) G.template load<true>(A, At<true>{first, 0, A.n});
     const LdsWorld w = stage_world(A.world, A.dims, lds);
 
     BlockStats bs;
     int32_t running = 0;  // this block's done records so far (block-uniform)
     for (int64_t k = 0; k < A.iters; ++k) {
-        const int64_t g = first + k * kBlock;
+        const int64_t g0 = first + k * kBlock, g = g0 + threadIdx.x;
         Finished F;
         if (g < full) {
-            step_group<kTyped, kReplay, kAuto, true>(A, w, G, g * 4, bs, F);
-            if (k + 1 < A.iters && g + kBlock < full) G.template load<true>(A, (g + kBlock) * 4);
-        } else if (g < groups) {  // the partial last group
-            G.template load<false>(A, g * 4);
-            step_group<kTyped, kReplay, kAuto, false>(A, w, G, g * 4, bs, F);
+            step_group<kTyped, kReplay, kAuto, true>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F);
+            if (k + 1 < A.iters && g + kBlock < full) G.template load<true>(A, At<true>{g0 + kBlock, 0, A.n});
         }
         if constexpr (kAuto) block_compact(A, F, g * 4, wtot, running, k + 1 == A.iters);
     }
@@ -688,17 +823,18 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs A) {
     if (kAuto) {
         if (threadIdx.x == 0) A.done_count[blockIdx.x] = running;
         // per-block statistics: fixed-order wave butterfly, then waves in order
+        double ret = bs.ret, eps = (double)bs.eps, len = (double)bs.len;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
-            bs.ret += __shfl_xor(bs.ret, off);
-            bs.eps += __shfl_xor(bs.eps, off);
-            bs.len += __shfl_xor(bs.len, off);
+            ret += __shfl_xor(ret, off);
+            eps += __shfl_xor(eps, off);
+            len += __shfl_xor(len, off);
         }
         const int wave = threadIdx.x >> 6;
         if ((threadIdx.x & 63) == 0) {
-            red[wave][0] = bs.ret;
-            red[wave][1] = bs.eps;
-            red[wave][2] = bs.len;
+            red[wave][0] = ret;
+            red[wave][1] = eps;
+            red[wave][2] = len;
         }
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -717,6 +853,57 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs A) {
         }
     }
 }
+
+// The partial last group (n % 4 envs), launched after step_kernel on the same
+// stream when n % 4 != 0: one thread steps it with guarded scalar accesses. Its
+// envs are the last of workgroup b's range, so auto-reset appends their records
+// to b's segment after step_kernel's and adds their statistics to b's slab entry
+// (env order and a fixed summation order, as in the main kernel).
+template <bool kTyped, bool kReplay, bool kAuto>
+__global__ __launch_bounds__(64) void step_tail_kernel(StepArgs A) {
+    extern __shared__ uint32_t lds[];
+    const LdsWorld w = stage_world(A.world, A.dims, lds);
+    if (threadIdx.x != 0) return;
+    const int64_t g = A.n >> 2;
+    const At<false> at{0, g * 4, A.n};
+    Group<kTyped, kAuto> G;
+    G.template load<false>(A, at);
+    BlockStats bs;
+    Finished F;
+    step_group<kTyped, kReplay, kAuto, false>(A, w, G, at, bs, F);
+    if constexpr (kAuto) {
+        const int64_t b = g / (A.iters * kBlock);
+        int32_t c = A.done_count[b];
+        for (int j = 0; j < 4; ++j)
+            if ((F.mask >> j) & 1u)
+                A.done_recs[b * A.seg + c++] = se_done_rec{(int32_t)(at.base + j), F.ret[j], F.len[j], (int32_t)A.t};
+        A.done_count[b] = c;
+        if (bs.eps != 0) {
+            double* sl = A.slab + 4 * b;
+            sl[0] += bs.ret;
+            sl[1] += (double)bs.eps;
+            sl[2] += (double)bs.len;
+        }
+    }
+}
+
+#ifdef SHIPENV_ISA_PROBE  // inspection only: one env's two halves in isolation
+__global__ void probe_kernel(const uint32_t* world, WorldDims d, const int* in, double* out) {
+    extern __shared__ uint32_t lds[];
+    const LdsWorld w = stage_world(world, d, lds);
+    const int i = threadIdx.x;
+    int ty, va, vb;
+    const int er = decode_agent(w.P, in[i], ty, va, vb);
+    Ship s{in[i + 64], in[i + 128], (double)in[i + 192], in[i + 256], in[i + 320], in[i + 384]};
+    asm volatile("; probe: begin" ::: "memory");
+    Pending p = env_begin<true, false>(w, s, er, ty, va, vb, u32((uint32_t)in[i + 448]), 0.0,
+                                       (uint32_t)in[i + 512]);
+    asm volatile("; probe: finish" ::: "memory");
+    env_finish(s, p, in[i + 576], u32((uint32_t)in[i + 640]), in[i + 704]);
+    asm volatile("; probe: end" ::: "memory");
+    out[i] = p.r + s.fuel + (double)(s.x + s.y + s.cargo + s.origin + s.dest + p.e + p.fires + p.arrive + p.dead);
+}
+#endif
 
 // Contiguous copy of the last step's per-block done lists (se_done_compact): block
 // b sums the counts before it (grid <= 2048 entries) and copies its segment.
@@ -1011,7 +1198,26 @@ int upload_world(se_env* env, int32_t P, const int32_t* px, const int32_t* py, c
     for (int c = 0; c < 50; ++c) {
         const double q = (double)c / kMaxCargo;
         memcpy(&img[d.frac() + 2 * c], &q, sizeof q);
+        img[d.gate() + c] = (uint32_t)floor(ldexp(q, 32));  // exact product, q < 1
     }
+    // step rewards before cargo loss / arrival, added in the reference's order:
+    // out of fuel (:288-290), ground (:293-294) or fuel + water (:296-300), closer (:307-315)
+    double rtab[10];
+    for (int k = 0; k < 8; ++k) {
+        double r = 0.0;
+        if (k & 4) r += -10.0;
+        if (k & 2) {
+            r += -5.0;
+        } else {
+            r += -0.0001;
+            r += -1.0;
+        }
+        r += (k & 1) ? 2.0 : -2.0;
+        rtab[k] = r;
+    }
+    rtab[8] = 0.05;  // TAKE_FUEL / TAKE_CARGO (:349, :357)
+    rtab[9] = 0.0;
+    memcpy(&img[d.rtab()], rtab, sizeof rtab);
     if (d.total() > env->world_cap) {
         if (env->d_world) HIP_TRY(hipFree(env->d_world));
         env->d_world = nullptr;
@@ -1073,6 +1279,14 @@ int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const 
         else if (typed && replay) step_kernel<true, true, false><<<grid, kBlock, lds, s>>>(A);
         else if (typed && !autoreset) step_kernel<true, false, false><<<grid, kBlock, lds, s>>>(A);
         else step_kernel<true, false, true><<<grid, kBlock, lds, s>>>(A);
+        HIP_TRY(hipGetLastError());
+    }
+    if (env->n & 3) {
+        if (!typed && !autoreset) step_tail_kernel<false, false, false><<<1, 64, lds, s>>>(A);
+        else if (!typed && autoreset) step_tail_kernel<false, false, true><<<1, 64, lds, s>>>(A);
+        else if (typed && replay) step_tail_kernel<true, true, false><<<1, 64, lds, s>>>(A);
+        else if (typed && !autoreset) step_tail_kernel<true, false, false><<<1, 64, lds, s>>>(A);
+        else step_tail_kernel<true, false, true><<<1, 64, lds, s>>>(A);
         HIP_TRY(hipGetLastError());
     }
     if (!replay) env->step_t += 1;

@@ -174,7 +174,10 @@ def test_config2_move_only_vs_oracle(oracle_mod, n):
     env.close()
 
 
-def test_config3_full_mix_vs_oracle(oracle_mod):
+@pytest.mark.parametrize("blocks", [None, "3"])
+def test_config3_full_mix_vs_oracle(oracle_mod, monkeypatch, blocks):
+    if blocks:  # several groups per thread, partial last workgroup
+        monkeypatch.setenv("SHIPENV_STEP_BLOCKS", blocks)
     O = oracle_mod
     seed, n = 77, 8192
     env = VecEnv(n, seed=seed)
@@ -198,11 +201,16 @@ def test_config3_full_mix_vs_oracle(oracle_mod):
     env.close()
 
 
-def test_config4_autoreset_64_ports_vs_oracle(oracle_mod, water):
+@pytest.mark.parametrize("n,blocks", [(8192, None), (8195, "3")])
+def test_config4_autoreset_64_ports_vs_oracle(oracle_mod, water, monkeypatch, n, blocks):
+    """blocks="3": 3 workgroups, several groups per thread (double-buffered loads),
+    a partial last workgroup and a tail group appended to its done segment."""
     from shippingenv_amd.vec import random_water_ports
 
+    if blocks:
+        monkeypatch.setenv("SHIPENV_STEP_BLOCKS", blocks)
     O = oracle_mod
-    seed, n = 4242, 8192
+    seed = 4242
     ports = random_water_ports(water, 64, seed=3)
     env = VecEnv(n, seed=seed, ports=ports, auto_reset=True)
     world, st = _oracle_pair(O, env)
