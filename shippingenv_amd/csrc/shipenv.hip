@@ -92,8 +92,10 @@ struct LdsWorld {
     const double* rtab;
     int32_t H, W, P;
 
+    // cell index x * W + y: coordinates and W are below 256, so 24-bit multiplies
+    // (full rate) are exact where a 32-bit one would be a 64-bit-product op
     __device__ bool is_ground(int x, int y) const {
-        const uint32_t c = (uint32_t)(x * W + y);
+        const uint32_t c = __umul24((uint32_t)x, (uint32_t)W) + (uint32_t)y;
         return (ground[c >> 5] >> (c & 31)) & 1u;
     }
     // _get_current_port_idx (:145-153): first port on the ship's cell, -1 if none.
@@ -101,7 +103,7 @@ struct LdsWorld {
     // at most P (rank2port has P + 1 entries), so the read is unconditional: no
     // branch (and exec mask) around it.
     __device__ int port_at(int x, int y) const {
-        const uint32_t c = (uint32_t)(x * W + y);
+        const uint32_t c = __umul24((uint32_t)x, (uint32_t)W) + (uint32_t)y;
         const uint32_t word = portbit[c >> 5], bit = c & 31;
         const int rank = (int)prefix[c >> 5] + __popc(word & ((1u << bit) - 1u));
         const int first = rank2port[rank];
@@ -222,8 +224,8 @@ __device__ __forceinline__ Pending env_begin(const LdsWorld& w, Ship& s, int e_i
     // distances are small integers, so comparing them is exact
     const int dcl = no_dest ? 0 : s.dest;
     const int px = w.px(dcl), py = w.py(dcl);
-    const int d_old = (s.x - px) * (s.x - px) + (s.y - py) * (s.y - py);
-    const int d_new = (cx - px) * (cx - px) + (cy - py) * (cy - py);
+    const int d_old = __mul24(s.x - px, s.x - px) + __mul24(s.y - py, s.y - py);  // |d| < 256
+    const int d_new = __mul24(cx - px, cx - px) + __mul24(cy - py, cy - py);
     const bool closer = d_old > d_new;
 
     // --- SELECT_PORT (_select_port :265-271)
