@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--no-config4", action="store_true")
     p.add_argument("--large-n", type=int, default=1 << 24,
                    help="extra HBM-resident run (working set beyond the 256 MiB MALL); 0 = skip")
+    p.add_argument("--rollouts", type=int, default=20,
+                   help="timed se_rollout launches (MCTS random rollouts, 2^20 x 100 steps); 0 = skip")
     return p.parse_args()
 
 
@@ -130,6 +132,8 @@ def run_config(n, ports, auto, args, dist, label):
     env.reset()
     for k in range(args.warmup):
         env.step(acts[k])
+    if auto:  # the stats path runs inside the timed region: load its kernels now
+        dist.D.reduce_episode_stats(env.episode_stats().clone())
     torch.cuda.synchronize()
     if auto:
         env.clear_stats()
@@ -144,6 +148,48 @@ def run_config(n, ports, auto, args, dist, label):
     del acts
     torch.cuda.empty_cache()
     return wall, k_ms, stats
+
+
+def run_rollouts(n, args, dist):
+    """MCTS random rollouts (agents/mcts.py:211-238, se_rollout): one rollout of up to
+    100 counted steps from each of the n envs of the config-3 set, after 50 policy
+    steps; rollout ids are fresh per launch. Rate = counted env-steps / time."""
+    from shippingenv_amd.vec import VecEnv
+
+    env = VecEnv(n, seed=args.seed, env_id_base=dist.rank * n, device=dist.dev)
+    env.reset()
+    for t in range(50):
+        env.step(env.gen_actions(t))
+    src = torch.arange(n, dtype=torch.int32, device=env.device)
+    for k in range(2):  # warm (and load the reduction kernel used after timing)
+        _, steps, _ = env.rollout(src, max_steps=100, rollout_base=(dist.rank * 1000 + k) * n)
+        int(steps.sum().item())
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(env.device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    kept = []  # counted steps per launch, summed after the timed region
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for k in range(args.rollouts):
+        kept.append(env.rollout(src, max_steps=100, rollout_base=(dist.rank * 1000 + 2 + k) * n)[1])
+    e1.record(stream)
+    torch.cuda.synchronize()
+    dist.barrier()
+    wall = dist.max(time.perf_counter() - t0)
+    total = float(sum(int(s.sum().item()) for s in kept))
+    env.close()
+    return {
+        "workload": "se_rollout: 2^20 rollouts/GPU from config-3 states, max 100 counted steps "
+                    "(sample_action + step, retries uncounted), Philox per rollout",
+        "launches": args.rollouts,
+        "value": round(total * dist.world / wall, 1),
+        "unit": "rollout env-steps/s",
+        "ms_per_launch": round(wall / args.rollouts * 1e3, 4),
+        "kernel_ms": round(e0.elapsed_time(e1) / args.rollouts, 4),
+        "mean_steps_per_rollout": round(total / (args.rollouts * n), 2),
+    }
 
 
 def roofline(bytes_per_step, n, k_ms, canonical):
@@ -254,6 +300,9 @@ def main():
             "mean_return": stats[0] / stats[1] if stats and stats[1] else None,
             "mean_len": stats[2] / stats[1] if stats and stats[1] else None,
         }
+
+    if args.rollouts:
+        out["rollouts"] = run_rollouts(n, args, dist)
 
     if args.large_n and dist.world == 1:
         small = argparse.Namespace(**vars(args))

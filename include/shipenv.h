@@ -164,6 +164,38 @@ int se_valid_mask(se_env* env, uint8_t* bits, void* stream);
  * bench mix (90% move, 5% take cargo U{1..20}, 3% take fuel U{1..20}, 2% select). */
 int se_gen_actions(se_env* env, int32_t* actions, uint32_t t, void* stream);
 
+/* sample_action() (environment.py:245-263), the random policy of MCTS rollouts and
+ * SARSA exploration, for every env from its current state, as typed actions (the
+ * input of se_step_typed). One draw per env: Philox(seed, env) at (t, slot 11) word 0.
+ *   at a port with no destination: SELECT_PORT uniform over the other ports   :247-253
+ *   at a port with cargo 0:        TAKE_CARGO U{1..port_cargo} (randint :160)  :255-257
+ *   at a port with fuel == 0:      the reference raises TypeError (self.fuel[idx], :163)
+ *   otherwise:                     MOVE_SHIP N/E/S/W uniform (random.choice :165-167)
+ * Where the reference raises (the fuel branch; randint(1, 0) on an empty port) the
+ * type is SE_SAMPLE_RAISES; where it never returns (no other port, :253) it is
+ * SE_SAMPLE_NO_OTHER_PORT. */
+#define SE_SAMPLE_RAISES (-1)
+#define SE_SAMPLE_NO_OTHER_PORT (-2)
+int se_sample_actions(se_env* env, int32_t* type, int32_t* a, int32_t* b, uint32_t t, void* stream);
+
+/* MCTS random rollouts (agents/mcts.py:211-238): rollout r starts from a copy of env
+ * src[r]'s state (env state is not modified) and repeats sample_action + step until
+ * the step reports done, max_steps steps have counted, or max_attempts attempts
+ * have run. An attempt whose step raises is retried without counting (the
+ * reference's `except Exception: continue`). Outputs (device, m entries):
+ * ret[r] = the step rewards summed in f64 in order (total_reward, :226-230);
+ * steps[r] = counted steps; status[r] = SE_ROLL_*.
+ * Draws: Philox(seed, rollout_base + r) at (attempt, slot 12): sample word, u_fuel,
+ * u_gate, u_type; and, for a partial loss or an arrival, (attempt, slot 13): three
+ * beta uniforms, the new destination. */
+#define SE_ROLL_DONE 0        /* the last counted step reported done */
+#define SE_ROLL_MAX_STEPS 1   /* max_steps steps counted */
+#define SE_ROLL_RAISED 2      /* sample_action raised; the exception leaves _rollout */
+#define SE_ROLL_ATTEMPTS 3    /* max_attempts reached (the reference keeps retrying) */
+#define SE_ROLL_BAD_SRC 4     /* src[r] outside [0, n) */
+int se_rollout(se_env* env, const int32_t* src, int64_t m, int32_t max_steps, int32_t max_attempts,
+               int64_t rollout_base, double* ret, int32_t* steps, int32_t* status, void* stream);
+
 /* Episode statistics accumulated by the auto-reset path since the last clear:
  * out[0] = sum of returns, out[1] = episodes, out[2] = sum of lengths (device
  * double[3]). Deterministic: per-block partials are summed in a fixed order. */

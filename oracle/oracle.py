@@ -46,6 +46,8 @@ def _lib():
     lib.orc_valid_mask.argtypes = [P, i64] + [P] * 4
     lib.orc_philox4x32_10.argtypes = [P, P, P]
     lib.orc_gen_actions.argtypes = [i64, i32, u64, i64, u32, P]
+    lib.orc_sample_actions.argtypes = [P, i64] + [P] * 6 + [u64, i64, u32, P, P, P]
+    lib.orc_rollout.argtypes = [P, i64] + [P] * 6 + [i64, P, i32, i32, u64, i64, P, P, P]
     return lib
 
 
@@ -167,3 +169,22 @@ def gen_actions(n, P, seed, env_id_base=0, t=0):
     out = np.zeros(n, np.int32)
     lib().orc_gen_actions(n, P, seed, env_id_base, t, _p(out))
     return out
+
+
+def sample_actions(world, st, *, seed, env_id_base=0, t=0):
+    """sample_action (environment.py:245-263) per env -> (type, a, b) int32 arrays."""
+    ty, a, b = (np.zeros(st.n, np.int32) for _ in range(3))
+    lib().orc_sample_actions(world.ref, st.n, *st.fields(), seed, env_id_base, t, _p(ty), _p(a), _p(b))
+    return ty, a, b
+
+
+def rollout(world, st, src, *, max_steps, max_attempts, seed, rollout_base=0):
+    """MCTS random rollouts (agents/mcts.py:211-238) -> (ret f64, steps i32, status i32)."""
+    s = np.ascontiguousarray(src, np.int32)
+    m = len(s)
+    ret = np.zeros(m, np.float64)
+    steps = np.zeros(m, np.int32)
+    status = np.zeros(m, np.int32)
+    lib().orc_rollout(world.ref, st.n, *st.fields(), m, _p(s), max_steps, max_attempts, seed,
+                      rollout_base, _p(ret), _p(steps), _p(status))
+    return ret, steps, status

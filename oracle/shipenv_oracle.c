@@ -47,7 +47,11 @@ enum { U_FUEL_GATE = 1, U_LOSS_TYPE = 2, U_BETA = 4, U_ARRIVE = 8 };
  * explicit reset and the synthetic agent draw one block per env. */
 enum { SLOT_FUEL = 0, SLOT_LOSS = 1, SLOT_BETA1 = 2, SLOT_ARRIVE = 3, SLOT_RESET = 4,
        SLOT_EXPLICIT_RESET = 5, SLOT_ACTION = 6, SLOT_GATE = 7, SLOT_BETA2 = 8, SLOT_BETA3 = 9,
-       SLOT_RESET_DEST = 10 };
+       SLOT_RESET_DEST = 10, SLOT_SAMPLE = 11, SLOT_ROLLOUT = 12, SLOT_ROLLOUT_B = 13 };
+
+/* sample_action results where the reference raises / never returns (include/shipenv.h) */
+enum { SAMPLE_RAISES = -1, SAMPLE_NO_OTHER_PORT = -2 };
+enum { ROLL_DONE = 0, ROLL_MAX_STEPS = 1, ROLL_RAISED = 2, ROLL_ATTEMPTS = 3, ROLL_BAD_SRC = 4 };
 
 /* ------------------------------------------------------------------ Philox4x32-10 */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
@@ -96,7 +100,16 @@ typedef struct {
     uint32_t t;
     int32_t used;         /* U_* bits of the draws consumed */
     int need;             /* replay: a consumed draw is missing from the tape */
+    const uint32_t* roll; /* rollout attempt t of rollout `env`: block A words (sample,
+                             u_fuel, u_gate, u_type); block B (slot ROLLOUT_B) on demand */
 } source;
+
+/* rollout block B word k (three beta uniforms, the arrival redraw) */
+static uint32_t roll_b(const source* s, int k) {
+    uint32_t o[4];
+    draw4(s->seed, s->env, s->t, SLOT_ROLLOUT_B, o);
+    return o[k];
+}
 
 /* Philox: env e takes word e & 3 of the block at counter (e >> 2, t, slot) as a
  * 32-bit value; uniforms are u = w * 2^-32. */
@@ -117,6 +130,11 @@ static void src_move(source* s, double* u_fuel, double* u_gate) {
         s->need |= isnan(*u_fuel) || isnan(*u_gate);
         return;
     }
+    if (s->roll) {
+        *u_fuel = u32(s->roll[1]);
+        *u_gate = u32(s->roll[2]);
+        return;
+    }
     *u_fuel = u32(quad_word(s->seed, s->env, s->t, SLOT_FUEL));
     *u_gate = u32(quad_word(s->seed, s->env, s->t, SLOT_GATE));
 }
@@ -127,6 +145,7 @@ static double src_loss_type(source* s) { /* environment.py:177 */
         s->need |= isnan(s->tape->u_type);
         return s->tape->u_type;
     }
+    if (s->roll) return u32(s->roll[3]);
     return u32(quad_word(s->seed, s->env, s->t, SLOT_LOSS));
 }
 
@@ -138,6 +157,7 @@ static double src_beta(source* s) {
         s->need |= isnan(s->tape->beta);
         return s->tape->beta;
     }
+    if (s->roll) return med3(u32(roll_b(s, 0)), u32(roll_b(s, 1)), u32(roll_b(s, 2)));
     return med3(u32(quad_word(s->seed, s->env, s->t, SLOT_BETA1)),
                 u32(quad_word(s->seed, s->env, s->t, SLOT_BETA2)),
                 u32(quad_word(s->seed, s->env, s->t, SLOT_BETA3)));
@@ -149,6 +169,7 @@ static int32_t src_arrive(source* s, int32_t P, int32_t origin) { /* :333-335 */
         s->need |= s->tape->arrive_dest < 0;
         return s->tape->arrive_dest;
     }
+    if (s->roll) return pick_other(roll_b(s, 3), P, origin);
     return pick_other(quad_word(s->seed, s->env, s->t, SLOT_ARRIVE), P, origin);
 }
 
@@ -320,7 +341,7 @@ int orc_step_batch(const orc_world* w, int64_t n, int act_mode, const int32_t* a
     for (int64_t i = 0; i < n; ++i) {
         ship s;
         load(&s, i, x, y, fuel, cargo, origin, dest);
-        source src = {tape ? tape + i : NULL, seed, env_id_base + i, t, 0, 0};
+        source src = {tape ? tape + i : NULL, seed, env_id_base + i, t, 0, 0, NULL};
         int32_t ty = 0, a = 0, b = 0;
         int e;
         double r = 0.0;
@@ -409,6 +430,98 @@ int orc_step_batch_autoreset(const orc_world* w, int64_t n, const int32_t* actio
             ep_return[i] = 0.0f;
             ep_len[i] = 0;
         }
+    }
+    return 0;
+}
+
+/* sample_action, environment.py:245-263, from one Philox word r. Returns the
+ * action type, or SAMPLE_RAISES / SAMPLE_NO_OTHER_PORT where the reference raises
+ * or never returns. */
+static int32_t sample_action(const orc_world* w, const ship* s, uint32_t r, int32_t* a, int32_t* b) {
+    static const int32_t mx[4] = {0, -1, 0, 1}; /* random.choice([NORTH, EAST, SOUTH, WEST]) :165-167 */
+    static const int32_t my[4] = {-1, 0, 1, 0};
+    const int32_t cur = current_port(w, s); /* _get_current_port_idx :145-153 */
+    *a = 0;
+    *b = 0;
+    if (s->dest < 0 && cur >= 0) { /* :247-253: randint until != current port */
+        if (w->P < 2) return SAMPLE_NO_OTHER_PORT;
+        *a = pick_other(r, w->P, cur);
+        return SELECT_PORT;
+    }
+    if (s->cargo == 0 && cur >= 0) { /* :255-257, randint(1, port_cargo[idx]) :160 */
+        if (w->port_cargo[cur] < 1) return SAMPLE_RAISES; /* randint(1, 0): ValueError */
+        *a = 1 + uniform_int(r, w->port_cargo[cur]);
+        return TAKE_CARGO;
+    }
+    if (s->fuel == 0.0 && cur >= 0) return SAMPLE_RAISES; /* self.fuel[idx]: TypeError :163 */
+    *a = mx[r & 3];
+    *b = my[r & 3];
+    return MOVE_SHIP;
+}
+
+int orc_sample_actions(const orc_world* w, int64_t n, const int32_t* x, const int32_t* y,
+                       const double* fuel, const int32_t* cargo, const int32_t* origin,
+                       const int32_t* dest, uint64_t seed, int64_t env_id_base, uint32_t t,
+                       int32_t* type, int32_t* a, int32_t* b) {
+    for (int64_t i = 0; i < n; ++i) {
+        ship s;
+        load(&s, i, x, y, fuel, cargo, origin, dest);
+        uint32_t o[4];
+        draw4(seed, env_id_base + i, t, SLOT_SAMPLE, o);
+        type[i] = sample_action(w, &s, o[0], &a[i], &b[i]);
+    }
+    return 0;
+}
+
+/* MCTSAgent._rollout, agents/mcts.py:211-238: sample_action + step until done or
+ * max_steps counted steps; a raising step is retried without counting (:231-233),
+ * a raising sample_action leaves the loop (it sits outside the try, :227). The
+ * reference retries without bound; max_attempts bounds it. */
+int orc_rollout(const orc_world* w, int64_t n, const int32_t* x, const int32_t* y,
+                const double* fuel, const int32_t* cargo, const int32_t* origin,
+                const int32_t* dest, int64_t m, const int32_t* src, int32_t max_steps,
+                int32_t max_attempts, uint64_t seed, int64_t rollout_base, double* ret,
+                int32_t* steps, int32_t* status) {
+    for (int64_t r = 0; r < m; ++r) {
+        const int64_t i = src[r];
+        if (i < 0 || i >= n) {
+            ret[r] = 0.0;
+            steps[r] = 0;
+            status[r] = ROLL_BAD_SRC;
+            continue;
+        }
+        ship s;
+        load(&s, i, x, y, fuel, cargo, origin, dest);
+        double total = 0.0;
+        int32_t counted = 0, st = ROLL_ATTEMPTS;
+        for (int32_t k = 0; k < max_attempts; ++k) {
+            if (counted >= max_steps) { /* while not done and steps < max_rollout_steps (:225) */
+                st = ROLL_MAX_STEPS;
+                break;
+            }
+            uint32_t blk[4];
+            draw4(seed, rollout_base + r, (uint32_t)k, SLOT_ROLLOUT, blk);
+            int32_t a, b;
+            const int32_t ty = sample_action(w, &s, blk[0], &a, &b);
+            if (ty < 0) {
+                st = ROLL_RAISED;
+                break;
+            }
+            source src = {NULL, seed, rollout_base + r, (uint32_t)k, 0, 0, blk};
+            double rw = 0.0;
+            int32_t d = 0;
+            if (step_typed(w, &s, ty, a, b, &src, &rw, &d) != E_OK) continue;
+            total += rw; /* total_reward += reward (:229) */
+            counted += 1;
+            if (d) {
+                st = ROLL_DONE;
+                break;
+            }
+        }
+        if (st == ROLL_ATTEMPTS && counted >= max_steps) st = ROLL_MAX_STEPS;
+        ret[r] = total;
+        steps[r] = counted;
+        status[r] = st;
     }
     return 0;
 }

@@ -76,6 +76,21 @@ int orc_valid_mask(const orc_world* w, int64_t n, const int32_t* x, const int32_
                    const int32_t* origin, uint8_t* bits);
 
 /* Philox4x32-10 block, for known-answer tests. */
+/* sample_action (environment.py:245-263) per env from Philox(seed, env) at (t, slot
+ * 11) word 0; type < 0 where the reference raises (-1) or never returns (-2). */
+int orc_sample_actions(const orc_world* w, int64_t n, const int32_t* x, const int32_t* y,
+                       const double* fuel, const int32_t* cargo, const int32_t* origin,
+                       const int32_t* dest, uint64_t seed, int64_t env_id_base, uint32_t t,
+                       int32_t* type, int32_t* a, int32_t* b);
+
+/* MCTS random rollouts (agents/mcts.py:211-238) from copies of envs src[r]; draws
+ * Philox(seed, rollout_base + r) at (attempt, slots 12 and 13). */
+int orc_rollout(const orc_world* w, int64_t n, const int32_t* x, const int32_t* y,
+                const double* fuel, const int32_t* cargo, const int32_t* origin,
+                const int32_t* dest, int64_t m, const int32_t* src, int32_t max_steps,
+                int32_t max_attempts, uint64_t seed, int64_t rollout_base, double* ret,
+                int32_t* steps, int32_t* status);
+
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 
 /* synthetic action stream used by the bench (config 3/4 mix), oracle side. */

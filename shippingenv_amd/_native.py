@@ -24,10 +24,15 @@ ERR_NEED_DRAW = 10
 # se_tape.used bits
 USED_FUEL_GATE, USED_LOSS_TYPE, USED_BETA, USED_ARRIVE, USED_MOVED = 1, 2, 4, 8, 16
 
+# se_sample_actions special types, se_rollout statuses
+SAMPLE_RAISES, SAMPLE_NO_OTHER_PORT = -1, -2
+ROLL_DONE, ROLL_MAX_STEPS, ROLL_RAISED, ROLL_ATTEMPTS, ROLL_BAD_SRC = 0, 1, 2, 3, 4
+
 # every symbol include/shipenv.h declares
 EXPORTS = (
     "se_create", "se_set_ports", "se_bind", "se_reset", "se_reset_to", "se_step",
     "se_step_typed", "se_step_replay", "se_observe", "se_valid_mask", "se_gen_actions",
+    "se_sample_actions", "se_rollout",
     "se_episode_stats", "se_clear_stats", "se_done_layout", "se_done_list", "se_done_compact",
     "se_get_counters", "se_set_counters",
     "se_destroy", "se_last_error", "se_abi_version",
@@ -70,6 +75,8 @@ def _declare(lib):
         "se_observe": [P, P, i64, P],
         "se_valid_mask": [P, P, P],
         "se_gen_actions": [P, P, u32, P],
+        "se_sample_actions": [P, P, P, P, u32, P],
+        "se_rollout": [P, P, i64, i32, i32, i64, P, P, P, P],
         "se_episode_stats": [P, P, P],
         "se_clear_stats": [P, P],
         "se_done_layout": [P, C.POINTER(i64), C.POINTER(i32)],

@@ -26,6 +26,9 @@ enum Slot : uint32_t {
     kSlotBeta2 = 8,
     kSlotBeta3 = 9,
     kSlotResetDest = 10,     // auto-reset inside step t: destination
+    kSlotSample = 11,        // se_sample_actions, per env: word 0
+    kSlotRollout = 12,       // rollout attempt, per rollout: sample word, u_fuel, u_gate, u_type
+    kSlotRolloutB = 13,      // rollout attempt (partial loss / arrival): 3 beta uniforms, dest
 };
 
 struct U4 {

@@ -1072,6 +1072,133 @@ __global__ __launch_bounds__(kBlock) void gen_actions_kernel(int64_t n, int64_t 
     }
 }
 
+// ------------------------------------------------------------------ random policy
+// sample_action() (environment.py:245-263) on one env from one Philox word r.
+__device__ __forceinline__ void sample_action(const LdsWorld& w, const Ship& s, uint32_t r, int& type,
+                                              int& a, int& b) {
+    const int cur = w.port_at(s.x, s.y);  // _get_current_port_idx (:145-153)
+    a = 0;
+    b = 0;
+    if (s.dest == SE_NONE && cur >= 0) {  // :247-253, redraw while == current port
+        type = w.P < 2 ? SE_SAMPLE_NO_OTHER_PORT : 2;
+        a = pick_other(r, w.P, cur);
+    } else if (s.cargo == 0 && cur >= 0) {  // :255-257, randint(1, port_cargo[idx]) :160
+        const int stock = w.pcargo[cur];
+        type = stock < 1 ? SE_SAMPLE_RAISES : 4;  // randint(1, 0): ValueError
+        a = 1 + uniform_int(r, (uint32_t)max(stock, 1));
+    } else if (s.fuel == 0.0 && cur >= 0) {  // :258-260: self.fuel[idx] raises TypeError (:163)
+        type = SE_SAMPLE_RAISES;
+    } else {  // random.choice([NORTH, EAST, SOUTH, WEST]) (:165-167, shipping/type.py:8-16)
+        const int k = (int)(r & 3u), odd = k & 1;
+        type = 1;
+        a = odd * (k - 2);
+        b = (1 - odd) * (k - 1);
+    }
+    if (type < 0) {  // no action: the reference raises / never returns
+        a = 0;
+        b = 0;
+    }
+}
+
+struct SampleArgs {
+    const uint32_t* world;
+    WorldDims dims;
+    int64_t n, env_base;
+    uint64_t seed;
+    uint32_t t;
+    se_state st;
+    int32_t* type;
+    int32_t* a;
+    int32_t* b;
+};
+
+__global__ __launch_bounds__(kBlock) void sample_kernel(SampleArgs A) {
+    extern __shared__ uint32_t lds[];
+    const LdsWorld w = stage_world(A.world, A.dims, lds);
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < A.n;
+         i += (int64_t)gridDim.x * kBlock) {
+        const Ship s{A.st.x[i], A.st.y[i], A.st.fuel[i], A.st.cargo[i], A.st.origin[i], A.st.dest[i]};
+        const U4 d = draw(env_key(A.seed, A.env_base + i), A.t, kSlotSample);
+        int ty, va, vb;
+        sample_action(w, s, d.v[0], ty, va, vb);
+        A.type[i] = ty;
+        A.a[i] = va;
+        A.b[i] = vb;
+    }
+}
+
+// MCTS rollouts (agents/mcts.py:211-238), one per thread: a private copy of env
+// src[r], then sample_action + step until done / max_steps counted steps /
+// max_attempts attempts. A raising step is retried without counting (:231-233);
+// a raising sample_action ends the rollout (it sits outside the try, :227).
+struct RolloutArgs {
+    const uint32_t* world;
+    WorldDims dims;
+    int64_t n, m, rollout_base;
+    uint64_t seed;
+    int32_t max_steps, max_attempts;
+    se_state st;
+    const int32_t* src;
+    double* ret;
+    int32_t* steps;
+    int32_t* status;
+};
+
+__global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs A) {
+    extern __shared__ uint32_t lds[];
+    const LdsWorld w = stage_world(A.world, A.dims, lds);
+    for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < A.m;
+         r += (int64_t)gridDim.x * kBlock) {
+        const int64_t i = A.src[r];
+        if (i < 0 || i >= A.n) {
+            A.ret[r] = 0.0;
+            A.steps[r] = 0;
+            A.status[r] = SE_ROLL_BAD_SRC;
+            continue;
+        }
+        Ship s{A.st.x[i], A.st.y[i], A.st.fuel[i], A.st.cargo[i], A.st.origin[i], A.st.dest[i]};
+        const Key key = env_key(A.seed, A.rollout_base + r);
+        double total = 0.0;
+        int32_t steps = 0, status = SE_ROLL_ATTEMPTS;
+        for (int32_t k = 0; k < A.max_attempts; ++k) {
+            if (steps >= A.max_steps) {  // while not done and steps < max_rollout_steps (:225)
+                status = SE_ROLL_MAX_STEPS;
+                break;
+            }
+            const U4 d = draw(key, (uint32_t)k, kSlotRollout);
+            int ty, va, vb;
+            sample_action(w, s, d.v[0], ty, va, vb);
+            if (ty < 0) {
+                status = SE_ROLL_RAISED;
+                break;
+            }
+            Pending p = env_begin<true, false>(w, s, SE_ERR_OK, ty, va, vb, u32(d.v[1]), 0.0, d.v[2]);
+            if (p.e != SE_ERR_OK) continue;  // except Exception: continue (state untouched)
+            const int total_kind = d.v[3] > kTypeHi ? kLossTotal : kLossPartial;
+            const int kind = d.v[3] < kTypeLo ? kLossNone : total_kind;
+            double beta = 0.0;
+            int nd = 0;
+            if ((p.fires & (kind == kLossPartial)) | p.arrive) {
+                const U4 e = draw(key, (uint32_t)k, kSlotRolloutB);
+                const uint32_t lo = min(e.v[0], e.v[1]), hi = max(e.v[0], e.v[1]);
+                beta = u32(max(lo, min(hi, e.v[2])));
+                nd = pick_other(e.v[3], w.P, s.dest);
+            }
+            env_finish(s, p, kind, beta, nd);
+            total += p.r;  // total_reward += reward (:229)
+            steps += 1;
+            if (p.dead) {
+                status = SE_ROLL_DONE;
+                break;
+            }
+        }
+        if (status == SE_ROLL_ATTEMPTS && steps >= A.max_steps) status = SE_ROLL_MAX_STEPS;
+        A.ret[r] = total;
+        A.steps[r] = steps;
+        A.status[r] = status;
+    }
+}
+
 // ------------------------------------------------------------------ stats reduce
 __global__ __launch_bounds__(64) void stats_kernel(const double* __restrict__ slab, int blocks,
                                                    double* __restrict__ out) {
@@ -1467,6 +1594,46 @@ int se_gen_actions(se_env* env, int32_t* actions, uint32_t t, void* stream) {
             env->n, env->env_base, env->seed, t, env->dims.P, actions);
         HIP_TRY(hipGetLastError());
     }
+    return SE_OK;
+}
+
+int se_sample_actions(se_env* env, int32_t* type, int32_t* a, int32_t* b, uint32_t t, void* stream) {
+    int rc = check_ready(env);
+    if (rc) return rc;
+    if (!type || !a || !b) return fail(SE_EINVAL, "null output pointer");
+    if (env->n == 0) return SE_OK;
+    DeviceGuard g(env->device);
+    SampleArgs A{env->d_world, env->dims, env->n, env->env_base, env->seed, t, env->st, type, a, b};
+    sample_kernel<<<grid_for(env->n), kBlock, lds_bytes(env), (hipStream_t)stream>>>(A);
+    HIP_TRY(hipGetLastError());
+    return SE_OK;
+}
+
+int se_rollout(se_env* env, const int32_t* src, int64_t m, int32_t max_steps, int32_t max_attempts,
+               int64_t rollout_base, double* ret, int32_t* steps, int32_t* status, void* stream) {
+    int rc = check_ready(env);
+    if (rc) return rc;
+    if (m < 0 || max_steps < 0 || max_attempts < 0 || rollout_base < 0)
+        return fail(SE_EINVAL, "m, max_steps, max_attempts and rollout_base must be >= 0");
+    if (m > 0 && (!src || !ret || !steps || !status)) return fail(SE_EINVAL, "null rollout buffer");
+    if (m == 0) return SE_OK;
+    DeviceGuard g(env->device);
+    RolloutArgs A{};
+    A.world = env->d_world;
+    A.dims = env->dims;
+    A.n = env->n;
+    A.m = m;
+    A.rollout_base = rollout_base;
+    A.seed = env->seed;
+    A.max_steps = max_steps;
+    A.max_attempts = max_attempts;
+    A.st = env->st;
+    A.src = src;
+    A.ret = ret;
+    A.steps = steps;
+    A.status = status;
+    rollout_kernel<<<grid_for(m), kBlock, lds_bytes(env), (hipStream_t)stream>>>(A);
+    HIP_TRY(hipGetLastError());
     return SE_OK;
 }
 

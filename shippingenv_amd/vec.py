@@ -128,14 +128,16 @@ class VecEnv:
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
-    def _dev(self, t, dtype):
+    def _dev(self, t, dtype, count=None):
+        """A contiguous, 16-byte aligned device tensor of `count` (default n) entries."""
         if not isinstance(t, torch.Tensor):
             t = torch.as_tensor(np.asarray(t), device=self.device)
         t = t.to(device=self.device, dtype=dtype)
         if not t.is_contiguous() or t.data_ptr() % 16:
             t = t.contiguous().clone()
-        if t.numel() != self.n:
-            raise ValueError(f"expected {self.n} entries, got {t.numel()}")
+        want = self.n if count is None else count
+        if t.numel() != want:
+            raise ValueError(f"expected {want} entries, got {t.numel()}")
         return t
 
     # ------------------------------------------------------------------ API
@@ -208,6 +210,38 @@ class VecEnv:
             out = torch.empty(self.n, dtype=torch.int32, device=self.device)
         N.check(N.lib().se_gen_actions(self._h, _ptr(out), int(t) & 0xFFFFFFFF, self._stream()))
         return out
+
+    def sample_actions(self, t, out=None):
+        """sample_action() (environment.py:245-263) of every env as typed actions
+        (type, a, b) int32 tensors for step_typed; type < 0 where the reference raises
+        (SAMPLE_RAISES) or never returns (SAMPLE_NO_OTHER_PORT). t selects the draw."""
+        if out is None:
+            out = tuple(torch.empty(self.n, dtype=torch.int32, device=self.device) for _ in range(3))
+        ty, a, b = out
+        N.check(N.lib().se_sample_actions(self._h, _ptr(ty), _ptr(a), _ptr(b),
+                                          int(t) & 0xFFFFFFFF, self._stream()))
+        return ty, a, b
+
+    def rollout(self, src, max_steps=100, max_attempts=None, rollout_base=0):
+        """MCTS random rollouts (agents/mcts.py:211-238) from copies of envs src (int32 [m]):
+        returns (ret f64, steps i32, status i32) device tensors; env state is untouched.
+        max_attempts bounds the reference's unbounded retry of raising steps (default
+        8 * max_steps). Rollout r draws from Philox(seed, rollout_base + r): pass fresh
+        bases for independent rollouts."""
+        if not isinstance(src, torch.Tensor):
+            src = torch.as_tensor(np.asarray(src))
+        m = src.numel()
+        s = self._dev(src, torch.int32, count=m)
+        if max_attempts is None:
+            max_attempts = 8 * max_steps
+        ret = torch.empty(m, dtype=torch.float64, device=self.device)
+        steps = torch.empty(m, dtype=torch.int32, device=self.device)
+        status = torch.empty(m, dtype=torch.int32, device=self.device)
+        N.check(N.lib().se_rollout(self._h, _ptr(s), m, int(max_steps), int(max_attempts),
+                                   int(rollout_base), _ptr(ret), _ptr(steps), _ptr(status),
+                                   self._stream()))
+        self._keep = s
+        return ret, steps, status
 
     def episode_stats(self):
         """Device f64[3] {sum of returns, episodes, sum of lengths} since the last clear."""
