@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--no-config4", action="store_true")
     p.add_argument("--large-n", type=int, default=1 << 24,
                    help="extra HBM-resident run (working set beyond the 256 MiB MALL); 0 = skip")
+    p.add_argument("--dqn-steps", type=int, default=50,
+                   help="config 5: timed DQN policy + step iterations at N envs/GPU; 0 = skip")
     p.add_argument("--rollouts", type=int, default=20,
                    help="timed se_rollout launches (MCTS random rollouts, 2^20 x 100 steps); 0 = skip")
     return p.parse_args()
@@ -192,6 +194,83 @@ def run_rollouts(n, args, dist):
     }
 
 
+BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, no sparsity)
+
+
+def run_dqn(n, args, dist):
+    """Config 5: the DQN rollout consumer. Per iteration: the fused policy
+    step (observation, DQNNetwork 26->128->128->259 on bf16 MFMA, masked first-max
+    argmax, epsilon-greedy; se_policy) then the env step, on N envs per GPU with
+    random-init weights (no checkpoint: no network). Also timed: the policy launch
+    alone, and the unfused torch path (observe -> nn.Module fp32 -> masked argmax)."""
+    from shippingenv_amd.policy import DQNNetwork, QPolicy
+    from shippingenv_amd.vec import VecEnv
+
+    env = VecEnv(n, seed=args.seed, env_id_base=dist.rank * n, device=dist.dev)
+    env.reset()
+    torch.manual_seed(args.seed)
+    model = DQNNetwork(env.obs_size, env.action_space_size).to(env.device)
+    pol = QPolicy(env, model)
+    eps = 0.1
+    for t in range(5):
+        env.step(pol.act(eps, t))
+    stream = torch.cuda.current_stream(env.device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for t in range(args.dqn_steps):
+        env.step(pol.act(eps, 5 + t))
+    e1.record(stream)
+    torch.cuda.synchronize()
+    dist.barrier()
+    wall = dist.max(time.perf_counter() - t0)
+    e2e_ms = e0.elapsed_time(e1) / args.dqn_steps
+    # the policy launch alone (same state, fresh draws)
+    e0.record(stream)
+    for t in range(args.dqn_steps):
+        pol.act(eps, 1000 + t)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    pol_ms = e0.elapsed_time(e1) / args.dqn_steps
+    # unfused torch reference path, fp32 as agents/dqn.py runs it (a few iterations)
+    A = env.action_space_size
+    shifts = torch.arange(7, -1, -1, device=env.device, dtype=torch.uint8)
+
+    def torch_policy():
+        with torch.no_grad():
+            q = model(env.observe())
+            bits = ((env.valid_mask().unsqueeze(-1) >> shifts) & 1).flatten(1)[:, :A].bool()
+            return q.masked_fill(~bits, float("-inf")).argmax(1).to(torch.int32)
+
+    torch_policy()
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for _ in range(5):
+        torch_policy()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    torch_ms = e0.elapsed_time(e1) / 5
+    flop_env = 2 * (env.obs_size * 128 + 128 * 128 + 128 * A)  # the reference network's MACs x 2
+    achieved = flop_env * n / (pol_ms * 1e-3) / 1e12
+    pol.close()
+    env.close()
+    return {
+        "workload": "config 5: fused DQN policy (se_policy: obs + DQNNetwork 26->128->128->259 bf16 "
+                    "MFMA + masked argmax + eps-greedy 0.1) then se_step, N envs/GPU, random-init weights",
+        "value": round(n * dist.world * args.dqn_steps / wall, 1),
+        "unit": "env-steps/s (policy + step)",
+        "ms_per_step": round(wall / args.dqn_steps * 1e3, 4),
+        "e2e_kernel_ms": round(e2e_ms, 4),
+        "policy_ms": round(pol_ms, 4),
+        "torch_unfused_policy_ms": round(torch_ms, 4),
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": BF16_DENSE_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4),
+                     "flop_per_env": flop_env, "traffic": None},
+    }
+
+
 def roofline(bytes_per_step, n, k_ms, canonical):
     achieved = bytes_per_step * n / (k_ms * 1e-3) / 1e9
     return {
@@ -303,6 +382,9 @@ def main():
 
     if args.rollouts:
         out["rollouts"] = run_rollouts(n, args, dist)
+
+    if args.dqn_steps:
+        out["config5_dqn"] = run_dqn(n, args, dist)
 
     if args.large_n and dist.world == 1:
         small = argparse.Namespace(**vars(args))

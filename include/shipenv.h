@@ -196,6 +196,29 @@ int se_sample_actions(se_env* env, int32_t* type, int32_t* a, int32_t* b, uint32
 int se_rollout(se_env* env, const int32_t* src, int64_t m, int32_t max_steps, int32_t max_attempts,
                int64_t rollout_base, double* ret, int32_t* steps, int32_t* status, void* stream);
 
+/* DQN policy step fused on the GPU (agents/dqn.py): DQNNetwork 6+4P -> 128 -> 128 -> A
+ * (A = 4+P+250, :21-33) evaluated with bf16 MFMA and f32 accumulation on the
+ * observation preprocess_state builds (utils/preprocessing.py:25-62; its constant port
+ * block is folded into fc1's bias), fused with choose_action (:177-203): the first
+ * maximum of Q over is_valid_action (:125-175), and epsilon-greedy exploration
+ * (np.random.rand() <= epsilon, then random.choice over the valid actions). The
+ * N x A Q matrix never reaches HBM (unless q_out asks for it). */
+typedef struct se_qnet se_qnet;
+int se_qnet_create(se_qnet** out, se_env* env);
+/* Weights: DEVICE f32 arrays in torch nn.Linear layout (weight [out][in], bias [out]):
+ * w1 [128][6+4P], b1 [128], w2 [128][128], b2 [128], w3 [A][128], b3 [A]. Packed on the
+ * stream (bf16, MFMA fragment order). Call again after se_set_ports (the port block is
+ * folded with the ports of that moment; se_policy refuses a stale packing). */
+int se_qnet_set_weights(se_qnet* q, const float* w1, const float* b1, const float* w2,
+                        const float* b2, const float* w3, const float* b3, void* stream);
+/* actions[i]: the agent-index action (se_step input) for every env. Exploration draws
+ * Philox(seed, env) at (t, slot 14): word 0 * 2^-32 <= epsilon explores, and word 1
+ * picks the k-th valid action (ascending index) uniformly. q_out (optional, NULL):
+ * the Q rows as computed, [n][ldq] f32, ldq >= A. */
+int se_policy(se_qnet* q, int32_t* actions, double epsilon, uint32_t t, float* q_out, int64_t ldq,
+              void* stream);
+int se_qnet_destroy(se_qnet* q);  /* destroy a qnet before the env it was created on */
+
 /* Episode statistics accumulated by the auto-reset path since the last clear:
  * out[0] = sum of returns, out[1] = episodes, out[2] = sum of lengths (device
  * double[3]). Deterministic: per-block partials are summed in a fixed order. */

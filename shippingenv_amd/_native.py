@@ -32,7 +32,8 @@ ROLL_DONE, ROLL_MAX_STEPS, ROLL_RAISED, ROLL_ATTEMPTS, ROLL_BAD_SRC = 0, 1, 2, 3
 EXPORTS = (
     "se_create", "se_set_ports", "se_bind", "se_reset", "se_reset_to", "se_step",
     "se_step_typed", "se_step_replay", "se_observe", "se_valid_mask", "se_gen_actions",
-    "se_sample_actions", "se_rollout",
+    "se_sample_actions", "se_rollout", "se_qnet_create", "se_qnet_set_weights", "se_policy",
+    "se_qnet_destroy",
     "se_episode_stats", "se_clear_stats", "se_done_layout", "se_done_list", "se_done_compact",
     "se_get_counters", "se_set_counters",
     "se_destroy", "se_last_error", "se_abi_version",
@@ -77,6 +78,10 @@ def _declare(lib):
         "se_gen_actions": [P, P, u32, P],
         "se_sample_actions": [P, P, P, P, u32, P],
         "se_rollout": [P, P, i64, i32, i32, i64, P, P, P, P],
+        "se_qnet_create": [C.POINTER(P), P],
+        "se_qnet_set_weights": [P, P, P, P, P, P, P, P],
+        "se_policy": [P, P, C.c_double, u32, P, i64, P],
+        "se_qnet_destroy": [P],
         "se_episode_stats": [P, P, P],
         "se_clear_stats": [P, P],
         "se_done_layout": [P, C.POINTER(i64), C.POINTER(i32)],

@@ -29,6 +29,7 @@ enum Slot : uint32_t {
     kSlotSample = 11,        // se_sample_actions, per env: word 0
     kSlotRollout = 12,       // rollout attempt, per rollout: sample word, u_fuel, u_gate, u_type
     kSlotRolloutB = 13,      // rollout attempt (partial loss / arrival): 3 beta uniforms, dest
+    kSlotPolicy = 14,        // se_policy, per env: explore draw, random.choice index
 };
 
 struct U4 {

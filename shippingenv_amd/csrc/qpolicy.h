@@ -1,0 +1,417 @@
+// qpolicy.h — the DQN policy step fused on MFMA.
+//
+// Part of shipenv.hip's translation unit (included at its end): it shares the
+// world image, the env handle and Philox. Reference: agents/dqn.py DQNNetwork
+// (:21-33: fc1 6+4P -> 128, relu, fc2 128 -> 128, relu, fc3 128 -> A = 4+P+250)
+// and choose_action (:177-203), on preprocess_state rows (utils/preprocessing.py:25-62).
+//
+// Shape of the work: per env ~50 K MACs (fc2 + fc3) against 16 bytes of state, so
+// the step is MFMA-bound, not HBM-bound. One wave takes 32 envs at a time with
+// the batch on the MFMA's column (N) dimension: every layer is D = W·X with the
+// weights W as the A operand (bf16 fragments pre-permuted into LDS, lane-linear,
+// one ds_read_b128 per MFMA) and the activations X as the B operand in registers.
+// A v_mfma_f32_32x32x16_bf16 result keeps the env on the lane and the feature rows
+// in its 16 registers, so relu + bf16 packing of registers 8s..8s+7 is directly
+// the next layer's k-step s (cdna_hip_programming.md §3, "accumulator tile as the
+// next MFMA's operand"); the weights are stored in that step's permuted k order.
+// fc1 has 6 live inputs (the port block is constant: folded into the bias) and
+// runs as one k-step per row tile, with fuel split into bf16 hi + lo parts. Biases
+// are the accumulators' initial values (f32). fc3's epilogue is the masked
+// argmax: each lane keeps the first maximum over the valid rows it holds, and the
+// two lane halves that share an env merge with one shuffle. Q never reaches HBM.
+//
+// LDS: the packed network (113 KB at P = 5) plus the world image, one 512-thread
+// workgroup (8 waves) per CU, one workgroup per CU for the whole launch.
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+constexpr int kQHidden = 128;     // DQNNetwork hidden_size (dqn.py:24, default 128)
+constexpr int kPolicyBlock = 512; // 8 waves share one LDS copy of the weights
+constexpr int kPolicyWaves = kPolicyBlock / 64;
+
+// Packed network image (bytes). Fragments are 64 lanes x 8 bf16 = 1 KB.
+struct QnetDims {
+    int32_t P, A, mt3;  // ports, actions, fc3 row tiles (A rounded up to 32)
+    __host__ __device__ int in1() const { return 6 + 4 * P; }
+    __host__ __device__ int w1() const { return 0; }                    // 4 fc1 tiles
+    __host__ __device__ int w2() const { return 4 * 1024; }              // 4 x 4 x 2 fc2 fragments
+    __host__ __device__ int w3() const { return w2() + 32 * 1024; }      // mt3 x 4 x 2 fc3 fragments
+    __host__ __device__ int b1() const { return w3() + mt3 * 8 * 1024; } // 128 f32, port block folded
+    __host__ __device__ int b2() const { return b1() + 4 * kQHidden; }
+    __host__ __device__ int b3() const { return b2() + 4 * kQHidden; }   // mt3 * 32 f32 (0 beyond A)
+    __host__ __device__ int next() const { return b3() + mt3 * 128; }    // P int32: next port on the cell
+    __host__ __device__ int bytes() const { return (next() + 4 * P + 15) & ~15; }
+};
+
+QnetDims qnet_dims(int P) {
+    QnetDims q;
+    q.P = P;
+    q.A = 4 + P + 250;  // utils/preprocessing.py:93-108
+    q.mt3 = (q.A + 31) / 32;
+    return q;
+}
+
+// ------------------------------------------------------------------ packing
+// One thread per 16-byte fragment slot / bias entry. Fragment (tile, step) lane
+// (r = lane & 31, h = lane >> 5) element j holds W[tile*32 + r][k] with
+//   fc1: k = column map of j (h = 0 only; the obs fragment below uses the same map)
+//   fc2, fc3: k = kt*32 + 16s + 8(j >> 2) + 4h + (j & 3), the row of the previous
+//   layer's accumulator that register 8s + j of lane half h holds.
+struct PackArgs {
+    const float *w1, *b1, *w2, *b2, *w3, *b3;
+    const uint32_t* world;
+    WorldDims dims;
+    QnetDims q;
+    uint8_t* img;
+};
+
+// fc1 input column of fragment element j: x, y, fuel (hi), fuel (lo), "cargo" = fuel
+// (hi, lo; environment.py:206), origin, dest (utils/preprocessing.py:51-58)
+__device__ __forceinline__ int fc1_col(int j) {
+    return j < 2 ? j : (j < 4 ? 2 : (j < 6 ? 3 : j - 2));
+}
+
+__device__ __forceinline__ int acc_row(int s, int j, int h) { return 16 * s + 8 * (j >> 2) + 4 * h + (j & 3); }
+
+__global__ __launch_bounds__(256) void qnet_pack_kernel(PackArgs A) {
+    const QnetDims q = A.q;
+    const int in1 = q.in1();
+    const int n_w1 = 4 * 64, n_w2 = 32 * 64, n_w3 = q.mt3 * 8 * 64;
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n_w1 + n_w2 + n_w3 + 2 * kQHidden + q.mt3 * 32 + q.P;
+         t += gridDim.x * blockDim.x) {
+        if (t < n_w1 + n_w2 + n_w3) {
+            int f = t >> 6;
+            const int lane = t & 63, r = lane & 31, h = lane >> 5;
+            bf16x8 v;
+            uint8_t* dst;
+            if (t < n_w1) {  // fc1 tile f
+                const int row = f * 32 + r;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = h == 0 ? (__bf16)A.w1[row * in1 + fc1_col(j)] : (__bf16)0.0f;
+                dst = A.img + q.w1() + f * 1024 + lane * 16;
+            } else {
+                const bool second = t < n_w1 + n_w2;
+                f -= second ? 4 : 4 + 32;  // fragment index ((mt*4 + kt)*2 + s)
+                const int s = f & 1, kt = (f >> 1) & 3, mt = f >> 3;
+                const int row = mt * 32 + r;
+                const float* W = second ? A.w2 : A.w3;
+                const bool in = second || row < q.A;
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    v[j] = in ? (__bf16)W[row * kQHidden + kt * 32 + acc_row(s, j, h)] : (__bf16)0.0f;
+                dst = A.img + (second ? q.w2() : q.w3()) + f * 1024 + lane * 16;
+            }
+            *reinterpret_cast<bf16x8*>(dst) = v;
+            continue;
+        }
+        int u = t - (n_w1 + n_w2 + n_w3);
+        const uint32_t* pos = A.world + A.dims.pos();
+        const int P = q.P;
+        if (u < kQHidden) {  // b1 + fc1 over the constant port block (x, y, fuel, cargo per port)
+            double acc = (double)A.b1[u];
+            for (int p = 0; p < P; ++p) {
+                const float* w = A.w1 + u * in1 + 6 + 4 * p;
+                acc += (double)w[0] * (double)(pos[p] & 0xffu) + (double)w[1] * (double)((pos[p] >> 8) & 0xffu) +
+                       (double)w[2] * (double)(int32_t)A.world[A.dims.pos() + P + p] +
+                       (double)w[3] * (double)(int32_t)A.world[A.dims.pos() + 2 * P + p];
+            }
+            reinterpret_cast<float*>(A.img + q.b1())[u] = (float)acc;
+        } else if ((u -= kQHidden) < kQHidden) {
+            reinterpret_cast<float*>(A.img + q.b2())[u] = A.b2[u];
+        } else if ((u -= kQHidden) < q.mt3 * 32) {
+            reinterpret_cast<float*>(A.img + q.b3())[u] = u < q.A ? A.b3[u] : 0.0f;
+        } else {
+            u -= q.mt3 * 32;  // next port on the same cell, ascending (-1: none)
+            int nx = -1;
+            for (int p = u + 1; p < P && nx < 0; ++p)
+                if (pos[p] == pos[u]) nx = p;
+            reinterpret_cast<int32_t*>(A.img + q.next())[u] = nx;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ the policy step
+struct PolicyArgs {
+    const uint32_t* world;
+    WorldDims dims;
+    const uint4* qimg;
+    QnetDims q;
+    int64_t n, env_base;
+    uint64_t seed;
+    uint32_t t;
+    double eps;
+    se_state st;
+    int32_t* actions;
+    float* q_out;
+    int64_t ldq;
+};
+
+// accumulator initial value: bias rows (reg & 3) + 8 (reg >> 2) + 4h of a 32-row tile
+__device__ __forceinline__ f32x16 bias_frag(const float* b) {
+    const float4 a = *reinterpret_cast<const float4*>(b), c = *reinterpret_cast<const float4*>(b + 8),
+                 d = *reinterpret_cast<const float4*>(b + 16), e = *reinterpret_cast<const float4*>(b + 24);
+    return f32x16{a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w, e.x, e.y, e.z, e.w};
+}
+
+// relu, then registers 8s..8s+7 -> the bf16 B fragment of k-step s
+__device__ __forceinline__ void relu_pack(const f32x16& c, bf16x8 (&out)[2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) out[s][j] = (__bf16)fmaxf(c[8 * s + j], 0.0f);
+}
+
+// bits i of [0, 32) with lo <= i <= hi
+__device__ __forceinline__ uint32_t range_bits(int lo, int hi) {
+    lo = max(lo, 0);
+    hi = min(hi, 31);
+    const uint32_t top = hi >= 31 ? 0xffffffffu : ((1u << (hi + 1)) - 1u);
+    const uint32_t low = lo >= 32 ? 0xffffffffu : ((1u << lo) - 1u);
+    return lo > hi ? 0u : (top & ~low);
+}
+
+__global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
+    extern __shared__ uint4 smem[];
+    const QnetDims q = A.q;
+    const int qwords = q.bytes() / 16;
+    for (int i = threadIdx.x; i < qwords; i += kPolicyBlock) smem[i] = A.qimg[i];
+    const LdsWorld w = stage_world(A.world, A.dims, reinterpret_cast<uint32_t*>(smem + qwords));
+    const uint8_t* qb = reinterpret_cast<const uint8_t*>(smem);
+    const bf16x8* W1f = reinterpret_cast<const bf16x8*>(qb + q.w1());
+    const bf16x8* W2f = reinterpret_cast<const bf16x8*>(qb + q.w2());
+    const bf16x8* W3f = reinterpret_cast<const bf16x8*>(qb + q.w3());
+    const float* B1 = reinterpret_cast<const float*>(qb + q.b1());
+    const float* B2 = reinterpret_cast<const float*>(qb + q.b2());
+    const float* B3 = reinterpret_cast<const float*>(qb + q.b3());
+    const int32_t* NEXT = reinterpret_cast<const int32_t*>(qb + q.next());
+
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+    const int P = q.P;
+    const int64_t tiles = (A.n + 31) >> 5;
+    for (int64_t tile = (int64_t)blockIdx.x * kPolicyWaves + (threadIdx.x >> 6); tile < tiles;
+         tile += (int64_t)gridDim.x * kPolicyWaves) {
+        const int64_t e = tile * 32 + r;
+        const bool live = e < A.n;
+        const int64_t ei = live ? e : A.n - 1;
+        const int x = A.st.x[ei], y = A.st.y[ei];
+        const int o8 = A.st.origin[ei], d8 = A.st.dest[ei];
+        const int origin = o8 == SE_NONE ? -1 : o8, dest = d8 == SE_NONE ? -1 : d8;
+        // the observation row (preprocess_state): torch's .float() of the f64 fuel,
+        // as bf16 hi + lo so fc1 sees ~16 bits of it
+        const float ff = (float)A.st.fuel[ei];
+        const __bf16 fh = (__bf16)ff, fl = (__bf16)(ff - (float)fh);
+        bf16x8 ob;
+        ob[0] = (__bf16)(float)x;
+        ob[1] = (__bf16)(float)y;
+        ob[2] = fh;
+        ob[3] = fl;
+        ob[4] = fh;
+        ob[5] = fl;
+        ob[6] = (__bf16)(float)origin;
+        ob[7] = (__bf16)(float)dest;
+        if (h) ob = bf16x8{};  // k = 8..15 of the single fc1 step are padding
+
+        bf16x8 h1[4][2], h2[4][2];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {  // fc1 + relu
+            f32x16 c = bias_frag(B1 + mt * 32 + 4 * h);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(W1f[mt * 64 + lane], ob, c, 0, 0, 0);
+            relu_pack(c, h1[mt]);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {  // fc2 + relu
+            f32x16 c = bias_frag(B2 + mt * 32 + 4 * h);
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(W2f[((mt * 4 + kt) * 2 + s) * 64 + lane],
+                                                                 h1[kt][s], c, 0, 0, 0);
+            relu_pack(c, h2[mt]);
+        }
+
+        // is_valid_action (dqn.py:125-175): moves always; SELECT p at the ship's cell
+        // and != origin; TAKE_CARGO / TAKE_FUEL at a port with 0 < amount <= stock
+        const int cur = w.port_at(x, y);
+        const int cst = cur >= 0 ? min(w.pcargo[max(cur, 0)], 49) : 0;
+        const int fst = cur >= 0 ? min(w.pfuel[max(cur, 0)], 199) : 0;
+        const int c_lo = 5 + P, c_hi = 4 + P + cst, f_lo = 55 + P, f_hi = 54 + P + fst;
+        float best = -INFINITY;
+        int bidx = 0x7fffffff;
+        for (int mt = 0; mt < q.mt3; ++mt) {  // fc3 + the masked first-maximum argmax
+            f32x16 c = bias_frag(B3 + mt * 32 + 4 * h);
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(W3f[((mt * 4 + kt) * 2 + s) * 64 + lane],
+                                                                 h2[kt][s], c, 0, 0, 0);
+            const int base = mt * 32;
+            uint32_t m = range_bits(-base, 3 - base) | range_bits(c_lo - base, c_hi - base) |
+                         range_bits(f_lo - base, f_hi - base);
+            if (base < 4 + P) {  // SELECT rows live in this tile (uniform)
+                for (int p = cur; p >= 0; p = NEXT[p]) {
+                    const int i = 4 + p - base;
+                    if (p != origin && i >= 0 && i < 32) m |= 1u << i;
+                }
+            }
+            m >>= 4 * h;  // register reg holds row base + 4h + (reg & 3) + 8 (reg >> 2)
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int i = (reg & 3) + 8 * (reg >> 2);
+                const bool better = ((m >> i) & 1u) && c[reg] > best;  // ascending rows: first max
+                best = better ? c[reg] : best;
+                bidx = better ? base + 4 * h + i : bidx;
+            }
+            if (A.q_out && live) {
+#pragma unroll
+                for (int reg = 0; reg < 16; ++reg) {
+                    const int row = base + 4 * h + (reg & 3) + 8 * (reg >> 2);
+                    if (row < q.A) A.q_out[e * A.ldq + row] = c[reg];
+                }
+            }
+        }
+        // the two lane halves hold the same env: larger value, then lower index
+        const float ob2 = __shfl_xor(best, 32);
+        const int oi = __shfl_xor(bidx, 32);
+        if (ob2 > best || (ob2 == best && oi < bidx)) {
+            best = ob2;
+            bidx = oi;
+        }
+        if (h == 0 && live) {
+            int act = bidx == 0x7fffffff ? 0 : bidx;  // no valid action: 0 (:188-189)
+            if (A.eps > 0.0) {
+                const U4 d = draw(env_key(A.seed, A.env_base + e), A.t, kSlotPolicy);
+                if (u32(d.v[0]) <= A.eps) {  // np.random.rand() <= epsilon (:191)
+                    // random.choice(valid_actions) (:192): the k-th valid action, ascending
+                    int nsel = 0;
+                    for (int p = cur; p >= 0; p = NEXT[p]) nsel += p != origin;
+                    int k = uniform_int(d.v[1], (uint32_t)(4 + nsel + cst + fst));
+                    if (k < 4) {
+                        act = k;
+                    } else if ((k -= 4) < nsel) {
+                        for (int p = cur; p >= 0; p = NEXT[p])
+                            if (p != origin && k-- == 0) act = 4 + p;
+                    } else {
+                        k -= nsel;
+                        act = k < cst ? c_lo + k : f_lo + (k - cst);
+                    }
+                }
+            }
+            A.actions[e] = act;
+        }
+        (void)dest;
+    }
+}
+
+}  // namespace
+
+struct se_qnet {
+    se_env* env = nullptr;  // must outlive the qnet (destroy the qnet first)
+    int device = 0;
+    QnetDims q{};
+    uint8_t* d_img = nullptr;
+    int img_bytes = 0;
+    uint64_t world_version = 0;
+    bool packed = false;
+};
+
+extern "C" {
+
+int se_qnet_create(se_qnet** out, se_env* env) {
+    if (!out) return fail(SE_EINVAL, "null out");
+    *out = nullptr;
+    int rc = check_ready(env);
+    if (rc) return rc;
+    se_qnet* qn = new se_qnet;
+    qn->env = env;
+    qn->device = env->device;
+    *out = qn;
+    return SE_OK;
+}
+
+int se_qnet_set_weights(se_qnet* qn, const float* w1, const float* b1, const float* w2, const float* b2,
+                        const float* w3, const float* b3, void* stream) {
+    if (!qn) return fail(SE_EINVAL, "null qnet");
+    if (!w1 || !b1 || !w2 || !b2 || !w3 || !b3) return fail(SE_EINVAL, "null weight pointer");
+    se_env* env = qn->env;
+    if (env->dims.P < 1) return fail(SE_EINVAL, "the policy needs at least one port");
+    DeviceGuard g(env->device);
+    const QnetDims q = qnet_dims(env->dims.P);
+    if (q.bytes() > qn->img_bytes) {
+        if (qn->d_img) HIP_TRY(hipFree(qn->d_img));
+        qn->d_img = nullptr;
+        HIP_TRY(hipMalloc(&qn->d_img, (size_t)q.bytes()));
+        qn->img_bytes = q.bytes();
+    }
+    qn->q = q;
+    PackArgs A{w1, b1, w2, b2, w3, b3, env->d_world, env->dims, q, qn->d_img};
+    qnet_pack_kernel<<<64, 256, 0, (hipStream_t)stream>>>(A);
+    HIP_TRY(hipGetLastError());
+    qn->world_version = env->world_version;
+    qn->packed = true;
+    return SE_OK;
+}
+
+int se_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, float* q_out, int64_t ldq,
+              void* stream) {
+    if (!qn) return fail(SE_EINVAL, "null qnet");
+    se_env* env = qn->env;
+    int rc = check_ready(env);
+    if (rc) return rc;
+    if (!qn->packed) return fail(SE_ESTATE, "se_qnet_set_weights has not been called");
+    if (qn->world_version != env->world_version)
+        return fail(SE_ESTATE, "ports changed since se_qnet_set_weights (the port block is folded into fc1)");
+    if (!actions) return fail(SE_EINVAL, "null actions");
+    if (q_out && ldq < qn->q.A) return fail(SE_EINVAL, "ldq < number of actions");
+    if (!(epsilon >= 0.0)) return fail(SE_EINVAL, "epsilon must be >= 0");
+    if (env->n == 0) return SE_OK;
+    DeviceGuard g(env->device);
+    const size_t lds = (size_t)qn->q.bytes() + lds_bytes(env);
+    static bool attr_set = false;
+    if (!attr_set) {
+        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(policy_kernel),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr_set = true;
+    }
+    if (lds > 160 * 1024) return fail(SE_EINVAL, "network + world image exceed the 160 KB LDS");
+    int dev_cus = 256;
+    if (hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, env->device) != hipSuccess)
+        dev_cus = 256;
+    const int64_t tiles = (env->n + 31) / 32;
+    const int64_t want = (tiles + kPolicyWaves - 1) / kPolicyWaves;
+    const int grid = (int)(want < dev_cus ? want : dev_cus);  // one resident workgroup per CU
+    PolicyArgs A{};
+    A.world = env->d_world;
+    A.dims = env->dims;
+    A.qimg = reinterpret_cast<const uint4*>(qn->d_img);
+    A.q = qn->q;
+    A.n = env->n;
+    A.env_base = env->env_base;
+    A.seed = env->seed;
+    A.t = t;
+    A.eps = epsilon;
+    A.st = env->st;
+    A.actions = actions;
+    A.q_out = q_out;
+    A.ldq = ldq;
+    policy_kernel<<<grid, kPolicyBlock, lds, (hipStream_t)stream>>>(A);
+    HIP_TRY(hipGetLastError());
+    return SE_OK;
+}
+
+int se_qnet_destroy(se_qnet* qn) {
+    if (!qn) return SE_OK;
+    if (qn->d_img) {  // does not touch the env, which may be gone already
+        DeviceGuard g(qn->device);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(qn->d_img);
+    }
+    delete qn;
+    return SE_OK;
+}
+
+}  // extern "C"

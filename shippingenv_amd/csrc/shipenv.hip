@@ -1236,6 +1236,7 @@ struct se_env {
     int64_t seg = 0;    // done-list segment stride (records per workgroup)
     int64_t iters = 1;  // groups per thread of the step kernel
     int world_cap = 0;  // words allocated
+    uint64_t world_version = 0;  // bumped by every world upload (se_qnet folds the ports)
     se_state st{};
     bool bound = false;
     double* d_slab = nullptr;       // [grid][4]
@@ -1355,6 +1356,7 @@ int upload_world(se_env* env, int32_t P, const int32_t* px, const int32_t* py, c
     }
     HIP_TRY(hipMemcpy(env->d_world, img.data(), (size_t)d.total() * 4, hipMemcpyHostToDevice));
     env->dims = d;
+    env->world_version += 1;
     return SE_OK;
 }
 
@@ -1710,3 +1712,6 @@ int se_destroy(se_env* env) {
 }
 
 }  // extern "C"
+
+// the fused DQN policy step (same translation unit: world image, env handle, Philox)
+#include "qpolicy.h"

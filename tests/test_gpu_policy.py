@@ -1,0 +1,175 @@
+"""The fused DQN policy step (se_policy) vs torch and the reference's choose_action.
+
+Bars (agents/dqn.py:21-33 network, :125-203 action choice):
+* Q vs a float64 emulation of the network the kernel evaluates (bf16 weights and
+  layer inputs, f32 folded fc1 bias, fuel as bf16 hi + lo): mean |dQ| / (|Q| + 0.1)
+  <= 2e-4 and max |dQ| <= 1e-2 max |Q| (the kernel rounds f32-accumulated
+  activations to bf16, the emulation f64 ones: a value at a rounding tie moves one
+  bf16 ulp and shifts the Q values downstream of it).
+* Q vs the fp32 torch DQNNetwork: |dQ| <= 0.03 max|Q| (bf16 weights and activations).
+* epsilon = 0: the action is the FIRST maximum of the kernel's own Q over
+  is_valid_action (the valid_mask kernel, pinned vs the oracle in test_gpu_parity),
+  bit for bit; and it is the fp32 argmax wherever the fp32 top-2 gap exceeds the
+  bf16 tolerance.
+* epsilon = 1: the k-th valid action, k = umulhi(word 1, #valid) of Philox(seed, env)
+  at (t, slot 14) (random.choice over valid_actions), bit for bit.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+O = pytest.importorskip("oracle.oracle")
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    from shippingenv_amd import build
+
+    build.build(verbose=False)
+
+
+_OPEN = []
+
+
+@pytest.fixture(autouse=True)
+def _close_after():
+    yield
+    while _OPEN:  # policy before its env, also when the test failed
+        _OPEN.pop().close()
+
+
+def make(n, ports=None, seed=3, steps=0, scale=1.0):
+    from shippingenv_amd.policy import DQNNetwork, QPolicy
+    from shippingenv_amd.vec import VecEnv
+
+    env = VecEnv(n, seed=seed, ports=ports)
+    _OPEN.append(env)
+    env.reset()  # every ship at its origin port: SELECT / TAKE rows are live
+    for t in range(steps):
+        env.step(env.gen_actions(t))
+    torch.manual_seed(seed)
+    model = DQNNetwork(env.obs_size, env.action_space_size)
+    with torch.no_grad():  # spread the outputs so that argmaxes are well separated
+        model.fc3.weight.mul_(scale)
+        model.fc3.bias.mul_(scale)
+    pol = QPolicy(env, model)
+    _OPEN.append(pol)
+    return env, model, pol
+
+
+def valid_bool(env):
+    bits = env.valid_mask().cpu().numpy()
+    return np.unpackbits(bits, axis=1)[:, : env.action_space_size].astype(bool)
+
+
+def emulate_bf16(env, model):
+    """The network as the kernel evaluates it, in float64."""
+    obs = env.observe().double()
+    bf = lambda t: t.to(torch.bfloat16).double()  # noqa: E731
+    w1, b1 = model.fc1.weight.detach().double(), model.fc1.bias.detach().double()
+    P = env.P
+    b1f = (b1 + obs[0, 6:] @ w1[:, 6:].T).float().double()  # the port block, folded (f32)
+    f32 = env.fuel.double().float()
+    fh = f32.to(torch.bfloat16).float()
+    fl = (f32 - fh).to(torch.bfloat16).float()
+    fuel = (fh.double() + fl.double()).to(obs.device)
+    dyn = torch.stack([obs[:, 0], obs[:, 1], fuel, fuel, obs[:, 4], obs[:, 5]], 1)
+    h1 = torch.relu(dyn @ bf(w1[:, :6]).T + b1f)
+    h2 = torch.relu(bf(h1) @ bf(model.fc2.weight.detach().double()).T + model.fc2.bias.detach().double())
+    q = bf(h2) @ bf(model.fc3.weight.detach().double()).T + model.fc3.bias.detach().double()
+    assert P == (obs.shape[1] - 6) // 4
+    return q
+
+
+def first_masked_argmax(q, valid):
+    qm = np.where(valid, q, -np.inf)
+    return qm.argmax(axis=1)  # numpy argmax returns the first maximum
+
+
+@pytest.mark.parametrize("n,ports,steps", [(4096, None, 0), (4096 + 13, None, 30), (2048, "64", 5)])
+def test_q_values_vs_torch(n, ports, steps):
+    from shippingenv_amd.vec import random_water_ports
+    from conftest import golden_water
+
+    if ports == "64":
+        ports = random_water_ports(golden_water(), 64, seed=3)
+    env, model, pol = make(n, ports, steps=steps)
+    A = env.action_space_size
+    q_out = torch.full((n, A + 3), float("nan"), dtype=torch.float32, device=env.device)
+    pol.act(0.0, 0, q_out=q_out)
+    qk = q_out[:, :A].double()
+    assert torch.isfinite(qk).all()
+    qe = emulate_bf16(env, model)
+    rel = (qk - qe).abs() / (qe.abs() + 0.1)
+    worst = float((qk - qe).abs().max()) / float(qe.abs().max())
+    assert float(rel.mean()) <= 2e-4 and worst <= 1e-2, (float(rel.mean()), worst)
+    with torch.no_grad():
+        q32 = model(env.observe()).double()
+    assert float((qk - q32).abs().max()) <= 0.03 * float(q32.abs().max())
+
+
+@pytest.mark.parametrize("steps", [0, 40])
+def test_greedy_is_first_masked_argmax(steps):
+    env, model, pol = make(8192 + 7, steps=steps, scale=20.0)
+    A = env.action_space_size
+    q_out = torch.empty((env.n, A), dtype=torch.float32, device=env.device)
+    act = pol.act(0.0, 5, q_out=q_out).cpu().numpy()
+    qk = q_out.cpu().numpy()
+    valid = valid_bool(env)
+    np.testing.assert_array_equal(act, first_masked_argmax(qk, valid))
+    assert valid[np.arange(env.n), act].all()
+    if steps == 0:  # at ports: non-move actions are chosen too
+        assert (act >= 4).any()
+    # fp32 agreement wherever the fp32 decision is not within the bf16 tolerance
+    q32 = model(env.observe()).detach().double().cpu().numpy()
+    m32 = np.where(valid, q32, -np.inf)
+    ref = m32.argmax(axis=1)
+    top2 = np.sort(m32, axis=1)[:, -2:]
+    gap = top2[:, 1] - top2[:, 0]
+    clear = gap > 0.03 * np.abs(q32).max()
+    assert clear.mean() > 0.5
+    np.testing.assert_array_equal(act[clear], ref[clear])
+
+
+def explore_expected(env, valid, t):
+    n = env.n
+    out, u = np.zeros(n, np.int64), np.zeros(n)
+    for i in range(n):
+        w = O.philox([i & 0xFFFFFFFF, i >> 32, t, 14], [env.seed & 0xFFFFFFFF, env.seed >> 32])
+        idx = np.flatnonzero(valid[i])
+        out[i] = idx[(int(w[1]) * len(idx)) >> 32]
+        u[i] = float(w[0]) / 2**32
+    return out, u
+
+
+@pytest.mark.parametrize("steps", [0, 25])
+def test_explore_is_uniform_over_valid_actions(steps):
+    env, model, pol = make(3000, steps=steps)
+    valid = valid_bool(env)
+    act = pol.act(1.0, 9).cpu().numpy()
+    want, _ = explore_expected(env, valid, 9)
+    np.testing.assert_array_equal(act, want)
+    # epsilon = 0.3: explore exactly where u <= 0.3, greedy elsewhere
+    q_out = torch.empty((env.n, env.action_space_size), dtype=torch.float32, device=env.device)
+    act = pol.act(0.3, 11, q_out=q_out).cpu().numpy()
+    want, u = explore_expected(env, valid, 11)
+    greedy = first_masked_argmax(q_out.cpu().numpy(), valid)
+    np.testing.assert_array_equal(act, np.where(u <= 0.3, want, greedy))
+    assert 0.2 < (u <= 0.3).mean() < 0.4
+
+
+def test_stale_packing_is_refused():
+    from shippingenv_amd import _native as N
+    from shippingenv_amd.vec import DEFAULT_PORTS
+
+    env, model, pol = make(256)
+    pol.act(0.0, 0)
+    env.set_ports(DEFAULT_PORTS, env.port_fuel + 1, env.port_cargo)  # stocks change the folded bias
+    with pytest.raises(N.ShipEnvError, match="ports changed"):
+        pol.act(0.0, 1)
+    pol.set_weights()
+    pol.act(0.0, 1)
