@@ -20,8 +20,8 @@
 // argmax: each lane keeps the first maximum over the valid rows it holds, and the
 // two lane halves that share an env merge with one shuffle. Q never reaches HBM.
 //
-// LDS: the packed network (113 KB at P = 5) plus the world image, one 512-thread
-// workgroup (8 waves) per CU, one workgroup per CU for the whole launch.
+// LDS: the packed network (113 KB at P = 5) plus the world image, one 768-thread
+// workgroup (12 waves, 3 per SIMD) per CU for the whole launch.
 
 namespace {
 
@@ -29,7 +29,7 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 constexpr int kQHidden = 128;     // DQNNetwork hidden_size (dqn.py:24, default 128)
-constexpr int kPolicyBlock = 512; // 8 waves share one LDS copy of the weights
+constexpr int kPolicyBlock = 768; // 12 waves (3 per SIMD, <= 170 VGPRs) share one LDS copy
 constexpr int kPolicyWaves = kPolicyBlock / 64;
 
 // Packed network image (bytes). Fragments are 64 lanes x 8 bf16 = 1 KB.
@@ -156,12 +156,16 @@ __device__ __forceinline__ f32x16 bias_frag(const float* b) {
     return f32x16{a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w, e.x, e.y, e.z, e.w};
 }
 
-// relu, then registers 8s..8s+7 -> the bf16 B fragment of k-step s
+// relu, then registers 8s..8s+7 -> the bf16 B fragment of k-step s. The relu is a
+// signed integer max with 0 on the f32 pattern (a non-negative float orders like
+// its int32 pattern, a negative one has the sign bit): one op, where fmaxf costs
+// two (IEEE mode canonicalises its input first).
 __device__ __forceinline__ void relu_pack(const f32x16& c, bf16x8 (&out)[2]) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) out[s][j] = (__bf16)fmaxf(c[8 * s + j], 0.0f);
+        for (int j = 0; j < 8; ++j)
+            out[s][j] = (__bf16)__int_as_float(max(__float_as_int(c[8 * s + j]), 0));
 }
 
 // bits i of [0, 32) with lo <= i <= hi
@@ -191,17 +195,31 @@ __global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
     const int P = q.P;
     const int64_t tiles = (A.n + 31) >> 5;
-    for (int64_t tile = (int64_t)blockIdx.x * kPolicyWaves + (threadIdx.x >> 6); tile < tiles;
-         tile += (int64_t)gridDim.x * kPolicyWaves) {
+    const int64_t stride = (int64_t)gridDim.x * kPolicyWaves;
+    // env state of one tile (lane & 31 = env); the next tile's is loaded while this
+    // one computes, so the wave does not wait on HBM at the top of every tile
+    struct EnvIn {
+        double fuel;
+        uint32_t x, y, o8, d8;
+    };
+    auto load_env = [&](int64_t tile) {
+        const int64_t e = tile * 32 + r;
+        const int64_t ei = e < A.n ? e : A.n - 1;
+        return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei]};
+    };
+    int64_t tile = (int64_t)blockIdx.x * kPolicyWaves + (threadIdx.x >> 6);
+    EnvIn nxt = load_env(tile < tiles ? tile : 0);
+    for (; tile < tiles; tile += stride) {
+        const EnvIn cur_in = nxt;
+        if (tile + stride < tiles) nxt = load_env(tile + stride);
         const int64_t e = tile * 32 + r;
         const bool live = e < A.n;
-        const int64_t ei = live ? e : A.n - 1;
-        const int x = A.st.x[ei], y = A.st.y[ei];
-        const int o8 = A.st.origin[ei], d8 = A.st.dest[ei];
-        const int origin = o8 == SE_NONE ? -1 : o8, dest = d8 == SE_NONE ? -1 : d8;
+        const int x = (int)cur_in.x, y = (int)cur_in.y;
+        const int origin = cur_in.o8 == SE_NONE ? -1 : (int)cur_in.o8;
+        const int dest = cur_in.d8 == SE_NONE ? -1 : (int)cur_in.d8;
         // the observation row (preprocess_state): torch's .float() of the f64 fuel,
         // as bf16 hi + lo so fc1 sees ~16 bits of it
-        const float ff = (float)A.st.fuel[ei];
+        const float ff = (float)cur_in.fuel;
         const __bf16 fh = (__bf16)ff, fl = (__bf16)(ff - (float)fh);
         bf16x8 ob;
         ob[0] = (__bf16)(float)x;
@@ -221,16 +239,24 @@ __global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(W1f[mt * 64 + lane], ob, c, 0, 0, 0);
             relu_pack(c, h1[mt]);
         }
+        {  // fc2 + relu: the 4 row tiles advance together, so consecutive MFMAs are
+           // independent and each k-step's 4 fragments are read in one batch
+            f32x16 c2[4];
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {  // fc2 + relu
-            f32x16 c = bias_frag(B2 + mt * 32 + 4 * h);
+            for (int mt = 0; mt < 4; ++mt) c2[mt] = bias_frag(B2 + mt * 32 + 4 * h);
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-                for (int s = 0; s < 2; ++s)
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(W2f[((mt * 4 + kt) * 2 + s) * 64 + lane],
-                                                                 h1[kt][s], c, 0, 0, 0);
-            relu_pack(c, h2[mt]);
+                for (int s = 0; s < 2; ++s) {
+                    bf16x8 wf[4];
+#pragma unroll
+                    for (int mt = 0; mt < 4; ++mt) wf[mt] = W2f[((mt * 4 + kt) * 2 + s) * 64 + lane];
+#pragma unroll
+                    for (int mt = 0; mt < 4; ++mt)
+                        c2[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[mt], h1[kt][s], c2[mt], 0, 0, 0);
+                }
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) relu_pack(c2[mt], h2[mt]);
         }
 
         // is_valid_action (dqn.py:125-175): moves always; SELECT p at the ship's cell
@@ -242,14 +268,14 @@ __global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
         float best = -INFINITY;
         int bidx = 0x7fffffff;
         for (int mt = 0; mt < q.mt3; ++mt) {  // fc3 + the masked first-maximum argmax
-            f32x16 c = bias_frag(B3 + mt * 32 + 4 * h);
-#pragma unroll
-            for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-                for (int s = 0; s < 2; ++s)
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(W3f[((mt * 4 + kt) * 2 + s) * 64 + lane],
-                                                                 h2[kt][s], c, 0, 0, 0);
-            const int base = mt * 32;
+            const int base = mt * 32, top = base + 31;
+            // a tile no env of the wave can choose from is skipped, MFMAs included
+            // (exact: its rows are invalid for all 32 envs); with port stocks <= 20
+            // (add_port's randint(5, 20)) the valid rows sit in the first few tiles
+            const bool maybe = (mt == 0) | ((cur >= 0) & (base < 4 + P)) |
+                               ((cst > 0) & (c_lo <= top) & (c_hi >= base)) |
+                               ((fst > 0) & (f_lo <= top) & (f_hi >= base));
+            if (!A.q_out && !__any(maybe)) continue;
             uint32_t m = range_bits(-base, 3 - base) | range_bits(c_lo - base, c_hi - base) |
                          range_bits(f_lo - base, f_hi - base);
             if (base < 4 + P) {  // SELECT rows live in this tile (uniform)
@@ -258,6 +284,13 @@ __global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
                     if (p != origin && i >= 0 && i < 32) m |= 1u << i;
                 }
             }
+            bf16x8 wf[8];  // the tile's 8 fragments, read before the chain consumes them
+#pragma unroll
+            for (int k = 0; k < 8; ++k) wf[k] = W3f[(mt * 8 + k) * 64 + lane];
+            f32x16 c = bias_frag(B3 + mt * 32 + 4 * h);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k], h2[k >> 1][k & 1], c, 0, 0, 0);
             m >>= 4 * h;  // register reg holds row base + 4h + (reg & 3) + 8 (reg >> 2)
 #pragma unroll
             for (int reg = 0; reg < 16; ++reg) {
