@@ -287,14 +287,14 @@ def roofline(bytes_per_step, n, k_ms, canonical):
     }
 
 
-def pmc_traffic():
+def pmc_traffic(key="step_kernel_bytes_per_launch"):
     """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if any."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
         d = json.load(f)
-    return d.get("step_kernel_bytes_per_launch"), os.path.relpath(path, ROOT)
+    return d.get(key), os.path.relpath(path, ROOT)
 
 
 def cpu_baseline(n_workload, ports_seed, budget_s):
@@ -368,6 +368,7 @@ def main():
     if not args.no_config4:
         ports64 = random_water_ports(builtin_water(), 64, seed=3)
         el4, k4, stats = run_config(n, ports64, True, args, dist, "config4")
+        t4, src4 = pmc_traffic("step_kernel_auto_bytes_per_launch")
         out["config4"] = {
             "workload": "BASELINE configs[3]: N=2^20 envs/GPU, 64 random ports, auto-reset, "
                         "ballot-compacted done list, per-block return reduction, RCCL all-reduce "
@@ -379,6 +380,9 @@ def main():
             "mean_return": stats[0] / stats[1] if stats and stats[1] else None,
             "mean_len": stats[2] / stats[1] if stats and stats[1] else None,
         }
+        if t4:
+            out["config4"]["roofline"]["traffic"] = t4
+            out["config4"]["roofline"]["traffic_source"] = src4
 
     if args.rollouts:
         out["rollouts"] = run_rollouts(n, args, dist)

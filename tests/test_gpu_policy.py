@@ -173,3 +173,20 @@ def test_stale_packing_is_refused():
         pol.act(0.0, 1)
     pol.set_weights()
     pol.act(0.0, 1)
+
+
+def test_shard_invariance():
+    """A shard (env_id_base = 2048) holding envs [2048, 3072) of a full run chooses
+    exactly what the full run chooses there: exploration is keyed by the global id."""
+    from shippingenv_amd.policy import QPolicy
+    from shippingenv_amd.vec import VecEnv
+
+    env, model, pol = make(4096, steps=7)
+    full = pol.act(0.5, 21).cpu().numpy()
+    part = VecEnv(1024, seed=env.seed, env_id_base=2048)
+    _OPEN.append(part)
+    for f in ("x", "y", "fuel", "cargo", "origin", "dest"):
+        getattr(part, f).copy_(getattr(env, f)[2048:3072])
+    ppol = QPolicy(part, model)
+    _OPEN.append(ppol)
+    np.testing.assert_array_equal(ppol.act(0.5, 21).cpu().numpy(), full[2048:3072])

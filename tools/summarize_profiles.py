@@ -43,16 +43,17 @@ def main():
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     summary = {"tag": tag, "kernels": {}, "pmc": {}}
-    for name in ("kt_c3", "kt_c4", "kt_big"):
+    for name in ("kt_c3", "kt_c4", "kt_big", "kt_roll", "kt_pol"):
         f = os.path.join(src, f"{name}_kernel_stats.csv")
         if os.path.exists(f):
             shutil.copy(f, os.path.join(dst, f"{name}_kernel_stats.csv"))
             summary["kernels"][name] = kstats(f)
-    for name in ("fetch_c3", "write_c3", "fetch_big", "write_big", "sq_c3", "sq2_c3"):
+    for name in ("fetch_c3", "write_c3", "fetch_big", "write_big", "fetch_c4", "write_c4", "sq_c3",
+                 "sq2_c3"):
         summary["pmc"][name] = counters(os.path.join(src, f"pmc_{name}_counter_collection.csv"))
-    n = {"c3": 1 << 20, "big": 1 << 24}
+    n = {"c3": 1 << 20, "big": 1 << 24, "c4": 1 << 20}
     traffic = {}
-    for k in ("c3", "big"):
+    for k in ("c3", "big", "c4"):
         fe = summary["pmc"].get(f"fetch_{k}", {}).get("FETCH_SIZE")
         wr = summary["pmc"].get(f"write_{k}", {}).get("WRITE_SIZE")
         if fe is not None and wr is not None:
@@ -70,6 +71,9 @@ def main():
             json.dump({"source": f"profiles/{tag}/summary.json",
                        "step_kernel_bytes_per_launch": round(traffic["c3"]["bytes_per_launch"]),
                        "workload": "config 3, N=2^20",
+                       "step_kernel_auto_bytes_per_launch":
+                           round(traffic["c4"]["bytes_per_launch"]) if "c4" in traffic else None,
+                       "workload_auto": "config 4, N=2^20 (done-list records and the stats slab included)",
                        "correction": "FETCH_SIZE x2 (gfx950 half-count), WRITE_SIZE x1, KiB->B"},
                       f, indent=1)
     print(json.dumps({"traffic": traffic, "kernels": {k: {n: v["avg_us"] for n, v in d.items()
