@@ -57,6 +57,9 @@ def parse():
                    help="extra HBM-resident run (working set beyond the 256 MiB MALL); 0 = skip")
     p.add_argument("--dqn-steps", type=int, default=50,
                    help="config 5: timed DQN policy + step iterations at N envs/GPU; 0 = skip")
+    p.add_argument("--train-steps", type=int, default=30,
+                   help="timed vectorised DQN training iterations (policy, step, replay, update); 0 = skip")
+    p.add_argument("--train-batch", type=int, default=8192, help="DQN minibatch per update")
     p.add_argument("--rollouts", type=int, default=20,
                    help="timed se_rollout launches (MCTS random rollouts, 2^20 x 100 steps); 0 = skip")
     return p.parse_args()
@@ -271,6 +274,61 @@ def run_dqn(n, args, dist):
     }
 
 
+def run_dqn_train(n, args, dist):
+    """the vectorised DQN training loop (shippingenv_amd.dqn.VecDQNAgent).
+    One iteration for all N envs: fused policy, replay begin, se_step (auto-reset),
+    replay end and cut, reset of cut envs, then one update. The update is captured as
+    one HIP graph: minibatch sample, DQNNetwork forward and backward at batch B, Adam,
+    and the policy repack. Random-init weights; the reference's hyperparameters
+    (gamma 0.95, lr 1e-3, epsilon decay 0.995), with B = --train-batch."""
+    from shippingenv_amd.dqn import VecDQNAgent
+    from shippingenv_amd.vec import VecEnv
+
+    env = VecEnv(n, seed=args.seed, env_id_base=dist.rank * n, device=dist.dev, auto_reset=True)
+    env.reset()
+    torch.manual_seed(args.seed)
+    agent = VecDQNAgent(env, batch_size=args.train_batch, memory_size=4 * n, graph=True)
+    for _ in range(6):  # eager warm-up updates, then the graph capture
+        agent.step()
+    stream = torch.cuda.current_stream(env.device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.train_steps):
+        loss = agent.step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    dist.barrier()
+    wall = dist.max(time.perf_counter() - t0)
+    kern_ms = e0.elapsed_time(e1) / args.train_steps
+    e0.record(stream)
+    for _ in range(args.train_steps):
+        agent.update()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    upd_ms = e0.elapsed_time(e1) / args.train_steps
+    out = {
+        "workload": "8f row 3: vectorised DQN training, N envs/GPU (auto-reset, default ports): "
+                    "fused policy + se_step + device replay ring + one graph-captured update "
+                    f"(B = {args.train_batch}) per iteration; random-init weights",
+        "value": round(n * dist.world * args.train_steps / wall, 1),
+        "unit": "env-steps/s (training loop)",
+        "ms_per_step": round(wall / args.train_steps * 1e3, 4),
+        "stream_ms_per_step": round(kern_ms, 4),
+        "update_ms": round(upd_ms, 4),
+        "updates_per_s": round(1e3 / upd_ms, 1),
+        "batch": args.train_batch,
+        "replay_capacity": agent.memory.capacity,
+        "final_loss": float(loss),
+        "epsilon": agent.epsilon,
+    }
+    agent.close()
+    env.close()
+    return out
+
+
 def roofline(bytes_per_step, n, k_ms, canonical):
     achieved = bytes_per_step * n / (k_ms * 1e-3) / 1e9
     return {
@@ -389,6 +447,9 @@ def main():
 
     if args.dqn_steps:
         out["config5_dqn"] = run_dqn(n, args, dist)
+
+    if args.train_steps and dist.world == 1:  # one learner per GPU; no gradient exchange is built
+        out["dqn_train"] = run_dqn_train(n, args, dist)
 
     if args.large_n and dist.world == 1:
         small = argparse.Namespace(**vars(args))

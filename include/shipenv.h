@@ -219,6 +219,63 @@ int se_policy(se_qnet* q, int32_t* actions, double epsilon, uint32_t t, float* q
               void* stream);
 int se_qnet_destroy(se_qnet* q);  /* destroy a qnet before the env it was created on */
 
+/* DQN experience replay on the device (agents/dqn.py): remember (:117-123) into a ring of
+ * `capacity` transitions (deque(maxlen=memory_size)), and update()'s minibatch (:213-224:
+ * random.sample, then the preprocess_state rows as f32). A transition is stored compactly
+ * (ship bytes, f32 fuel, action, f32 reward, flags) for s and s'; the constant port block
+ * of the rows is rebuilt from the world when sampling. capacity in [max(n, 1), 2^31). */
+typedef struct se_replay se_replay;
+int se_replay_create(se_replay** out, se_env* env, int64_t capacity);
+/* Record s and the agent-index actions of every env: call right before se_step. */
+int se_replay_begin(se_replay* r, const int32_t* actions, void* stream);
+/* Record reward, done and s' after se_step: appends n transitions (FIFO eviction). A
+ * step that raised (err != 0) is stored flagged and never sampled: the reference's loop
+ * breaks before remember (:304-309). cut (optional, device u8[n]): 1 where the episode must
+ * restart, i.e. the step raised or ep_len >= max_steps (max_steps > 0 needs an auto-reset
+ * env, :281); pass it to se_reset. */
+int se_replay_end(se_replay* r, uint8_t* cut, int32_t max_steps, void* stream);
+int se_replay_size(se_replay* r, int64_t* size, int64_t* capacity);
+/* A minibatch of `batch` distinct transitions: batch position j takes logical index
+ * perm(j) of a 4-round Feistel permutation of [0, size) keyed by Philox(seed, 2^64 - 1) at
+ * (t, slot 15), skipping flagged ones through positions j + B, j + 2B, j + 3B (weight 0 if
+ * all four are flagged or beyond size). t is read from t_dev (device u32) when non-NULL, so
+ * the launch can be captured in a graph with a device-side update counter. Outputs
+ * (device): obs and next_obs [batch][6+4P] f32 rows, actions int64, rewards, dones
+ * (1.0 / 0.0) and weights (1.0 / 0.0) f32 [batch]. */
+int se_replay_sample(se_replay* r, int64_t batch, const uint32_t* t_dev, uint32_t t, float* obs,
+                     float* next_obs, int64_t* actions, float* rewards, float* dones, float* weights,
+                     void* stream);
+int se_replay_destroy(se_replay* r);  /* destroy a replay before the env it was created on */
+
+/* The DQN update (agents/dqn.py:206-245) fused on f32 MFMA: two kernels per update.
+ * Target y = r + gamma * max_a target(s')[a] * (1 - done), loss = sum w (q - y)^2 / sum w
+ * (nn.MSELoss when every w is 1), backward, and one Adam step (torch.optim.Adam, no weight
+ * decay) on the online parameters in place. Deterministic: no atomics, fixed summation
+ * orders. Parameters: DEVICE f32 tensors of DQNNetwork (hidden 128, torch nn.Linear layout);
+ * adam_m / adam_v: zero-initialised tensors of the same shapes (exp_avg, exp_avg_sq). */
+typedef struct se_mlp {
+    float* w1; float* b1;  /* fc1 [128][6+4P], [128] */
+    float* w2; float* b2;  /* fc2 [128][128], [128] */
+    float* w3; float* b3;  /* fc3 [A][128], [A]; A = 4+P+250 */
+} se_mlp;
+typedef struct se_qtrain se_qtrain;
+int se_qtrain_create(se_qtrain** out, se_env* env, int64_t max_batch);  /* 1 <= P <= 64 */
+/* Bind the parameter sets and build the kernel's images of both networks (fragment order,
+ * fc1's port block folded with the env's ports of this moment). */
+int se_qtrain_bind(se_qtrain* q, const se_mlp* online, const se_mlp* target, const se_mlp* adam_m,
+                   const se_mlp* adam_v, void* stream);
+/* Rebuild the images of one network (0 online, 1 target) after its parameters changed
+ * outside se_qtrain_step (e.g. the target-network copy, update_target_model :109-111). */
+int se_qtrain_pack(se_qtrain* q, int32_t which, void* stream);
+/* One update on a minibatch (se_replay_sample's outputs, batch <= max_batch). step_dev:
+ * device int32 holding the number of Adam steps already taken (bias correction uses it
+ * + 1; the caller increments it). loss_out: device f32. Capturable in a graph. */
+int se_qtrain_step(se_qtrain* q, int64_t batch, const float* obs, const float* next_obs, const int64_t* act,
+                   const float* rew, const float* done, const float* weight, float gamma, float lr,
+                   float beta1, float beta2, float eps, const int32_t* step_dev, float* loss_out,
+                   void* stream);
+int se_qtrain_destroy(se_qtrain* q);  /* destroy before the env it was created on */
+
 /* Episode statistics accumulated by the auto-reset path since the last clear:
  * out[0] = sum of returns, out[1] = episodes, out[2] = sum of lengths (device
  * double[3]). Deterministic: per-block partials are summed in a fixed order. */

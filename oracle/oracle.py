@@ -47,6 +47,9 @@ def _lib():
     lib.orc_philox4x32_10.argtypes = [P, P, P]
     lib.orc_gen_actions.argtypes = [i64, i32, u64, i64, u32, P]
     lib.orc_sample_actions.argtypes = [P, i64] + [P] * 6 + [u64, i64, u32, P, P, P]
+    lib.orc_feistel_perm.argtypes = [u32, u32, P]
+    lib.orc_feistel_perm.restype = u32
+    lib.orc_replay_pick.argtypes = [i64, i64, P, u64, u32, P]
     lib.orc_rollout.argtypes = [P, i64] + [P] * 6 + [i64, P, i32, i32, u64, i64, P, P, P]
     return lib
 
@@ -188,3 +191,55 @@ def rollout(world, st, src, *, max_steps, max_attempts, seed, rollout_base=0):
     lib().orc_rollout(world.ref, st.n, *st.fields(), m, _p(s), max_steps, max_attempts, seed,
                       rollout_base, _p(ret), _p(steps), _p(status))
     return ret, steps, status
+
+
+def feistel_perm(p, D, key):
+    k = np.ascontiguousarray(key, np.uint32)
+    return int(lib().orc_feistel_perm(p, D, _p(k)))
+
+
+def replay_pick(size, batch, invalid, *, seed, t):
+    """update()'s minibatch indices (agents/dqn.py:213) under the sampler contract."""
+    inv = np.ascontiguousarray(invalid, np.uint8)
+    assert len(inv) >= size
+    slot = np.zeros(batch, np.int64)
+    lib().orc_replay_pick(size, batch, _p(inv), seed, t, _p(slot))
+    return slot
+
+
+class ReplayMemory:
+    """DQNAgent.memory (agents/dqn.py:86, :117-123) as the reference keeps it: a FIFO of
+    (preprocess_state row, action, reward, next row, done) of capacity `maxlen`, as
+    numpy rows, here in ring order (slot = push index mod maxlen) so that indices
+    line up with the device ring. `invalid` marks transitions whose step raised (the
+    reference never stores them; the device ring keeps them flagged)."""
+
+    def __init__(self, maxlen, width):
+        self.maxlen, self.size, self.head = maxlen, 0, 0
+        self.obs = np.zeros((maxlen, width), np.float32)
+        self.next_obs = np.zeros((maxlen, width), np.float32)
+        self.act = np.zeros(maxlen, np.int64)
+        self.rew = np.zeros(maxlen, np.float32)
+        self.done = np.zeros(maxlen, np.float32)
+        self.invalid = np.zeros(maxlen, np.uint8)
+
+    def push(self, obs, act, rew, next_obs, done, invalid):
+        for i in range(len(act)):
+            s = self.head
+            self.obs[s], self.next_obs[s] = obs[i], next_obs[i]
+            self.act[s], self.rew[s], self.done[s] = act[i], rew[i], float(bool(done[i]))
+            self.invalid[s] = 1 if invalid[i] else 0
+            self.head = (self.head + 1) % self.maxlen
+        self.size = min(self.size + len(act), self.maxlen)
+
+    def sample(self, batch, *, seed, t):
+        """-> obs, next_obs, act, rew, done, weight exactly as se_replay_sample writes them."""
+        slot = replay_pick(self.size, batch, self.invalid, seed=seed, t=t)
+        ok = slot >= 0
+        s = np.where(ok, slot, 0)
+        w = self.obs.shape[1]
+        z = np.zeros(w, np.float32)
+        obs = np.where(ok[:, None], self.obs[s], z)
+        nxt = np.where(ok[:, None], self.next_obs[s], z)
+        return (obs, nxt, np.where(ok, self.act[s], 0), np.where(ok, self.rew[s], 0).astype(np.float32),
+                np.where(ok, self.done[s], 0).astype(np.float32), ok.astype(np.float32))

@@ -47,7 +47,8 @@ enum { U_FUEL_GATE = 1, U_LOSS_TYPE = 2, U_BETA = 4, U_ARRIVE = 8 };
  * explicit reset and the synthetic agent draw one block per env. */
 enum { SLOT_FUEL = 0, SLOT_LOSS = 1, SLOT_BETA1 = 2, SLOT_ARRIVE = 3, SLOT_RESET = 4,
        SLOT_EXPLICIT_RESET = 5, SLOT_ACTION = 6, SLOT_GATE = 7, SLOT_BETA2 = 8, SLOT_BETA3 = 9,
-       SLOT_RESET_DEST = 10, SLOT_SAMPLE = 11, SLOT_ROLLOUT = 12, SLOT_ROLLOUT_B = 13 };
+       SLOT_RESET_DEST = 10, SLOT_SAMPLE = 11, SLOT_ROLLOUT = 12, SLOT_ROLLOUT_B = 13,
+       SLOT_REPLAY = 15 };
 
 /* sample_action results where the reference raises / never returns (include/shipenv.h) */
 enum { SAMPLE_RAISES = -1, SAMPLE_NO_OTHER_PORT = -2 };
@@ -589,6 +590,56 @@ int orc_gen_actions(int64_t n, int32_t P, uint64_t seed, int64_t env_id_base, ui
         else if (c < 98) a = 4 + P + 50 + 1 + uniform_int(o[1], 20);
         else a = 4 + uniform_int(o[2], P);
         actions[i] = a;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ DQN replay minibatch */
+/* update()'s random.sample(memory, batch_size) (agents/dqn.py:213) under the build's
+ * contract: a 4-round Feistel permutation of [0, size) on 2h bits (2h >= log2 size),
+ * round function lowbias32(R ^ key[r]) masked to h bits, cycle-walked into the domain;
+ * keys = Philox(seed, env id 2^64 - 1) at (t, SLOT_REPLAY). Batch position j takes the
+ * first unflagged index among perm(j + k * B), k < 4, positions < size; else -1. */
+static uint32_t lowbias32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+uint32_t orc_feistel_perm(uint32_t p, uint32_t D, const uint32_t key[4]) {
+    uint32_t bits = 2;
+    while (bits < 32 && ((uint64_t)1 << bits) < (uint64_t)D) bits += 2;
+    const uint32_t h = bits / 2, m = (1u << h) - 1u;
+    do {
+        uint32_t L = p >> h, R = p & m;
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t nl = R;
+            R = L ^ (lowbias32(R ^ key[r]) & m);
+            L = nl;
+        }
+        p = (L << h) | R;
+    } while (p >= D);
+    return p;
+}
+
+int orc_replay_pick(int64_t size, int64_t batch, const uint8_t* invalid, uint64_t seed, uint32_t t,
+                    int64_t* slot) {
+    uint32_t key[4];
+    draw4(seed, -1, t, SLOT_REPLAY, key);
+    for (int64_t j = 0; j < batch; ++j) {
+        slot[j] = -1;
+        for (int k = 0; k < 4; ++k) {
+            const int64_t pos = j + k * batch;
+            if (pos >= size) break;
+            const uint32_t l = orc_feistel_perm((uint32_t)pos, (uint32_t)size, key);
+            if (!invalid[l]) {
+                slot[j] = l;
+                break;
+            }
+        }
     }
     return 0;
 }

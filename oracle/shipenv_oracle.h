@@ -97,6 +97,12 @@ void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t ou
 int orc_gen_actions(int64_t n, int32_t P, uint64_t seed, int64_t env_id_base, uint32_t t,
                     int32_t* actions);
 
+/* update()'s minibatch indices (agents/dqn.py:213) under the build's sampler contract
+ * (include/shipenv.h se_replay_sample): slot[j] in [0, size) or -1. */
+uint32_t orc_feistel_perm(uint32_t p, uint32_t D, const uint32_t key[4]);
+int orc_replay_pick(int64_t size, int64_t batch, const uint8_t* invalid, uint64_t seed, uint32_t t,
+                    int64_t* slot);
+
 #ifdef __cplusplus
 }
 #endif

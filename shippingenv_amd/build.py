@@ -15,7 +15,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "shipenv.hip")
-DEPS = [SRC, os.path.join(HERE, "csrc", "philox.h"), os.path.join(HERE, "csrc", "qpolicy.h"),
+DEPS = [SRC, os.path.join(HERE, "csrc", "philox.h"), os.path.join(HERE, "csrc", "qpolicy.h"), os.path.join(HERE, "csrc", "replay.h"),
+        os.path.join(HERE, "csrc", "qtrain.h"),
         os.path.join(ROOT, "include", "shipenv.h")]
 OUT = os.path.join(HERE, "_lib", "libshipenv_hip.so")
 ARCH = os.environ.get("SHIPENV_OFFLOAD_ARCH", "gfx950")

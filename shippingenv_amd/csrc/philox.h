@@ -30,6 +30,7 @@ enum Slot : uint32_t {
     kSlotRollout = 12,       // rollout attempt, per rollout: sample word, u_fuel, u_gate, u_type
     kSlotRolloutB = 13,      // rollout attempt (partial loss / arrival): 3 beta uniforms, dest
     kSlotPolicy = 14,        // se_policy, per env: explore draw, random.choice index
+    kSlotReplay = 15,        // se_replay_sample, key (seed, 2^64 - 1), t = update: Feistel round keys
 };
 
 struct U4 {

@@ -1,0 +1,717 @@
+// qtrain.h — the DQN update fused on fp32 MFMA.
+//
+// Part of shipenv.hip's translation unit (included at its end, after replay.h).
+// Reference: agents/dqn.py DQNAgent.update (:206-245) on a sampled minibatch.
+// It computes q = DQNNetwork(states)[a] and y = r + gamma * max target(next_states) * (1 - done),
+// then nn.MSELoss and backward, then Adam (lr, betas (0.9, 0.999), eps 1e-8).
+//
+// The torch version is about 50 small kernels per update, launch-bound below B = 2^13.
+// Here it is two kernels, all in f32 (v_mfma_f32_32x32x2_f32 is an exact f32 fma chain,
+// and gfx950 has no xf32), deterministic (fixed summation orders, no atomics):
+//
+// T1, qtrain_tile_kernel (one workgroup per 32 samples, 4 waves, one 32-row feature tile
+// per wave):
+// * Target net forward: fc1, fc2, then fc3 over all A rows, with a per-sample max.
+// * Online net forward: fc1, fc2.
+// * q_j = W3[a_j] . h2_j + b3[a_j]. Only the chosen action's Q gets a gradient, so fc3
+//   is a row gather here, not a GEMM.
+// * g_j = 2 w_j (q_j - y_j), then dH2 = g_j W3[a_j] (a gather too) and dZ2 = dH2 (h2 > 0).
+// * dH1 = W2^T dZ2 on MFMA, then dZ1 = dH1 (h1 > 0).
+// * Per-tile partial gradients: dW2 = dZ2 H1^T (MFMA, K = 32 samples), dW1 of the six
+//   dynamic columns, db1, db2, the loss sum and the weight sum.
+// * Per-tile partial dW3 = G H2^T on MFMA, with G[a][j] = (a_j == a) g_j built in the
+//   operand from the tile's action list. Only the 32-row action tiles that hold one of
+//   the tile's actions are computed and stored; a presence bitmask marks them.
+// * The port block of every observation row is the same, so fc1 runs on the six
+//   dynamic columns with W1[:, 6:] . port + b1 folded into its bias. dW1[:, 6:] is then
+//   db1 (x) port.
+//
+// T2, qtrain_adam_kernel (256-thread workgroups over 64-element parameter blocks, and one
+// per W1 row):
+// * Sums the tile partials with the threads spread over the tiles: 16 tile groups x 16
+//   float4 columns, then a fixed tree. Every load is independent, so the reduction
+//   streams instead of walking one dependent load per tile.
+// * Divides by sum(w): the MSE mean, since w = 1 on a full batch.
+// * Takes one Adam step on the parameters in place (torch nn.Linear layout).
+// * Rewrites the online net's MFMA fragment images, and refolds fc1's bias for the
+//   next update.
+//
+// The weight operands are pre-permuted into A-fragment order, [row tile][k step][lane],
+// one coalesced 256-byte load per MFMA per wave. Activations are [feature][sample]
+// LDS tiles with a 33-float row stride, so both operand orientations read
+// conflict-free.
+
+namespace {
+
+constexpr int kQT = 32;       // samples per T1 workgroup
+constexpr int kLS = 33;       // LDS row stride (floats) of a [feature][sample] tile
+constexpr int kQTBlock = 256; // T1: 4 waves
+constexpr int kQABlock = 128; // fold / pack workgroups
+constexpr int kQRBlock = 256; // T2 workgroups
+
+struct QtDims {
+    int32_t P, in, A, mt3;  // in = 6 + 4P; mt3 = fc3 row tiles (A rounded up to 32)
+};
+
+struct Mlp {
+    float *w1, *b1, *w2, *b2, *w3, *b3;  // DQNNetwork, torch nn.Linear layout
+};
+
+struct QtWork {
+    float* pw1[2];   // [4 tiles][3 steps][64]: fc1 over the dynamic columns (online, target)
+    float* pw2[2];   // [4][64][64]: fc2
+    float* pw2t;     // [4][64][64]: online fc2 transposed (backward)
+    float* pw3t;     // [mt3][64][64]: target fc3
+    float* c1[2];    // [128]: b1 + W1[:, 6:] . port
+    float* portvec;  // [in - 6]: the preprocess_state port block
+    float* part_w2;  // [tiles][128][128]
+    float* part_w1d; // [tiles][128][6]
+    float* part_b1;  // [tiles][128]
+    float* part_b2;  // [tiles][128]
+    float* part_lw;  // [tiles][2]: sum w d^2, sum w
+    float* part_w3;  // [tiles][mt3][32][128]: only the action tiles present in the tile
+    float* part_b3;  // [tiles][mt3][32]
+    uint32_t* present; // [tiles]: bit rt = the tile holds an action of fc3 row tile rt
+};
+
+__device__ __forceinline__ int acc_r(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
+
+__device__ __forceinline__ f32x16 mfma_f32(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// acc += A (packed fragments of one row tile) x B (an LDS [k][kLS] tile), kSteps k-pairs.
+// All A fragments are loaded before the first MFMA: one L2 round trip per layer.
+template <int kSteps>
+__device__ __forceinline__ f32x16 gemm_lds(const float* __restrict__ pa, const float* src, f32x16 acc, int lane) {
+    const int h = lane >> 5, c = lane & 31;
+    float a[kSteps];
+#pragma unroll
+    for (int s = 0; s < kSteps; ++s) a[s] = pa[s * 64 + lane];
+#pragma unroll
+    for (int s = 0; s < kSteps; ++s) acc = mfma_f32(a[s], src[(2 * s + h) * kLS + c], acc);
+    return acc;
+}
+
+__device__ __forceinline__ f32x16 bias_init(const float* bias, int tile, int lane, int rows) {
+    f32x16 a;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = tile * 32 + acc_r(r, lane);
+        a[r] = row < rows ? bias[row] : 0.0f;
+    }
+    return a;
+}
+
+__device__ __forceinline__ void store_relu(float* dst, int tile, const f32x16& acc, int lane) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float x = acc[r];
+        dst[(tile * 32 + acc_r(r, lane)) * kLS + (lane & 31)] = x > 0.0f ? x : 0.0f;
+    }
+}
+
+// sum over the 128 threads of a workgroup in a fixed tree order (all threads get it)
+__device__ __forceinline__ float block_sum128(float x, float* red) {
+    const int t = threadIdx.x;
+    red[t] = x;
+    __syncthreads();
+#pragma unroll
+    for (int s = 64; s > 0; s >>= 1) {
+        if (t < s) red[t] += red[t + s];
+        __syncthreads();
+    }
+    const float r = red[0];
+    __syncthreads();
+    return r;
+}
+
+// fc1 row f's port block folded into its bias: thread t sums the columns c = 6 + t,
+// 6 + t + 128, ... in order, then the fixed tree. The pack and the Adam kernel share it.
+__device__ __forceinline__ float fold_row(const float* w1row, int in, const float* portvec, float* red) {
+    float x = 0.0f;
+    for (int c = 6 + (int)threadIdx.x; c < in; c += kQABlock) x += w1row[c] * portvec[c - 6];
+    return block_sum128(x, red);
+}
+
+__device__ __forceinline__ int frag_index(int row, int k) {  // [row tile][k step][lane]
+    return ((row >> 5) * 64 + (k >> 1)) * 64 + (row & 31) + 32 * (k & 1);
+}
+
+struct QtPackArgs {
+    Mlp net;
+    int which;  // 0 online, 1 target
+    QtDims d;
+    QtWork W;
+    const uint32_t* world;
+    WorldDims wd;
+};
+
+// workgroup f < 128: the port vector (workgroup 0 stores it) and row f's fold; every
+// workgroup then packs a strided share of the fragments
+__global__ __launch_bounds__(kQABlock) void qtrain_pack_kernel(QtPackArgs A) {
+    __shared__ float red[kQABlock];
+    __shared__ float port[4 * SE_MAX_PORTS];
+    const int P = A.d.P, in = A.d.in;
+    for (int c = threadIdx.x; c < 4 * P; c += kQABlock) {
+        const int p = c >> 2, f = c & 3;
+        const uint32_t pos = A.world[A.wd.pos() + p];
+        port[c] = f == 0 ? (float)(pos & 0xffu)
+                : f == 1 ? (float)((pos >> 8) & 0xffu)
+                : f == 2 ? (float)(int32_t)A.world[A.wd.pos() + P + p]
+                         : (float)(int32_t)A.world[A.wd.pos() + 2 * P + p];
+        if (blockIdx.x == 0) A.W.portvec[c] = port[c];
+    }
+    __syncthreads();
+    const int f = blockIdx.x;
+    if (f < 128) {
+        const float fold = fold_row(A.net.w1 + (int64_t)f * in, in, port, red);
+        if (threadIdx.x == 0) A.W.c1[A.which][f] = A.net.b1[f] + fold;
+    }
+    const int n1 = 4 * 3 * 64, n2 = 4 * 64 * 64, n3 = A.which ? A.d.mt3 * 64 * 64 : 0;
+    const int total = n1 + 2 * n2 + n3;
+    for (int e = blockIdx.x * kQABlock + threadIdx.x; e < total; e += gridDim.x * kQABlock) {
+        if (e < n1) {
+            const int lane = e & 63, s = (e >> 6) % 3, tile = e / (3 * 64);
+            const int row = tile * 32 + (lane & 31), k = 2 * s + (lane >> 5);
+            A.W.pw1[A.which][e] = A.net.w1[(int64_t)row * in + k];
+        } else if (e < n1 + n2) {
+            const int i = e - n1, lane = i & 63, s = (i >> 6) & 63, tile = i >> 12;
+            A.W.pw2[A.which][i] = A.net.w2[(tile * 32 + (lane & 31)) * 128 + 2 * s + (lane >> 5)];
+        } else if (e < n1 + 2 * n2) {
+            if (A.which) continue;  // the transposed image is the online net's (backward)
+            const int i = e - n1 - n2, lane = i & 63, s = (i >> 6) & 63, tile = i >> 12;
+            A.W.pw2t[i] = A.net.w2[(2 * s + (lane >> 5)) * 128 + tile * 32 + (lane & 31)];
+        } else {
+            const int i = e - n1 - 2 * n2, lane = i & 63, s = (i >> 6) & 63, tile = i >> 12;
+            const int row = tile * 32 + (lane & 31);
+            A.W.pw3t[i] = row < A.d.A ? A.net.w3[row * 128 + 2 * s + (lane >> 5)] : 0.0f;
+        }
+    }
+}
+
+struct QtStepArgs {
+    QtWork W;
+    Mlp on, tg;
+    QtDims d;
+    int64_t B;
+    const float *obs, *next_obs;
+    const int64_t* act;
+    const float *rew, *done, *weight;
+    float gamma;
+};
+
+__global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
+    extern __shared__ float sm[];
+    float* X = sm;                  // [8][kLS] obs, dynamic columns (rows 6, 7 zero)
+    float* XN = X + 8 * kLS;        // next obs
+    float* HA = XN + 8 * kLS;       // [128][kLS] h1 (target, then online)
+    float* HB = HA + 128 * kLS;     // h2
+    float* DZ2 = HB + 128 * kLS;
+    float* DZ1 = DZ2 + 128 * kLS;
+    float* QM = DZ1 + 128 * kLS;    // [4][32] per-wave max of the target Q
+    float* Y = QM + 4 * 32;         // [32] targets
+    float* G = Y + 32;              // [32] g_j
+    float* LW = G + 32;             // [32] w_j d_j^2
+    float* WT = LW + 32;            // [32] w_j
+    int* ACT = reinterpret_cast<int*>(WT + 32);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t r0 = (int64_t)blockIdx.x * kQT;
+    const int in = A.d.in;
+
+    for (int e = tid; e < 2 * 8 * 32; e += kQTBlock) {
+        const int which = e >> 8, c = (e >> 5) & 7, j = e & 31;
+        const int64_t row = r0 + j;
+        float v = 0.0f;
+        if (c < 6 && row < A.B) v = (which ? A.next_obs : A.obs)[row * in + c];
+        (which ? XN : X)[c * kLS + j] = v;
+    }
+    if (tid < 32) {
+        const int64_t row = r0 + tid;
+        const bool live = row < A.B;
+        ACT[tid] = live ? (int)A.act[row] : 0;
+        WT[tid] = live ? A.weight[row] : 0.0f;
+    }
+    __syncthreads();
+
+    // target network on next_states: fc1, fc2, fc3 and the max over actions
+    {
+        f32x16 acc = bias_init(A.W.c1[1], wave, lane, 128);
+        acc = gemm_lds<3>(A.W.pw1[1] + wave * 3 * 64, XN, acc, lane);
+        store_relu(HA, wave, acc, lane);
+    }
+    __syncthreads();
+    {
+        f32x16 acc = bias_init(A.tg.b2, wave, lane, 128);
+        acc = gemm_lds<64>(A.W.pw2[1] + wave * 64 * 64, HA, acc, lane);
+        store_relu(HB, wave, acc, lane);
+    }
+    __syncthreads();
+    {
+        float m = -INFINITY;
+        for (int t = wave; t < A.d.mt3; t += 4) {
+            f32x16 acc = bias_init(A.tg.b3, t, lane, A.d.A);
+            acc = gemm_lds<64>(A.W.pw3t + t * 64 * 64, HB, acc, lane);
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (t * 32 + acc_r(r, lane) < A.d.A) m = fmaxf(m, acc[r]);
+        }
+        m = fmaxf(m, __shfl_xor(m, 32));
+        if (lane < 32) QM[wave * 32 + lane] = m;
+    }
+    __syncthreads();
+    if (tid < 32) {
+        const int64_t row = r0 + tid;
+        const float mx = fmaxf(fmaxf(QM[tid], QM[32 + tid]), fmaxf(QM[64 + tid], QM[96 + tid]));
+        Y[tid] = row < A.B ? A.rew[row] + (A.gamma * mx) * (1.0f - A.done[row]) : 0.0f;
+    }
+
+    // online network on states: fc1, fc2 (h1 -> HA, h2 -> HB; the target's are consumed)
+    {
+        f32x16 acc = bias_init(A.W.c1[0], wave, lane, 128);
+        acc = gemm_lds<3>(A.W.pw1[0] + wave * 3 * 64, X, acc, lane);
+        store_relu(HA, wave, acc, lane);
+    }
+    __syncthreads();
+    {
+        f32x16 acc = bias_init(A.on.b2, wave, lane, 128);
+        acc = gemm_lds<64>(A.W.pw2[0] + wave * 64 * 64, HA, acc, lane);
+        store_relu(HB, wave, acc, lane);
+    }
+    __syncthreads();
+
+    // q_j = W3[a_j] . h2_j + b3[a_j]; g_j = 2 w_j (q_j - y_j)
+    {
+        const int j = tid >> 3, part = tid & 7, a = ACT[j];
+        const float* w3r = A.on.w3 + (int64_t)a * 128 + part * 16;
+        float s = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) s += w3r[k] * HB[(part * 16 + k) * kLS + j];
+        s += __shfl_xor(s, 1);
+        s += __shfl_xor(s, 2);
+        s += __shfl_xor(s, 4);
+        if (part == 0) {
+            const float d = (s + A.on.b3[a]) - Y[j];
+            G[j] = 2.0f * WT[j] * d;
+            LW[j] = WT[j] * d * d;
+        }
+    }
+    __syncthreads();
+
+    // dZ2 = (h2 > 0) g_j W3[a_j]
+    {
+        const int j = tid & 31, f0 = (tid >> 5) * 16, a = ACT[j];
+        const float g = G[j];
+        const float* w3r = A.on.w3 + (int64_t)a * 128 + f0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) DZ2[(f0 + k) * kLS + j] = HB[(f0 + k) * kLS + j] > 0.0f ? g * w3r[k] : 0.0f;
+    }
+    __syncthreads();
+
+    // dH1 = W2^T dZ2 -> dZ1 = (h1 > 0) dH1
+    {
+        f32x16 acc = {};
+        acc = gemm_lds<64>(A.W.pw2t + wave * 64 * 64, DZ2, acc, lane);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int f = wave * 32 + acc_r(r, lane), c = lane & 31;
+            DZ1[f * kLS + c] = HA[f * kLS + c] > 0.0f ? acc[r] : 0.0f;
+        }
+    }
+    __syncthreads();
+
+    // partial dW2[f2][f1] = sum_j dZ2[f2][j] h1[f1][j]: row tile = wave, 4 column tiles
+    {
+        float* out = A.W.part_w2 + (int64_t)blockIdx.x * 128 * 128;
+        const int h = lane >> 5, c = lane & 31;
+        for (int ct = 0; ct < 4; ++ct) {
+            f32x16 acc = {};
+#pragma unroll
+            for (int s = 0; s < 16; ++s)
+                acc = mfma_f32(DZ2[(wave * 32 + c) * kLS + 2 * s + h], HA[(ct * 32 + c) * kLS + 2 * s + h], acc);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) out[(wave * 32 + acc_r(r, lane)) * 128 + ct * 32 + c] = acc[r];
+        }
+    }
+    // partial dW3[a][f] = sum_j (a_j == a) g_j h2[f][j] for the action tiles present:
+    // row tile rt, column tile = wave; db3 likewise
+    {
+        uint32_t present = 0;
+        for (int j = 0; j < 32; ++j)
+            if (r0 + j < A.B) present |= 1u << (ACT[j] >> 5);
+        const int h = lane >> 5, c = lane & 31;
+        for (int rt = 0; rt < A.d.mt3; ++rt) {
+            if (!((present >> rt) & 1u)) continue;  // block-uniform
+            const int a = rt * 32 + c;
+            f32x16 acc = {};
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                const int j = 2 * s + h;
+                acc = mfma_f32(ACT[j] == a ? G[j] : 0.0f, HB[(wave * 32 + c) * kLS + j], acc);
+            }
+            float* out = A.W.part_w3 + (((int64_t)blockIdx.x * A.d.mt3 + rt) * 32) * 128;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) out[acc_r(r, lane) * 128 + wave * 32 + c] = acc[r];
+            if (tid < 32) {
+                float s3 = 0.0f;
+                for (int j = 0; j < 32; ++j) s3 += ACT[j] == rt * 32 + tid ? G[j] : 0.0f;
+                A.W.part_b3[((int64_t)blockIdx.x * A.d.mt3 + rt) * 32 + tid] = s3;
+            }
+        }
+        if (tid == 0) A.W.present[blockIdx.x] = present;
+    }
+    // partial dW1 (dynamic columns), db1, db2, loss and weight sums
+    {
+        const int f = tid >> 1, c0 = (tid & 1) * 3;
+        float* o = A.W.part_w1d + ((int64_t)blockIdx.x * 128 + f) * 6 + c0;
+        for (int c = c0; c < c0 + 3; ++c) {
+            float s = 0.0f;
+            for (int j = 0; j < 32; ++j) s += DZ1[f * kLS + j] * X[c * kLS + j];
+            o[c - c0] = s;
+        }
+        const float* src = tid < 128 ? DZ2 + tid * kLS : DZ1 + (tid - 128) * kLS;
+        float s = 0.0f;
+        for (int j = 0; j < 32; ++j) s += src[j];
+        (tid < 128 ? A.W.part_b2 : A.W.part_b1)[(int64_t)blockIdx.x * 128 + (tid & 127)] = s;
+        if (tid == 0) {
+            float l = 0.0f, w = 0.0f;
+            for (int j = 0; j < 32; ++j) {
+                l += LW[j];
+                w += WT[j];
+            }
+            A.W.part_lw[2 * blockIdx.x] = l;
+            A.W.part_lw[2 * blockIdx.x + 1] = w;
+        }
+    }
+}
+
+struct QtAdamArgs {
+    QtWork W;
+    Mlp on, m, v;
+    QtDims d;
+    int64_t B, tiles;
+    const int64_t* act;
+    float lr, beta1, beta2, eps;
+    const int32_t* step_dev;  // Adam steps taken before this one
+    float* loss_out;
+};
+
+// torch.optim.Adam (foreach, capturable) for one element: m lerps to g, v = v b2 + (1 - b2) g g,
+// p += m / ((sqrt(v) / sqrt(1 - b2^t) + eps) / (-lr / (1 - b1^t)))
+struct AdamStep {
+    float b1, b2, eps, step_size, bc2_sqrt;
+    __device__ AdamStep(const QtAdamArgs& A) : b1(A.beta1), b2(A.beta2), eps(A.eps) {
+        const float t = (float)(*A.step_dev + 1);
+        step_size = 1.0f / ((powf(A.beta1, t) - 1.0f) / A.lr);
+        bc2_sqrt = sqrtf(-(powf(A.beta2, t) - 1.0f));
+    }
+    __device__ float operator()(float p, float g, float& m, float& v) const {
+        m = m + (1.0f - b1) * (g - m);
+        v = v * b2;
+        v = v + ((1.0f - b2) * g) * g;
+        const float denom = ((sqrtf(v) / bc2_sqrt) + eps) / step_size;
+        return p + m / denom;
+    }
+};
+
+// sum over the 256 threads of a workgroup in a fixed tree order (all threads get it)
+__device__ __forceinline__ float block_sum256(float x, float* red) {
+    const int t = threadIdx.x;
+    red[t] = x;
+    __syncthreads();
+#pragma unroll
+    for (int s = 128; s > 0; s >>= 1) {
+        if (t < s) red[t] += red[t + s];
+        __syncthreads();
+    }
+    const float r = red[0];
+    __syncthreads();
+    return r;
+}
+
+// sum over the tiles of 64 consecutive floats (src + t * stride + e0): thread (grp, q) adds
+// float4 q of tiles grp, grp + 16, ... (skipping tiles without `bit` in present[] when
+// present is given), then a fixed tree over the 16 groups. Threads 0..15 return float4 q.
+__device__ __forceinline__ float4 tile_sum64(const float* src, int64_t stride, int64_t e0, int64_t tiles,
+                                             const uint32_t* present, uint32_t bit, float4* red) {
+    const int t = threadIdx.x, q = t & 15, grp = t >> 4;
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll 4
+    for (int64_t k = grp; k < tiles; k += 16) {
+        if (present && !(present[k] & bit)) continue;
+        const float4 v = *reinterpret_cast<const float4*>(src + k * stride + e0 + 4 * q);
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+    }
+    red[t] = acc;
+    __syncthreads();
+#pragma unroll
+    for (int s = 8; s > 0; s >>= 1) {
+        if (grp < s) {
+            const float4 o = red[t + 16 * s];
+            red[t].x += o.x;
+            red[t].y += o.y;
+            red[t].z += o.z;
+            red[t].w += o.w;
+        }
+        __syncthreads();
+    }
+    const float4 r = red[q];
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ float comp(const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+
+// Workgroups: [0, 128) W1 row f (+ b1, the fold, the loss at f = 0); [128, 384) W2 64-element
+// blocks (+ b2 on a row's first block); then mt3 x 64 W3 blocks of the [rt][32][128] layout
+// (+ b3 of tile rt on its first block).
+__global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
+    __shared__ float red[kQRBlock];
+    __shared__ float4 red4[kQRBlock];
+    __shared__ float sums[8];
+    const int tid = threadIdx.x, in = A.d.in;
+    const AdamStep adam(A);
+    float wsum = 0.0f;
+    for (int64_t t = tid; t < A.tiles; t += kQRBlock) wsum += A.W.part_lw[2 * t + 1];
+    const float inv = 1.0f / fmaxf(block_sum256(wsum, red), 1.0f);
+    const int b = blockIdx.x;
+    if (b < 128) {  // W1 row f: 6 dynamic columns + db1 reduced over the tiles, the port columns
+        const int f = b;
+        float x[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int64_t t = tid; t < A.tiles; t += kQRBlock) {
+            const float* p = A.W.part_w1d + (t * 128 + f) * 6;
+#pragma unroll
+            for (int c = 0; c < 6; ++c) x[c] += p[c];
+            x[6] += A.W.part_b1[t * 128 + f];
+        }
+#pragma unroll
+        for (int c = 0; c < 7; ++c) {
+            const float v = block_sum256(x[c], red);
+            if (tid == 0) sums[c] = v;
+        }
+        __syncthreads();
+        const float s1 = sums[6];
+        float* w1row = A.on.w1 + (int64_t)f * in;
+        for (int c = tid; c < in; c += kQRBlock) {
+            const float g = (c < 6 ? sums[c] : s1 * A.W.portvec[c - 6]) * inv;
+            const int64_t i = (int64_t)f * in + c;
+            const float p = adam(w1row[c], g, A.m.w1[i], A.v.w1[i]);
+            w1row[c] = p;
+            if (c < 6) A.W.pw1[0][((f >> 5) * 3 + (c >> 1)) * 64 + (f & 31) + 32 * (c & 1)] = p;
+        }
+        if (tid == 0) sums[7] = adam(A.on.b1[f], s1 * inv, A.m.b1[f], A.v.b1[f]);
+        __syncthreads();  // the new row and b1 are complete before the fold reads them
+        const float b1 = sums[7];
+        if (tid == 0) A.on.b1[f] = b1;
+        if (tid < kQABlock) {
+            float xf = 0.0f;  // fold_row's order (the pack kernel's), on the first 128 threads
+            for (int c = 6 + tid; c < in; c += kQABlock) xf += w1row[c] * A.W.portvec[c - 6];
+            red[tid] = xf;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 64; s > 0; s >>= 1) {
+            if (tid < s) red[tid] += red[tid + s];
+            __syncthreads();
+        }
+        if (tid == 0) A.W.c1[0][f] = b1 + red[0];
+        __syncthreads();
+        if (f == 0) {  // the loss: sum w d^2 / sum w
+            float l = 0.0f;
+            for (int64_t t = tid; t < A.tiles; t += kQRBlock) l += A.W.part_lw[2 * t];
+            const float loss = block_sum256(l, red);
+            if (tid == 0) *A.loss_out = loss * inv;
+        }
+    } else if (b < 384) {  // W2 elements e0 .. e0 + 63 (row-major [f2][f1])
+        const int64_t e0 = (int64_t)(b - 128) * 64;
+        tile_sum64(A.W.part_w2, 128 * 128, e0, A.tiles, nullptr, 0, red4);
+        if (tid < 64) {
+            const int e = (int)e0 + tid, f2 = e >> 7, f1 = e & 127;
+            const float g = comp(red4[tid >> 2], tid & 3);
+            const float p = adam(A.on.w2[e], g * inv, A.m.w2[e], A.v.w2[e]);
+            A.on.w2[e] = p;
+            A.W.pw2[0][frag_index(f2, f1)] = p;
+            A.W.pw2t[frag_index(f1, f2)] = p;
+        }
+        if ((e0 & 127) == 0) {
+            const int f2 = (int)(e0 >> 7);
+            float x = 0.0f;
+            for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[t * 128 + f2];
+            const float s2 = block_sum256(x, red);
+            if (tid == 0) A.on.b2[f2] = adam(A.on.b2[f2], s2 * inv, A.m.b2[f2], A.v.b2[f2]);
+        }
+    } else {  // W3 block: tile rt, elements e0 .. e0 + 63 of its [32][128]
+        const int k = b - 384, rt = k >> 6;
+        const int64_t e0 = (int64_t)(k & 63) * 64;
+        const uint32_t bit = 1u << rt;
+        tile_sum64(A.W.part_w3 + (int64_t)rt * 32 * 128, (int64_t)A.d.mt3 * 32 * 128, e0, A.tiles, A.W.present,
+                   bit, red4);
+        if (tid < 64) {
+            const int e = (int)e0 + tid, a = rt * 32 + (e >> 7), f = e & 127;
+            if (a < A.d.A) {
+                const float g = comp(red4[tid >> 2], tid & 3);
+                const int64_t i = (int64_t)a * 128 + f;
+                A.on.w3[i] = adam(A.on.w3[i], g * inv, A.m.w3[i], A.v.w3[i]);
+            }
+        }
+        if (e0 == 0) {  // b3 of rows 32 rt .. 32 rt + 31: 32 rows x 8 tile groups
+            const int r = tid & 31, grp = tid >> 5;
+            float x = 0.0f;
+            for (int64_t t = grp; t < A.tiles; t += 8)
+                if (A.W.present[t] & bit) x += A.W.part_b3[(t * A.d.mt3 + rt) * 32 + r];
+            __syncthreads();
+            red[tid] = x;
+            __syncthreads();
+#pragma unroll
+            for (int s = 4; s > 0; s >>= 1) {
+                if (grp < s) red[tid] += red[tid + 32 * s];
+                __syncthreads();
+            }
+            const int a = rt * 32 + r;
+            if (tid < 32 && a < A.d.A) A.on.b3[a] = adam(A.on.b3[a], red[tid] * inv, A.m.b3[a], A.v.b3[a]);
+        }
+    }
+}
+
+}  // namespace
+
+struct se_qtrain {
+    se_env* env = nullptr;
+    int device = 0;
+    QtDims d{};
+    int64_t max_batch = 0, max_tiles = 0;
+    void* d_ws = nullptr;
+    QtWork W{};
+    Mlp on{}, tg{}, m{}, v{};
+    bool bound = false;
+    uint64_t world_version = 0;
+};
+
+namespace {
+
+Mlp mlp_of(const se_mlp* p) { return Mlp{p->w1, p->b1, p->w2, p->b2, p->w3, p->b3}; }
+
+bool mlp_ok(const se_mlp* p) { return p && p->w1 && p->b1 && p->w2 && p->b2 && p->w3 && p->b3; }
+
+int qtrain_pack(se_qtrain* q, int which, hipStream_t s) {
+    se_env* env = q->env;
+    QtPackArgs A{which ? q->tg : q->on, which, q->d, q->W, env->d_world, env->dims};
+    qtrain_pack_kernel<<<256, kQABlock, 0, s>>>(A);
+    HIP_TRY(hipGetLastError());
+    return SE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int se_qtrain_create(se_qtrain** out, se_env* env, int64_t max_batch) {
+    if (!out) return fail(SE_EINVAL, "null out");
+    *out = nullptr;
+    int rc = check_ready(env);
+    if (rc) return rc;
+    const int P = env->dims.P;
+    if (P < 1 || P > 64) return fail(SE_EINVAL, "the fused update supports 1..64 ports");
+    if (max_batch < 1 || max_batch > (int64_t(1) << 20)) return fail(SE_EINVAL, "max_batch must be in [1, 2^20]");
+    DeviceGuard g(env->device);
+    se_qtrain* q = new se_qtrain;
+    q->env = env;
+    q->device = env->device;
+    q->d = QtDims{P, 6 + 4 * P, 4 + P + 250, (4 + P + 250 + 31) / 32};
+    q->max_batch = max_batch;
+    q->max_tiles = (max_batch + kQT - 1) / kQT;
+    const size_t T = (size_t)q->max_tiles;
+    const size_t mt3 = (size_t)q->d.mt3;
+    const size_t sizes[] = {4 * 3 * 64, 4 * 3 * 64, 4 * 64 * 64, 4 * 64 * 64, 4 * 64 * 64,
+                            mt3 * 64 * 64, 128, 128, (size_t)(4 * P),
+                            T * 128 * 128, T * 128 * 6, T * 128, T * 128, T * 2, T * mt3 * 32 * 128,
+                            T * mt3 * 32, T};
+    size_t total = 0, off[17];
+    for (int i = 0; i < 17; ++i) {
+        off[i] = total;
+        total += (sizes[i] * 4 + 255) & ~(size_t)255;
+    }
+    if (hipMalloc(&q->d_ws, total) != hipSuccess) {
+        delete q;
+        return fail(SE_EHIP, "hipMalloc of the update workspace failed");
+    }
+    float* b = static_cast<float*>(q->d_ws);
+    auto at = [&](int i) { return b + off[i] / 4; };
+    q->W = QtWork{{at(0), at(1)}, {at(2), at(3)}, at(4), at(5), {at(6), at(7)}, at(8),
+                  at(9), at(10), at(11), at(12), at(13), at(14), at(15),
+                  reinterpret_cast<uint32_t*>(at(16))};
+    *out = q;
+    return SE_OK;
+}
+
+int se_qtrain_bind(se_qtrain* q, const se_mlp* online, const se_mlp* target, const se_mlp* adam_m,
+                   const se_mlp* adam_v, void* stream) {
+    if (!q) return fail(SE_EINVAL, "null qtrain");
+    if (!mlp_ok(online) || !mlp_ok(target) || !mlp_ok(adam_m) || !mlp_ok(adam_v))
+        return fail(SE_EINVAL, "null parameter pointer");
+    DeviceGuard g(q->device);
+    q->on = mlp_of(online);
+    q->tg = mlp_of(target);
+    q->m = mlp_of(adam_m);
+    q->v = mlp_of(adam_v);
+    int rc = qtrain_pack(q, 0, (hipStream_t)stream);
+    if (rc) return rc;
+    rc = qtrain_pack(q, 1, (hipStream_t)stream);
+    if (rc) return rc;
+    q->world_version = q->env->world_version;
+    q->bound = true;
+    return SE_OK;
+}
+
+int se_qtrain_pack(se_qtrain* q, int32_t which, void* stream) {
+    if (!q) return fail(SE_EINVAL, "null qtrain");
+    if (!q->bound) return fail(SE_ESTATE, "se_qtrain_bind has not been called");
+    if (which != 0 && which != 1) return fail(SE_EINVAL, "which must be 0 (online) or 1 (target)");
+    DeviceGuard g(q->device);
+    return qtrain_pack(q, which, (hipStream_t)stream);
+}
+
+int se_qtrain_step(se_qtrain* q, int64_t batch, const float* obs, const float* next_obs, const int64_t* act,
+                   const float* rew, const float* done, const float* weight, float gamma, float lr, float beta1,
+                   float beta2, float eps, const int32_t* step_dev, float* loss_out, void* stream) {
+    if (!q) return fail(SE_EINVAL, "null qtrain");
+    if (!q->bound) return fail(SE_ESTATE, "se_qtrain_bind has not been called");
+    if (q->world_version != q->env->world_version)
+        return fail(SE_ESTATE, "ports changed since se_qtrain_bind (the port block is folded into fc1)");
+    if (batch < 1 || batch > q->max_batch) return fail(SE_EINVAL, "batch must be in [1, max_batch]");
+    if (!obs || !next_obs || !act || !rew || !done || !weight || !step_dev || !loss_out)
+        return fail(SE_EINVAL, "null batch / counter / loss pointer");
+    DeviceGuard g(q->device);
+    const hipStream_t s = (hipStream_t)stream;
+    const int64_t tiles = (batch + kQT - 1) / kQT;
+    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 6 * 32) * 4;
+    static bool attr_set = false;
+    if (!attr_set) {
+        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(qtrain_tile_kernel),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr_set = true;
+    }
+    QtStepArgs A{q->W, q->on, q->tg, q->d, batch, obs, next_obs, act, rew, done, weight, gamma};
+    qtrain_tile_kernel<<<(unsigned)tiles, kQTBlock, lds, s>>>(A);
+    HIP_TRY(hipGetLastError());
+    QtAdamArgs B{q->W, q->on, q->m, q->v, q->d, batch, tiles, act, lr, beta1, beta2, eps, step_dev, loss_out};
+    qtrain_adam_kernel<<<384 + 64 * q->d.mt3, kQRBlock, 0, s>>>(B);
+    HIP_TRY(hipGetLastError());
+    return SE_OK;
+}
+
+int se_qtrain_destroy(se_qtrain* q) {
+    if (!q) return SE_OK;
+    if (q->d_ws) {
+        DeviceGuard g(q->device);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(q->d_ws);
+    }
+    delete q;
+    return SE_OK;
+}
+
+}  // extern "C"

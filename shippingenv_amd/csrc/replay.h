@@ -1,0 +1,324 @@
+// replay.h — the DQN experience replay ring on the device.
+//
+// Part of shipenv.hip's translation unit (included at its end, after qpolicy.h).
+// Reference: agents/dqn.py DQNAgent.remember (:117-123, a deque(maxlen=memory_size)
+// of (state, action, reward, next_state, done)) and the minibatch of update()
+// (:213-224: random.sample(memory, batch_size), np.vstack of the preprocess_state
+// rows, FloatTensor / LongTensor).
+//
+// A transition is kept in its compact form, 25 bytes, instead of two observation
+// rows (2 x 104 B at P = 5, 2 x 1048 B at P = 64):
+// * the ship's x, y, origin and dest bytes;
+// * f32 fuel (the row's f32 value: FloatTensor rounds the f64 fuel once);
+// * the agent-index action;
+// * the f32 reward (the reference's f64 reward rounded once, as FloatTensor does);
+// * a flags byte.
+// for s and s'. The port block of a row is constant, so the sampler rebuilds it
+// from the world image in LDS. The ring is SoA, written by one coalesced pass before
+// and one after each vector step (se_replay_begin / _end: 13 + 17 bytes per env).
+//
+// Sampling without replacement, like random.sample: batch position j takes
+// logical index perm(j) of a keyed 4-round Feistel permutation of [0, size)
+// (cycle-walking over the next even power of two), so the B indices are distinct
+// with no sort, no rejection table and no atomics, each thread on its own. A
+// transition whose step raised (err != 0: the reference's loop breaks before
+// remember, :281-309) is stored but flagged; its batch slot moves on to position
+// j + B, j + 2B, ... (still distinct), and a slot that finds none in kReplayTries
+// positions gets weight 0.
+
+namespace {
+
+constexpr uint8_t kRecDone = 1, kRecInvalid = 2;  // flags byte
+constexpr int kReplayTries = 4;
+constexpr int kSampleRows = 64;                   // transitions per sample workgroup
+constexpr int64_t kReplayKeyId = -1;              // Philox key (seed, 2^64 - 1): no env has this id
+
+struct Ring {
+    uint32_t* s_pos;  // x | y << 8 | origin << 16 | dest << 24 of s
+    float* s_fuel;
+    int32_t* act;
+    float* rew;
+    uint8_t* flags;
+    uint32_t* n_pos;  // s'
+    float* n_fuel;
+    int64_t* d_size;  // transitions stored (device copy, read by the sampler)
+};
+
+__device__ __forceinline__ uint32_t pack_pos(const se_state& st, int64_t i) {
+    return (uint32_t)st.x[i] | (uint32_t)st.y[i] << 8 | (uint32_t)st.origin[i] << 16 | (uint32_t)st.dest[i] << 24;
+}
+
+struct RecordArgs {
+    int64_t n, cap, head, new_size;
+    se_state st;
+    const int32_t* act;
+    Ring ring;
+    uint8_t* cut;
+    int32_t max_steps;
+};
+
+// s and a of every env, before se_step (remember's state, action)
+__global__ __launch_bounds__(kBlock) void replay_begin_kernel(RecordArgs A) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < A.n; i += (int64_t)gridDim.x * kBlock) {
+        int64_t slot = A.head + i;
+        slot -= slot >= A.cap ? A.cap : 0;
+        A.ring.s_pos[slot] = pack_pos(A.st, i);
+        A.ring.s_fuel[slot] = (float)A.st.fuel[i];
+        A.ring.act[slot] = A.act[i];
+    }
+}
+
+// reward, done and s' after se_step; cut[i]: the episode must restart now (the
+// step raised: the reference's loop breaks, :304-309; or it reached max_steps, :281)
+__global__ __launch_bounds__(kBlock) void replay_end_kernel(RecordArgs A) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *A.ring.d_size = A.new_size;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < A.n; i += (int64_t)gridDim.x * kBlock) {
+        int64_t slot = A.head + i;
+        slot -= slot >= A.cap ? A.cap : 0;
+        const bool raised = A.st.err[i] != SE_ERR_OK;
+        A.ring.rew[slot] = A.st.reward[i];
+        A.ring.flags[slot] = (uint8_t)((A.st.done[i] ? kRecDone : 0) | (raised ? kRecInvalid : 0));
+        A.ring.n_pos[slot] = pack_pos(A.st, i);
+        A.ring.n_fuel[slot] = (float)A.st.fuel[i];
+        if (A.cut) A.cut[i] = (uint8_t)(raised | (A.max_steps > 0 && A.st.ep_len[i] >= A.max_steps));
+    }
+}
+
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {  // lowbias32 finaliser
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+// Feistel half width for a domain of D elements: 2h >= ceil(log2 D), h >= 1
+__host__ __device__ __forceinline__ uint32_t feistel_half(uint32_t D) {
+    uint32_t bits = 2;
+    while (bits < 32 && (1ull << bits) < (uint64_t)D) bits += 2;
+    return bits / 2;
+}
+
+// A keyed permutation of [0, D), D <= 2^31: 4 Feistel rounds on 2h bits,
+// cycle-walked back into the domain (p < D terminates: p lies on its own cycle).
+__host__ __device__ __forceinline__ uint32_t feistel_perm(uint32_t p, uint32_t D, uint32_t h, const uint32_t* k) {
+    const uint32_t m = (1u << h) - 1u;
+    do {
+        uint32_t L = p >> h, R = p & m;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t f = mix32(R ^ k[r]) & m;
+            const uint32_t nl = R;
+            R = L ^ f;
+            L = nl;
+        }
+        p = (L << h) | R;
+    } while (p >= D);
+    return p;
+}
+
+struct SampleBatchArgs {
+    const uint32_t* world;
+    WorldDims dims;
+    Ring ring;
+    int64_t B;
+    int32_t width;
+    uint64_t seed;
+    const uint32_t* t_dev;  // update counter in device memory (graph replay) or null
+    uint32_t t;
+    float* obs;
+    float* next_obs;
+    int64_t* act;
+    float* rew;
+    float* done;
+    float* weight;
+};
+
+// one preprocess_state column of a stored ship (utils/preprocessing.py:25-62;
+// column 3 is fuel again: _build_state's cargo = fuel, environment.py:206)
+__device__ __forceinline__ float ship_col(uint32_t pos, float fuel, int c) {
+    const uint32_t b = c < 2 ? (pos >> (8 * c)) & 0xffu : (pos >> (8 * (c - 2))) & 0xffu;
+    const float v = b == SE_NONE ? -1.0f : (float)b;
+    return c == 2 || c == 3 ? fuel : v;
+}
+
+__device__ __forceinline__ float port_col(const LdsWorld& w, int c) {
+    const int p = (c - 6) >> 2, f = (c - 6) & 3;
+    return f == 0 ? (float)w.px(p) : f == 1 ? (float)w.py(p) : f == 2 ? (float)w.pfuel[p] : (float)w.pcargo[p];
+}
+
+// kSampleRows transitions per workgroup: the first wave picks the slots, then all
+// threads write the two [rows][width] f32 blocks with coalesced row-major stores.
+__global__ __launch_bounds__(kBlock) void replay_sample_kernel(SampleBatchArgs A) {
+    extern __shared__ uint32_t lds[];
+    __shared__ int64_t slot_of[kSampleRows];
+    const LdsWorld w = stage_world(A.world, A.dims, lds);
+    const int64_t r0 = (int64_t)blockIdx.x * kSampleRows;
+    if (threadIdx.x < kSampleRows) {
+        const int64_t size = *A.ring.d_size;
+        const uint32_t t = A.t_dev ? *A.t_dev : A.t;
+        const U4 key = draw(env_key(A.seed, kReplayKeyId), t, kSlotReplay);
+        const uint32_t h = feistel_half((uint32_t)size);
+        const int64_t j = r0 + threadIdx.x;
+        int64_t slot = -1;
+        if (j < A.B) {
+            for (int k = 0; k < kReplayTries; ++k) {
+                const int64_t pos = j + (int64_t)k * A.B;
+                if (pos >= size) break;
+                const uint32_t l = feistel_perm((uint32_t)pos, (uint32_t)size, h, key.v);
+                if (!(A.ring.flags[l] & kRecInvalid)) {
+                    slot = l;
+                    break;
+                }
+            }
+            const bool ok = slot >= 0;
+            A.act[j] = ok ? (int64_t)A.ring.act[slot] : 0;
+            A.rew[j] = ok ? A.ring.rew[slot] : 0.0f;
+            A.done[j] = ok && (A.ring.flags[slot] & kRecDone) ? 1.0f : 0.0f;
+            A.weight[j] = ok ? 1.0f : 0.0f;
+        }
+        slot_of[threadIdx.x] = slot;
+    }
+    __syncthreads();
+    const int64_t rows = min((int64_t)kSampleRows, A.B - r0);
+    const int width = A.width;
+    for (int e = threadIdx.x; e < rows * width; e += kBlock) {
+        const int r = e / width, c = e - r * width;
+        const int64_t slot = slot_of[r];
+        float a = 0.0f, b = 0.0f;
+        if (slot >= 0) {
+            if (c < 6) {
+                a = ship_col(A.ring.s_pos[slot], A.ring.s_fuel[slot], c);
+                b = ship_col(A.ring.n_pos[slot], A.ring.n_fuel[slot], c);
+            } else {
+                a = b = port_col(w, c);
+            }
+        }
+        A.obs[(r0 + r) * width + c] = a;
+        A.next_obs[(r0 + r) * width + c] = b;
+    }
+}
+
+}  // namespace
+
+struct se_replay {
+    se_env* env = nullptr;
+    int device = 0;
+    int64_t cap = 0, head = 0, size = 0;
+    bool open = false;  // se_replay_begin called, se_replay_end pending
+    void* d_block = nullptr;
+    Ring ring{};
+};
+
+extern "C" {
+
+int se_replay_create(se_replay** out, se_env* env, int64_t capacity) {
+    if (!out) return fail(SE_EINVAL, "null out");
+    *out = nullptr;
+    int rc = check_ready(env);
+    if (rc) return rc;
+    if (capacity < env->n || capacity < 1 || capacity >= (int64_t(1) << 31))
+        return fail(SE_EINVAL, "replay capacity must be in [max(n, 1), 2^31)");
+    DeviceGuard g(env->device);
+    const size_t C = (size_t)capacity;
+    auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t o_sfuel = up(4 * C), o_act = o_sfuel + up(4 * C), o_rew = o_act + up(4 * C),
+                 o_flags = o_rew + up(4 * C), o_npos = o_flags + up(C), o_nfuel = o_npos + up(4 * C),
+                 o_size = o_nfuel + up(4 * C), total = o_size + 256;
+    se_replay* r = new se_replay;
+    r->env = env;
+    r->device = env->device;
+    r->cap = capacity;
+    if (hipMalloc(&r->d_block, total) != hipSuccess) {
+        delete r;
+        return fail(SE_EHIP, "hipMalloc of the replay ring failed");
+    }
+    char* b = static_cast<char*>(r->d_block);
+    r->ring = Ring{reinterpret_cast<uint32_t*>(b), reinterpret_cast<float*>(b + o_sfuel),
+                   reinterpret_cast<int32_t*>(b + o_act), reinterpret_cast<float*>(b + o_rew),
+                   reinterpret_cast<uint8_t*>(b + o_flags), reinterpret_cast<uint32_t*>(b + o_npos),
+                   reinterpret_cast<float*>(b + o_nfuel), reinterpret_cast<int64_t*>(b + o_size)};
+    if (hipMemset(r->d_block, 0, total) != hipSuccess) {
+        (void)hipFree(r->d_block);
+        delete r;
+        return fail(SE_EHIP, "hipMemset of the replay ring failed");
+    }
+    *out = r;
+    return SE_OK;
+}
+
+int se_replay_begin(se_replay* r, const int32_t* actions, void* stream) {
+    if (!r) return fail(SE_EINVAL, "null replay");
+    int rc = check_ready(r->env);
+    if (rc) return rc;
+    if (!actions) return fail(SE_EINVAL, "null actions");
+    if (r->open) return fail(SE_ESTATE, "se_replay_begin twice without se_replay_end");
+    se_env* env = r->env;
+    DeviceGuard g(env->device);
+    RecordArgs A{env->n, r->cap, r->head, 0, env->st, actions, r->ring, nullptr, 0};
+    if (env->n > 0) {
+        replay_begin_kernel<<<grid_for(env->n), kBlock, 0, (hipStream_t)stream>>>(A);
+        HIP_TRY(hipGetLastError());
+    }
+    r->open = true;
+    return SE_OK;
+}
+
+int se_replay_end(se_replay* r, uint8_t* cut, int32_t max_steps, void* stream) {
+    if (!r) return fail(SE_EINVAL, "null replay");
+    int rc = check_ready(r->env);
+    if (rc) return rc;
+    if (!r->open) return fail(SE_ESTATE, "se_replay_end without se_replay_begin");
+    se_env* env = r->env;
+    if (max_steps > 0 && (!cut || !env->st.ep_len))
+        return fail(SE_EINVAL, "max_steps needs a cut buffer and an auto-reset env (ep_len)");
+    DeviceGuard g(env->device);
+    const int64_t new_size = std::min(r->size + env->n, r->cap);
+    RecordArgs A{env->n, r->cap, r->head, new_size, env->st, nullptr, r->ring, cut, max_steps};
+    replay_end_kernel<<<grid_for(std::max<int64_t>(env->n, 1)), kBlock, 0, (hipStream_t)stream>>>(A);
+    HIP_TRY(hipGetLastError());
+    r->head = (r->head + env->n) % r->cap;
+    r->size = new_size;
+    r->open = false;
+    return SE_OK;
+}
+
+int se_replay_size(se_replay* r, int64_t* size, int64_t* capacity) {
+    if (!r) return fail(SE_EINVAL, "null replay");
+    if (size) *size = r->size;
+    if (capacity) *capacity = r->cap;
+    return SE_OK;
+}
+
+int se_replay_sample(se_replay* r, int64_t batch, const uint32_t* t_dev, uint32_t t, float* obs,
+                     float* next_obs, int64_t* actions, float* rewards, float* dones, float* weights,
+                     void* stream) {
+    if (!r) return fail(SE_EINVAL, "null replay");
+    int rc = check_ready(r->env);
+    if (rc) return rc;
+    if (batch < 1 || batch > (int64_t(1) << 24)) return fail(SE_EINVAL, "batch must be in [1, 2^24]");
+    if (!obs || !next_obs || !actions || !rewards || !dones || !weights)
+        return fail(SE_EINVAL, "null batch buffer");
+    se_env* env = r->env;
+    DeviceGuard g(env->device);
+    SampleBatchArgs A{env->d_world, env->dims, r->ring, batch, 6 + 4 * env->dims.P, env->seed, t_dev, t,
+                      obs, next_obs, actions, rewards, dones, weights};
+    const int grid = (int)((batch + kSampleRows - 1) / kSampleRows);
+    replay_sample_kernel<<<grid, kBlock, lds_bytes(env), (hipStream_t)stream>>>(A);
+    HIP_TRY(hipGetLastError());
+    return SE_OK;
+}
+
+int se_replay_destroy(se_replay* r) {
+    if (!r) return SE_OK;
+    if (r->d_block) {  // does not touch the env, which may be gone already
+        DeviceGuard g(r->device);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(r->d_block);
+    }
+    delete r;
+    return SE_OK;
+}
+
+}  // extern "C"

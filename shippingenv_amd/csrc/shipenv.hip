@@ -1715,3 +1715,5 @@ int se_destroy(se_env* env) {
 
 // the fused DQN policy step (same translation unit: world image, env handle, Philox)
 #include "qpolicy.h"
+#include "replay.h"
+#include "qtrain.h"

@@ -1,0 +1,320 @@
+"""Vectorised DQN training on the device (agents/dqn.py DQNAgent).
+
+One ``VecDQNAgent.step()`` is one iteration of the reference's training loop
+(agents/dqn.py:276-300) for every env of an auto-reset VecEnv at once:
+
+* choose_action (:177-203): ``se_policy``, the fused MFMA policy step (policy.py).
+* env.step, then remember (:117-123): ``se_replay_begin`` / ``se_step`` /
+  ``se_replay_end``, which append to the device replay ring (include/shipenv.h).
+* the loop's episode breaks: a step that raised (:304-309) or ``max_steps``
+  (:281). ``se_replay_end`` marks these envs and ``se_reset`` restarts them.
+* update() (:206-245): ``se_replay_sample`` draws the minibatch. ``se_qtrain_step``
+  (FusedUpdate, csrc/qtrain.h) computes the MSE to r + gamma * max target Q * (1 - done),
+  the backward pass and Adam in two f32 MFMA kernels. Then comes the epsilon decay.
+  ``fused=False`` runs the same update with torch autograd and torch.optim.Adam.
+
+After ``graph_warmup`` eager updates, the update is captured in one HIP graph. The
+graph holds the sampler, the update kernels, the repacking of the policy's bf16
+weights and the update counter's increment, so each later update is one graph launch.
+
+Differences from the single-env reference, by construction:
+* The batch holds distinct transitions, like random.sample; see se_replay_sample.
+* A raised step is stored flagged and never sampled.
+* The target network is synchronised every ``target_update_every`` updates instead
+  of every ``target_update_freq`` episodes. With N envs, episodes end N at a time.
+* ``len(memory)`` counts ring slots.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _native as N
+from .policy import HIDDEN, DQNNetwork, QPolicy
+
+# utils/constants.py TrainingDefaults (DQN_*): the reference's defaults
+DQN_BATCH_SIZE = 32
+DQN_MEMORY_SIZE = 2000
+DQN_GAMMA = 0.95
+DQN_EPSILON = 1.0
+DQN_EPSILON_MIN = 0.01
+DQN_EPSILON_DECAY = 0.995
+DQN_LEARNING_RATE = 0.001
+MAX_STEPS_PER_EPISODE = 1000
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+class MiniBatch:
+    """The static minibatch tensors se_replay_sample writes (graph-replay safe)."""
+
+    def __init__(self, batch, width, device):
+        f32 = dict(dtype=torch.float32, device=device)
+        self.obs = torch.zeros((batch, width), **f32)
+        self.next_obs = torch.zeros((batch, width), **f32)
+        self.act = torch.zeros(batch, dtype=torch.int64, device=device)
+        self.rew = torch.zeros(batch, **f32)
+        self.done = torch.zeros(batch, **f32)
+        self.weight = torch.zeros(batch, **f32)
+        self.batch = batch
+
+
+class ReplayBuffer:
+    """DQNAgent.memory (agents/dqn.py:86) on the device: a ring of `capacity` compact
+    transitions of one VecEnv (se_replay_*)."""
+
+    def __init__(self, env, capacity: int):
+        self.env = env
+        self._h = C.c_void_p()
+        N.check(N.lib().se_replay_create(C.byref(self._h), env._h, int(capacity)))
+
+    def __len__(self):
+        return self.size
+
+    @property
+    def size(self) -> int:
+        s = C.c_int64()
+        N.check(N.lib().se_replay_size(self._h, C.byref(s), None))
+        return s.value
+
+    @property
+    def capacity(self) -> int:
+        c = C.c_int64()
+        N.check(N.lib().se_replay_size(self._h, None, C.byref(c)))
+        return c.value
+
+    def begin(self, actions: torch.Tensor):
+        """remember's state and action, before env.step(actions)."""
+        self._act = actions  # kept alive until the launch has run
+        N.check(N.lib().se_replay_begin(self._h, _ptr(actions), self.env._stream()))
+
+    def end(self, cut: torch.Tensor | None = None, max_steps: int = 0):
+        """reward, done and next_state, after env.step; cut[i] = 1 where the episode must restart."""
+        N.check(N.lib().se_replay_end(self._h, _ptr(cut), int(max_steps), self.env._stream()))
+
+    def sample(self, out: MiniBatch, t: int = 0, t_dev: torch.Tensor | None = None) -> MiniBatch:
+        """update()'s minibatch (agents/dqn.py:213-224) into `out`; the sampler key is t, or
+        the device counter t_dev (uint32 viewed as int32) when given."""
+        N.check(N.lib().se_replay_sample(self._h, out.batch, _ptr(t_dev), int(t) & 0xFFFFFFFF,
+                                         _ptr(out.obs), _ptr(out.next_obs), _ptr(out.act),
+                                         _ptr(out.rew), _ptr(out.done), _ptr(out.weight),
+                                         self.env._stream()))
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            torch.cuda.synchronize(self.env.device)
+            N.lib().se_replay_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
+class SeMlp(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("w1", "b1", "w2", "b2", "w3", "b3")]
+
+
+def _linear_params(model):
+    ps = [model.fc1.weight, model.fc1.bias, model.fc2.weight, model.fc2.bias, model.fc3.weight, model.fc3.bias]
+    for p in ps:
+        if p.dtype != torch.float32 or not p.is_contiguous() or not p.is_cuda:
+            raise ValueError("the fused update needs contiguous f32 device parameters")
+    return ps
+
+
+def _mlp(tensors):
+    return SeMlp(*[t.data_ptr() for t in tensors])
+
+
+class FusedUpdate:
+    """update()'s loss, backward and Adam step (agents/dqn.py:226-242) fused on f32 MFMA
+    (se_qtrain_*: two kernels per update). The parameters stay the torch modules' tensors,
+    updated in place. Adam's exp_avg / exp_avg_sq live here."""
+
+    def __init__(self, env, model, target_model, max_batch: int, lr: float,
+                 betas=(0.9, 0.999), eps: float = 1e-8):
+        if model.fc1.out_features != HIDDEN or model.fc2.out_features != HIDDEN:
+            raise ValueError(f"the fused update is built for hidden_size {HIDDEN}")
+        self.env, self.lr, self.betas, self.eps = env, float(lr), tuple(map(float, betas)), float(eps)
+        self.params = _linear_params(model)
+        self.target = _linear_params(target_model)
+        self.exp_avg = [torch.zeros_like(p) for p in self.params]
+        self.exp_avg_sq = [torch.zeros_like(p) for p in self.params]
+        self._structs = [_mlp(t) for t in (self.params, self.target, self.exp_avg, self.exp_avg_sq)]
+        self._h = C.c_void_p()
+        N.check(N.lib().se_qtrain_create(C.byref(self._h), env._h, int(max_batch)))
+        N.check(N.lib().se_qtrain_bind(self._h, *[C.byref(x) for x in self._structs], env._stream()))
+
+    def pack(self, which: int):
+        """Rebuild the kernel's image of the online (0) or target (1) network."""
+        N.check(N.lib().se_qtrain_pack(self._h, int(which), self.env._stream()))
+
+    def step(self, b: MiniBatch, gamma: float, step_dev: torch.Tensor, loss_out: torch.Tensor):
+        N.check(N.lib().se_qtrain_step(self._h, b.batch, _ptr(b.obs), _ptr(b.next_obs), _ptr(b.act),
+                                       _ptr(b.rew), _ptr(b.done), _ptr(b.weight), float(gamma),
+                                       self.lr, self.betas[0], self.betas[1], self.eps,
+                                       _ptr(step_dev), _ptr(loss_out), self.env._stream()))
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            torch.cuda.synchronize(self.env.device)
+            N.lib().se_qtrain_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
+def dqn_loss(model, target_model, b: MiniBatch, gamma: float) -> torch.Tensor:
+    """update()'s loss (agents/dqn.py:226-234) over the minibatch; weight-0 rows (no
+    valid transition found) are left out of the mean, which is nn.MSELoss when all
+    weights are 1."""
+    q = model(b.obs).gather(1, b.act.unsqueeze(1)).squeeze(1)
+    with torch.no_grad():
+        next_q = target_model(b.next_obs).max(1)[0]
+        target_q = b.rew + gamma * next_q * (1 - b.done)
+    d = q - target_q
+    return (b.weight * d * d).sum() / b.weight.sum().clamp_min(1.0)
+
+
+class VecDQNAgent:
+    """DQNAgent (agents/dqn.py:36-245) over every env of an auto-reset VecEnv."""
+
+    def __init__(self, env, learning_rate: float = DQN_LEARNING_RATE, gamma: float = DQN_GAMMA,
+                 epsilon: float = DQN_EPSILON, epsilon_min: float = DQN_EPSILON_MIN,
+                 epsilon_decay: float = DQN_EPSILON_DECAY, memory_size: int | None = None,
+                 batch_size: int = DQN_BATCH_SIZE, target_update_every: int = 1000,
+                 hidden_size: int = HIDDEN, max_steps: int = MAX_STEPS_PER_EPISODE,
+                 updates_per_step: int = 1, graph: bool = True, graph_warmup: int = 3,
+                 fused: bool = True, model: DQNNetwork | None = None):
+        if not env.auto_reset:
+            raise ValueError("VecDQNAgent needs an auto-reset VecEnv (finished episodes restart in se_step)")
+        self.env = env
+        self.state_size, self.action_size = env.obs_size, env.action_space_size
+        self.gamma, self.epsilon = float(gamma), float(epsilon)
+        self.epsilon_min, self.epsilon_decay = float(epsilon_min), float(epsilon_decay)
+        self.learning_rate, self.batch_size = float(learning_rate), int(batch_size)
+        self.target_update_every, self.max_steps = int(target_update_every), int(max_steps)
+        self.updates_per_step = int(updates_per_step)
+        dev = env.device
+        self.model = (model if model is not None else
+                      DQNNetwork(self.state_size, self.action_size, hidden_size)).to(dev)
+        self.target_model = DQNNetwork(self.state_size, self.action_size, hidden_size).to(dev)
+        self.fused = bool(fused)
+        self.trainer = None
+        self.update_target_model()
+        if self.fused:  # se_qtrain: the update on f32 MFMA, Adam state on the device
+            self.trainer = FusedUpdate(env, self.model, self.target_model, self.batch_size,
+                                       self.learning_rate)
+            self.optimizer = None
+        else:  # torch autograd + Adam (capturable: eager and graph replays run the same kernels)
+            self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.learning_rate,
+                                              capturable=True)
+        cap = memory_size if memory_size is not None else max(DQN_MEMORY_SIZE, 4 * env.n)
+        self.memory = ReplayBuffer(env, cap)
+        self.policy = QPolicy(env, self.model)
+        self.batch = MiniBatch(self.batch_size, self.state_size, dev)
+        self.cut = torch.zeros(env.n, dtype=torch.uint8, device=dev)
+        self.t = 0         # vector steps taken (policy exploration counter)
+        self.updates = 0   # update() calls that trained
+        self._ctr = torch.zeros(1, dtype=torch.int32, device=dev)  # sampler key, = updates
+        self.use_graph, self.graph_warmup = bool(graph), int(graph_warmup)
+        self._graph = None
+        self._loss = torch.zeros((), dtype=torch.float32, device=dev)
+
+    def update_target_model(self):
+        """agents/dqn.py:109-111 (an in-place copy: the graph keeps the same tensors)."""
+        with torch.no_grad():
+            for d, s in zip(self.target_model.parameters(), self.model.parameters()):
+                d.copy_(s)
+        if self.trainer is not None:
+            self.trainer.pack(1)
+
+    # ------------------------------------------------------------------ update
+    def _update_body(self):
+        self.memory.sample(self.batch, t_dev=self._ctr)
+        if self.fused:  # _ctr = Adam steps taken so far
+            self.trainer.step(self.batch, self.gamma, self._ctr, self._loss)
+        else:
+            loss = dqn_loss(self.model, self.target_model, self.batch, self.gamma)
+            self.optimizer.zero_grad(set_to_none=False)
+            loss.backward()
+            self.optimizer.step()
+            self._loss.copy_(loss.detach())
+        self._ctr.add_(1)
+        self.policy.set_weights()  # the next choose_action sees the new weights
+
+    def _capture(self):
+        for p in self.model.parameters():  # static gradient buffers for the graph (torch path)
+            if p.grad is None and not self.fused:
+                p.grad = torch.zeros_like(p)
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(self.env.device)
+        side.wait_stream(torch.cuda.current_stream(self.env.device))
+        with torch.cuda.stream(side), torch.cuda.graph(g, stream=side):
+            self._update_body()
+        torch.cuda.current_stream(self.env.device).wait_stream(side)
+        self._graph = g
+
+    def update(self):
+        """agents/dqn.py:206-245. Returns the loss as a device scalar (no host sync), or
+        None while the memory holds fewer than batch_size transitions."""
+        if self.memory.size < self.batch_size:
+            return None
+        if self.use_graph and self._graph is None and self.updates >= self.graph_warmup:
+            self._capture()  # capturing records the update; it runs on replay below
+        if self._graph is not None:
+            self._graph.replay()
+        else:
+            self._update_body()
+        self.updates += 1
+        if self.epsilon > self.epsilon_min:
+            self.epsilon *= self.epsilon_decay
+        if self.target_update_every > 0 and self.updates % self.target_update_every == 0:
+            self.update_target_model()
+        return self._loss
+
+    # ------------------------------------------------------------------ acting
+    def choose_actions(self, deterministic: bool = False) -> torch.Tensor:
+        """choose_action (agents/dqn.py:177-203) for every env."""
+        return self.policy.act(0.0 if deterministic else self.epsilon, self.t)
+
+    def step(self):
+        """One training-loop iteration for every env; returns the last update's loss (or None)."""
+        env = self.env
+        a = self.choose_actions()
+        self.memory.begin(a)
+        env.step(a)
+        self.memory.end(self.cut, self.max_steps)
+        env.reset(self.cut)  # episodes that raised or reached max_steps start over
+        loss = None
+        for _ in range(self.updates_per_step):
+            loss = self.update()
+        self.t += 1
+        return loss
+
+    def train(self, steps: int):
+        """`steps` vector steps; returns the final loss as a float (one sync), or None."""
+        loss = None
+        for _ in range(int(steps)):
+            loss = self.step()
+        return None if loss is None else float(loss)
+
+    def close(self):
+        for obj in (getattr(self, "policy", None), getattr(self, "memory", None),
+                    getattr(self, "trainer", None)):
+            if obj is not None:
+                obj.close()
+
+
+__all__ = ["DQNNetwork", "FusedUpdate", "MiniBatch", "ReplayBuffer", "VecDQNAgent", "dqn_loss"]

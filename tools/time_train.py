@@ -1,0 +1,70 @@
+"""Time the parts of one vectorised DQN training iteration (shippingenv_amd.dqn) on one GPU.
+
+    python tools/time_train.py [--n N] [--batch B] [--iters K] [--eager]
+
+Prints one JSON line: HIP-event ms per iteration of each part on the launch stream
+(policy, replay begin, step, replay end, reset of cut envs, update) and the whole loop.
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--n", type=int, default=1 << 20)
+    p.add_argument("--batch", type=int, default=8192)
+    p.add_argument("--iters", type=int, default=30)
+    p.add_argument("--eager", action="store_true", help="no graph capture of the update")
+    a = p.parse_args()
+    from shippingenv_amd.dqn import VecDQNAgent
+    from shippingenv_amd.vec import VecEnv
+
+    env = VecEnv(a.n, seed=2026, auto_reset=True, device="cuda:0")
+    env.reset()
+    torch.manual_seed(2026)
+    agent = VecDQNAgent(env, batch_size=a.batch, memory_size=4 * a.n, graph=not a.eager)
+    for _ in range(6):
+        agent.step()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    parts = ("policy", "begin", "step", "end", "reset", "update")
+    ev = {k: [] for k in parts}
+
+    def mark(name, fn):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        r = fn()
+        e1.record(s)
+        ev[name].append((e0, e1))
+        return r
+
+    g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    g0.record(s)
+    for _ in range(a.iters):
+        act = mark("policy", agent.choose_actions)
+        mark("begin", lambda: agent.memory.begin(act))
+        mark("step", lambda: env.step(act))
+        mark("end", lambda: agent.memory.end(agent.cut, agent.max_steps))
+        mark("reset", lambda: env.reset(agent.cut))
+        mark("update", agent.update)
+        agent.t += 1
+    g1.record(s)
+    torch.cuda.synchronize()
+    out = {"n": a.n, "batch": a.batch, "graph": not a.eager,
+           "loop_ms": round(g0.elapsed_time(g1) / a.iters, 4)}
+    for k in parts:
+        out[k + "_ms"] = round(sum(x.elapsed_time(y) for x, y in ev[k]) / a.iters, 4)
+    agent.close()
+    env.close()
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
