@@ -9,8 +9,8 @@
 // Here it is two kernels, all in f32 (v_mfma_f32_32x32x2_f32 is an exact f32 fma chain,
 // and gfx950 has no xf32), deterministic (fixed summation orders, no atomics):
 //
-// T1, qtrain_tile_kernel (one workgroup per 32 samples, 4 waves, one 32-row feature tile
-// per wave):
+// T1, qtrain_tile_kernel (one workgroup per 32 samples, 8 waves: the online and the
+// target net's four 32-row feature tiles side by side):
 // * Target net forward: fc1, fc2, then fc3 over all A rows, with a per-sample max.
 // * Online net forward: fc1, fc2.
 // * q_j = W3[a_j] . h2_j + b3[a_j]. Only the chosen action's Q gets a gradient, so fc3
@@ -45,7 +45,7 @@ namespace {
 
 constexpr int kQT = 32;       // samples per T1 workgroup
 constexpr int kLS = 33;       // LDS row stride (floats) of a [feature][sample] tile
-constexpr int kQTBlock = 256; // T1: 4 waves
+constexpr int kQTBlock = 512; // T1: 8 waves
 constexpr int kQABlock = 128; // fold / pack workgroups
 constexpr int kQRBlock = 256; // T2 workgroups
 
@@ -80,16 +80,23 @@ __device__ __forceinline__ f32x16 mfma_f32(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
-// acc += A (packed fragments of one row tile) x B (an LDS [k][kLS] tile), kSteps k-pairs.
-// All A fragments are loaded before the first MFMA: one L2 round trip per layer.
+// The A operands of one row tile (packed fragments, kSteps k-pairs) in registers; loaded
+// ahead of the MFMAs that use them, so the L2 round trip hides under the previous layer.
 template <int kSteps>
-__device__ __forceinline__ f32x16 gemm_lds(const float* __restrict__ pa, const float* src, f32x16 acc, int lane) {
+struct Frags {
+    float v[kSteps];
+    __device__ __forceinline__ void load(const float* __restrict__ pa, int lane) {
+#pragma unroll
+        for (int s = 0; s < kSteps; ++s) v[s] = pa[s * 64 + lane];
+    }
+};
+
+// acc += A (fragments in registers) x B (an LDS [k][kLS] tile)
+template <int kSteps>
+__device__ __forceinline__ f32x16 gemm_lds(const Frags<kSteps>& a, const float* src, f32x16 acc, int lane) {
     const int h = lane >> 5, c = lane & 31;
-    float a[kSteps];
 #pragma unroll
-    for (int s = 0; s < kSteps; ++s) a[s] = pa[s * 64 + lane];
-#pragma unroll
-    for (int s = 0; s < kSteps; ++s) acc = mfma_f32(a[s], src[(2 * s + h) * kLS + c], acc);
+    for (int s = 0; s < kSteps; ++s) acc = mfma_f32(a.v[s], src[(2 * s + h) * kLS + c], acc);
     return acc;
 }
 
@@ -201,21 +208,26 @@ struct QtStepArgs {
     float gamma;
 };
 
+// 8 waves: 0-3 the online net's feature tiles, 4-7 the target net's, concurrently; fc3
+// of the target net and the dW3 tiles over all 8; then dH1 (waves 0-3) beside dW2 (4-7).
 __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     extern __shared__ float sm[];
     float* X = sm;                  // [8][kLS] obs, dynamic columns (rows 6, 7 zero)
     float* XN = X + 8 * kLS;        // next obs
-    float* HA = XN + 8 * kLS;       // [128][kLS] h1 (target, then online)
-    float* HB = HA + 128 * kLS;     // h2
-    float* DZ2 = HB + 128 * kLS;
-    float* DZ1 = DZ2 + 128 * kLS;
-    float* QM = DZ1 + 128 * kLS;    // [4][32] per-wave max of the target Q
-    float* Y = QM + 4 * 32;         // [32] targets
+    float* HA = XN + 8 * kLS;       // [128][kLS] online h1
+    float* HB = HA + 128 * kLS;     // online h2
+    float* TA = HB + 128 * kLS;     // target h1, then dZ2
+    float* TB = TA + 128 * kLS;     // target h2, then dZ1
+    float* DZ2 = TA;
+    float* DZ1 = TB;
+    float* QM = TB + 128 * kLS;     // [8][32] per-wave max of the target Q
+    float* Y = QM + 8 * 32;         // [32] targets
     float* G = Y + 32;              // [32] g_j
     float* LW = G + 32;             // [32] w_j d_j^2
     float* WT = LW + 32;            // [32] w_j
     int* ACT = reinterpret_cast<int*>(WT + 32);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wt = wave & 3;
+    const bool tgt = wave >= 4;
     const int64_t r0 = (int64_t)blockIdx.x * kQT;
     const int in = A.d.in;
 
@@ -234,24 +246,52 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     }
     __syncthreads();
 
-    // target network on next_states: fc1, fc2, fc3 and the max over actions
+    // this thread's slice of W3[a_j] (q_j and dZ2 below): sample j = tid >> 4, features
+    // 8 (tid & 15) .. + 7
+    const int qj = tid >> 4, qpart = tid & 15;
+    float w3s[8];
     {
-        f32x16 acc = bias_init(A.W.c1[1], wave, lane, 128);
-        acc = gemm_lds<3>(A.W.pw1[1] + wave * 3 * 64, XN, acc, lane);
-        store_relu(HA, wave, acc, lane);
+        const float* w3r = A.on.w3 + (int64_t)ACT[qj] * 128 + qpart * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w3s[k] = w3r[k];
+    }
+
+    // fc1, fc2 of both networks: online on states, target on next_states
+    const int net = tgt ? 1 : 0;
+    Frags<64> fa, fb;  // fc2, then fc3 / W2^T: each loaded one layer ahead
+    {
+        Frags<3> f1;
+        f1.load(A.W.pw1[net] + wt * 3 * 64, lane);
+        fa.load(A.W.pw2[net] + wt * 64 * 64, lane);
+        f32x16 acc = bias_init(A.W.c1[net], wt, lane, 128);
+        acc = gemm_lds(f1, tgt ? XN : X, acc, lane);
+        store_relu(tgt ? TA : HA, wt, acc, lane);
     }
     __syncthreads();
+    if (wave < A.d.mt3) fb.load(A.W.pw3t + wave * 64 * 64, lane);
     {
-        f32x16 acc = bias_init(A.tg.b2, wave, lane, 128);
-        acc = gemm_lds<64>(A.W.pw2[1] + wave * 64 * 64, HA, acc, lane);
-        store_relu(HB, wave, acc, lane);
+        f32x16 acc = bias_init(tgt ? A.tg.b2 : A.on.b2, wt, lane, 128);
+        acc = gemm_lds(fa, tgt ? TA : HA, acc, lane);
+        store_relu(tgt ? TB : HB, wt, acc, lane);
     }
     __syncthreads();
+    // target fc3 over all A rows and the max over actions: tiles wave, wave + 8
     {
+        const bool second = wave + 8 < A.d.mt3;
+        if (second) fa.load(A.W.pw3t + (wave + 8) * 64 * 64, lane);
         float m = -INFINITY;
-        for (int t = wave; t < A.d.mt3; t += 4) {
+        if (wave < A.d.mt3) {
+            f32x16 acc = bias_init(A.tg.b3, wave, lane, A.d.A);
+            acc = gemm_lds(fb, TB, acc, lane);
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (wave * 32 + acc_r(r, lane) < A.d.A) m = fmaxf(m, acc[r]);
+        }
+        if (!tgt) fb.load(A.W.pw2t + wt * 64 * 64, lane);  // dH1's operands
+        if (second) {
+            const int t = wave + 8;
             f32x16 acc = bias_init(A.tg.b3, t, lane, A.d.A);
-            acc = gemm_lds<64>(A.W.pw3t + t * 64 * 64, HB, acc, lane);
+            acc = gemm_lds(fa, TB, acc, lane);
 #pragma unroll
             for (int r = 0; r < 16; ++r)
                 if (t * 32 + acc_r(r, lane) < A.d.A) m = fmaxf(m, acc[r]);
@@ -262,96 +302,81 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     __syncthreads();
     if (tid < 32) {
         const int64_t row = r0 + tid;
-        const float mx = fmaxf(fmaxf(QM[tid], QM[32 + tid]), fmaxf(QM[64 + tid], QM[96 + tid]));
+        float mx = QM[tid];
+        for (int w = 1; w < 8; ++w) mx = fmaxf(mx, QM[w * 32 + tid]);
         Y[tid] = row < A.B ? A.rew[row] + (A.gamma * mx) * (1.0f - A.done[row]) : 0.0f;
     }
-
-    // online network on states: fc1, fc2 (h1 -> HA, h2 -> HB; the target's are consumed)
-    {
-        f32x16 acc = bias_init(A.W.c1[0], wave, lane, 128);
-        acc = gemm_lds<3>(A.W.pw1[0] + wave * 3 * 64, X, acc, lane);
-        store_relu(HA, wave, acc, lane);
-    }
-    __syncthreads();
-    {
-        f32x16 acc = bias_init(A.on.b2, wave, lane, 128);
-        acc = gemm_lds<64>(A.W.pw2[0] + wave * 64 * 64, HA, acc, lane);
-        store_relu(HB, wave, acc, lane);
-    }
     __syncthreads();
 
-    // q_j = W3[a_j] . h2_j + b3[a_j]; g_j = 2 w_j (q_j - y_j)
+    // q_j = W3[a_j] . h2_j + b3[a_j]; g_j = 2 w_j (q_j - y_j): 16 threads per sample
     {
-        const int j = tid >> 3, part = tid & 7, a = ACT[j];
-        const float* w3r = A.on.w3 + (int64_t)a * 128 + part * 16;
         float s = 0.0f;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) s += w3r[k] * HB[(part * 16 + k) * kLS + j];
+        for (int k = 0; k < 8; ++k) s += w3s[k] * HB[(qpart * 8 + k) * kLS + qj];
         s += __shfl_xor(s, 1);
         s += __shfl_xor(s, 2);
         s += __shfl_xor(s, 4);
-        if (part == 0) {
-            const float d = (s + A.on.b3[a]) - Y[j];
-            G[j] = 2.0f * WT[j] * d;
-            LW[j] = WT[j] * d * d;
+        s += __shfl_xor(s, 8);
+        if (qpart == 0) {
+            const float d = (s + A.on.b3[ACT[qj]]) - Y[qj];
+            G[qj] = 2.0f * WT[qj] * d;
+            LW[qj] = WT[qj] * d * d;
+        }
+    }
+    __syncthreads();
+    // dZ2 = (h2 > 0) g_j W3[a_j] (into the target's dead h1 buffer)
+    {
+        const float g = G[qj];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int f = qpart * 8 + k;
+            DZ2[f * kLS + qj] = HB[f * kLS + qj] > 0.0f ? g * w3s[k] : 0.0f;
         }
     }
     __syncthreads();
 
-    // dZ2 = (h2 > 0) g_j W3[a_j]
-    {
-        const int j = tid & 31, f0 = (tid >> 5) * 16, a = ACT[j];
-        const float g = G[j];
-        const float* w3r = A.on.w3 + (int64_t)a * 128 + f0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) DZ2[(f0 + k) * kLS + j] = HB[(f0 + k) * kLS + j] > 0.0f ? g * w3r[k] : 0.0f;
-    }
-    __syncthreads();
-
-    // dH1 = W2^T dZ2 -> dZ1 = (h1 > 0) dH1
-    {
+    const int h = lane >> 5, c = lane & 31;
+    if (!tgt) {  // dH1 = W2^T dZ2 -> dZ1 = (h1 > 0) dH1
         f32x16 acc = {};
-        acc = gemm_lds<64>(A.W.pw2t + wave * 64 * 64, DZ2, acc, lane);
+        acc = gemm_lds(fb, DZ2, acc, lane);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int f = wave * 32 + acc_r(r, lane), c = lane & 31;
+            const int f = wt * 32 + acc_r(r, lane);
             DZ1[f * kLS + c] = HA[f * kLS + c] > 0.0f ? acc[r] : 0.0f;
         }
-    }
-    __syncthreads();
-
-    // partial dW2[f2][f1] = sum_j dZ2[f2][j] h1[f1][j]: row tile = wave, 4 column tiles
-    {
+    } else {  // partial dW2[f2][f1] = sum_j dZ2[f2][j] h1[f1][j]: row tile wt, 4 column tiles
         float* out = A.W.part_w2 + (int64_t)blockIdx.x * 128 * 128;
-        const int h = lane >> 5, c = lane & 31;
         for (int ct = 0; ct < 4; ++ct) {
             f32x16 acc = {};
 #pragma unroll
             for (int s = 0; s < 16; ++s)
-                acc = mfma_f32(DZ2[(wave * 32 + c) * kLS + 2 * s + h], HA[(ct * 32 + c) * kLS + 2 * s + h], acc);
+                acc = mfma_f32(DZ2[(wt * 32 + c) * kLS + 2 * s + h], HA[(ct * 32 + c) * kLS + 2 * s + h], acc);
 #pragma unroll
-            for (int r = 0; r < 16; ++r) out[(wave * 32 + acc_r(r, lane)) * 128 + ct * 32 + c] = acc[r];
+            for (int r = 0; r < 16; ++r) out[(wt * 32 + acc_r(r, lane)) * 128 + ct * 32 + c] = acc[r];
         }
     }
-    // partial dW3[a][f] = sum_j (a_j == a) g_j h2[f][j] for the action tiles present:
-    // row tile rt, column tile = wave; db3 likewise
+    // partial dW3[a][f] = sum_j (a_j == a) g_j h2[f][j] over the action tiles present:
+    // (row tile, column tile) pairs round-robin over the 8 waves; db3 alike
+    uint32_t present = 0;
+    for (int j = 0; j < 32; ++j)
+        if (r0 + j < A.B) present |= 1u << (ACT[j] >> 5);
     {
-        uint32_t present = 0;
-        for (int j = 0; j < 32; ++j)
-            if (r0 + j < A.B) present |= 1u << (ACT[j] >> 5);
-        const int h = lane >> 5, c = lane & 31;
+        int k = 0;
         for (int rt = 0; rt < A.d.mt3; ++rt) {
             if (!((present >> rt) & 1u)) continue;  // block-uniform
-            const int a = rt * 32 + c;
-            f32x16 acc = {};
+            for (int ct = 0; ct < 4; ++ct, ++k) {
+                if ((k & 7) != wave) continue;  // wave-uniform
+                const int a = rt * 32 + c;
+                f32x16 acc = {};
 #pragma unroll
-            for (int s = 0; s < 16; ++s) {
-                const int j = 2 * s + h;
-                acc = mfma_f32(ACT[j] == a ? G[j] : 0.0f, HB[(wave * 32 + c) * kLS + j], acc);
+                for (int s = 0; s < 16; ++s) {
+                    const int j = 2 * s + h;
+                    acc = mfma_f32(ACT[j] == a ? G[j] : 0.0f, HB[(ct * 32 + c) * kLS + j], acc);
+                }
+                float* out = A.W.part_w3 + (((int64_t)blockIdx.x * A.d.mt3 + rt) * 32) * 128;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) out[acc_r(r, lane) * 128 + ct * 32 + c] = acc[r];
             }
-            float* out = A.W.part_w3 + (((int64_t)blockIdx.x * A.d.mt3 + rt) * 32) * 128;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) out[acc_r(r, lane) * 128 + wave * 32 + c] = acc[r];
             if (tid < 32) {
                 float s3 = 0.0f;
                 for (int j = 0; j < 32; ++j) s3 += ACT[j] == rt * 32 + tid ? G[j] : 0.0f;
@@ -360,20 +385,23 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         }
         if (tid == 0) A.W.present[blockIdx.x] = present;
     }
+    __syncthreads();  // dZ1 complete
     // partial dW1 (dynamic columns), db1, db2, loss and weight sums
-    {
+    if (tid < 256) {
         const int f = tid >> 1, c0 = (tid & 1) * 3;
         float* o = A.W.part_w1d + ((int64_t)blockIdx.x * 128 + f) * 6 + c0;
-        for (int c = c0; c < c0 + 3; ++c) {
+        for (int cc = c0; cc < c0 + 3; ++cc) {
             float s = 0.0f;
-            for (int j = 0; j < 32; ++j) s += DZ1[f * kLS + j] * X[c * kLS + j];
-            o[c - c0] = s;
+            for (int j = 0; j < 32; ++j) s += DZ1[f * kLS + j] * X[cc * kLS + j];
+            o[cc - c0] = s;
         }
-        const float* src = tid < 128 ? DZ2 + tid * kLS : DZ1 + (tid - 128) * kLS;
+    } else {
+        const int t = tid - 256;
+        const float* src = t < 128 ? DZ2 + t * kLS : DZ1 + (t - 128) * kLS;
         float s = 0.0f;
         for (int j = 0; j < 32; ++j) s += src[j];
-        (tid < 128 ? A.W.part_b2 : A.W.part_b1)[(int64_t)blockIdx.x * 128 + (tid & 127)] = s;
-        if (tid == 0) {
+        (t < 128 ? A.W.part_b2 : A.W.part_b1)[(int64_t)blockIdx.x * 128 + (t & 127)] = s;
+        if (t == 0) {
             float l = 0.0f, w = 0.0f;
             for (int j = 0; j < 32; ++j) {
                 l += LW[j];
@@ -436,14 +464,25 @@ __device__ __forceinline__ float4 tile_sum64(const float* src, int64_t stride, i
                                              const uint32_t* present, uint32_t bit, float4* red) {
     const int t = threadIdx.x, q = t & 15, grp = t >> 4;
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#pragma unroll 4
-    for (int64_t k = grp; k < tiles; k += 16) {
-        if (present && !(present[k] & bit)) continue;
-        const float4 v = *reinterpret_cast<const float4*>(src + k * stride + e0 + 4 * q);
-        acc.x += v.x;
-        acc.y += v.y;
-        acc.z += v.z;
-        acc.w += v.w;
+    for (int64_t k0 = grp; k0 < tiles; k0 += 16 * 8) {  // 8 tiles per round, loads independent
+        uint32_t pm[8];
+        float4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int64_t k = k0 + 16 * i;
+            pm[i] = k < tiles ? (present ? present[k] & bit : 1u) : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            v[i] = pm[i] ? *reinterpret_cast<const float4*>(src + (k0 + 16 * i) * stride + e0 + 4 * q)
+                         : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            acc.x += v[i].x;
+            acc.y += v[i].y;
+            acc.z += v[i].z;
+            acc.w += v[i].w;
+        }
     }
     red[t] = acc;
     __syncthreads();
@@ -687,7 +726,7 @@ int se_qtrain_step(se_qtrain* q, int64_t batch, const float* obs, const float* n
     DeviceGuard g(q->device);
     const hipStream_t s = (hipStream_t)stream;
     const int64_t tiles = (batch + kQT - 1) / kQT;
-    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 6 * 32) * 4;
+    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 5 * 32) * 4;
     static bool attr_set = false;
     if (!attr_set) {
         HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(qtrain_tile_kernel),
