@@ -197,6 +197,7 @@ def run_rollouts(n, args, dist):
     }
 
 
+F32_MFMA_PEAK_TFLOPS = 157.3  # v_mfma_f32_32x32x2_f32, MI355X_MICROARCH.md
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, no sparsity)
 
 
@@ -309,6 +310,12 @@ def run_dqn_train(n, args, dist):
     e1.record(stream)
     torch.cuda.synchronize()
     upd_ms = e0.elapsed_time(e1) / args.train_steps
+    # algorithmic f32 FLOPs of one fused update per sample (csrc/qtrain.h): online fc1 (6
+    # dynamic inputs; the constant port block is folded), fc2, the gathered q; target fc1,
+    # fc2, fc3 over all A rows; backward dH2 and dW3 (row gathers), dW2, dH1 and dW1 (6 cols)
+    H, Aa = 128, env.action_space_size
+    flop = 2 * (6 * H + H * H + H) + 2 * (6 * H + H * H + H * Aa) + 2 * (2 * H + 2 * H * H + 6 * H)
+    upd_tf = flop * args.train_batch / (upd_ms * 1e-3) / 1e12
     out = {
         "workload": "8f row 3: vectorised DQN training, N envs/GPU (auto-reset, default ports): "
                     "fused policy + se_step + device replay ring + one graph-captured update "
@@ -319,6 +326,10 @@ def run_dqn_train(n, args, dist):
         "stream_ms_per_step": round(kern_ms, 4),
         "update_ms": round(upd_ms, 4),
         "updates_per_s": round(1e3 / upd_ms, 1),
+        "update_roofline": {"bound": "mfma (f32)", "achieved": round(upd_tf, 2), "peak": F32_MFMA_PEAK_TFLOPS,
+                            "unit": "TFLOP/s", "frac": round(upd_tf / F32_MFMA_PEAK_TFLOPS, 4),
+                            "flop_per_sample": flop,
+                            "note": "whole update (sample + 2 kernels + policy repack + counter), graph replay"},
         "batch": args.train_batch,
         "replay_capacity": agent.memory.capacity,
         "final_loss": float(loss),

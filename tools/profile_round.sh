@@ -24,6 +24,7 @@ run kt_c4 240 --kernel-trace --stats --output-format csv -d "$OUT" -o kt_c4 -- $
 run kt_big 240 --kernel-trace --stats --output-format csv -d "$OUT" -o kt_big -- $PY --config 3 --n 16777216 --steps 40 &&
 run kt_roll 240 --kernel-trace --stats --output-format csv -d "$OUT" -o kt_roll -- python3 $R/tools/time_rollout.py --launches 10 &&
 run kt_pol 240 --kernel-trace --stats --output-format csv -d "$OUT" -o kt_pol -- python3 $R/tools/time_policy.py --launches 20 &&
+run kt_train 240 --kernel-trace --stats --output-format csv -d "$OUT" -o kt_train -- python3 $R/tools/time_train.py --iters 20 &&
 run pmc_fetch_c4 240 --pmc FETCH_SIZE --output-format csv -d "$OUT" -o pmc_fetch_c4 -- $PY --config 4 --steps 20 &&
 run pmc_write_c4 240 --pmc WRITE_SIZE --output-format csv -d "$OUT" -o pmc_write_c4 -- $PY --config 4 --steps 20 &&
 run pmc_fetch_c3 240 --pmc FETCH_SIZE --output-format csv -d "$OUT" -o pmc_fetch_c3 -- $PY --config 3 --steps 20 &&

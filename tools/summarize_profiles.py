@@ -43,7 +43,7 @@ def main():
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     summary = {"tag": tag, "kernels": {}, "pmc": {}}
-    for name in ("kt_c3", "kt_c4", "kt_big", "kt_roll", "kt_pol"):
+    for name in ("kt_c3", "kt_c4", "kt_big", "kt_roll", "kt_pol", "kt_train"):
         f = os.path.join(src, f"{name}_kernel_stats.csv")
         if os.path.exists(f):
             shutil.copy(f, os.path.join(dst, f"{name}_kernel_stats.csv"))
