@@ -69,6 +69,8 @@ constexpr double kMaxCargo = 50.0;
 //                   [0, 8) a move, index out_of_fuel*4 + ground*2 + closer, summed in
 //                   the reference's order (:288-315); [8] a take (0.05); [9] else 0
 // For the 100x100 map with 5 ports that is 4.5 KB.
+constexpr int kStageRows = 6;  // 256-dword rows of the world image the step kernel stages unguarded
+
 struct WorldDims {
     int32_t H, W, P, words;
     __host__ __device__ int pos() const { return 3 * words; }
@@ -77,6 +79,12 @@ struct WorldDims {
     __host__ __device__ int gate() const { return frac() + 2 * 50; }
     __host__ __device__ int rtab() const { return (gate() + 50 + 1) & ~1; }
     __host__ __device__ int total() const { return rtab() + 2 * 10; }
+    // device image / LDS size: whole 256-dword rows, at least the step kernel's
+    // unguarded staging window (kStageRows rows)
+    __host__ __device__ int padded() const {
+        const int t = (total() + 255) & ~255;
+        return t > 256 * kStageRows ? t : 256 * kStageRows;
+    }
 };
 
 struct LdsWorld {
@@ -115,11 +123,61 @@ struct LdsWorld {
     __device__ double likelihood(int cargo) const { return frac[cargo]; }
 };
 
+// Staging in two halves. stage_issue puts every thread's share of the image in
+// flight at once (independent loads into registers); stage_finish writes it to LDS
+// and holds the barrier. A load -> wait -> ds_write loop would make each of the ~5
+// rounds a full L2 round trip behind whatever the wave loaded before it (its
+// s_waitcnt vmcnt(0) also waits for those). The step kernel issues its first
+// group's loads between the halves, so the image (first in the in-order vmcnt
+// queue) is written while the group's data is still on its way.
+struct Staged {
+    uint32_t r[kStageRows];
+};
+
+// The step kernel's half (256 threads): the image is padded to whole rows of at
+// least kStageRows (WorldDims::padded), so these loads need no guard and no branch.
+__device__ __forceinline__ Staged stage_issue(const uint32_t* __restrict__ g) {
+    Staged st;
+#pragma unroll
+    for (int k = 0; k < kStageRows; ++k) st.r[k] = g[threadIdx.x + 256 * k];
+    return st;
+}
+
+__device__ __forceinline__ LdsWorld world_view(WorldDims d, const uint32_t* lds);
+
+__device__ __forceinline__ LdsWorld stage_finish(const uint32_t* __restrict__ g, WorldDims d,
+                                                 uint32_t* lds, const Staged& st) {
+#pragma unroll
+    for (int k = 0; k < kStageRows; ++k) lds[threadIdx.x + 256 * k] = st.r[k];
+    for (int i = (int)threadIdx.x + 256 * kStageRows; i < d.total(); i += 256)
+        lds[i] = g[i];  // larger maps / port tables: the remainder
+    __syncthreads();
+    return world_view(d, lds);
+}
+
+// Any block size (the other kernels): every thread's loads issued before any store.
 __device__ __forceinline__ LdsWorld stage_world(const uint32_t* __restrict__ g, WorldDims d,
                                                 uint32_t* lds) {
     const int total = d.total();
-    for (int i = threadIdx.x; i < total; i += blockDim.x) lds[i] = g[i];
+    constexpr int kR = 4;
+    for (int i0 = 0; i0 < total; i0 += kR * (int)blockDim.x) {
+        uint32_t r[kR];
+#pragma unroll
+        for (int k = 0; k < kR; ++k) {
+            const int i = i0 + (int)threadIdx.x + k * (int)blockDim.x;
+            r[k] = i < d.padded() ? g[i] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kR; ++k) {
+            const int i = i0 + (int)threadIdx.x + k * (int)blockDim.x;
+            if (i < d.padded()) lds[i] = r[k];
+        }
+    }
     __syncthreads();
+    return world_view(d, lds);
+}
+
+__device__ __forceinline__ LdsWorld world_view(WorldDims d, const uint32_t* lds) {
     LdsWorld w;
     w.ground = lds;
     w.portbit = lds + d.words;
@@ -136,6 +194,7 @@ __device__ __forceinline__ LdsWorld stage_world(const uint32_t* __restrict__ g, 
     w.P = d.P;
     return w;
 }
+
 
 // ------------------------------------------------------------------ one env
 struct Ship {
@@ -365,15 +424,16 @@ __device__ __forceinline__ T* slab_of(T* p, int64_t g0) {
 }
 
 template <typename T>
-__device__ __forceinline__ void ld4_full(const T* __restrict__ p, int64_t g0, T (&v)[4]) {
+__device__ __forceinline__ void ld4_full(const T* __restrict__ p, int64_t g0, T (&v)[4],
+                                         uint32_t lane = threadIdx.x) {
     if constexpr (sizeof(T) == 4) {
-        const uint4 w = reinterpret_cast<const uint4*>(slab_of(p, g0))[threadIdx.x];
+        const uint4 w = reinterpret_cast<const uint4*>(slab_of(p, g0))[lane];
         v[0] = __builtin_bit_cast(T, w.x);
         v[1] = __builtin_bit_cast(T, w.y);
         v[2] = __builtin_bit_cast(T, w.z);
         v[3] = __builtin_bit_cast(T, w.w);
     } else {
-        const double2* q = reinterpret_cast<const double2*>(slab_of(p, g0)) + 2 * threadIdx.x;
+        const double2* q = reinterpret_cast<const double2*>(slab_of(p, g0)) + 2 * lane;
         const double2 a = q[0], b = q[1];
         v[0] = a.x;
         v[1] = a.y;
@@ -409,8 +469,9 @@ __device__ __forceinline__ void st4_tail(T* __restrict__ p, int64_t base, int64_
         if (base + j < n) p[base + j] = v[j];
 }
 
-__device__ __forceinline__ uint32_t ld4u8_full(const uint8_t* __restrict__ p, int64_t g0) {
-    return reinterpret_cast<const uint32_t*>(slab_of(p, g0))[threadIdx.x];
+__device__ __forceinline__ uint32_t ld4u8_full(const uint8_t* __restrict__ p, int64_t g0,
+                                               uint32_t lane = threadIdx.x) {
+    return reinterpret_cast<const uint32_t*>(slab_of(p, g0))[lane];
 }
 __device__ __forceinline__ void st4u8_full(uint8_t* __restrict__ p, int64_t g0, uint32_t w) {
     reinterpret_cast<uint32_t*>(slab_of(p, g0))[threadIdx.x] = w;
@@ -446,20 +507,22 @@ struct Group {
     float e[4];               // ep_return
     int32_t l[4];             // ep_len
 
+    // lane: the group within the block's row (threadIdx.x; the kernel's first load
+    // clamps it into range instead of branching around the load)
     template <bool kFull>
-    __device__ __forceinline__ void load(const StepArgs& A, At<kFull> at) {
+    __device__ __forceinline__ void load(const StepArgs& A, At<kFull> at, uint32_t lane = threadIdx.x) {
         const se_state& S = A.st;
         if constexpr (kFull) {
-            x = ld4u8_full(S.x, at.g0);
-            y = ld4u8_full(S.y, at.g0);
-            org = ld4u8_full(S.origin, at.g0);
-            dst = ld4u8_full(S.dest, at.g0);
-            ld4_full(S.cargo, at.g0, c);
-            ld4_full(S.fuel, at.g0, f);
-            ld4_full(A.act, at.g0, a);
+            x = ld4u8_full(S.x, at.g0, lane);
+            y = ld4u8_full(S.y, at.g0, lane);
+            org = ld4u8_full(S.origin, at.g0, lane);
+            dst = ld4u8_full(S.dest, at.g0, lane);
+            ld4_full(S.cargo, at.g0, c, lane);
+            ld4_full(S.fuel, at.g0, f, lane);
+            ld4_full(A.act, at.g0, a, lane);
             if (kTyped) {
-                ld4_full(A.act_a, at.g0, p);
-                ld4_full(A.act_b, at.g0, q);
+                ld4_full(A.act_a, at.g0, p, lane);
+                ld4_full(A.act_b, at.g0, q, lane);
             }
         } else {
             x = ld4u8_tail(S.x, at.base, at.n);
@@ -798,24 +861,41 @@ __device__ __forceinline__ void block_compact(const StepArgs& A, const Finished&
 // the staging hides under them; each iteration loads the next group before storing
 // the current one. The trip count is uniform over the block (the auto-reset
 // compaction holds barriers).
-template <bool kTyped, bool kReplay, bool kAuto>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void step_kernel(StepArgs A) {
+template <bool kTyped, bool kReplay, bool kAuto, bool kPipe = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPipe ? 2 : 4))) void step_kernel(StepArgs A) {
     extern __shared__ uint32_t lds[];
     __shared__ double red[kBlock / 64][3];
     __shared__ int32_t wtot[kBlock / 64];
     const int64_t full = A.n >> 2;
     const int64_t first = (int64_t)blockIdx.x * A.iters * kBlock;  // block-uniform first group
 
+    const Staged st = stage_issue(A.world);
+    // first group: an unconditional load (lanes past the end re-read the last full
+    // group; the host launches this kernel only when there is one), so the staging
+    // writes below wait for exactly the image's loads
     Group<kTyped, kAuto> G;
-    if (first + threadIdx.x < full) G.template load<true>(A, At<true>{first, 0, A.n});
-    const LdsWorld w = stage_world(A.world, A.dims, lds);
+    {
+        const int64_t last = full - 1 - first;  // block-uniform
+        const uint32_t lane = last < (int64_t)threadIdx.x ? (uint32_t)(last < 0 ? 0 : last) : threadIdx.x;
+        G.template load<true>(A, At<true>{last < 0 ? full - 1 : first, 0, A.n}, lane);
+    }
+    const LdsWorld w = stage_finish(A.world, A.dims, lds, st);
 
     BlockStats bs;
     int32_t running = 0;  // this block's done records so far (block-uniform)
     for (int64_t k = 0; k < A.iters; ++k) {
         const int64_t g0 = first + k * kBlock, g = g0 + threadIdx.x;
         Finished F;
-        if (g < full) {
+        // the next group's loads go out before this group's compute, so its data
+        // streams in while the VALU works (a load issued after the stores would
+        // wait out the whole memory latency again)
+        if constexpr (kPipe) {
+            Group<kTyped, kAuto> Gn;
+            const bool more = k + 1 < A.iters && g + kBlock < full;
+            if (more) Gn.template load<true>(A, At<true>{g0 + kBlock, 0, A.n});
+            if (g < full) step_group<kTyped, kReplay, kAuto, true>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F);
+            if (more) G = Gn;
+        } else if (g < full) {
             step_group<kTyped, kReplay, kAuto, true>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F);
             if (k + 1 < A.iters && g + kBlock < full) G.template load<true>(A, At<true>{g0 + kBlock, 0, A.n});
         }
@@ -875,7 +955,7 @@ __global__ __launch_bounds__(64) void step_tail_kernel(StepArgs A) {
     step_group<kTyped, kReplay, kAuto, false>(A, w, G, at, bs, F);
     if constexpr (kAuto) {
         const int64_t b = g / (A.iters * kBlock);
-        int32_t c = A.done_count[b];
+        int32_t c = g == 0 ? 0 : A.done_count[b];  // g == 0: step_kernel did not run
         for (int j = 0; j < 4; ++j)
             if ((F.mask >> j) & 1u)
                 A.done_recs[b * A.seg + c++] = se_done_rec{(int32_t)(at.base + j), F.ret[j], F.len[j], (int32_t)A.t};
@@ -1286,7 +1366,13 @@ int step_block_cap() {
     return c > 0 ? c : kStepBlocks;
 }
 
-size_t lds_bytes(const se_env* env) { return (size_t)env->dims.total() * 4; }
+// software-pipelined step kernel (next group's loads before this group's compute)
+bool step_pipe() {
+    const char* v = getenv("SHIPENV_STEP_PIPE");
+    return v ? atoi(v) != 0 : true;
+}
+
+size_t lds_bytes(const se_env* env) { return (size_t)env->dims.padded() * 4; }
 
 int upload_world(se_env* env, int32_t P, const int32_t* px, const int32_t* py, const int32_t* pf,
                  const int32_t* pc) {
@@ -1348,13 +1434,14 @@ int upload_world(se_env* env, int32_t P, const int32_t* px, const int32_t* py, c
     rtab[8] = 0.05;  // TAKE_FUEL / TAKE_CARGO (:349, :357)
     rtab[9] = 0.0;
     memcpy(&img[d.rtab()], rtab, sizeof rtab);
-    if (d.total() > env->world_cap) {
+    img.resize((size_t)d.padded(), 0u);
+    if (d.padded() > env->world_cap) {
         if (env->d_world) HIP_TRY(hipFree(env->d_world));
         env->d_world = nullptr;
-        HIP_TRY(hipMalloc(&env->d_world, (size_t)d.total() * 4));
-        env->world_cap = d.total();
+        HIP_TRY(hipMalloc(&env->d_world, (size_t)d.padded() * 4));
+        env->world_cap = d.padded();
     }
-    HIP_TRY(hipMemcpy(env->d_world, img.data(), (size_t)d.total() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(env->d_world, img.data(), (size_t)d.padded() * 4, hipMemcpyHostToDevice));
     env->dims = d;
     env->world_version += 1;
     return SE_OK;
@@ -1404,8 +1491,11 @@ int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const 
     const hipStream_t s = (hipStream_t)stream;
     const size_t lds = lds_bytes(env);
     const int grid = env->grid;
-    if (env->n > 0) {
-        if (!typed && !autoreset) step_kernel<false, false, false><<<grid, kBlock, lds, s>>>(A);
+    const bool pipe = env->iters > 1 && step_pipe();
+    if (env->n >= kEnvsPerThread) {  // at least one full group (step_kernel's first load assumes it)
+        if (!typed && !autoreset && pipe) step_kernel<false, false, false, true><<<grid, kBlock, lds, s>>>(A);
+        else if (!typed && autoreset && pipe) step_kernel<false, false, true, true><<<grid, kBlock, lds, s>>>(A);
+        else if (!typed && !autoreset) step_kernel<false, false, false><<<grid, kBlock, lds, s>>>(A);
         else if (!typed && autoreset) step_kernel<false, false, true><<<grid, kBlock, lds, s>>>(A);
         else if (typed && replay) step_kernel<true, true, false><<<grid, kBlock, lds, s>>>(A);
         else if (typed && !autoreset) step_kernel<true, false, false><<<grid, kBlock, lds, s>>>(A);
