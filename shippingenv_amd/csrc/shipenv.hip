@@ -32,6 +32,14 @@
 #include "../../include/shipenv.h"
 #include "philox.h"
 
+#ifndef SHIPENV_TRACE
+#define SHIPENV_TRACE 0  // 1 = diagnostic build: per-wave phase timestamps (tools/wave_trace.py)
+#endif
+
+#ifndef SHIPENV_NORARE
+#define SHIPENV_NORARE 0  // 1 = timing-only ablation: no Philox for the loss / beta / arrival draws
+#endif
+
 #ifndef SHIPENV_ABLATE
 #define SHIPENV_ABLATE 0  // 0 = the product; 1 = timing-only memory-traffic build (tools/ablate.sh)
 #endif
@@ -394,6 +402,22 @@ __device__ __forceinline__ uint32_t count_below(uint64_t mask) {
 }
 
 // ------------------------------------------------------------------ step kernel
+#if SHIPENV_TRACE
+// [wave][8] s_memrealtime stamps (100 MHz): start, staged, stepped, end
+constexpr int kTraceWaves = 1 << 16;
+__device__ uint64_t g_trace[kTraceWaves * 8];
+#define TRACE_STAMP(k)                                                                        \
+    do {                                                                                      \
+        const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                                 \
+        const uint32_t w_ = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);                  \
+        if ((threadIdx.x & 63) == 0 && w_ < kTraceWaves) g_trace[w_ * 8 + (k)] = t_;          \
+    } while (0)
+#else
+#define TRACE_STAMP(k) \
+    do {               \
+    } while (0)
+#endif
+
 struct StepArgs {
     const uint32_t* world;
     WorldDims dims;
@@ -423,18 +447,50 @@ __device__ __forceinline__ T* slab_of(T* p, int64_t g0) {
     return p + g0 * 4;
 }
 
-template <typename T>
+// Streaming accesses: state is touched once per step, so stores carry the
+// nontemporal hint (written lines do not linger dirty in L2 until the end-of-kernel
+// writeback). Loads take it only when the step's working set is cache-resident
+// (kNt, chosen per launch by step_nt_loads): measured faster at N = 2^20, slower
+// at 2^24. SHIPENV_NT (bit 0 loads, bit 1 stores) masks them for experiments.
+#ifndef SHIPENV_NT
+#define SHIPENV_NT 3
+#endif
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <bool kNt = false, typename V>
+__device__ __forceinline__ V ld_stream(const V* p) {
+    if constexpr (kNt && (SHIPENV_NT & 1) != 0) {
+        if constexpr (sizeof(V) == 16)
+            return __builtin_bit_cast(V, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p)));
+        else
+            return __builtin_nontemporal_load(p);
+    } else {
+        return *p;
+    }
+}
+template <typename V>
+__device__ __forceinline__ void st_stream(V* p, V v) {
+    if constexpr ((SHIPENV_NT & 2) != 0) {
+        if constexpr (sizeof(V) == 16)
+            __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), reinterpret_cast<u32x4*>(p));
+        else
+            __builtin_nontemporal_store(v, p);
+    } else {
+        *p = v;
+    }
+}
+
+template <bool kNt = false, typename T>
 __device__ __forceinline__ void ld4_full(const T* __restrict__ p, int64_t g0, T (&v)[4],
                                          uint32_t lane = threadIdx.x) {
     if constexpr (sizeof(T) == 4) {
-        const uint4 w = reinterpret_cast<const uint4*>(slab_of(p, g0))[lane];
+        const uint4 w = ld_stream<kNt>(reinterpret_cast<const uint4*>(slab_of(p, g0)) + lane);
         v[0] = __builtin_bit_cast(T, w.x);
         v[1] = __builtin_bit_cast(T, w.y);
         v[2] = __builtin_bit_cast(T, w.z);
         v[3] = __builtin_bit_cast(T, w.w);
     } else {
         const double2* q = reinterpret_cast<const double2*>(slab_of(p, g0)) + 2 * lane;
-        const double2 a = q[0], b = q[1];
+        const double2 a = ld_stream<kNt>(q), b = ld_stream<kNt>(q + 1);
         v[0] = a.x;
         v[1] = a.y;
         v[2] = b.x;
@@ -450,11 +506,11 @@ __device__ __forceinline__ void st4_full(T* __restrict__ p, int64_t g0, const T 
         w.y = __builtin_bit_cast(uint32_t, v[1]);
         w.z = __builtin_bit_cast(uint32_t, v[2]);
         w.w = __builtin_bit_cast(uint32_t, v[3]);
-        reinterpret_cast<uint4*>(slab_of(p, g0))[threadIdx.x] = w;
+        st_stream(reinterpret_cast<uint4*>(slab_of(p, g0)) + threadIdx.x, w);
     } else {
         double2* q = reinterpret_cast<double2*>(slab_of(p, g0)) + 2 * threadIdx.x;
-        q[0] = make_double2(v[0], v[1]);
-        q[1] = make_double2(v[2], v[3]);
+        st_stream(q, make_double2(v[0], v[1]));
+        st_stream(q + 1, make_double2(v[2], v[3]));
     }
 }
 
@@ -469,12 +525,13 @@ __device__ __forceinline__ void st4_tail(T* __restrict__ p, int64_t base, int64_
         if (base + j < n) p[base + j] = v[j];
 }
 
+template <bool kNt = false>
 __device__ __forceinline__ uint32_t ld4u8_full(const uint8_t* __restrict__ p, int64_t g0,
                                                uint32_t lane = threadIdx.x) {
-    return reinterpret_cast<const uint32_t*>(slab_of(p, g0))[lane];
+    return ld_stream<kNt>(reinterpret_cast<const uint32_t*>(slab_of(p, g0)) + lane);
 }
 __device__ __forceinline__ void st4u8_full(uint8_t* __restrict__ p, int64_t g0, uint32_t w) {
-    reinterpret_cast<uint32_t*>(slab_of(p, g0))[threadIdx.x] = w;
+    st_stream(reinterpret_cast<uint32_t*>(slab_of(p, g0)) + threadIdx.x, w);
 }
 __device__ __forceinline__ uint32_t ld4u8_tail(const uint8_t* __restrict__ p, int64_t base, int64_t n) {
     uint32_t w = 0;
@@ -497,7 +554,7 @@ struct At {
 };
 
 // The inputs of the 4 envs of one group.
-template <bool kTyped, bool kAuto>
+template <bool kTyped, bool kAuto, bool kNt = false>
 struct Group {
     uint32_t x, y, org, dst;  // packed u8 x4
     int32_t c[4];             // cargo
@@ -513,16 +570,16 @@ struct Group {
     __device__ __forceinline__ void load(const StepArgs& A, At<kFull> at, uint32_t lane = threadIdx.x) {
         const se_state& S = A.st;
         if constexpr (kFull) {
-            x = ld4u8_full(S.x, at.g0, lane);
-            y = ld4u8_full(S.y, at.g0, lane);
-            org = ld4u8_full(S.origin, at.g0, lane);
-            dst = ld4u8_full(S.dest, at.g0, lane);
-            ld4_full(S.cargo, at.g0, c, lane);
-            ld4_full(S.fuel, at.g0, f, lane);
-            ld4_full(A.act, at.g0, a, lane);
+            x = ld4u8_full<kNt>(S.x, at.g0, lane);
+            y = ld4u8_full<kNt>(S.y, at.g0, lane);
+            org = ld4u8_full<kNt>(S.origin, at.g0, lane);
+            dst = ld4u8_full<kNt>(S.dest, at.g0, lane);
+            ld4_full<kNt>(S.cargo, at.g0, c, lane);
+            ld4_full<kNt>(S.fuel, at.g0, f, lane);
+            ld4_full<kNt>(A.act, at.g0, a, lane);
             if (kTyped) {
-                ld4_full(A.act_a, at.g0, p, lane);
-                ld4_full(A.act_b, at.g0, q, lane);
+                ld4_full<kNt>(A.act_a, at.g0, p, lane);
+                ld4_full<kNt>(A.act_b, at.g0, q, lane);
             }
         } else {
             x = ld4u8_tail(S.x, at.base, at.n);
@@ -545,8 +602,8 @@ struct Group {
     // episode counters of a full group: loaded late (step_group), they would
     // otherwise hold 8 registers across the whole step
     __device__ __forceinline__ void load_episode(const StepArgs& A, At<true> at) {
-        ld4_full(A.st.ep_return, at.g0, e);
-        ld4_full(A.st.ep_len, at.g0, l);
+        ld4_full<kNt>(A.st.ep_return, at.g0, e);
+        ld4_full<kNt>(A.st.ep_len, at.g0, l);
     }
     __device__ __forceinline__ void load_episode(const StepArgs&, At<false>) {}  // loaded with the rest
 };
@@ -635,9 +692,9 @@ __device__ __forceinline__ void store_rest(const se_state& S, At<kFull> at, cons
 // Registers: x, y, fuel, done and err are stored as soon as the first half has
 // run (and auto-reset has replaced the finished envs' positions), so only cargo,
 // origin, dest and the reward stay live across the loss / arrival blocks.
-template <bool kTyped, bool kReplay, bool kAuto, bool kFull>
+template <bool kTyped, bool kReplay, bool kAuto, bool kFull, bool kNt = false>
 __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
-                                           Group<kTyped, kAuto>& G, At<kFull> at, BlockStats& bs,
+                                           Group<kTyped, kAuto, kNt>& G, At<kFull> at, BlockStats& bs,
                                            Finished& F) {
     const se_state& S = A.st;
     const int64_t n = A.n, base = at.base;
@@ -772,6 +829,16 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
         store_moved(S, at, s, p);
 
         U4 lb{{0u, 0u, 0u, 0u}}, b1 = lb, b2 = lb, b3 = lb, ab = lb;
+#if SHIPENV_NORARE  // timing-only ablation: the rare blocks replaced by cheap words
+        for (int j = 0; j < 4; ++j) {
+            lb.v[j] = fb.v[j] * 0x9E3779B9u;
+            b1.v[j] = fb.v[j] ^ 0x55555555u;
+            b2.v[j] = gb.v[j] * 3u;
+            b3.v[j] = lb.v[j] + gb.v[j];
+            ab.v[j] = b3.v[j] ^ fb.v[j];
+        }
+        if (0)
+#endif
         if (fire) lb = draw(qk, t, kSlotLoss);
         int kind[4];
         uint32_t partial = 0;
@@ -781,11 +848,17 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
             kind[j] = lb.v[j] < kTypeLo ? kLossNone : total;
             partial |= (uint32_t)(p[j].fires & (kind[j] == kLossPartial)) << j;
         }
+#if SHIPENV_NORARE
+        if (0)
+#endif
         if (partial) {
             b1 = draw(qk, t, kSlotBeta1);
             b2 = draw(qk, t, kSlotBeta2);
             b3 = draw(qk, t, kSlotBeta3);
         }
+#if SHIPENV_NORARE
+        if (0)
+#endif
         if (arrive) ab = draw(qk, t, kSlotArrive);
         float rw[4], epr[4];
         int32_t epl[4];
@@ -861,47 +934,47 @@ __device__ __forceinline__ void block_compact(const StepArgs& A, const Finished&
 // the staging hides under them; each iteration loads the next group before storing
 // the current one. The trip count is uniform over the block (the auto-reset
 // compaction holds barriers).
-template <bool kTyped, bool kReplay, bool kAuto, bool kPipe = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPipe ? 2 : 4))) void step_kernel(StepArgs A) {
+template <bool kTyped, bool kReplay, bool kAuto, bool kNt = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void step_kernel(StepArgs A) {
     extern __shared__ uint32_t lds[];
     __shared__ double red[kBlock / 64][3];
     __shared__ int32_t wtot[kBlock / 64];
     const int64_t full = A.n >> 2;
     const int64_t first = (int64_t)blockIdx.x * A.iters * kBlock;  // block-uniform first group
 
+    TRACE_STAMP(0);
     const Staged st = stage_issue(A.world);
     // first group: an unconditional load (lanes past the end re-read the last full
     // group; the host launches this kernel only when there is one), so the staging
     // writes below wait for exactly the image's loads
-    Group<kTyped, kAuto> G;
+    Group<kTyped, kAuto, kNt> G;
     {
         const int64_t last = full - 1 - first;  // block-uniform
         const uint32_t lane = last < (int64_t)threadIdx.x ? (uint32_t)(last < 0 ? 0 : last) : threadIdx.x;
         G.template load<true>(A, At<true>{last < 0 ? full - 1 : first, 0, A.n}, lane);
     }
     const LdsWorld w = stage_finish(A.world, A.dims, lds, st);
+    TRACE_STAMP(1);
 
     BlockStats bs;
     int32_t running = 0;  // this block's done records so far (block-uniform)
     for (int64_t k = 0; k < A.iters; ++k) {
         const int64_t g0 = first + k * kBlock, g = g0 + threadIdx.x;
         Finished F;
-        // the next group's loads go out before this group's compute, so its data
-        // streams in while the VALU works (a load issued after the stores would
-        // wait out the whole memory latency again)
-        if constexpr (kPipe) {
-            Group<kTyped, kAuto> Gn;
-            const bool more = k + 1 < A.iters && g + kBlock < full;
-            if (more) Gn.template load<true>(A, At<true>{g0 + kBlock, 0, A.n});
-            if (g < full) step_group<kTyped, kReplay, kAuto, true>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F);
-            if (more) G = Gn;
-        } else if (g < full) {
-            step_group<kTyped, kReplay, kAuto, true>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F);
+        // (Loading the next group before this group's compute instead measured
+        // slower: the extra registers cost a wave per SIMD, which hid more.)
+        if (g < full) {
+            step_group<kTyped, kReplay, kAuto, true, kNt>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F);
+            if (k == 0) TRACE_STAMP(2);
             if (k + 1 < A.iters && g + kBlock < full) G.template load<true>(A, At<true>{g0 + kBlock, 0, A.n});
         }
         if constexpr (kAuto) block_compact(A, F, g * 4, wtot, running, k + 1 == A.iters);
     }
 
+#if SHIPENV_TRACE
+    __builtin_amdgcn_s_waitcnt(0);  // stores acknowledged
+    TRACE_STAMP(3);
+#endif
     if (kAuto) {
         if (threadIdx.x == 0) A.done_count[blockIdx.x] = running;
         // per-block statistics: fixed-order wave butterfly, then waves in order
@@ -1366,10 +1439,12 @@ int step_block_cap() {
     return c > 0 ? c : kStepBlocks;
 }
 
-// software-pipelined step kernel (next group's loads before this group's compute)
-bool step_pipe() {
-    const char* v = getenv("SHIPENV_STEP_PIPE");
-    return v ? atoi(v) != 0 : true;
+// Nontemporal state loads when one step's traffic (~42-58 B per env) stays well
+// inside the 256 MiB Infinity Cache (measured: faster at N = 2^20, slower at 2^24).
+bool step_nt_loads(const se_env* env) {
+    const char* v = getenv("SHIPENV_NT_LOADS");
+    if (v) return atoi(v) != 0;
+    return env->n * 64 <= (int64_t)128 << 20;
 }
 
 size_t lds_bytes(const se_env* env) { return (size_t)env->dims.padded() * 4; }
@@ -1491,10 +1566,10 @@ int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const 
     const hipStream_t s = (hipStream_t)stream;
     const size_t lds = lds_bytes(env);
     const int grid = env->grid;
-    const bool pipe = env->iters > 1 && step_pipe();
+    const bool ntl = step_nt_loads(env);
     if (env->n >= kEnvsPerThread) {  // at least one full group (step_kernel's first load assumes it)
-        if (!typed && !autoreset && pipe) step_kernel<false, false, false, true><<<grid, kBlock, lds, s>>>(A);
-        else if (!typed && autoreset && pipe) step_kernel<false, false, true, true><<<grid, kBlock, lds, s>>>(A);
+        if (!typed && !autoreset && ntl) step_kernel<false, false, false, true><<<grid, kBlock, lds, s>>>(A);
+        else if (!typed && autoreset && ntl) step_kernel<false, false, true, true><<<grid, kBlock, lds, s>>>(A);
         else if (!typed && !autoreset) step_kernel<false, false, false><<<grid, kBlock, lds, s>>>(A);
         else if (!typed && autoreset) step_kernel<false, false, true><<<grid, kBlock, lds, s>>>(A);
         else if (typed && replay) step_kernel<true, true, false><<<grid, kBlock, lds, s>>>(A);
@@ -1517,6 +1592,12 @@ int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const 
 }  // namespace
 
 extern "C" {
+
+#if SHIPENV_TRACE
+extern "C" int se_trace_read(void* host, size_t bytes) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_trace), bytes) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int se_abi_version(void) { return SHIPENV_ABI_VERSION; }
 
