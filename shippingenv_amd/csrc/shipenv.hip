@@ -403,14 +403,15 @@ __device__ __forceinline__ uint32_t count_below(uint64_t mask) {
 
 // ------------------------------------------------------------------ step kernel
 #if SHIPENV_TRACE
-// [wave][8] s_memrealtime stamps (100 MHz): start, staged, stepped, end
+// [step parity][wave][8] s_memrealtime stamps (100 MHz): start, staged, stepped, end
 constexpr int kTraceWaves = 1 << 16;
 __device__ uint64_t g_trace[kTraceWaves * 8];
 #define TRACE_STAMP(k)                                                                        \
     do {                                                                                      \
         const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                                 \
         const uint32_t w_ = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);                  \
-        if ((threadIdx.x & 63) == 0 && w_ < kTraceWaves) g_trace[w_ * 8 + (k)] = t_;          \
+        if ((threadIdx.x & 63) == 0 && w_ < kTraceWaves / 2)                                  \
+            g_trace[((A.t & 1u) * (kTraceWaves / 2) + w_) * 8 + (k)] = t_;                    \
     } while (0)
 #else
 #define TRACE_STAMP(k) \

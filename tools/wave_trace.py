@@ -45,7 +45,11 @@ def main():
     buf = np.zeros((1 << 16) * 8, dtype=np.uint64)
     lib = ctypes.CDLL(_native.LIB_PATH)
     assert lib.se_trace_read(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes)) == 0
-    tr = buf.reshape(-1, 8)[:waves, :4].astype(np.int64)
+    half = (1 << 16) // 2
+    both = buf.reshape(-1, 8)[:, :4].astype(np.int64)
+    last = (a.steps - 1) & 1  # the last step's parity (t counts from the first step after reset)
+    tr = both[last * half:last * half + waves]
+    prev = both[(1 - last) * half:(1 - last) * half + waves]
     t0 = tr[:, 0].min()
     us = (tr - t0) / 100.0  # 100 MHz ticks -> us
     pct = lambda x: [round(float(np.percentile(x, q)), 2) for q in (0, 10, 50, 90, 100)]
@@ -53,6 +57,8 @@ def main():
            "start": pct(us[:, 0]), "staged": pct(us[:, 1]), "stepped": pct(us[:, 2]), "end": pct(us[:, 3]),
            "stage_dur": pct(us[:, 1] - us[:, 0]), "step_dur": pct(us[:, 2] - us[:, 1]),
            "drain_dur": pct(us[:, 3] - us[:, 2]), "life": pct(us[:, 3] - us[:, 0])}
+    out["prev_end_to_start_us"] = round(float((t0 - prev[:, 3].max()) / 100.0), 2)
+    out["prev_first_start_to_start_us"] = round(float((t0 - prev[:, 0].min()) / 100.0), 2)
     # waves alive over time (10 bins per us)
     edges = np.arange(0, us[:, 3].max() + 0.1, 0.5)
     alive = [int(((us[:, 0] <= e) & (us[:, 3] > e)).sum()) for e in edges]
