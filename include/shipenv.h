@@ -299,6 +299,25 @@ int se_get_counters(se_env* env, uint64_t* step, uint64_t* epoch);
 int se_set_counters(se_env* env, uint64_t step, uint64_t epoch);
 
 int se_destroy(se_env* env);
+/* ---- Map loader (host only, no GPU): Environment._initialize_map
+ * (shipping/environment.py:45-55) without OpenCV. csrc/mapload.cpp. */
+
+/* The luma (Y) plane of a JPEG as cv2.imread(IMREAD_GRAYSCALE) returns it:
+ * baseline / extended / progressive Huffman, 8-bit, 1 or 3 components,
+ * libjpeg's accurate integer IDCT. *height / *width are always set on success;
+ * `out` (row-major, height*width bytes, may be NULL to query the size) is
+ * written when cap is large enough. SE_EINVAL on a corrupt or unsupported file. */
+int se_map_decode_luma(const uint8_t* data, size_t len, uint8_t* out, size_t cap,
+                       int32_t* height, int32_t* width);
+/* gray[row0:row1, col0:col1] -> cv2.resize((W, H), INTER_AREA) (generic,
+ * downscaling) -> resized (H*W, may be NULL) and mask = resized > threshold (may be NULL). */
+int se_map_area_threshold(const uint8_t* gray, int32_t height, int32_t width, int32_t row0,
+                          int32_t row1, int32_t col0, int32_t col1, int32_t H, int32_t W,
+                          uint8_t threshold, uint8_t* resized, uint8_t* mask);
+/* The whole of _initialize_map: decode, crop rows 50:200 / cols 100:300, INTER_AREA
+ * to W x H, > 128. water[x * W + y] = 1 for a non-GROUND cell (x = row, :65). */
+int se_map_from_jpeg(const uint8_t* data, size_t len, int32_t H, int32_t W, uint8_t* water);
+
 const char* se_last_error(void);
 int se_abi_version(void);
 

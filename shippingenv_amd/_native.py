@@ -38,6 +38,7 @@ EXPORTS = (
     "se_qtrain_step", "se_qtrain_destroy",
     "se_episode_stats", "se_clear_stats", "se_done_layout", "se_done_list", "se_done_compact",
     "se_get_counters", "se_set_counters",
+    "se_map_decode_luma", "se_map_area_threshold", "se_map_from_jpeg",
     "se_destroy", "se_last_error", "se_abi_version",
 )
 
@@ -102,6 +103,9 @@ def _declare(lib):
         "se_done_compact": [P, P, P, P],
         "se_get_counters": [P, C.POINTER(u64), C.POINTER(u64)],
         "se_set_counters": [P, u64, u64],
+        "se_map_decode_luma": [C.c_char_p, C.c_size_t, P, C.c_size_t, C.POINTER(i32), C.POINTER(i32)],
+        "se_map_area_threshold": [P, i32, i32, i32, i32, i32, i32, i32, i32, C.c_uint8, P, P],
+        "se_map_from_jpeg": [C.c_char_p, C.c_size_t, i32, i32, P],
         "se_destroy": [P],
         "se_last_error": [],
         "se_abi_version": [],

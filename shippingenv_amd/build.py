@@ -15,7 +15,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "shipenv.hip")
-DEPS = [SRC, os.path.join(HERE, "csrc", "philox.h"), os.path.join(HERE, "csrc", "qpolicy.h"), os.path.join(HERE, "csrc", "replay.h"),
+MAPSRC = os.path.join(HERE, "csrc", "mapload.cpp")  # host-only: the JPEG map loader
+DEPS = [SRC, MAPSRC, os.path.join(HERE, "csrc", "philox.h"), os.path.join(HERE, "csrc", "qpolicy.h"), os.path.join(HERE, "csrc", "replay.h"),
         os.path.join(HERE, "csrc", "qtrain.h"),
         os.path.join(ROOT, "include", "shipenv.h")]
 OUT = os.path.join(HERE, "_lib", "libshipenv_hip.so")
@@ -44,7 +45,7 @@ def build(force=False, verbose=True):
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     tmp = OUT + ".tmp"
-    cmd = [hipcc()] + FLAGS + ["-o", tmp, SRC]
+    cmd = [hipcc()] + FLAGS + ["-o", tmp, SRC, MAPSRC]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -1592,6 +1592,9 @@ int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const 
 
 }  // namespace
 
+// error text for se_last_error from the host-only sources (mapload.cpp)
+void shipenv_set_error(const std::string& msg) { g_err = msg; }
+
 extern "C" {
 
 #if SHIPENV_TRACE
