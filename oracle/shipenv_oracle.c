@@ -42,13 +42,17 @@ enum {
 /* tape.used bits (include/shipenv.h SE_USED_*) */
 enum { U_FUEL_GATE = 1, U_LOSS_TYPE = 2, U_BETA = 4, U_ARRIVE = 8 };
 
-/* Philox counter slots (DESIGN.md "RNG contract", v4). Every draw of a step is a
- * quad block: counter (k, t, slot) for envs 4k..4k+3, word j for env 4k+j. The
- * explicit reset and the synthetic agent draw one block per env. */
-enum { SLOT_FUEL = 0, SLOT_LOSS = 1, SLOT_BETA1 = 2, SLOT_ARRIVE = 3, SLOT_RESET = 4,
-       SLOT_EXPLICIT_RESET = 5, SLOT_ACTION = 6, SLOT_GATE = 7, SLOT_BETA2 = 8, SLOT_BETA3 = 9,
+/* Philox counter slots (DESIGN.md "RNG contract", v5). Step draws are keyed by the
+ * quad k = env / 4 at counter (k, t, slot): quad blocks give word j to env 4k+j
+ * (FUEL, GATE, ARRIVE, RESET, RESET_DEST); a LOSS_r block (slots 1, 2, 8, 9 for
+ * r = 0..3) belongs whole to the r-th env of the quad, in env order, whose gate
+ * fired with cargo > 0: word 0 the loss type, words 1-3 the Beta(2, 2) uniforms.
+ * The explicit reset and the synthetic agent draw one block per env. */
+enum { SLOT_FUEL = 0, SLOT_LOSS0 = 1, SLOT_LOSS1 = 2, SLOT_ARRIVE = 3, SLOT_RESET = 4,
+       SLOT_EXPLICIT_RESET = 5, SLOT_ACTION = 6, SLOT_GATE = 7, SLOT_LOSS2 = 8, SLOT_LOSS3 = 9,
        SLOT_RESET_DEST = 10, SLOT_SAMPLE = 11, SLOT_ROLLOUT = 12, SLOT_ROLLOUT_B = 13,
        SLOT_REPLAY = 15 };
+static const uint32_t LOSS_SLOT[4] = {SLOT_LOSS0, SLOT_LOSS1, SLOT_LOSS2, SLOT_LOSS3};
 
 /* sample_action results where the reference raises / never returns (include/shipenv.h) */
 enum { SAMPLE_RAISES = -1, SAMPLE_NO_OTHER_PORT = -2 };
@@ -103,6 +107,8 @@ typedef struct {
     int need;             /* replay: a consumed draw is missing from the tape */
     const uint32_t* roll; /* rollout attempt t of rollout `env`: block A words (sample,
                              u_fuel, u_gate, u_type); block B (slot ROLLOUT_B) on demand */
+    int32_t loss_rank;    /* Philox step: firing envs of this quad before this one */
+    int32_t loss_drawn;   /* out: this env took a LOSS_r block */
 } source;
 
 /* rollout block B word k (three beta uniforms, the arrival redraw) */
@@ -140,6 +146,12 @@ static void src_move(source* s, double* u_fuel, double* u_gate) {
     *u_gate = u32(quad_word(s->seed, s->env, s->t, SLOT_GATE));
 }
 
+/* Philox step: the env's LOSS_r block (r = its rank among the quad's firing envs) */
+static void loss_block(source* s, uint32_t o[4]) {
+    draw4(s->seed, (int64_t)((uint64_t)s->env >> 2), s->t, LOSS_SLOT[s->loss_rank & 3], o);
+    s->loss_drawn = 1;
+}
+
 static double src_loss_type(source* s) { /* environment.py:177 */
     s->used |= U_LOSS_TYPE;
     if (s->tape) {
@@ -147,7 +159,9 @@ static double src_loss_type(source* s) { /* environment.py:177 */
         return s->tape->u_type;
     }
     if (s->roll) return u32(s->roll[3]);
-    return u32(quad_word(s->seed, s->env, s->t, SLOT_LOSS));
+    uint32_t o[4];
+    loss_block(s, o);
+    return u32(o[0]);
 }
 
 /* environment.py:195, betavariate(2, 2): the median of three uniforms has the
@@ -159,9 +173,9 @@ static double src_beta(source* s) {
         return s->tape->beta;
     }
     if (s->roll) return med3(u32(roll_b(s, 0)), u32(roll_b(s, 1)), u32(roll_b(s, 2)));
-    return med3(u32(quad_word(s->seed, s->env, s->t, SLOT_BETA1)),
-                u32(quad_word(s->seed, s->env, s->t, SLOT_BETA2)),
-                u32(quad_word(s->seed, s->env, s->t, SLOT_BETA3)));
+    uint32_t o[4]; /* the same LOSS_r block as the loss type */
+    draw4(s->seed, (int64_t)((uint64_t)s->env >> 2), s->t, LOSS_SLOT[s->loss_rank & 3], o);
+    return med3(u32(o[1]), u32(o[2]), u32(o[3]));
 }
 
 static int32_t src_arrive(source* s, int32_t P, int32_t origin) { /* :333-335 */
@@ -236,8 +250,10 @@ static int move_ship(const orc_world* w, ship* s, int64_t mx, int64_t my, source
     else r += P_FARTHER;
     /* :318-323: loss gate normalize(cargo, 50, 0) = cargo / 50 (util.py:6-8) */
     double likelihood = (double)s->cargo / (double)MAX_CARGO_CAPACITY;
-    if (u_gate <= likelihood) {
-        /* _calculate_cargo_loss :169-200: the loss-type draw happens first, always */
+    const int production = !src->tape && !src->roll;
+    if (u_gate <= likelihood && !(production && s->cargo == 0)) {
+        /* _calculate_cargo_loss :169-200: the loss-type draw happens first, always
+         * (production skips cargo 0, which loses nothing whatever the draw) */
         double lt = src_loss_type(src);
         int32_t loss;
         if (s->cargo == 0) loss = 0;
@@ -339,10 +355,17 @@ int orc_step_batch(const orc_world* w, int64_t n, int act_mode, const int32_t* a
                    int64_t env_id_base, uint32_t t, int32_t* x, int32_t* y, double* fuel,
                    int32_t* cargo, int32_t* origin, int32_t* dest, double* reward, int32_t* done,
                    int32_t* err) {
+    int64_t quad = -1;
+    int32_t fired = 0; /* envs of the current quad that took a LOSS_r block */
     for (int64_t i = 0; i < n; ++i) {
         ship s;
         load(&s, i, x, y, fuel, cargo, origin, dest);
-        source src = {tape ? tape + i : NULL, seed, env_id_base + i, t, 0, 0, NULL};
+        const int64_t e_id = env_id_base + i;
+        if ((e_id >> 2) != quad) {
+            quad = e_id >> 2;
+            fired = 0;
+        }
+        source src = {tape ? tape + i : NULL, seed, e_id, t, 0, 0, NULL, fired, 0};
         int32_t ty = 0, a = 0, b = 0;
         int e;
         double r = 0.0;
@@ -364,6 +387,7 @@ int orc_step_batch(const orc_world* w, int64_t n, int act_mode, const int32_t* a
             r = 0.0;
             d = 0;
         }
+        fired += src.loss_drawn;
         if (tape) ((orc_tape*)tape)[i].pad = e == E_NEED_DRAW ? src.used : (e == E_OK ? src.used : 0);
         store(&s, i, x, y, fuel, cargo, origin, dest);
         reward[i] = r;
@@ -508,7 +532,7 @@ int orc_rollout(const orc_world* w, int64_t n, const int32_t* x, const int32_t* 
                 st = ROLL_RAISED;
                 break;
             }
-            source src = {NULL, seed, rollout_base + r, (uint32_t)k, 0, 0, blk};
+            source src = {NULL, seed, rollout_base + r, (uint32_t)k, 0, 0, blk, 0, 0};
             double rw = 0.0;
             int32_t d = 0;
             if (step_typed(w, &s, ty, a, b, &src, &rw, &d) != E_OK) continue;

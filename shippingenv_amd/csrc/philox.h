@@ -11,20 +11,22 @@
 
 namespace shipenv {
 
-// Step draws are quad blocks: counter env word = env / 4, word j for env 4k+j, each
-// word a 32-bit uniform u = w * 2^-32 (or an integer draw). The reset kernel and the
-// synthetic agent draw one block per env.
+// Step draws (contract v5) are keyed by the quad k = env / 4: quad blocks, where word
+// j belongs to env 4k+j (a 32-bit uniform u = w * 2^-32 or an integer draw), and the
+// LOSS_r blocks, which belong whole to the r-th env of the quad whose gate fired.
+// The reset kernel and the synthetic agent draw one block per env.
 enum Slot : uint32_t {
     kSlotFuel = 0,           // u_fuel (fuel-cost noise, every step)
-    kSlotLoss = 1,           // u_type (loss type) when the gate fired
-    kSlotBeta1 = 2,          // first of three Beta(2,2) uniforms (partial loss)
+    kSlotLoss0 = 1,          // LOSS_r, r = 0..3 at slots 1, 2, 8, 9 (kSlotLoss[r]): the r-th env
+    kSlotLoss1 = 2,          // of the quad whose gate fired takes the whole block: word 0
+                             // u_type, words 1-3 the Beta(2,2) uniforms
     kSlotArrive = 3,         // new destination != origin on arrival
     kSlotReset = 4,          // auto-reset inside step t: origin
     kSlotExplicitReset = 5,  // se_reset, per env, epoch in the t word: words 0 origin, 1 dest
     kSlotAction = 6,         // synthetic bench agent, per env
     kSlotGate = 7,           // u_gate (cargo-loss gate)
-    kSlotBeta2 = 8,
-    kSlotBeta3 = 9,
+    kSlotLoss2 = 8,
+    kSlotLoss3 = 9,
     kSlotResetDest = 10,     // auto-reset inside step t: destination
     kSlotSample = 11,        // se_sample_actions, per env: word 0
     kSlotRollout = 12,       // rollout attempt, per rollout: sample word, u_fuel, u_gate, u_type
@@ -32,6 +34,11 @@ enum Slot : uint32_t {
     kSlotPolicy = 14,        // se_policy, per env: explore draw, random.choice index
     kSlotReplay = 15,        // se_replay_sample, key (seed, 2^64 - 1), t = update: Feistel round keys
 };
+
+// LOSS_r slot of the r-th firing env of a quad
+__host__ __device__ constexpr uint32_t loss_slot(uint32_t r) {
+    return r == 0 ? kSlotLoss0 : r == 1 ? kSlotLoss1 : r == 2 ? kSlotLoss2 : kSlotLoss3;
+}
 
 struct U4 {
     uint32_t v[4];

@@ -36,10 +36,6 @@
 #define SHIPENV_TRACE 0  // 1 = diagnostic build: per-wave phase timestamps (tools/wave_trace.py)
 #endif
 
-#ifndef SHIPENV_NORARE
-#define SHIPENV_NORARE 0  // 1 = timing-only ablation: no Philox for the loss / beta / arrival draws
-#endif
-
 #ifndef SHIPENV_ABLATE
 #define SHIPENV_ABLATE 0  // 0 = the product; 1 = timing-only memory-traffic build (tools/ablate.sh)
 #endif
@@ -829,45 +825,56 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
         }
         store_moved(S, at, s, p);
 
-        U4 lb{{0u, 0u, 0u, 0u}}, b1 = lb, b2 = lb, b3 = lb, ab = lb;
-#if SHIPENV_NORARE  // timing-only ablation: the rare blocks replaced by cheap words
-        for (int j = 0; j < 4; ++j) {
-            lb.v[j] = fb.v[j] * 0x9E3779B9u;
-            b1.v[j] = fb.v[j] ^ 0x55555555u;
-            b2.v[j] = gb.v[j] * 3u;
-            b3.v[j] = lb.v[j] + gb.v[j];
-            ab.v[j] = b3.v[j] ^ fb.v[j];
+        // Cargo loss (contract v5): the r-th env of the quad whose gate fired takes
+        // the whole block LOSS_r: word 0 the loss type, words 1-3 the Beta(2, 2)
+        // uniforms. LOSS_0 runs whenever any env of the wave fired; LOSS_1..3 only
+        // where a quad had two or more (a few percent of waves). Envs take the
+        // words of the block matching their rank; non-firing envs ignore theirs.
+        uint32_t lt[4], v1[4], v2[4], v3[4];
+        {
+            const uint32_t f1 = fire & 1u, f2 = __popc(fire & 3u), f3 = __popc(fire & 7u);
+            const uint32_t rk[4] = {0u, f1, f2, f3};
+            U4 r{{0u, 0u, 0u, 0u}};
+            if (fire) r = draw(qk, t, loss_slot(0));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                lt[j] = r.v[0];
+                v1[j] = r.v[1];
+                v2[j] = r.v[2];
+                v3[j] = r.v[3];
+            }
+#pragma unroll
+            for (uint32_t q = 1; q < 4; ++q) {
+                if (fire >> q) {  // some env after the first fired too: rank q exists
+                    if (__popc(fire) > q) {
+                        r = draw(qk, t, loss_slot(q));
+#pragma unroll
+                        for (int j = (int)q; j < 4; ++j) {
+                            const bool take = rk[j] >= q;
+                            lt[j] = take ? r.v[0] : lt[j];
+                            v1[j] = take ? r.v[1] : v1[j];
+                            v2[j] = take ? r.v[2] : v2[j];
+                            v3[j] = take ? r.v[3] : v3[j];
+                        }
+                    }
+                }
+            }
         }
-        if (0)
-#endif
-        if (fire) lb = draw(qk, t, kSlotLoss);
         int kind[4];
-        uint32_t partial = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int total = lb.v[j] > kTypeHi ? kLossTotal : kLossPartial;
-            kind[j] = lb.v[j] < kTypeLo ? kLossNone : total;
-            partial |= (uint32_t)(p[j].fires & (kind[j] == kLossPartial)) << j;
+            const int total = lt[j] > kTypeHi ? kLossTotal : kLossPartial;
+            kind[j] = lt[j] < kTypeLo ? kLossNone : total;
         }
-#if SHIPENV_NORARE
-        if (0)
-#endif
-        if (partial) {
-            b1 = draw(qk, t, kSlotBeta1);
-            b2 = draw(qk, t, kSlotBeta2);
-            b3 = draw(qk, t, kSlotBeta3);
-        }
-#if SHIPENV_NORARE
-        if (0)
-#endif
+        U4 ab{{0u, 0u, 0u, 0u}};
         if (arrive) ab = draw(qk, t, kSlotArrive);
         float rw[4], epr[4];
         int32_t epl[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             // median of the three words, then one exact conversion (monotone)
-            const uint32_t lo = min(b1.v[j], b2.v[j]), hi = max(b1.v[j], b2.v[j]);
-            const double beta = u32(max(lo, min(hi, b3.v[j])));  // v_med3_u32
+            const uint32_t lo = min(v1[j], v2[j]), hi = max(v1[j], v2[j]);
+            const double beta = u32(max(lo, min(hi, v3[j])));  // v_med3_u32
             env_finish(s[j], p[j], kind[j], beta, pick_other(ab.v[j], w.P, s[j].dest));
             rw[j] = (float)p[j].r;  // one rounding of the reference's f64 reward
             epr[j] = 0.0f;
