@@ -647,11 +647,18 @@ __device__ __forceinline__ void store_moved(const se_state& S, At<kFull> at, con
         ee |= (uint32_t)(p[j].e & 0xff) << sh;
         fuel[j] = s[j].fuel;
     }
+    // The two 16-byte halves of a lane's 32 bytes of fuel are two store
+    // instructions, each writing every other 16 bytes of the wave's span. Issued
+    // apart, the nontemporal halves reach memory as separate partial-line writes
+    // (measured: +4.5 MB per launch at N = 2^20); the scheduling barriers keep the
+    // pair, and the whole group of stores, back to back.
+    __builtin_amdgcn_sched_barrier(0);
     store4u8(S.x, at, ox);
     store4u8(S.y, at, oy);
     store4(S.fuel, at, fuel);
     store4u8(S.done, at, dn);
     store4u8(reinterpret_cast<uint8_t*>(S.err), at, ee);
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 // cargo, origin, dest, reward (+ the episode counters): final after the second half.
