@@ -45,6 +45,10 @@ using namespace shipenv;
 namespace {
 
 constexpr int kBlock = 256;       // 4 waves
+#ifndef SHIPENV_STEP_BLOCK
+#define SHIPENV_STEP_BLOCK 256
+#endif
+constexpr int kStepBlock = SHIPENV_STEP_BLOCK;  // step kernel workgroup (one LDS world copy each)
 constexpr int kEnvsPerThread = 4; // one 4-byte / 16-byte lane access per field
 constexpr int kMaxBlocks = 2048;  // 256 CUs x 8; grid-stride beyond
 constexpr int kStepBlocks = 2048; // step kernel default cap (SHIPENV_STEP_BLOCKS overrides)
@@ -61,7 +65,8 @@ constexpr double kMaxCargo = 50.0;
 // One device buffer of 32-bit words, staged as-is into LDS by every workgroup:
 //   [0, w)          ground bitmap  (bit = 1: np_game[x, y] == GROUND)
 //   [w, 2w)         port bitmap    (bit = 1: some port sits on the cell)
-//   [2w, 3w)        port-bit prefix counts (set bits in the words before)
+//   [2w, 2w+w/4)    port-bit prefix counts, one byte per bitmap word (set bits in
+//                   the words before; at most P <= 254)
 //   [3w, 3w+P)      port position  (x | y << 8)
 //   [+P)            port fuel stock
 //   [+P)            port cargo stock
@@ -73,28 +78,30 @@ constexpr double kMaxCargo = 50.0;
 //                   [0, 8) a move, index out_of_fuel*4 + ground*2 + closer, summed in
 //                   the reference's order (:288-315); [8] a take (0.05); [9] else 0
 // For the 100x100 map with 5 ports that is 4.5 KB.
-constexpr int kStageRows = 6;  // 256-dword rows of the world image the step kernel stages unguarded
+// kStepBlock-dword rows of the world image the step kernel stages unguarded: >= 1280
+// dwords, the 100x100 image with up to 98 ports (5 ports: ~900, 64 ports: ~1160)
+constexpr int kStageRows = (1280 + kStepBlock - 1) / kStepBlock;
 
 struct WorldDims {
     int32_t H, W, P, words;
-    __host__ __device__ int pos() const { return 3 * words; }
-    __host__ __device__ int rank2port() const { return 3 * words + 3 * P; }
+    __host__ __device__ int pos() const { return 2 * words + (words + 3) / 4; }
+    __host__ __device__ int rank2port() const { return pos() + 3 * P; }
     __host__ __device__ int frac() const { return (rank2port() + P + 1 + 1) & ~1; }
     __host__ __device__ int gate() const { return frac() + 2 * 50; }
     __host__ __device__ int rtab() const { return (gate() + 50 + 1) & ~1; }
     __host__ __device__ int total() const { return rtab() + 2 * 10; }
-    // device image / LDS size: whole 256-dword rows, at least the step kernel's
-    // unguarded staging window (kStageRows rows)
+    // device image / LDS size: whole kStepBlock-dword rows, at least the step
+    // kernel's unguarded staging window (kStageRows rows)
     __host__ __device__ int padded() const {
-        const int t = (total() + 255) & ~255;
-        return t > 256 * kStageRows ? t : 256 * kStageRows;
+        const int t = (total() + kStepBlock - 1) / kStepBlock * kStepBlock;
+        return t > kStepBlock * kStageRows ? t : kStepBlock * kStageRows;
     }
 };
 
 struct LdsWorld {
     const uint32_t* ground;
     const uint32_t* portbit;
-    const uint32_t* prefix;
+    const uint8_t* prefix;
     const uint32_t* pos;
     const int32_t* pfuel;
     const int32_t* pcargo;
@@ -138,12 +145,12 @@ struct Staged {
     uint32_t r[kStageRows];
 };
 
-// The step kernel's half (256 threads): the image is padded to whole rows of at
+// The step kernel's half (kStepBlock threads): the image is padded to whole rows of at
 // least kStageRows (WorldDims::padded), so these loads need no guard and no branch.
 __device__ __forceinline__ Staged stage_issue(const uint32_t* __restrict__ g) {
     Staged st;
 #pragma unroll
-    for (int k = 0; k < kStageRows; ++k) st.r[k] = g[threadIdx.x + 256 * k];
+    for (int k = 0; k < kStageRows; ++k) st.r[k] = g[threadIdx.x + kStepBlock * k];
     return st;
 }
 
@@ -152,8 +159,8 @@ __device__ __forceinline__ LdsWorld world_view(WorldDims d, const uint32_t* lds)
 __device__ __forceinline__ LdsWorld stage_finish(const uint32_t* __restrict__ g, WorldDims d,
                                                  uint32_t* lds, const Staged& st) {
 #pragma unroll
-    for (int k = 0; k < kStageRows; ++k) lds[threadIdx.x + 256 * k] = st.r[k];
-    for (int i = (int)threadIdx.x + 256 * kStageRows; i < d.total(); i += 256)
+    for (int k = 0; k < kStageRows; ++k) lds[threadIdx.x + kStepBlock * k] = st.r[k];
+    for (int i = (int)threadIdx.x + kStepBlock * kStageRows; i < d.total(); i += kStepBlock)
         lds[i] = g[i];  // larger maps / port tables: the remainder
     __syncthreads();
     return world_view(d, lds);
@@ -185,7 +192,7 @@ __device__ __forceinline__ LdsWorld world_view(WorldDims d, const uint32_t* lds)
     LdsWorld w;
     w.ground = lds;
     w.portbit = lds + d.words;
-    w.prefix = lds + 2 * d.words;
+    w.prefix = reinterpret_cast<const uint8_t*>(lds + 2 * d.words);
     w.pos = lds + d.pos();
     w.pfuel = (const int32_t*)(lds + d.pos() + d.P);
     w.pcargo = (const int32_t*)(lds + d.pos() + 2 * d.P);
@@ -405,7 +412,7 @@ __device__ uint64_t g_trace[kTraceWaves * 8];
 #define TRACE_STAMP(k)                                                                        \
     do {                                                                                      \
         const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                                 \
-        const uint32_t w_ = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);                  \
+        const uint32_t w_ = blockIdx.x * (kStepBlock / 64) + (threadIdx.x >> 6);                  \
         if ((threadIdx.x & 63) == 0 && w_ < kTraceWaves / 2)                                  \
             g_trace[((A.t & 1u) * (kTraceWaves / 2) + w_) * 8 + (k)] = t_;                    \
     } while (0)
@@ -923,7 +930,7 @@ __device__ __forceinline__ void block_compact(const StepArgs& A, const Finished&
     if (!__syncthreads_or(nd)) return;  // nothing finished in the block: no second barrier
     int32_t before = 0, block_total = 0;
 #pragma unroll
-    for (int k = 0; k < kBlock / 64; ++k) {
+    for (int k = 0; k < kStepBlock / 64; ++k) {
         const int32_t v = wtot[k];
         before += k < wave ? v : 0;
         block_total += v;
@@ -950,12 +957,12 @@ __device__ __forceinline__ void block_compact(const StepArgs& A, const Finished&
 // the current one. The trip count is uniform over the block (the auto-reset
 // compaction holds barriers).
 template <bool kTyped, bool kReplay, bool kAuto, bool kNt = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void step_kernel(StepArgs A) {
+__global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4))) void step_kernel(StepArgs A) {
     extern __shared__ uint32_t lds[];
-    __shared__ double red[kBlock / 64][3];
-    __shared__ int32_t wtot[kBlock / 64];
+    __shared__ double red[kStepBlock / 64][3];
+    __shared__ int32_t wtot[kStepBlock / 64];
     const int64_t full = A.n >> 2;
-    const int64_t first = (int64_t)blockIdx.x * A.iters * kBlock;  // block-uniform first group
+    const int64_t first = (int64_t)blockIdx.x * A.iters * kStepBlock;  // block-uniform first group
 
     TRACE_STAMP(0);
     const Staged st = stage_issue(A.world);
@@ -974,14 +981,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     BlockStats bs;
     int32_t running = 0;  // this block's done records so far (block-uniform)
     for (int64_t k = 0; k < A.iters; ++k) {
-        const int64_t g0 = first + k * kBlock, g = g0 + threadIdx.x;
+        const int64_t g0 = first + k * kStepBlock, g = g0 + threadIdx.x;
         Finished F;
         // (Loading the next group before this group's compute instead measured
         // slower: the extra registers cost a wave per SIMD, which hid more.)
         if (g < full) {
             step_group<kTyped, kReplay, kAuto, true, kNt>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F);
             if (k == 0) TRACE_STAMP(2);
-            if (k + 1 < A.iters && g + kBlock < full) G.template load<true>(A, At<true>{g0 + kBlock, 0, A.n});
+            if (k + 1 < A.iters && g + kStepBlock < full) G.template load<true>(A, At<true>{g0 + kStepBlock, 0, A.n});
         }
         if constexpr (kAuto) block_compact(A, F, g * 4, wtot, running, k + 1 == A.iters);
     }
@@ -1009,7 +1016,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         __syncthreads();
         if (threadIdx.x == 0) {
             double a = 0.0, b = 0.0, c = 0.0;
-            for (int k = 0; k < kBlock / 64; ++k) {
+            for (int k = 0; k < kStepBlock / 64; ++k) {
                 a += red[k][0];
                 b += red[k][1];
                 c += red[k][2];
@@ -1042,7 +1049,7 @@ __global__ __launch_bounds__(64) void step_tail_kernel(StepArgs A) {
     Finished F;
     step_group<kTyped, kReplay, kAuto, false>(A, w, G, at, bs, F);
     if constexpr (kAuto) {
-        const int64_t b = g / (A.iters * kBlock);
+        const int64_t b = g / (A.iters * kStepBlock);
         int32_t c = g == 0 ? 0 : A.done_count[b];  // g == 0: step_kernel did not run
         for (int j = 0; j < 4; ++j)
             if ((F.mask >> j) & 1u)
@@ -1487,16 +1494,17 @@ int upload_world(se_env* env, int32_t P, const int32_t* px, const int32_t* py, c
         img[d.pos() + P + i] = (uint32_t)pf[i];
         img[d.pos() + 2 * P + i] = (uint32_t)pc[i];
     }
+    uint8_t* prefix = reinterpret_cast<uint8_t*>(&img[2 * words]);
     uint32_t run = 0;
     for (int k = 0; k < words; ++k) {
-        img[2 * words + k] = run;
+        prefix[k] = (uint8_t)run;  // run <= P <= 254
         run += (uint32_t)__builtin_popcount(img[words + k]);
     }
     // rank -> first port (in port order) on that cell
     for (int i = P - 1; i >= 0; --i) {
         const uint32_t c = (uint32_t)(px[i] * W + py[i]);
         const uint32_t word = img[words + (c >> 5)];
-        const uint32_t rank = img[2 * words + (c >> 5)] + (uint32_t)__builtin_popcount(word & ((1u << (c & 31)) - 1u));
+        const uint32_t rank = prefix[c >> 5] + (uint32_t)__builtin_popcount(word & ((1u << (c & 31)) - 1u));
         img[d.rank2port() + rank] = (uint32_t)i;
     }
     // normalize(cargo, 50, 0) = cargo / 50 (util.py:6-8): Python's int / int true
@@ -1583,13 +1591,13 @@ int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const 
     const int grid = env->grid;
     const bool ntl = step_nt_loads(env);
     if (env->n >= kEnvsPerThread) {  // at least one full group (step_kernel's first load assumes it)
-        if (!typed && !autoreset && ntl) step_kernel<false, false, false, true><<<grid, kBlock, lds, s>>>(A);
-        else if (!typed && autoreset && ntl) step_kernel<false, false, true, true><<<grid, kBlock, lds, s>>>(A);
-        else if (!typed && !autoreset) step_kernel<false, false, false><<<grid, kBlock, lds, s>>>(A);
-        else if (!typed && autoreset) step_kernel<false, false, true><<<grid, kBlock, lds, s>>>(A);
-        else if (typed && replay) step_kernel<true, true, false><<<grid, kBlock, lds, s>>>(A);
-        else if (typed && !autoreset) step_kernel<true, false, false><<<grid, kBlock, lds, s>>>(A);
-        else step_kernel<true, false, true><<<grid, kBlock, lds, s>>>(A);
+        if (!typed && !autoreset && ntl) step_kernel<false, false, false, true><<<grid, kStepBlock, lds, s>>>(A);
+        else if (!typed && autoreset && ntl) step_kernel<false, false, true, true><<<grid, kStepBlock, lds, s>>>(A);
+        else if (!typed && !autoreset) step_kernel<false, false, false><<<grid, kStepBlock, lds, s>>>(A);
+        else if (!typed && autoreset) step_kernel<false, false, true><<<grid, kStepBlock, lds, s>>>(A);
+        else if (typed && replay) step_kernel<true, true, false><<<grid, kStepBlock, lds, s>>>(A);
+        else if (typed && !autoreset) step_kernel<true, false, false><<<grid, kStepBlock, lds, s>>>(A);
+        else step_kernel<true, false, true><<<grid, kStepBlock, lds, s>>>(A);
         HIP_TRY(hipGetLastError());
     }
     if (env->n & 3) {
@@ -1657,9 +1665,9 @@ int se_create(se_env** out, int device, int64_t n, int64_t env_id_base, int32_t 
         // workgroup b owns iters * 256 consecutive groups of 4 envs
         const int64_t groups = (n + kEnvsPerThread - 1) / kEnvsPerThread;
         const int64_t cap = step_block_cap();
-        env->iters = groups > 0 ? (groups + cap * kBlock - 1) / (cap * kBlock) : 1;
-        env->grid = (int)(groups > 0 ? (groups + env->iters * kBlock - 1) / (env->iters * kBlock) : 1);
-        env->seg = env->iters * kBlock * kEnvsPerThread;
+        env->iters = groups > 0 ? (groups + cap * kStepBlock - 1) / (cap * kStepBlock) : 1;
+        env->grid = (int)(groups > 0 ? (groups + env->iters * kStepBlock - 1) / (env->iters * kStepBlock) : 1);
+        env->seg = env->iters * kStepBlock * kEnvsPerThread;
     }
     hipError_t e = hipMalloc(&env->d_slab, (size_t)env->grid * 4 * sizeof(double));
     if (e == hipSuccess) e = hipMemset(env->d_slab, 0, (size_t)env->grid * 4 * sizeof(double));
