@@ -20,7 +20,12 @@ def main():
     p.add_argument("--launches", type=int, default=20)
     p.add_argument("--steps", type=int, default=20, help="policy+step iterations before timing")
     p.add_argument("--eps", type=float, default=0.1)
+    p.add_argument("--lib", default=None)
     a = p.parse_args()
+    if a.lib:
+        from shippingenv_amd import _native
+
+        _native.LIB_PATH = os.path.abspath(a.lib)
     from shippingenv_amd.policy import DQNNetwork, QPolicy
     from shippingenv_amd.vec import VecEnv
 
@@ -41,7 +46,7 @@ def main():
         pol.act(a.eps, 1000 + k)
     e1.record()
     torch.cuda.synchronize()
-    print(json.dumps({"n": a.n, "ms_per_launch": round(e0.elapsed_time(e1) / a.launches, 4),
+    print(json.dumps({"lib": os.path.basename(a.lib or "default"), "n": a.n, "ms_per_launch": round(e0.elapsed_time(e1) / a.launches, 4),
                       "at_port": float(at.float().mean()), "wave32_with_port": float(waves_any)}))
 
 
