@@ -282,7 +282,7 @@ int se_qtrain_destroy(se_qtrain* q);  /* destroy before the env it was created o
 int se_episode_stats(se_env* env, double* out, void* stream);
 int se_clear_stats(se_env* env, void* stream);
 
-/* Done lists (auto-reset). Every workgroup of the step kernel writes the envs it
+/* Done lists (auto-reset). Every wave of the step kernel writes the envs it
  * finished, in env order, into its own segment; no global atomics, so the list is
  * deterministic. se_done_layout gives the segment stride and count the done_recs /
  * done_count buffers must be sized for (2 * segments * seg_stride records,

@@ -915,52 +915,38 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
 #endif
 }
 
-// Done-list compaction of one grid-stride iteration (auto-reset), no global
-// atomics: a wave-exclusive prefix of the per-lane counts (0..4) from three
-// ballots, a block prefix over the 4 wave totals in LDS, and the records go to
-// this workgroup's own segment of the list in env order (deterministic).
-// All threads of the block call it (it holds two barriers).
-__device__ __forceinline__ void block_compact(const StepArgs& A, const Finished& F, int64_t base,
-                                              int32_t* wtot, int32_t& running, bool last) {
+// Done-list compaction of one iteration (auto-reset): no atomics, no LDS and no
+// barrier. A wave-exclusive prefix of the per-lane counts (0..4) comes from three
+// ballot bit-planes; the records go to this wave's own segment of the list in env
+// order (deterministic). An earlier version ranked the waves of a workgroup through
+// LDS behind two barriers: 1.4 us of a 15.4 us config-4 step.
+__device__ __forceinline__ void wave_compact(const StepArgs& A, const Finished& F, int64_t base,
+                                             int64_t segment) {
     const int nd = __popc(F.mask);
     const uint64_t b0 = __ballot(nd & 1), b1 = __ballot(nd & 2), b2 = __ballot(nd & 4);
-    const uint32_t wave_total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
-    const int wave = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) wtot[wave] = (int32_t)wave_total;
-    if (!__syncthreads_or(nd)) return;  // nothing finished in the block: no second barrier
-    int32_t before = 0, block_total = 0;
-#pragma unroll
-    for (int k = 0; k < kStepBlock / 64; ++k) {
-        const int32_t v = wtot[k];
-        before += k < wave ? v : 0;
-        block_total += v;
-    }
     if (nd) {
-        int64_t slot = (int64_t)blockIdx.x * A.seg + running + before +
-                       (int32_t)(count_below(b0) + 2 * count_below(b1) + 4 * count_below(b2));
+        int64_t slot = segment * A.seg + (int32_t)(count_below(b0) + 2 * count_below(b1) + 4 * count_below(b2));
         const int32_t t = (int32_t)A.t;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             if ((F.mask >> j) & 1u) A.done_recs[slot++] = se_done_rec{(int32_t)(base + j), F.ret[j], F.len[j], t};
     }
-    running += block_total;
-    if (!last) __syncthreads();  // wtot is rewritten by the next iteration
+    if ((threadIdx.x & 63) == 0)
+        A.done_count[segment] = (int32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
 }
 
 // Workgroup b owns the contiguous groups [b*iters*256, (b+1)*iters*256) (a group is
-// 4 consecutive envs, one thread per group per iteration), so its done-list
-// segment follows env order and the concatenated segments are globally sorted.
-// Every field of a group is one 4- or 16-byte lane access. The partial last group
-// (n % 4 envs) is left to step_tail_kernel, so this loop carries no guarded scalar
-// path. The first group's loads are issued before the world is staged into LDS so
-// the staging hides under them; each iteration loads the next group before storing
-// the current one. The trip count is uniform over the block (the auto-reset
-// compaction holds barriers).
+// 4 consecutive envs, one lane per group per iteration), and wave w of it the
+// contiguous iters*64 groups from b*iters*256 + w*iters*64, 64 per iteration. Its
+// done-list segment (segment = b*4 + w) therefore follows env order, and the
+// concatenated segments are globally sorted. Every field of a group is one 4- or
+// 16-byte lane access. The partial last group (n % 4 envs) is left to
+// step_tail_kernel, so this loop carries no guarded scalar path. The world image's
+// loads, then the first group's, are all in flight before the LDS writes; each
+// iteration loads the next group after storing the current one.
 template <bool kTyped, bool kReplay, bool kAuto, bool kNt = false>
 __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4))) void step_kernel(StepArgs A) {
     extern __shared__ uint32_t lds[];
-    __shared__ double red[kStepBlock / 64][3];
-    __shared__ int32_t wtot[kStepBlock / 64];
     const int64_t full = A.n >> 2;
     const int64_t first = (int64_t)blockIdx.x * A.iters * kStepBlock;  // block-uniform first group
 
@@ -979,7 +965,6 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
     TRACE_STAMP(1);
 
     BlockStats bs;
-    int32_t running = 0;  // this block's done records so far (block-uniform)
     for (int64_t k = 0; k < A.iters; ++k) {
         const int64_t g0 = first + k * kStepBlock, g = g0 + threadIdx.x;
         Finished F;
@@ -990,7 +975,12 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
             if (k == 0) TRACE_STAMP(2);
             if (k + 1 < A.iters && g + kStepBlock < full) G.template load<true>(A, At<true>{g0 + kStepBlock, 0, A.n});
         }
-        if constexpr (kAuto) block_compact(A, F, g * 4, wtot, running, k + 1 == A.iters);
+#ifndef SHIPENV_NOCOMPACT
+        // done-list segment of this (iteration, wave): 64 groups, in env order
+        if constexpr (kAuto) wave_compact(A, F, g * 4, __builtin_amdgcn_readfirstlane((int32_t)(g >> 6)));
+#else
+        (void)F;
+#endif
     }
 
 #if SHIPENV_TRACE
@@ -998,8 +988,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
     TRACE_STAMP(3);
 #endif
     if (kAuto) {
-        if (threadIdx.x == 0) A.done_count[blockIdx.x] = running;
-        // per-block statistics: fixed-order wave butterfly, then waves in order
+        // per-wave statistics: a fixed-order butterfly, one slab entry per segment
         double ret = bs.ret, eps = (double)bs.eps, len = (double)bs.len;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
@@ -1007,25 +996,12 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
             eps += __shfl_xor(eps, off);
             len += __shfl_xor(len, off);
         }
-        const int wave = threadIdx.x >> 6;
-        if ((threadIdx.x & 63) == 0) {
-            red[wave][0] = ret;
-            red[wave][1] = eps;
-            red[wave][2] = len;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            double a = 0.0, b = 0.0, c = 0.0;
-            for (int k = 0; k < kStepBlock / 64; ++k) {
-                a += red[k][0];
-                b += red[k][1];
-                c += red[k][2];
-            }
-            if (b != 0.0) {
-                double* sl = A.slab + 4 * blockIdx.x;
-                sl[0] += a;
-                sl[1] += b;
-                sl[2] += c;
+        if ((threadIdx.x & 63) == 0 && eps != 0.0) {
+            {
+                double* sl = A.slab + 4 * (blockIdx.x * (kStepBlock / 64) + (threadIdx.x >> 6));
+                sl[0] += ret;
+                sl[1] += eps;
+                sl[2] += len;
             }
         }
     }
@@ -1049,14 +1025,16 @@ __global__ __launch_bounds__(64) void step_tail_kernel(StepArgs A) {
     Finished F;
     step_group<kTyped, kReplay, kAuto, false>(A, w, G, at, bs, F);
     if constexpr (kAuto) {
-        const int64_t b = g / (A.iters * kStepBlock);
-        int32_t c = g == 0 ? 0 : A.done_count[b];  // g == 0: step_kernel did not run
+        const int64_t b = g >> 6;  // the (iteration, wave) segment that owns group g
+        int32_t c = (g & 63) == 0 ? 0 : A.done_count[b];  // a fresh segment: step_kernel wrote none
         for (int j = 0; j < 4; ++j)
             if ((F.mask >> j) & 1u)
                 A.done_recs[b * A.seg + c++] = se_done_rec{(int32_t)(at.base + j), F.ret[j], F.len[j], (int32_t)A.t};
         A.done_count[b] = c;
         if (bs.eps != 0) {
-            double* sl = A.slab + 4 * b;
+            // the slab entry of the wave that owns group g
+            const int64_t bl = g / (A.iters * kStepBlock), wv = (g % kStepBlock) >> 6;
+            double* sl = A.slab + 4 * (bl * (kStepBlock / 64) + wv);
             sl[0] += bs.ret;
             sl[1] += (double)bs.eps;
             sl[2] += (double)bs.len;
@@ -1082,24 +1060,42 @@ __global__ void probe_kernel(const uint32_t* world, WorldDims d, const int* in, 
 }
 #endif
 
-// Contiguous copy of the last step's per-block done lists (se_done_compact): block
-// b sums the counts before it (grid <= 2048 entries) and copies its segment.
-__global__ __launch_bounds__(kBlock) void done_compact_kernel(const se_done_rec* __restrict__ recs,
-                                                              const int32_t* __restrict__ counts,
-                                                              int64_t seg, se_done_rec* __restrict__ out,
-                                                              int32_t* __restrict__ out_count) {
-    __shared__ int32_t part[kBlock];
-    int32_t acc = 0;
-    for (int i = threadIdx.x; i < (int)blockIdx.x; i += kBlock) acc += counts[i];
-    part[threadIdx.x] = acc;
+// Contiguous copy of the last step's done lists (se_done_compact), in two launches:
+// done_scan_kernel (one workgroup) turns the per-segment counts into exclusive
+// offsets, chunk by chunk in segment order; done_copy_kernel copies segment s to
+// out[offsets[s]...], one wave per segment.
+__global__ __launch_bounds__(1024) void done_scan_kernel(const int32_t* __restrict__ counts, int64_t nseg,
+                                                         int32_t* __restrict__ offsets,
+                                                         int32_t* __restrict__ out_count) {
+    __shared__ int32_t part[1024];
+    const int64_t chunk = (nseg + 1023) / 1024;
+    const int64_t lo = (int64_t)threadIdx.x * chunk, hi = lo + chunk < nseg ? lo + chunk : nseg;
+    int32_t sum = 0;
+    for (int64_t i = lo; i < hi; ++i) sum += counts[i];
+    part[threadIdx.x] = sum;
     __syncthreads();
-    for (int off = kBlock / 2; off > 0; off >>= 1) {
-        if ((int)threadIdx.x < off) part[threadIdx.x] += part[threadIdx.x + off];
+    for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan of the chunk sums
+        const int32_t v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0;
+        __syncthreads();
+        part[threadIdx.x] += v;
         __syncthreads();
     }
-    const int32_t start = part[0], cnt = counts[blockIdx.x];
-    for (int i = threadIdx.x; i < cnt; i += kBlock) out[start + i] = recs[(int64_t)blockIdx.x * seg + i];
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *out_count = start + cnt;
+    int32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+    for (int64_t i = lo; i < hi; ++i) {
+        offsets[i] = run;
+        run += counts[i];
+    }
+    if (threadIdx.x == 1023) *out_count = part[1023];
+}
+
+__global__ __launch_bounds__(kBlock) void done_copy_kernel(const se_done_rec* __restrict__ recs,
+                                                           const int32_t* __restrict__ counts,
+                                                           const int32_t* __restrict__ offsets, int64_t nseg,
+                                                           int64_t seg, se_done_rec* __restrict__ out) {
+    const int64_t s = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (s >= nseg) return;
+    const int32_t cnt = counts[s], start = offsets[s];
+    for (int i = threadIdx.x & 63; i < cnt; i += 64) out[start + i] = recs[s * seg + i];
 }
 
 // ------------------------------------------------------------------ reset kernel
@@ -1408,14 +1404,17 @@ struct se_env {
     uint64_t step_t = 0, epoch = 0;
     std::vector<uint8_t> water;  // H*W, 0 = ground
     uint32_t* d_world = nullptr;
-    int64_t seg = 0;    // done-list segment stride (records per workgroup)
+    int64_t seg = 0;    // done-list segment stride (records per wave-iteration: 256)
     int64_t iters = 1;  // groups per thread of the step kernel
     int world_cap = 0;  // words allocated
     uint64_t world_version = 0;  // bumped by every world upload (se_qnet folds the ports)
     se_state st{};
     bool bound = false;
-    double* d_slab = nullptr;       // [grid][4]
+    double* d_slab = nullptr;       // [nslab][4]
+    int32_t* d_offsets = nullptr;   // [nseg] se_done_compact scratch
     int grid = 0;
+    int64_t nseg = 0;   // done-list segments: one per (iteration, wave) of the step kernel
+    int64_t nslab = 0;  // stats slab entries: one per step-kernel wave
 };
 
 namespace {
@@ -1580,8 +1579,8 @@ int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const 
     // readable while step t runs; every block rewrites its own count each step.
     if (autoreset) {
         const size_t par = (size_t)(env->step_t & 1u);
-        A.done_recs = env->st.done_recs + par * (size_t)env->grid * (size_t)env->seg;
-        A.done_count = env->st.done_count + par * (size_t)env->grid;
+        A.done_recs = env->st.done_recs + par * (size_t)env->nseg * (size_t)env->seg;
+        A.done_count = env->st.done_count + par * (size_t)env->nseg;
     }
     A.seg = env->seg;
     A.iters = env->iters;
@@ -1667,10 +1666,12 @@ int se_create(se_env** out, int device, int64_t n, int64_t env_id_base, int32_t 
         const int64_t cap = step_block_cap();
         env->iters = groups > 0 ? (groups + cap * kStepBlock - 1) / (cap * kStepBlock) : 1;
         env->grid = (int)(groups > 0 ? (groups + env->iters * kStepBlock - 1) / (env->iters * kStepBlock) : 1);
-        env->seg = env->iters * kStepBlock * kEnvsPerThread;
+        env->seg = 64 * kEnvsPerThread;  // one done-list segment per (iteration, wave)
+        env->nseg = (int64_t)env->grid * env->iters * (kStepBlock / 64);
+        env->nslab = (int64_t)env->grid * (kStepBlock / 64);  // stats: one entry per wave
     }
-    hipError_t e = hipMalloc(&env->d_slab, (size_t)env->grid * 4 * sizeof(double));
-    if (e == hipSuccess) e = hipMemset(env->d_slab, 0, (size_t)env->grid * 4 * sizeof(double));
+    hipError_t e = hipMalloc(&env->d_slab, (size_t)env->nslab * 4 * sizeof(double));
+    if (e == hipSuccess) e = hipMemset(env->d_slab, 0, (size_t)env->nslab * 4 * sizeof(double));
     if (e != hipSuccess) {
         se_destroy(env);
         return fail(SE_EHIP, std::string("se_create allocation: ") + hipGetErrorString(e));
@@ -1703,7 +1704,7 @@ int se_bind(se_env* env, const se_state* st) {
         if (!aligned16(st->ep_return) || !aligned16(st->ep_len) || !aligned16(st->done_recs))
             return fail(SE_EINVAL, "state buffers must be 16-byte aligned");
         DeviceGuard g(env->device);
-        HIP_TRY(hipMemset(st->done_count, 0, 2 * (size_t)env->grid * sizeof(int32_t)));
+        HIP_TRY(hipMemset(st->done_count, 0, 2 * (size_t)env->nseg * sizeof(int32_t)));
     }
     env->st = *st;
     env->bound = true;
@@ -1839,7 +1840,7 @@ int se_rollout(se_env* env, const int32_t* src, int64_t m, int32_t max_steps, in
 int se_episode_stats(se_env* env, double* out, void* stream) {
     if (!env || !out) return fail(SE_EINVAL, "null argument");
     DeviceGuard g(env->device);
-    stats_kernel<<<1, 64, 0, (hipStream_t)stream>>>(env->d_slab, env->grid, out);
+    stats_kernel<<<1, 64, 0, (hipStream_t)stream>>>(env->d_slab, (int)env->nslab, out);
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }
@@ -1847,7 +1848,7 @@ int se_episode_stats(se_env* env, double* out, void* stream) {
 int se_clear_stats(se_env* env, void* stream) {
     if (!env) return fail(SE_EINVAL, "null env");
     DeviceGuard g(env->device);
-    HIP_TRY(hipMemsetAsync(env->d_slab, 0, (size_t)env->grid * 4 * sizeof(double),
+    HIP_TRY(hipMemsetAsync(env->d_slab, 0, (size_t)env->nslab * 4 * sizeof(double),
                            (hipStream_t)stream));
     return SE_OK;
 }
@@ -1855,7 +1856,7 @@ int se_clear_stats(se_env* env, void* stream) {
 int se_done_layout(se_env* env, int64_t* seg_stride, int32_t* segments) {
     if (!env) return fail(SE_EINVAL, "null env");
     if (seg_stride) *seg_stride = env->seg;
-    if (segments) *segments = env->grid;
+    if (segments) *segments = (int32_t)env->nseg;
     return SE_OK;
 }
 
@@ -1864,8 +1865,8 @@ int se_done_list(se_env* env, int64_t* rec_offset, int64_t* count_offset) {
     if (!(env->flags & SE_FLAG_AUTO_RESET)) return fail(SE_ESTATE, "no done list without auto-reset");
     if (env->step_t == 0) return fail(SE_ESTATE, "no step has run");
     const int64_t par = (int64_t)((env->step_t - 1) & 1u);
-    *rec_offset = par * (int64_t)env->grid * env->seg;
-    *count_offset = par * (int64_t)env->grid;
+    *rec_offset = par * (int64_t)env->nseg * env->seg;
+    *count_offset = par * (int64_t)env->nseg;
     return SE_OK;
 }
 
@@ -1875,8 +1876,12 @@ int se_done_compact(se_env* env, se_done_rec* out, int32_t* out_count, void* str
     if (rc) return rc;
     if (!out || !out_count) return fail(SE_EINVAL, "null output");
     DeviceGuard g(env->device);
-    done_compact_kernel<<<env->grid, kBlock, 0, (hipStream_t)stream>>>(
-        env->st.done_recs + ro, env->st.done_count + co, env->seg, out, out_count);
+    if (!env->d_offsets) HIP_TRY(hipMalloc(&env->d_offsets, (size_t)env->nseg * sizeof(int32_t)));
+    const hipStream_t s = (hipStream_t)stream;
+    done_scan_kernel<<<1, 1024, 0, s>>>(env->st.done_count + co, env->nseg, env->d_offsets, out_count);
+    const int64_t blocks = (env->nseg + kBlock / 64 - 1) / (kBlock / 64);
+    done_copy_kernel<<<(int)blocks, kBlock, 0, s>>>(env->st.done_recs + ro, env->st.done_count + co,
+                                                    env->d_offsets, env->nseg, env->seg, out);
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }
@@ -1893,7 +1898,7 @@ int se_set_counters(se_env* env, uint64_t step, uint64_t epoch) {
     DeviceGuard g(env->device);
     HIP_TRY(hipDeviceSynchronize());
     if (env->bound && env->st.done_count)
-        HIP_TRY(hipMemset(env->st.done_count, 0, 2 * (size_t)env->grid * sizeof(int32_t)));
+        HIP_TRY(hipMemset(env->st.done_count, 0, 2 * (size_t)env->nseg * sizeof(int32_t)));
     env->step_t = step;
     env->epoch = epoch;
     return SE_OK;
@@ -1904,6 +1909,7 @@ int se_destroy(se_env* env) {
     DeviceGuard g(env->device);
     if (env->d_world) (void)hipFree(env->d_world);
     if (env->d_slab) (void)hipFree(env->d_slab);
+    if (env->d_offsets) (void)hipFree(env->d_offsets);
     delete env;
     return SE_OK;
 }

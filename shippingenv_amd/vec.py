@@ -100,7 +100,7 @@ class VecEnv:
                                   self.port_y.ctypes.data_as(C.c_void_p),
                                   self.port_fuel.ctypes.data_as(C.c_void_p),
                                   self.port_cargo.ctypes.data_as(C.c_void_p), self.seed, flags))
-        # done lists (auto-reset): per-workgroup segments, double-buffered
+        # done lists (auto-reset): per-wave segments, double-buffered
         # (include/shipenv.h se_done_layout); records are {env, ep_return bits, ep_len, step}
         seg, nseg = C.c_int64(), C.c_int32()
         N.check(lib.se_done_layout(self._h, C.byref(seg), C.byref(nseg)))
