@@ -48,11 +48,14 @@ enum { U_FUEL_GATE = 1, U_LOSS_TYPE = 2, U_BETA = 4, U_ARRIVE = 8 };
  * r = 0..3) belongs whole to the r-th env of the quad, in env order, whose gate
  * fired with cargo > 0: word 0 the loss type, words 1-3 the Beta(2, 2) uniforms.
  * The explicit reset and the synthetic agent draw one block per env. */
-enum { SLOT_FUEL = 0, SLOT_LOSS0 = 1, SLOT_LOSS1 = 2, SLOT_ARRIVE = 3, SLOT_RESET = 4,
+enum { SLOT_FUEL = 0, SLOT_LOSS0 = 1, SLOT_LOSS1 = 2, SLOT_ARRIVE = 3, SLOT_RESET0 = 4,
        SLOT_EXPLICIT_RESET = 5, SLOT_ACTION = 6, SLOT_GATE = 7, SLOT_LOSS2 = 8, SLOT_LOSS3 = 9,
-       SLOT_RESET_DEST = 10, SLOT_SAMPLE = 11, SLOT_ROLLOUT = 12, SLOT_ROLLOUT_B = 13,
-       SLOT_REPLAY = 15 };
+       SLOT_RESET1 = 10, SLOT_SAMPLE = 11, SLOT_ROLLOUT = 12, SLOT_ROLLOUT_B = 13,
+       SLOT_REPLAY = 15, SLOT_RESET2 = 16, SLOT_RESET3 = 17 };
 static const uint32_t LOSS_SLOT[4] = {SLOT_LOSS0, SLOT_LOSS1, SLOT_LOSS2, SLOT_LOSS3};
+/* RESET_r (slots 4, 10, 16, 17): the r-th env of the quad auto-reset in step t takes
+ * the whole block: word 0 the origin, word 1 the destination */
+static const uint32_t RESET_SLOT[4] = {SLOT_RESET0, SLOT_RESET1, SLOT_RESET2, SLOT_RESET3};
 
 /* sample_action results where the reference raises / never returns (include/shipenv.h) */
 enum { SAMPLE_RAISES = -1, SAMPLE_NO_OTHER_PORT = -2 };
@@ -440,17 +443,26 @@ int orc_step_batch_autoreset(const orc_world* w, int64_t n, const int32_t* actio
     if (w->P < 2) return -1;
     orc_step_batch(w, n, 0, NULL, actions, NULL, NULL, seed, env_id_base, t, x, y, fuel, cargo,
                    origin, dest, reward, done, err);
+    int64_t quad = -1;
+    int32_t resets = 0; /* envs of the current quad reset so far (RESET_r rank) */
     for (int64_t i = 0; i < n; ++i) {
         float rf = (float)reward[i];
         ep_return[i] += rf;
         ep_len[i] += 1;
+        const int64_t e = env_id_base + i;
+        if ((e >> 2) != quad) {
+            quad = e >> 2;
+            resets = 0;
+        }
         if (done[i]) {
             stats[0] += (double)ep_return[i];
             stats[1] += 1.0;
             stats[2] += (double)ep_len[i];
             ship s;
-            const int64_t e = env_id_base + i; /* quad blocks RESET and RESET_DEST */
-            reset_words(w, &s, quad_word(seed, e, t, SLOT_RESET), quad_word(seed, e, t, SLOT_RESET_DEST));
+            uint32_t o[4];
+            draw4(seed, quad, t, RESET_SLOT[resets & 3], o);
+            resets += 1;
+            reset_words(w, &s, o[0], o[1]);
             store(&s, i, x, y, fuel, cargo, origin, dest);
             ep_return[i] = 0.0f;
             ep_len[i] = 0;

@@ -13,7 +13,8 @@ namespace shipenv {
 
 // Step draws (contract v5) are keyed by the quad k = env / 4: quad blocks, where word
 // j belongs to env 4k+j (a 32-bit uniform u = w * 2^-32 or an integer draw), and the
-// LOSS_r blocks, which belong whole to the r-th env of the quad whose gate fired.
+// LOSS_r / RESET_r blocks, which belong whole to the r-th env of the quad whose gate
+// fired / that auto-resets.
 // The reset kernel and the synthetic agent draw one block per env.
 enum Slot : uint32_t {
     kSlotFuel = 0,           // u_fuel (fuel-cost noise, every step)
@@ -21,19 +22,27 @@ enum Slot : uint32_t {
     kSlotLoss1 = 2,          // of the quad whose gate fired takes the whole block: word 0
                              // u_type, words 1-3 the Beta(2,2) uniforms
     kSlotArrive = 3,         // new destination != origin on arrival
-    kSlotReset = 4,          // auto-reset inside step t: origin
+    kSlotReset = 4,          // RESET_r, r = 0..3 at slots 4, 10, 16, 17 (reset_slot(r)): the
+                             // r-th env of the quad auto-reset in step t: word 0 origin, 1 dest
     kSlotExplicitReset = 5,  // se_reset, per env, epoch in the t word: words 0 origin, 1 dest
     kSlotAction = 6,         // synthetic bench agent, per env
     kSlotGate = 7,           // u_gate (cargo-loss gate)
     kSlotLoss2 = 8,
     kSlotLoss3 = 9,
-    kSlotResetDest = 10,     // auto-reset inside step t: destination
+    kSlotReset1 = 10,
     kSlotSample = 11,        // se_sample_actions, per env: word 0
     kSlotRollout = 12,       // rollout attempt, per rollout: sample word, u_fuel, u_gate, u_type
     kSlotRolloutB = 13,      // rollout attempt (partial loss / arrival): 3 beta uniforms, dest
     kSlotPolicy = 14,        // se_policy, per env: explore draw, random.choice index
     kSlotReplay = 15,        // se_replay_sample, key (seed, 2^64 - 1), t = update: Feistel round keys
+    kSlotReset2 = 16,
+    kSlotReset3 = 17,
 };
+
+// RESET_r slot of the r-th auto-reset env of a quad
+__host__ __device__ constexpr uint32_t reset_slot(uint32_t r) {
+    return r == 0 ? kSlotReset : r == 1 ? kSlotReset1 : r == 2 ? kSlotReset2 : kSlotReset3;
+}
 
 // LOSS_r slot of the r-th firing env of a quad
 __host__ __device__ constexpr uint32_t loss_slot(uint32_t r) {

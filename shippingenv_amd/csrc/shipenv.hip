@@ -816,17 +816,38 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
             arrive |= (uint32_t)p[j].arrive << j;
             fin |= (uint32_t)((kFull || base + j < n) & p[j].dead) << j;
         }
-        // auto-reset (:227-243) of the envs that ran out of fuel, from the quad's
-        // RESET blocks: their position and fuel now, cargo / origin / dest after the
-        // second half (whose reward the finished episode still collects)
+        // auto-reset (:227-243) of the envs that ran out of fuel: their position and
+        // fuel now, cargo / origin / dest after the second half (whose reward the
+        // finished episode still collects). Contract v5: the r-th finishing env of the
+        // quad takes block RESET_r (word 0 origin, word 1 destination), as LOSS_r.
         uint32_t reset_o = 0, reset_d = 0;  // reset origin / dest bytes of the 4 envs
         if constexpr (kAuto) {
             if (fin) {
-                const U4 o = draw(qk, t, kSlotReset), d = draw(qk, t, kSlotResetDest);
+                uint32_t ow[4], dw[4];
+                {
+                    const uint32_t rk[4] = {0u, fin & 1u, (uint32_t)__popc(fin & 3u), (uint32_t)__popc(fin & 7u)};
+                    U4 r = draw(qk, t, reset_slot(0));
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        ow[j] = r.v[0];
+                        dw[j] = r.v[1];
+                    }
+#pragma unroll
+                    for (uint32_t q = 1; q < 4; ++q) {
+                        if (__popc(fin) > q) {
+                            r = draw(qk, t, reset_slot(q));
+#pragma unroll
+                            for (int j = (int)q; j < 4; ++j) {
+                                ow[j] = rk[j] >= q ? r.v[0] : ow[j];
+                                dw[j] = rk[j] >= q ? r.v[1] : dw[j];
+                            }
+                        }
+                    }
+                }
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     Ship r;
-                    reset_ship(w, r, o.v[j], d.v[j]);
+                    reset_ship(w, r, ow[j], dw[j]);
                     reset_o |= (uint32_t)r.origin << (8 * j);
                     reset_d |= (uint32_t)r.dest << (8 * j);
                     const bool f = (fin >> j) & 1u;
