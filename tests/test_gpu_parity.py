@@ -371,3 +371,42 @@ def test_done_list_full_size_segments():
     assert got[1] == tot_eps and got[2] == tot_len
     np.testing.assert_allclose(got[0], tot_ret, rtol=1e-9)
     env.close()
+
+
+@pytest.mark.parametrize("auto", [False, True])
+def test_max_map_and_ports_vs_oracle(oracle_mod, auto):
+    """The largest world the ABI takes: a 256x256 map and 254 ports (SE_MAX_PORTS),
+    with repeated port cells (first port wins, environment.py:150-152). Its image
+    (~6 K dwords) exceeds the step kernel's unguarded staging rows, so the remainder
+    staging path and the byte prefix counts at their limits run; bit-exact against
+    the oracle for 300 steps with the synthetic agent (A = 4 + 254 + 250 actions)."""
+    O = oracle_mod
+    rng = np.random.default_rng(77)
+    water = (rng.random((256, 256)) < 0.6).astype(np.uint8)
+    cells = np.argwhere(water != 0)
+    pick = rng.choice(len(cells), size=240, replace=False)
+    ports = [[int(a), int(b)] for a, b in cells[pick]]
+    ports += ports[:14]  # 14 cells hold two ports each: 254 in total
+    n, seed = 6001, 99
+    env = VecEnv(n, seed=seed, water=water, ports=ports, auto_reset=auto)
+    assert env.P == 254
+    world, st = _oracle_pair(O, env)
+    env.reset()
+    O.reset(world, st, seed=seed, epoch=0)
+    stats = np.zeros(3)
+    for t in range(300):
+        acts = env.gen_actions(t)
+        ref = O.gen_actions(n, env.P, seed, 0, t)
+        assert np.array_equal(acts.cpu().numpy(), ref)
+        env.step(acts)
+        if auto:
+            O.step_autoreset(world, st, ref, seed=seed, t=t, stats=stats)
+        else:
+            O.step(world, st, actions=ref, seed=seed, t=t)
+        np.testing.assert_array_equal(env.reward.cpu().numpy(), st.reward.astype(np.float32))
+        np.testing.assert_array_equal(env.err.cpu().numpy().astype(np.int32), st.err)
+        if t % 50 == 49:
+            _assert_vs_oracle(env, st, f"t={t}")
+    # the TAKE_* / SELECT actions found ports (the O(1) lookup at 254 ports)
+    assert (st.err == 0).any()
+    env.close()
