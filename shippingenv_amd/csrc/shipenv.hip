@@ -298,9 +298,9 @@ __device__ __forceinline__ Pending env_begin(const LdsWorld& w, Ship& s, int e_i
     const int d_new = __mul24(cx - px, cx - px) + __mul24(cy - py, cy - py);
     const bool closer = d_old > d_new;
 
-    // --- SELECT_PORT (_select_port :265-271)
+    // --- SELECT_PORT (_select_port :265-271); an agent index always names a port in range
     const int e_same = s.origin == a ? SE_ERR_SAME_PORT : SE_ERR_OK;
-    const int e_sel = ((a < 0) | (a >= w.P)) ? SE_ERR_PORT_RANGE : e_same;
+    const int e_sel = (!kUnitMoves & ((a < 0) | (a >= w.P))) ? SE_ERR_PORT_RANGE : e_same;
     // --- TAKE_FUEL / TAKE_CARGO (:341-357)
     const int idx = w.port_at(s.x, s.y);
     const int sidx = idx < 0 ? 0 : idx;
@@ -313,7 +313,8 @@ __device__ __forceinline__ Pending env_begin(const LdsWorld& w, Ship& s, int e_i
 
     // Every ternary below has named values as arms: clang emits a nested or
     // computing arm as control flow, which becomes a divergent branch.
-    const int e4 = ((type == 3) | (type == 4)) ? e_take : SE_ERR_BAD_CATEGORY;  // :373-374
+    // :373-374; an agent index always decodes to a category in 1..4
+    const int e4 = (kUnitMoves | (type == 3) | (type == 4)) ? e_take : SE_ERR_BAD_CATEGORY;
     const int e3 = type == 2 ? e_sel : e4;
     const int e2 = type == 1 ? e_move : e3;
     const int e1 = w.P == 0 ? SE_ERR_NO_PORTS : e2;  // :360
