@@ -37,7 +37,7 @@
 #endif
 
 #ifndef SHIPENV_ABLATE
-#define SHIPENV_ABLATE 0  // 0 = the product; 1 = timing-only memory-traffic build (tools/ablate.sh)
+#define SHIPENV_ABLATE 0  // 0 = the product; 1 = timing-only memory-traffic build (tools/build_ablation.sh, tools/ablate_libs.sh)
 #endif
 
 using namespace shipenv;
@@ -728,7 +728,7 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
     const uint32_t t = A.t;
     Pending p[4];
 
-#if SHIPENV_ABLATE  // timing-only build (tools/ablate.sh): memory traffic, no logic or draws
+#if SHIPENV_ABLATE  // timing-only build (tools/build_ablation.sh, tools/ablate_libs.sh): memory traffic, no logic or draws
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         s[j].x ^= ty[j] & 1;
@@ -997,12 +997,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
             if (k == 0) TRACE_STAMP(2);
             if (k + 1 < A.iters && g + kStepBlock < full) G.template load<true>(A, At<true>{g0 + kStepBlock, 0, A.n});
         }
-#ifndef SHIPENV_NOCOMPACT
         // done-list segment of this (iteration, wave): 64 groups, in env order
         if constexpr (kAuto) wave_compact(A, F, g * 4, __builtin_amdgcn_readfirstlane((int32_t)(g >> 6)));
-#else
-        (void)F;
-#endif
     }
 
 #if SHIPENV_TRACE
