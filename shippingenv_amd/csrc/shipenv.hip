@@ -274,6 +274,12 @@ struct Pending {
 // firing gate then loses nothing, :180-181); replay keeps it because the reference
 // still draws the loss type there (:177) and replay tracks every draw. From cargo
 // 50 on the gate always fires (random() < 1 <= cargo/50).
+// u_fuel: replay, the tape's f64 uniform; production, the Philox word w as a double
+// (u = w * 2^-32), so 0.2 * u is one product with 0.2 * 2^-32: scaling by a power of
+// two is exact, so fl(w * fl(0.2) * 2^-32) == fl(fl(0.2) * u) bit for bit.
+constexpr double kFifthPerWord = 0x1.999999999999ap-35;  // fl(0.2) * 2^-32
+static_assert(kFifthPerWord * 4294967296.0 == 0.2, "0.2 * 2^-32 must be exact");
+
 template <bool kUnitMoves, bool kReplay>
 __device__ __forceinline__ Pending env_begin(const LdsWorld& w, Ship& s, int e_in, int type, int a,
                                              int b, double u_fuel, double u_gate, uint32_t gw) {
@@ -285,7 +291,8 @@ __device__ __forceinline__ Pending env_begin(const LdsWorld& w, Ship& s, int e_i
     const bool mv_ok = !no_dest & !oob;
     const int cx = mv_ok ? nx : s.x, cy = mv_ok ? ny : s.y;  // in-range cell for the lookups
     // fuel cost (:103-104): dist * (1 + uniform(-0.1, 0.1)), uniform = -0.1 + 0.2*u, unfused
-    const double scale = 1.0 + (-0.1 + 0.2 * u_fuel);
+    const double fifth_u = kReplay ? 0.2 * u_fuel : u_fuel * kFifthPerWord;
+    const double scale = 1.0 + (-0.1 + fifth_u);
     const double cost = kUnitMoves ? scale : int_sqrt_rn(big ? 1 : a * a + b * b) * scale;
     const bool out_of_fuel = s.fuel < cost;  // :288-290
     const bool ground = w.is_ground(cx, cy);  // :293: blocked (-5) or moved (-0.0001 then -1)
@@ -354,11 +361,20 @@ __device__ __forceinline__ Pending env_begin(const LdsWorld& w, Ship& s, int e_i
     return p;
 }
 
+// int(beta * cargo) (:195-197) for beta = m * 2^-32 (production: m the median word).
+// While m * cargo < 2^53 the f64 product is exact, and scaling by 2^-32 is too, so
+// the truncation is the high word of the 64-bit product: one v_mul_hi_u32 in place
+// of three conversions and a multiply. Larger cargo takes the f64 path.
+__device__ __forceinline__ int beta_part(uint32_t m, int cargo) {
+    const int hi = (int)__umulhi(m, (uint32_t)cargo);
+    const int f = (int)(((double)m * (1.0 / 4294967296.0)) * (double)cargo);
+    return cargo < (1 << 21) ? hi : f;
+}
+
 // Second half: cargo loss (_calculate_cargo_loss :169-200) of kind none / partial
-// (int(beta * cargo), :195-197) / total, then arrival (:325-337) with the redrawn
-// destination. Selects only.
-__device__ __forceinline__ void env_finish(Ship& s, Pending& p, int kind, double beta, int new_dest) {
-    const int part = (int)(beta * (double)s.cargo);
+// (part = int(beta * cargo), :195-197) / total, then arrival (:325-337) with the
+// redrawn destination. Selects only.
+__device__ __forceinline__ void env_finish(Ship& s, Pending& p, int kind, int part, int new_dest) {
     const int some = kind == kLossTotal ? s.cargo : part;
     const int loss = kind == kLossNone ? 0 : some;
     const double rl = p.r + (double)(-3 * loss);
@@ -781,7 +797,7 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
                 nd = tp->arrive_dest;
                 need = need || nd < 0;
             }
-            env_finish(s[j], p[j], kind, beta, nd);
+            env_finish(s[j], p[j], kind, (int)(beta * (double)s[j].cargo), nd);
             if (need) {  // ask the caller for the next variate; change nothing
                 s[j] = s0;
                 p[j].r = 0.0;
@@ -812,7 +828,7 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
         uint32_t fire = 0, arrive = 0, fin = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            p[j] = env_begin<!kTyped, false>(w, s[j], er[j], ty[j], va[j], vb[j], u32(fb.v[j]), 0.0, gb.v[j]);
+            p[j] = env_begin<!kTyped, false>(w, s[j], er[j], ty[j], va[j], vb[j], (double)fb.v[j], 0.0, gb.v[j]);
             fire |= (uint32_t)p[j].fires << j;
             arrive |= (uint32_t)p[j].arrive << j;
             fin |= (uint32_t)((kFull || base + j < n) & p[j].dead) << j;
@@ -908,10 +924,10 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
         int32_t epl[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            // median of the three words, then one exact conversion (monotone)
+            // beta = the median of the three words * 2^-32 (the conversion is monotone)
             const uint32_t lo = min(v1[j], v2[j]), hi = max(v1[j], v2[j]);
-            const double beta = u32(max(lo, min(hi, v3[j])));  // v_med3_u32
-            env_finish(s[j], p[j], kind[j], beta, pick_other(ab.v[j], w.P, s[j].dest));
+            const uint32_t med = max(lo, min(hi, v3[j]));  // v_med3_u32
+            env_finish(s[j], p[j], kind[j], beta_part(med, s[j].cargo), pick_other(ab.v[j], w.P, s[j].dest));
             rw[j] = (float)p[j].r;  // one rounding of the reference's f64 reward
             epr[j] = 0.0f;
             epl[j] = 0;
@@ -1069,10 +1085,10 @@ __global__ void probe_kernel(const uint32_t* world, WorldDims d, const int* in, 
     const int er = decode_agent(w.P, in[i], ty, va, vb);
     Ship s{in[i + 64], in[i + 128], (double)in[i + 192], in[i + 256], in[i + 320], in[i + 384]};
     asm volatile("; probe: begin" ::: "memory");
-    Pending p = env_begin<true, false>(w, s, er, ty, va, vb, u32((uint32_t)in[i + 448]), 0.0,
+    Pending p = env_begin<true, false>(w, s, er, ty, va, vb, (double)(uint32_t)in[i + 448], 0.0,
                                        (uint32_t)in[i + 512]);
     asm volatile("; probe: finish" ::: "memory");
-    env_finish(s, p, in[i + 576], u32((uint32_t)in[i + 640]), in[i + 704]);
+    env_finish(s, p, in[i + 576], beta_part((uint32_t)in[i + 640], s.cargo), in[i + 704]);
     asm volatile("; probe: end" ::: "memory");
     out[i] = p.r + s.fuel + (double)(s.x + s.y + s.cargo + s.origin + s.dest + p.e + p.fires + p.arrive + p.dead);
 }
@@ -1361,19 +1377,19 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs A) {
                 status = SE_ROLL_RAISED;
                 break;
             }
-            Pending p = env_begin<true, false>(w, s, SE_ERR_OK, ty, va, vb, u32(d.v[1]), 0.0, d.v[2]);
+            Pending p = env_begin<true, false>(w, s, SE_ERR_OK, ty, va, vb, (double)d.v[1], 0.0, d.v[2]);
             if (p.e != SE_ERR_OK) continue;  // except Exception: continue (state untouched)
             const int total_kind = d.v[3] > kTypeHi ? kLossTotal : kLossPartial;
             const int kind = d.v[3] < kTypeLo ? kLossNone : total_kind;
-            double beta = 0.0;
+            uint32_t med = 0u;
             int nd = 0;
             if ((p.fires & (kind == kLossPartial)) | p.arrive) {
                 const U4 e = draw(key, (uint32_t)k, kSlotRolloutB);
                 const uint32_t lo = min(e.v[0], e.v[1]), hi = max(e.v[0], e.v[1]);
-                beta = u32(max(lo, min(hi, e.v[2])));
+                med = max(lo, min(hi, e.v[2]));
                 nd = pick_other(e.v[3], w.P, s.dest);
             }
-            env_finish(s, p, kind, beta, nd);
+            env_finish(s, p, kind, beta_part(med, s.cargo), nd);
             total += p.r;  // total_reward += reward (:229)
             steps += 1;
             if (p.dead) {
