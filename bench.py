@@ -440,7 +440,7 @@ def main():
         t4, src4 = pmc_traffic("step_kernel_auto_bytes_per_launch")
         out["config4"] = {
             "workload": "BASELINE configs[3]: N=2^20 envs/GPU, 64 random ports, auto-reset, "
-                        "ballot-compacted done list, per-block return reduction, RCCL all-reduce "
+                        "ballot-compacted done list (per-wave segments), per-wave return reduction, RCCL all-reduce "
                         "of the stats every 100 steps (inside the timed region)",
             "value": round(n * dist.world * args.steps / el4, 1),
             "ms_per_step": round(el4 / args.steps * 1e3, 5),
