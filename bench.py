@@ -8,7 +8,7 @@ path over one batch). Workload for `value`: BASELINE config 3 — N = 2^20 envs
 per GPU, full step (moves, cargo pickup/delivery, rewards), the reference's 5
 default ports, synthetic agent actions (90 % move, 5 % take cargo, 3 % take
 fuel, 2 % select; Philox-generated, resident in HBM before timing). Config 4
-(64 random ports, auto-reset with ballot-compacted done list and per-block
+(64 random ports, auto-reset with ballot-compacted done list and per-wave
 episode-return reduction, RCCL all-reduce of the stats) is measured in the same
 run and reported under "config4". Weak scaling: every rank owns 2^20 envs with
 global ids rank*2^20 + i.

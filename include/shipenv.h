@@ -278,7 +278,7 @@ int se_qtrain_destroy(se_qtrain* q);  /* destroy before the env it was created o
 
 /* Episode statistics accumulated by the auto-reset path since the last clear:
  * out[0] = sum of returns, out[1] = episodes, out[2] = sum of lengths (device
- * double[3]). Deterministic: per-block partials are summed in a fixed order. */
+ * double[3]). Deterministic: per-wave partials are summed in a fixed order. */
 int se_episode_stats(se_env* env, double* out, void* stream);
 int se_clear_stats(se_env* env, void* stream);
 

@@ -12,9 +12,10 @@
 //     per workgroup into LDS; the per-env map lookups are LDS reads;
 //   * RNG is counter-based Philox keyed by (seed, global env id): 0 bytes of RNG
 //     state in HBM and shard-invariant results;
-//   * auto-reset compacts finished envs into a done list with one wave ballot
-//     prefix and one atomic per wave, and reduces episode statistics per
-//     workgroup into a fixed slab (deterministic sums, no float atomics).
+//   * auto-reset compacts finished envs into a done list with a wave ballot
+//     prefix into per-(iteration, wave) segments (no atomics, no barrier), and
+//     reduces episode statistics per wave into a fixed slab (deterministic sums,
+//     no float atomics).
 //
 // Built with -ffp-contract=off: the reference's f64 arithmetic (CPython float,
 // np.sqrt) is unfused, and an FMA in -0.1 + 0.2*u changes fuel bits.
@@ -451,11 +452,11 @@ struct StepArgs {
     const int32_t* act_a;
     const int32_t* act_b;
     se_tape* tape;           // replay: variates in, used flags out
-    se_done_rec* done_recs;  // this step's done list: per-block segments of `seg` records
-    int32_t* done_count;     // this step's per-block record counts
+    se_done_rec* done_recs;  // this step's done list: per-(iteration, wave) segments of `seg` records
+    int32_t* done_count;     // this step's per-segment record counts
     int64_t seg;             // segment stride (records) of one workgroup
     int64_t iters;           // groups per thread (each workgroup owns iters * 256 groups)
-    double* slab;            // per-block {sum_ret, n_eps, sum_len, pad}
+    double* slab;            // per-wave {sum_ret, n_eps, sum_len, pad}
 };
 
 // Field access for the 4 envs of one group. Full groups: the pointer advanced to
