@@ -344,14 +344,18 @@ def test_shard_invariance(oracle_mod):
     part.close()
 
 
-def test_done_list_full_size_segments():
+@pytest.mark.parametrize("blocks", [None, "64"])
+def test_done_list_full_size_segments(monkeypatch, blocks):
     """N = 2^20 + 3 (tail group) with auto-reset: the compacted done list of every
     step lists exactly the envs that reported done, in env order, with the
-    returns / lengths the stats slab accumulates."""
+    returns / lengths the stats slab accumulates. blocks="64": 17 iterations per
+    thread, so 4,352 (iteration, wave) segments go through se_done_compact's scan."""
     from shippingenv_amd.vec import random_water_ports
 
     from conftest import golden_water
 
+    if blocks:
+        monkeypatch.setenv("SHIPENV_STEP_BLOCKS", blocks)
     n = (1 << 20) + 3
     env = VecEnv(n, seed=11, ports=random_water_ports(golden_water(), 64, seed=3), auto_reset=True)
     env.reset()
