@@ -23,6 +23,10 @@
 // LDS: the packed network (113 KB at P = 5) plus the world image, one 768-thread
 // workgroup (12 waves, 3 per SIMD) per CU for the whole launch.
 
+#ifndef SHIPENV_POLICY_ABL
+#define SHIPENV_POLICY_ABL 0  // timing-only ablations of the policy kernel (1: plain max epilogue, 2: no fc3)
+#endif
+
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -43,7 +47,8 @@ struct QnetDims {
     __host__ __device__ int b2() const { return b1() + 4 * kQHidden; }
     __host__ __device__ int b3() const { return b2() + 4 * kQHidden; }   // mt3 * 32 f32 (0 beyond A)
     __host__ __device__ int next() const { return b3() + mt3 * 128; }    // P int32: next port on the cell
-    __host__ __device__ int bytes() const { return (next() + 4 * P + 15) & ~15; }
+    __host__ __device__ int regm() const { return next() + 4 * P; }      // mt3 uint32: fc3 epilogue regs
+    __host__ __device__ int bytes() const { return (regm() + 4 * mt3 + 15) & ~15; }
 };
 
 QnetDims qnet_dims(int P) {
@@ -80,8 +85,8 @@ __global__ __launch_bounds__(256) void qnet_pack_kernel(PackArgs A) {
     const QnetDims q = A.q;
     const int in1 = q.in1();
     const int n_w1 = 4 * 64, n_w2 = 32 * 64, n_w3 = q.mt3 * 8 * 64;
-    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n_w1 + n_w2 + n_w3 + 2 * kQHidden + q.mt3 * 32 + q.P;
-         t += gridDim.x * blockDim.x) {
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x;
+         t < n_w1 + n_w2 + n_w3 + 2 * kQHidden + q.mt3 * 32 + q.P + q.mt3; t += gridDim.x * blockDim.x) {
         if (t < n_w1 + n_w2 + n_w3) {
             int f = t >> 6;
             const int lane = t & 63, r = lane & 31, h = lane >> 5;
@@ -123,12 +128,32 @@ __global__ __launch_bounds__(256) void qnet_pack_kernel(PackArgs A) {
             reinterpret_cast<float*>(A.img + q.b2())[u] = A.b2[u];
         } else if ((u -= kQHidden) < q.mt3 * 32) {
             reinterpret_cast<float*>(A.img + q.b3())[u] = u < q.A ? A.b3[u] : 0.0f;
-        } else {
-            u -= q.mt3 * 32;  // next port on the same cell, ascending (-1: none)
+        } else if ((u -= q.mt3 * 32) < P) {  // next port on the same cell, ascending (-1: none)
             int nx = -1;
             for (int p = u + 1; p < P && nx < 0; ++p)
                 if (pos[p] == pos[u]) nx = p;
             reinterpret_cast<int32_t*>(A.img + q.next())[u] = nx;
+        } else {
+            // fc3 tile mt = u - P: bit reg set when accumulator register reg (rows
+            // base + (reg & 3) + 8 (reg >> 2) + 4h, h = 0, 1) can hold a valid action of
+            // ANY env: a move or SELECT (row < 4 + P), or an amount within the largest
+            // stock (is_valid_action, dqn.py:125-175). The epilogue skips the others.
+            const int mt = u - P, base = mt * 32;
+            int cmax = 0, fmax = 0;
+            for (int p = 0; p < P; ++p) {
+                cmax = max(cmax, min((int)A.world[A.dims.pos() + 2 * P + p], 49));
+                fmax = max(fmax, min((int)A.world[A.dims.pos() + P + p], 199));
+            }
+            const int c_lo = 5 + P, c_hi = 4 + P + cmax, f_lo = 55 + P, f_hi = 54 + P + fmax;
+            uint32_t rm = 0;
+            for (int reg = 0; reg < 16; ++reg)
+                for (int h = 0; h < 2; ++h) {
+                    const int row = base + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                    const bool ok = row < q.A && (row < 4 + P || (row >= c_lo && row <= c_hi) ||
+                                                  (row >= f_lo && row <= f_hi));
+                    rm |= (uint32_t)ok << reg;
+                }
+            reinterpret_cast<uint32_t*>(A.img + q.regm())[mt] = rm;
         }
     }
 }
@@ -191,6 +216,7 @@ __global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
     const float* B2 = reinterpret_cast<const float*>(qb + q.b2());
     const float* B3 = reinterpret_cast<const float*>(qb + q.b3());
     const int32_t* NEXT = reinterpret_cast<const int32_t*>(qb + q.next());
+    const uint32_t* REGM = reinterpret_cast<const uint32_t*>(qb + q.regm());
 
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
     const int P = q.P;
@@ -267,7 +293,11 @@ __global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
         const int c_lo = 5 + P, c_hi = 4 + P + cst, f_lo = 55 + P, f_hi = 54 + P + fst;
         float best = -INFINITY;
         int bidx = 0x7fffffff;
+#if SHIPENV_POLICY_ABL == 2  // timing-only: no fc3
+        for (int mt = 0; mt < 0; ++mt) {
+#else
         for (int mt = 0; mt < q.mt3; ++mt) {  // fc3 + the masked first-maximum argmax
+#endif
             const int base = mt * 32, top = base + 31;
             // a tile no env of the wave can choose from is skipped, MFMAs included
             // (exact: its rows are invalid for all 32 envs); with port stocks <= 20
@@ -292,13 +322,23 @@ __global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
             for (int k = 0; k < 8; ++k)
                 c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k], h2[k >> 1][k & 1], c, 0, 0, 0);
             m >>= 4 * h;  // register reg holds row base + 4h + (reg & 3) + 8 (reg >> 2)
+#if SHIPENV_POLICY_ABL == 1  // timing-only: the epilogue without masks or indices
+            (void)m;
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) best = fmaxf(best, c[reg]);
+            bidx = base;
+#else
+            // registers that hold no valid action for any env are skipped (wave-uniform)
+            const uint32_t rm = __builtin_amdgcn_readfirstlane(REGM[mt]);
 #pragma unroll
             for (int reg = 0; reg < 16; ++reg) {
+                if (!((rm >> reg) & 1u)) continue;
                 const int i = (reg & 3) + 8 * (reg >> 2);
                 const bool better = ((m >> i) & 1u) && c[reg] > best;  // ascending rows: first max
                 best = better ? c[reg] : best;
                 bidx = better ? base + 4 * h + i : bidx;
             }
+#endif
             if (A.q_out && live) {
 #pragma unroll
                 for (int reg = 0; reg < 16; ++reg) {
