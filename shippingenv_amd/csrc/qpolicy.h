@@ -314,6 +314,8 @@ __global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
                     if (p != origin && i >= 0 && i < 32) m |= 1u << i;
                 }
             }
+            // registers that hold no valid action for any env are skipped (wave-uniform)
+            const uint32_t rm = __builtin_amdgcn_readfirstlane(REGM[mt]);
             bf16x8 wf[8];  // the tile's 8 fragments, read before the chain consumes them
 #pragma unroll
             for (int k = 0; k < 8; ++k) wf[k] = W3f[(mt * 8 + k) * 64 + lane];
@@ -328,8 +330,6 @@ __global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
             for (int reg = 0; reg < 16; ++reg) best = fmaxf(best, c[reg]);
             bidx = base;
 #else
-            // registers that hold no valid action for any env are skipped (wave-uniform)
-            const uint32_t rm = __builtin_amdgcn_readfirstlane(REGM[mt]);
 #pragma unroll
             for (int reg = 0; reg < 16; ++reg) {
                 if (!((rm >> reg) & 1u)) continue;
