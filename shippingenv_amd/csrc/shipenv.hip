@@ -38,7 +38,7 @@
 #endif
 
 #ifndef SHIPENV_ABLATE
-#define SHIPENV_ABLATE 0  // 0 = the product; 1 = timing-only memory-traffic build (tools/build_ablation.sh, tools/ablate_libs.sh)
+#define SHIPENV_ABLATE 0  // 0 = the product; 1 = timing-only memory-traffic build, 2 = also no staging (tools/build_ablation.sh, tools/ablate_libs.sh)
 #endif
 
 using namespace shipenv;
@@ -990,7 +990,11 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
     const int64_t first = (int64_t)blockIdx.x * A.iters * kStepBlock;  // block-uniform first group
 
     TRACE_STAMP(0);
+#if SHIPENV_ABLATE >= 2  // timing-only: no world staging either
+    (void)lds;
+#else
     const Staged st = stage_issue(A.world);
+#endif
     // first group: an unconditional load (lanes past the end re-read the last full
     // group; the host launches this kernel only when there is one), so the staging
     // writes below wait for exactly the image's loads
@@ -1000,7 +1004,11 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
         const uint32_t lane = last < (int64_t)threadIdx.x ? (uint32_t)(last < 0 ? 0 : last) : threadIdx.x;
         G.template load<true>(A, At<true>{last < 0 ? full - 1 : first, 0, A.n}, lane);
     }
+#if SHIPENV_ABLATE >= 2
+    const LdsWorld w = world_view(A.dims, A.world);
+#else
     const LdsWorld w = stage_finish(A.world, A.dims, lds, st);
+#endif
     TRACE_STAMP(1);
 
     BlockStats bs;

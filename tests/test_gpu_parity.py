@@ -414,3 +414,39 @@ def test_max_map_and_ports_vs_oracle(oracle_mod, auto):
     # the TAKE_* / SELECT actions found ports (the O(1) lookup at 254 ports)
     assert (st.err == 0).any()
     env.close()
+
+
+@pytest.mark.parametrize("auto", [False, True])
+def test_graph_captured_steps_equal_eager(auto):
+    """K se_step launches captured in one HIP graph (bench.py's config-3 timing path)
+    and replayed once leave every field bit-identical to K eager calls."""
+    from shippingenv_amd.vec import random_water_ports
+
+    from conftest import golden_water
+
+    n, K = 50003, 40
+    ports = random_water_ports(golden_water(), 64, seed=3) if auto else None
+    a = VecEnv(n, seed=21, ports=ports, auto_reset=auto)
+    b = VecEnv(n, seed=21, ports=ports, auto_reset=auto)
+    acts = torch.stack([a.gen_actions(t) for t in range(K)])
+    a.reset()
+    b.reset()
+    for t in range(K):
+        a.step(acts[t])
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(g, stream=side):
+            for t in range(K):
+                b.step(acts[t])
+    with torch.cuda.stream(side):
+        g.replay()
+    torch.cuda.synchronize()
+    fa, fb = get_state(a), get_state(b)
+    for f in FIELDS:
+        np.testing.assert_array_equal(fa[f], fb[f], err_msg=f)
+    for f in ("reward", "done", "err", "ep_return", "ep_len"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    a.close()
+    b.close()

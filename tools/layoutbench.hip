@@ -5,6 +5,7 @@
 // K2: K1 + the per-workgroup LDS world staging (730 words) and barrier.
 // K3: x,y,origin,dest packed in one u32 "ship word" per env (16 B/lane).
 // Scalar variables only (no private arrays: hipcc promotes those to LDS).
+// Every kernel also has a nontemporal-store variant (the step kernel's stores).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -17,7 +18,21 @@ struct S {
     const uint32_t* world;
 };
 
-template <bool kStage>
+template <typename T>
+__device__ __forceinline__ void st(T* p, T v, bool nt) {
+    if (nt) {
+        if constexpr (sizeof(T) == 16) {
+            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(__builtin_bit_cast(u4, v), reinterpret_cast<u4*>(p));
+        } else {
+            __builtin_nontemporal_store(v, p);
+        }
+    } else {
+        *p = v;
+    }
+}
+
+template <bool kStage, bool kNt>
 __global__ __launch_bounds__(256) void k1(S s, int64_t groups) {
     extern __shared__ uint32_t lds[];
     int64_t g = blockIdx.x * 256ll + threadIdx.x;
@@ -36,19 +51,20 @@ __global__ __launch_bounds__(256) void k1(S s, int64_t groups) {
         c.x += a.z;
         f0.x -= 1.0;
         f1.y -= 1.0;
-        s.x[g] = x;
-        s.y[g] = y;
-        s.o[g] = o + 1;
-        s.d[g] = d + 1;
-        s.cargo[g] = c;
-        s.fuel[2 * g] = f0;
-        s.fuel[2 * g + 1] = f1;
-        s.reward[g] = make_float4((float)a.x, (float)a.y, (float)a.z, (float)a.w);
-        s.done[g] = x & 0x01010101u;
-        s.err[g] = y & 0x03030303u;
+        st(&s.x[g], x, kNt);
+        st(&s.y[g], y, kNt);
+        st(&s.o[g], o + 1, kNt);
+        st(&s.d[g], d + 1, kNt);
+        st(&s.cargo[g], c, kNt);
+        st(&s.fuel[2 * g], f0, kNt);
+        st(&s.fuel[2 * g + 1], f1, kNt);
+        st(&s.reward[g], make_float4((float)a.x, (float)a.y, (float)a.z, (float)a.w), kNt);
+        st(&s.done[g], x & 0x01010101u, kNt);
+        st(&s.err[g], y & 0x03030303u, kNt);
     }
 }
 
+template <bool kNt>
 __global__ __launch_bounds__(256) void k3(S s, int64_t groups) {
     for (int64_t g = blockIdx.x * 256ll + threadIdx.x; g < groups; g += (int64_t)gridDim.x * 256) {
         uint4 sh = ((uint4*)s.ship)[g];
@@ -59,13 +75,13 @@ __global__ __launch_bounds__(256) void k3(S s, int64_t groups) {
         c.x += a.z;
         f0.x -= 1.0;
         f1.y -= 1.0;
-        ((uint4*)s.ship)[g] = sh;
-        s.cargo[g] = c;
-        s.fuel[2 * g] = f0;
-        s.fuel[2 * g + 1] = f1;
-        s.reward[g] = make_float4((float)a.x, (float)a.y, (float)a.z, (float)a.w);
-        s.done[g] = sh.x & 0x01010101u;
-        s.err[g] = sh.y & 0x03030303u;
+        st(&((uint4*)s.ship)[g], sh, kNt);
+        st(&s.cargo[g], c, kNt);
+        st(&s.fuel[2 * g], f0, kNt);
+        st(&s.fuel[2 * g + 1], f1, kNt);
+        st(&s.reward[g], make_float4((float)a.x, (float)a.y, (float)a.z, (float)a.w), kNt);
+        st(&s.done[g], sh.x & 0x01010101u, kNt);
+        st(&s.err[g], sh.y & 0x03030303u, kNt);
     }
 }
 
@@ -103,12 +119,15 @@ int main() {
         const double bytes = 42.0 * n;
         const int reps = n > (1 << 20) ? 100 : 400;
         for (int blocks : {1024, 2048}) {
-            float t1 = time_it([&] { k1<false><<<blocks, 256, 0>>>(s, groups); }, reps);
-            float t2 = time_it([&] { k1<true><<<blocks, 256, 4096>>>(s, groups); }, reps);
-            float t3 = time_it([&] { k3<<<blocks, 256>>>(s, groups); }, reps);
+            float t1 = time_it([&] { k1<false, false><<<blocks, 256, 0>>>(s, groups); }, reps);
+            float t2 = time_it([&] { k1<true, false><<<blocks, 256, 4096>>>(s, groups); }, reps);
+            float t3 = time_it([&] { k3<false><<<blocks, 256>>>(s, groups); }, reps);
+            float t4 = time_it([&] { k1<false, true><<<blocks, 256, 0>>>(s, groups); }, reps);
+            float t5 = time_it([&] { k1<true, true><<<blocks, 256, 4096>>>(s, groups); }, reps);
+            float t6 = time_it([&] { k3<true><<<blocks, 256>>>(s, groups); }, reps);
             printf("{\"n\": %lld, \"blocks\": %d, \"k1_us\": %.2f, \"k1_lds_us\": %.2f, \"k3_ship_us\": %.2f, "
-                   "\"k1_GBps\": %.0f, \"k1_lds_GBps\": %.0f, \"k3_GBps\": %.0f}\n",
-                   (long long)n, blocks, t1, t2, t3, bytes / t1 / 1e3, bytes / t2 / 1e3, bytes / t3 / 1e3);
+                   "\"k1_nt_us\": %.2f, \"k1_lds_nt_us\": %.2f, \"k3_ship_nt_us\": %.2f, \"k1_nt_GBps\": %.0f}\n",
+                   (long long)n, blocks, t1, t2, t3, t4, t5, t6, bytes / t4 / 1e3);
         }
     }
     return 0;
