@@ -975,10 +975,10 @@ __device__ __forceinline__ void wave_compact(const StepArgs& A, const Finished& 
 }
 
 // Workgroup b owns the contiguous groups [b*iters*256, (b+1)*iters*256) (a group is
-// 4 consecutive envs, one lane per group per iteration), and wave w of it the
-// contiguous iters*64 groups from b*iters*256 + w*iters*64, 64 per iteration. Its
-// done-list segment (segment = b*4 + w) therefore follows env order, and the
-// concatenated segments are globally sorted. Every field of a group is one 4- or
+// 4 consecutive envs, one lane per group per iteration). In iteration k, wave w
+// steps the 64 groups from b*iters*256 + k*256 + w*64: its done-list segment
+// (segment = global group / 64) covers them in env order, so the concatenated
+// segments are globally sorted. Every field of a group is one 4- or
 // 16-byte lane access. The partial last group (n % 4 envs) is left to
 // step_tail_kernel, so this loop carries no guarded scalar path. The world image's
 // loads, then the first group's, are all in flight before the LDS writes; each
@@ -1052,9 +1052,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
 
 // The partial last group (n % 4 envs), launched after step_kernel on the same
 // stream when n % 4 != 0: one thread steps it with guarded scalar accesses. Its
-// envs are the last of workgroup b's range, so auto-reset appends their records
-// to b's segment after step_kernel's and adds their statistics to b's slab entry
-// (env order and a fixed summation order, as in the main kernel).
+// envs come last in env order, so auto-reset appends their records to the done
+// segment of group n/4 after step_kernel's and adds their statistics to the slab
+// entry of the wave that owns that group (env order and a fixed summation order,
+// as in the main kernel).
 template <bool kTyped, bool kReplay, bool kAuto>
 __global__ __launch_bounds__(64) void step_tail_kernel(StepArgs A) {
     extern __shared__ uint32_t lds[];
