@@ -37,6 +37,11 @@
 #define SHIPENV_TRACE 0  // 1 = diagnostic build: per-wave phase timestamps (tools/wave_trace.py)
 #endif
 
+#ifndef SHIPENV_ABL4
+// timing-only auto-reset ablations (bits): 1 reset words without Philox, 2 no done
+// list, 4 no episode statistics, 8 no auto-reset at all (tools/build_ablation.sh)
+#define SHIPENV_ABL4 0
+#endif
 #ifndef SHIPENV_ABLATE
 #define SHIPENV_ABLATE 0  // 0 = the product; 1 = timing-only memory-traffic build, 2 = also no staging (tools/build_ablation.sh, tools/ablate_libs.sh)
 #endif
@@ -375,19 +380,20 @@ __device__ __forceinline__ int beta_part(uint32_t m, int cargo) {
 // Second half: cargo loss (_calculate_cargo_loss :169-200) of kind none / partial
 // (part = int(beta * cargo), :195-197) / total, then arrival (:325-337) with the
 // redrawn destination. Selects only.
-__device__ __forceinline__ void env_finish(Ship& s, Pending& p, int kind, int part, int new_dest) {
+__device__ __forceinline__ void env_finish(Ship& s, Pending& p, int kind, int part, int new_dest,
+                                           bool fires, bool arrive) {
     const int some = kind == kLossTotal ? s.cargo : part;
     const int loss = kind == kLossNone ? 0 : some;
     const double rl = p.r + (double)(-3 * loss);
     const int kept = s.cargo - loss;
-    p.r = p.fires ? rl : p.r;
-    s.cargo = p.fires ? kept : s.cargo;
+    p.r = fires ? rl : p.r;
+    s.cargo = fires ? kept : s.cargo;
     const double ra = (p.r + (double)(2 * s.cargo)) + 10.0;
-    p.r = p.arrive ? ra : p.r;
-    s.cargo = p.arrive ? 0 : s.cargo;
+    p.r = arrive ? ra : p.r;
+    s.cargo = arrive ? 0 : s.cargo;
     const int dest = s.dest;
-    s.dest = p.arrive ? new_dest : dest;
-    s.origin = p.arrive ? dest : s.origin;
+    s.dest = arrive ? new_dest : dest;
+    s.origin = arrive ? dest : s.origin;
 }
 
 // utils/preprocessing.py:111-137 (moves N, E, S, W; Python wraps -4..-1), in
@@ -458,6 +464,20 @@ struct StepArgs {
     int64_t iters;           // groups per thread (each workgroup owns iters * 256 groups)
     double* slab;            // per-wave {sum_ret, n_eps, sum_len, pad}
 };
+
+// The kernel's StepArgs re-read from the kernarg segment where a late phase needs
+// them. The empty asm makes the compiler forget its SGPR copies, so pointers used
+// only after the Philox / select stretch (store_rest, the episode counters, the done
+// list, the slab) are fetched with s_load where they are used instead of staying
+// live in SGPRs across it (the config-4 kernel spilled 44 SGPRs to VGPR lanes:
+// ~135 v_writelane / v_readlane). StepArgs is the kernels' only argument, so it
+// starts the kernarg segment.
+typedef const __attribute__((address_space(4))) StepArgs* StepArgsK;
+__device__ __forceinline__ const StepArgs& late_args() {
+    StepArgsK p = (StepArgsK)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const StepArgs*)p;
+}
 
 // Field access for the 4 envs of one group. Full groups: the pointer advanced to
 // the block-uniform first group g0 stays scalar and the lane offset is
@@ -798,7 +818,7 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
                 nd = tp->arrive_dest;
                 need = need || nd < 0;
             }
-            env_finish(s[j], p[j], kind, (int)(beta * (double)s[j].cargo), nd);
+            env_finish(s[j], p[j], kind, (int)(beta * (double)s[j].cargo), nd, p[j].fires, p[j].arrive);
             if (need) {  // ask the caller for the next variate; change nothing
                 s[j] = s0;
                 p[j].r = 0.0;
@@ -834,6 +854,13 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
             arrive |= (uint32_t)p[j].arrive << j;
             fin |= (uint32_t)((kFull || base + j < n) & p[j].dead) << j;
         }
+#if SHIPENV_ABL4 & 8
+        fin = 0;
+#endif
+        // The per-env flags travel as these VGPR bit masks from here on: opaque to
+        // the compiler, so it does not keep 4 x 3 lane masks (SGPR pairs) live
+        // across the draw blocks below, which spilled them to VGPR lanes.
+        asm volatile("" : "+v"(fire), "+v"(arrive), "+v"(fin));
         // auto-reset (:227-243) of the envs that ran out of fuel: their position and
         // fuel now, cargo / origin / dest after the second half (whose reward the
         // finished episode still collects). Contract v5: the r-th finishing env of the
@@ -844,7 +871,11 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
                 uint32_t ow[4], dw[4];
                 {
                     const uint32_t rk[4] = {0u, fin & 1u, (uint32_t)__popc(fin & 3u), (uint32_t)__popc(fin & 7u)};
+#if SHIPENV_ABL4 & 1
+                    U4 r{{qk.e0 ^ t, qk.e0 + t, 0u, 0u}};
+#else
                     U4 r = draw(qk, t, reset_slot(0));
+#endif
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         ow[j] = r.v[0];
@@ -853,7 +884,11 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
 #pragma unroll
                     for (uint32_t q = 1; q < 4; ++q) {
                         if (__popc(fin) > q) {
+#if SHIPENV_ABL4 & 1
+                            r = U4{{r.v[1], r.v[0] * 3u, 0u, 0u}};
+#else
                             r = draw(qk, t, reset_slot(q));
+#endif
 #pragma unroll
                             for (int j = (int)q; j < 4; ++j) {
                                 ow[j] = rk[j] >= q ? r.v[0] : ow[j];
@@ -874,7 +909,7 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
                     s[j].fuel = f ? r.fuel : s[j].fuel;
                 }
             }
-            G.load_episode(A, at);
+            G.load_episode(late_args(), at);
         }
         store_moved(S, at, s, p);
 
@@ -928,7 +963,8 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
             // beta = the median of the three words * 2^-32 (the conversion is monotone)
             const uint32_t lo = min(v1[j], v2[j]), hi = max(v1[j], v2[j]);
             const uint32_t med = max(lo, min(hi, v3[j]));  // v_med3_u32
-            env_finish(s[j], p[j], kind[j], beta_part(med, s[j].cargo), pick_other(ab.v[j], w.P, s[j].dest));
+            env_finish(s[j], p[j], kind[j], beta_part(med, s[j].cargo), pick_other(ab.v[j], w.P, s[j].dest),
+                       (fire >> j) & 1u, (arrive >> j) & 1u);
             rw[j] = (float)p[j].r;  // one rounding of the reference's f64 reward
             epr[j] = 0.0f;
             epl[j] = 0;
@@ -936,7 +972,7 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
                 const bool f = (fin >> j) & 1u;
                 F.ret[j] = G.e[j] + rw[j];
                 F.len[j] = G.l[j] + 1;
-                if (f) {
+                if ((SHIPENV_ABL4 & 4) == 0 && f) {
                     bs.ret += (double)F.ret[j];
                     bs.eps += 1;
                     bs.len += F.len[j];
@@ -949,9 +985,59 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
             }
         }
         if constexpr (kAuto) F.mask = fin;
-        store_rest<kAuto>(S, at, s, rw, epr, epl);
+        store_rest<kAuto>(late_args().st, at, s, rw, epr, epl);
     }
 #endif
+}
+
+// Sum over the wave's 64 lanes in a fixed tree, so the result does not depend on
+// timing: within each row of 16 lanes, DPP exchanges with lane^1, lane^2, the
+// mirrored lane of the half row and of the row (every lane then holds its row's
+// sum; each exchange pairs two lanes symmetrically and f64 addition commutes, so
+// both hold identical bits), then the four row sums as (r0 + r1) + (r2 + r3).
+// No LDS round trips (a shuffle butterfly cost 36 ds_bpermute and 6 dependent
+// waits at the end of every wave).
+template <int kCtrl>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)b, kCtrl, 0xf, 0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), kCtrl, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+constexpr int kDppXor1 = 0xb1;        // quad_perm [1, 0, 3, 2]
+constexpr int kDppXor2 = 0x4e;        // quad_perm [2, 3, 0, 1]
+constexpr int kDppHalfMirror = 0x141; // row_half_mirror
+constexpr int kDppMirror = 0x140;     // row_mirror
+__device__ __forceinline__ double wave_sum(double v) {
+    v += dpp_f64<kDppXor1>(v);
+    v += dpp_f64<kDppXor2>(v);
+    v += dpp_f64<kDppHalfMirror>(v);
+    v += dpp_f64<kDppMirror>(v);
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    double r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, 16 * k);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), 16 * k);
+        r[k] = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+    }
+    return (r[0] + r[1]) + (r[2] + r[3]);
+}
+__device__ __forceinline__ int wave_sum_int(int v) {
+    v += __builtin_amdgcn_mov_dpp(v, kDppXor1, 0xf, 0xf, false);
+    v += __builtin_amdgcn_mov_dpp(v, kDppXor2, 0xf, 0xf, false);
+    v += __builtin_amdgcn_mov_dpp(v, kDppHalfMirror, 0xf, 0xf, false);
+    v += __builtin_amdgcn_mov_dpp(v, kDppMirror, 0xf, 0xf, false);
+    return (__builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16)) +
+           (__builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48));
+}
+
+// slab[i] += v without reading it back into the wave: the add runs in L2 and the
+// wave does not wait for it. Only this wave's lane 0 adds to its own entry during
+// a launch (step_tail_kernel adds in a later launch), so the order of additions is
+// fixed and the sums are deterministic.
+__device__ __forceinline__ void slab_add(double* p, double v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Done-list compaction of one iteration (auto-reset): no atomics, no LDS and no
@@ -1023,29 +1109,23 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
             if (k + 1 < A.iters && g + kStepBlock < full) G.template load<true>(A, At<true>{g0 + kStepBlock, 0, A.n});
         }
         // done-list segment of this (iteration, wave): 64 groups, in env order
-        if constexpr (kAuto) wave_compact(A, F, g * 4, __builtin_amdgcn_readfirstlane((int32_t)(g >> 6)));
+        if constexpr (kAuto && (SHIPENV_ABL4 & 2) == 0) wave_compact(late_args(), F, g * 4, __builtin_amdgcn_readfirstlane((int32_t)(g >> 6)));
     }
 
 #if SHIPENV_TRACE
     __builtin_amdgcn_s_waitcnt(0);  // stores acknowledged
     TRACE_STAMP(3);
 #endif
-    if (kAuto) {
-        // per-wave statistics: a fixed-order butterfly, one slab entry per segment
-        double ret = bs.ret, eps = (double)bs.eps, len = (double)bs.len;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            ret += __shfl_xor(ret, off);
-            eps += __shfl_xor(eps, off);
-            len += __shfl_xor(len, off);
-        }
-        if ((threadIdx.x & 63) == 0 && eps != 0.0) {
-            {
-                double* sl = A.slab + 4 * (blockIdx.x * (kStepBlock / 64) + (threadIdx.x >> 6));
-                sl[0] += ret;
-                sl[1] += eps;
-                sl[2] += len;
-            }
+    if (kAuto && (SHIPENV_ABL4 & 4) == 0) {
+        // per-wave statistics: a fixed-order tree (wave_sum), added to this wave's own
+        // slab entry
+        const double ret = wave_sum(bs.ret), len = wave_sum((double)bs.len);
+        const int eps = wave_sum_int(bs.eps);
+        if (eps != 0 && (threadIdx.x & 63) == 0) {
+            double* sl = late_args().slab + 4 * (blockIdx.x * (kStepBlock / 64) + (threadIdx.x >> 6));
+            slab_add(sl + 0, ret);
+            slab_add(sl + 1, (double)eps);
+            slab_add(sl + 2, len);
         }
     }
 }
@@ -1098,7 +1178,7 @@ __global__ void probe_kernel(const uint32_t* world, WorldDims d, const int* in, 
     Pending p = env_begin<true, false>(w, s, er, ty, va, vb, (double)(uint32_t)in[i + 448], 0.0,
                                        (uint32_t)in[i + 512]);
     asm volatile("; probe: finish" ::: "memory");
-    env_finish(s, p, in[i + 576], beta_part((uint32_t)in[i + 640], s.cargo), in[i + 704]);
+    env_finish(s, p, in[i + 576], beta_part((uint32_t)in[i + 640], s.cargo), in[i + 704], p.fires, p.arrive);
     asm volatile("; probe: end" ::: "memory");
     out[i] = p.r + s.fuel + (double)(s.x + s.y + s.cargo + s.origin + s.dest + p.e + p.fires + p.arrive + p.dead);
 }
@@ -1399,7 +1479,7 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs A) {
                 med = max(lo, min(hi, e.v[2]));
                 nd = pick_other(e.v[3], w.P, s.dest);
             }
-            env_finish(s, p, kind, beta_part(med, s.cargo), nd);
+            env_finish(s, p, kind, beta_part(med, s.cargo), nd, p.fires, p.arrive);
             total += p.r;  // total_reward += reward (:229)
             steps += 1;
             if (p.dead) {

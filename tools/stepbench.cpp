@@ -1,0 +1,177 @@
+// stepbench.cpp — K back-to-back se_step calls driven from C++ (tuning tool): the
+// step rate without the Python host path, for one or more library builds.
+//   hipcc -O2 -std=c++17 -o tools/stepbench tools/stepbench.cpp -ldl
+//   tools/stepbench [--n N] [--config 3|4] [--steps K] [--rows R] lib.so [lib2.so ...]
+// (--rows R: step t reads action row t % R, so R small keeps the actions cache-resident)
+// Config 3: the bundled map, the reference's 5 default ports; config 4: 64 ports on
+// water cells (any fixed set: this tool times, it does not check), auto-reset.
+// Prints one JSON line per library: us per step over K launches on a created
+// stream, bracketed by hipEvents (no per-launch events).
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../include/shipenv.h"
+
+#define CK(x)                                                              \
+    do {                                                                   \
+        hipError_t e_ = (x);                                               \
+        if (e_ != hipSuccess) {                                            \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));        \
+            exit(1);                                                       \
+        }                                                                  \
+    } while (0)
+
+struct Api {
+    decltype(&se_create) create;
+    decltype(&se_bind) bind;
+    decltype(&se_reset) reset;
+    decltype(&se_gen_actions) gen;
+    decltype(&se_step) step;
+    decltype(&se_done_layout) layout;
+    decltype(&se_destroy) destroy;
+    decltype(&se_map_from_jpeg) map;
+    decltype(&se_last_error) err;
+};
+
+template <typename F>
+static void sym(void* h, const char* name, F& f) {
+    f = (F)dlsym(h, name);
+    if (!f) {
+        fprintf(stderr, "missing %s\n", name);
+        exit(1);
+    }
+}
+
+static void* dev(size_t bytes) {
+    void* p = nullptr;
+    CK(hipMalloc(&p, bytes < 16 ? 16 : bytes));
+    CK(hipMemset(p, 0, bytes < 16 ? 16 : bytes));
+    return p;
+}
+
+int main(int argc, char** argv) {
+    int64_t n = 1 << 20;
+    int config = 3, steps = 1000, rows = 0;  // rows > 0: cycle through that many action rows
+    std::vector<std::string> libs;
+    for (int i = 1; i < argc; ++i) {
+        if (!strcmp(argv[i], "--n")) n = atoll(argv[++i]);
+        else if (!strcmp(argv[i], "--config")) config = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--steps")) steps = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--rows")) rows = atoi(argv[++i]);
+        else libs.push_back(argv[i]);
+    }
+    FILE* f = fopen("shippingenv_amd/data/mapa_mundi_binario.jpg", "rb");
+    if (!f) {
+        fprintf(stderr, "run from the repository root\n");
+        return 1;
+    }
+    std::vector<uint8_t> jpg;
+    for (int c; (c = fgetc(f)) != EOF;) jpg.push_back((uint8_t)c);
+    fclose(f);
+
+    for (const std::string& path : libs) {
+        void* h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            fprintf(stderr, "%s\n", dlerror());
+            return 1;
+        }
+        Api a;
+        sym(h, "se_create", a.create);
+        sym(h, "se_bind", a.bind);
+        sym(h, "se_reset", a.reset);
+        sym(h, "se_gen_actions", a.gen);
+        sym(h, "se_step", a.step);
+        sym(h, "se_done_layout", a.layout);
+        sym(h, "se_destroy", a.destroy);
+        sym(h, "se_map_from_jpeg", a.map);
+        sym(h, "se_last_error", a.err);
+#define SE(x)                                                   \
+        do {                                                    \
+            if ((x) != 0) {                                     \
+                fprintf(stderr, "%s: %s\n", #x, a.err());       \
+                return 1;                                       \
+            }                                                   \
+        } while (0)
+
+        std::vector<uint8_t> water(100 * 100);
+        SE(a.map(jpg.data(), jpg.size(), 100, 100, water.data()));
+        std::vector<int32_t> px, py, pf, pc;
+        if (config == 4) {
+            for (int c = 0; c < 100 * 100 && (int)px.size() < 64; c += 37)
+                if (water[c]) {
+                    px.push_back(c / 100);
+                    py.push_back(c % 100);
+                    pf.push_back(5 + (int)px.size() % 16);
+                    pc.push_back(20 - (int)px.size() % 16);
+                }
+        } else {
+            const int d[5][2] = {{41, 40}, {60, 22}, {78, 29}, {49, 72}, {62, 72}};
+            for (auto& p : d) {
+                px.push_back(p[0]);
+                py.push_back(p[1]);
+                pf.push_back(12);
+                pc.push_back(9);
+            }
+        }
+        se_env* env = nullptr;
+        SE(a.create(&env, 0, n, 0, 100, 100, water.data(), (int32_t)px.size(), px.data(), py.data(),
+                    pf.data(), pc.data(), 2026, config == 4 ? SE_FLAG_AUTO_RESET : 0));
+        se_state st{};
+        st.x = (uint8_t*)dev(n);
+        st.y = (uint8_t*)dev(n);
+        st.origin = (uint8_t*)dev(n);
+        st.dest = (uint8_t*)dev(n);
+        st.done = (uint8_t*)dev(n);
+        st.err = (int8_t*)dev(n);
+        st.fuel = (double*)dev(8 * n);
+        st.cargo = (int32_t*)dev(4 * n);
+        st.reward = (float*)dev(4 * n);
+        if (config == 4) {
+            int64_t stride = 0;
+            int32_t segs = 0;
+            SE(a.layout(env, &stride, &segs));
+            st.ep_return = (float*)dev(4 * n);
+            st.ep_len = (int32_t*)dev(4 * n);
+            st.done_recs = (se_done_rec*)dev(2 * (size_t)segs * stride * sizeof(se_done_rec));
+            st.done_count = (int32_t*)dev(2 * (size_t)segs * sizeof(int32_t));
+        }
+        SE(a.bind(env, &st));
+        hipStream_t s;
+        CK(hipStreamCreate(&s));
+        int32_t* acts = (int32_t*)dev((size_t)steps * n * 4);
+        for (int t = 0; t < steps; ++t) SE(a.gen(env, acts + (size_t)t * n, (uint32_t)t, s));
+        SE(a.reset(env, nullptr, s));
+        for (int t = 0; t < 20; ++t) SE(a.step(env, acts + (size_t)t * n, s));
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        CK(hipStreamSynchronize(s));
+        CK(hipEventRecord(e0, s));
+        const int r = rows > 0 && rows < steps ? rows : steps;
+        for (int t = 0; t < steps; ++t) SE(a.step(env, acts + (size_t)(t % r) * n, s));
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        const char* base = strrchr(path.c_str(), '/');
+        printf("{\"lib\": \"%s\", \"n\": %lld, \"config\": %d, \"steps\": %d, \"action_rows\": %d, "
+               "\"us_per_step\": %.3f}\n",
+               base ? base + 1 : path.c_str(), (long long)n, config, steps, r, 1000.0 * ms / steps);
+        fflush(stdout);
+        SE(a.destroy(env));
+        for (void* p : {(void*)st.x, (void*)st.y, (void*)st.origin, (void*)st.dest, (void*)st.done,
+                        (void*)st.err, (void*)st.fuel, (void*)st.cargo, (void*)st.reward,
+                        (void*)st.ep_return, (void*)st.ep_len, (void*)st.done_recs,
+                        (void*)st.done_count, (void*)acts})
+            if (p) CK(hipFree(p));
+        CK(hipStreamDestroy(s));
+    }
+    return 0;
+}
