@@ -1577,7 +1577,7 @@ int grid_for(int64_t items, int cap = kMaxBlocks) {
 }
 
 // Workgroup cap of the step kernel: each thread then walks ceil(groups / (cap*256))
-// groups with the next group's loads in flight while it computes the current one.
+// groups, loading the next group after storing the current one.
 int step_block_cap() {
     const char* v = getenv("SHIPENV_STEP_BLOCKS");
     const int c = v ? atoi(v) : 0;
