@@ -366,34 +366,61 @@ def pmc_traffic(key="step_kernel_bytes_per_launch"):
     return d.get(key), os.path.relpath(path, ROOT)
 
 
+def cpu_threads():
+    """Host threads for the threaded CPU leg: the job's CPU share (OMP_NUM_THREADS is
+    16 on the GPU box, whose nproc counts the whole machine), else the affinity set."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
 def cpu_baseline(n_workload, ports_seed, budget_s):
-    """The C restatement (oracle, Philox mode, 1 thread) on a bounded sample of the
-    same workload: 2^16 of the envs, as many whole steps as fit the budget."""
+    """The C restatement (oracle, Philox mode) on bounded samples of the same workload
+    (single-thread and over the host's cores, in the same run):
+      - 1 thread on 2^16 of the envs, as many whole steps as fit half the budget;
+      - T threads (cpu_threads()) on all n envs, each stepping a quad-aligned slice
+        (ctypes releases the GIL), as many whole steps as fit the other half.
+    The threaded figure is `value`; the single-thread one rides along."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from oracle import oracle as O
     from shippingenv_amd.maps import builtin_water
     from shippingenv_amd.vec import DEFAULT_PORTS, draw_port_stocks
 
-    n = min(n_workload, 1 << 16)
     water = builtin_water()
     pf, pc = draw_port_stocks(5, ports_seed)
     world = O.OracleWorld(water, [p[0] for p in DEFAULT_PORTS], [p[1] for p in DEFAULT_PORTS], pf, pc)
-    st = O.OracleState(n)
-    O.reset(world, st, seed=ports_seed, epoch=0)
-    acts = [O.gen_actions(n, 5, ports_seed, 0, t) for t in range(64)]
-    steps, spent, t = 0, 0.0, 0
-    while spent < budget_s:
-        t0 = time.perf_counter()
-        O.step(world, st, actions=acts[t % 64], seed=ports_seed, t=t)
-        spent += time.perf_counter() - t0
-        steps += 1
-        t += 1
+
+    def timed(n, threads, budget):
+        st = O.OracleState(n)
+        O.reset(world, st, seed=ports_seed, epoch=0)
+        acts = [O.gen_actions(n, 5, ports_seed, 0, t) for t in range(16)]
+        steps, spent = 0, 0.0
+        with ThreadPoolExecutor(threads) as pool:
+            while spent < budget:
+                t0 = time.perf_counter()
+                if threads == 1:
+                    O.step(world, st, actions=acts[steps % 16], seed=ports_seed, t=steps)
+                else:
+                    O.step_threaded(world, st, acts[steps % 16], pool, threads, seed=ports_seed, t=steps)
+                spent += time.perf_counter() - t0
+                steps += 1
+        return n * steps / spent, steps, spent
+
+    n1 = min(n_workload, 1 << 16)
+    v1, s1, t1 = timed(n1, 1, budget_s / 2)
+    threads = cpu_threads()
+    vt, st_, tt = timed(n_workload, threads, budget_s / 2)
     return {
-        "value": round(n * steps / spent, 1),
+        "value": round(vt, 1),
         "unit": "env-steps/s",
-        "cores": 1,
+        "cores": threads,
         "kind": "port",
-        "sample": f"oracle/shipenv_oracle.c (Philox mode, same action mix) on {n} envs x {steps} "
-                  f"steps ({spent:.1f} s, 1 thread); reference Python measured in the build "
+        "single_thread_value": round(v1, 1),
+        "sample": f"oracle/shipenv_oracle.c (Philox mode, same action mix): {threads} threads on "
+                  f"{n_workload} envs x {st_} steps ({tt:.1f} s); 1 thread on {n1} envs x {s1} steps "
+                  f"({t1:.1f} s) -> single_thread_value. Reference Python measured in the build "
                   "container: 1.0-1.2e5 env-steps/s on 1 core (BASELINE.md)",
     }
 

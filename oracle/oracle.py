@@ -126,6 +126,27 @@ def step(world, st, *, actions=None, act_type=None, act_a=None, act_b=None, tape
                          t, *st.fields(), _p(st.reward), _p(st.done), _p(st.err))
 
 
+def step_threaded(world, st, actions, pool, threads, *, seed, env_id_base=0, t=0):
+    """orc_step_batch (agent-index actions, Philox) over `threads` contiguous slices,
+    one per worker of `pool`. ctypes drops the GIL inside the call, so the slices run
+    in parallel; slice starts are multiples of 4 (a quad of envs shares its Philox
+    blocks), so the result equals one call over all n envs."""
+    n = st.n
+    per = max(4, (-(-n // threads) + 3) // 4 * 4)
+    a = np.ascontiguousarray(actions, np.int32)
+    L = lib()
+
+    def run(lo):
+        hi = min(n, lo + per)
+        sl = slice(lo, hi)
+        L.orc_step_batch(world.ref, hi - lo, 0, None, _p(a[sl]), None, None, seed, env_id_base + lo, t,
+                         _p(st.x[sl]), _p(st.y[sl]), _p(st.fuel[sl]), _p(st.cargo[sl]),
+                         _p(st.origin[sl]), _p(st.dest[sl]), _p(st.reward[sl]), _p(st.done[sl]),
+                         _p(st.err[sl]))
+
+    list(pool.map(run, range(0, n, per)))
+
+
 def step_autoreset(world, st, actions, *, seed, env_id_base=0, t=0, stats=None):
     stats = np.zeros(3, np.float64) if stats is None else stats
     a = np.ascontiguousarray(actions, np.int32)
