@@ -35,9 +35,14 @@ def init_from_env(backend=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal of the N-rank path on fewer GPUs (not for measurement):
+    # SHIPENV_SHARE_GPUS=1 maps local rank r to GPU r % device_count, and
+    # SHIPENV_DIST_BACKEND=gloo replaces RCCL, which refuses two ranks on one GPU.
+    backend = backend or os.environ.get("SHIPENV_DIST_BACKEND") or None
     if torch.cuda.is_available():
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        dev = local % torch.cuda.device_count() if os.environ.get("SHIPENV_SHARE_GPUS") == "1" else local
+        torch.cuda.set_device(dev)
+        device = torch.device("cuda", dev)
     else:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
