@@ -118,27 +118,28 @@ __device__ __forceinline__ void store_relu(float* dst, int tile, const f32x16& a
     }
 }
 
-// sum over the 128 threads of a workgroup in a fixed tree order (all threads get it)
-__device__ __forceinline__ float block_sum128(float x, float* red) {
-    const int t = threadIdx.x;
-    red[t] = x;
-    __syncthreads();
+// Sum over a wave in a fixed butterfly of __shfl_xor: lane i and lane i^m add the same
+// two values, so every lane ends with the same bits.
+__device__ __forceinline__ float wave_sum_f32(float x) {
 #pragma unroll
-    for (int s = 64; s > 0; s >>= 1) {
-        if (t < s) red[t] += red[t + s];
-        __syncthreads();
-    }
-    const float r = red[0];
-    __syncthreads();
-    return r;
+    for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m);
+    return x;
 }
 
-// fc1 row f's port block folded into its bias: thread t sums the columns c = 6 + t,
-// 6 + t + 128, ... in order, then the fixed tree. The pack and the Adam kernel share it.
+// fc1 row f's port block folded into its bias: thread t < 128 sums the columns c = 6 + t,
+// 6 + t + 128, ... in order, then waves 0 and 1 each reduce (wave_sum_f32) and the
+// result is w0 + w1. Called by every thread of a 128- or 256-thread workgroup, so the
+// pack and the Adam kernel compute identical bits. `red` holds 2 floats.
 __device__ __forceinline__ float fold_row(const float* w1row, int in, const float* portvec, float* red) {
     float x = 0.0f;
-    for (int c = 6 + (int)threadIdx.x; c < in; c += kQABlock) x += w1row[c] * portvec[c - 6];
-    return block_sum128(x, red);
+    if (threadIdx.x < kQABlock)
+        for (int c = 6 + (int)threadIdx.x; c < in; c += kQABlock) x += w1row[c] * portvec[c - 6];
+    x = wave_sum_f32(x);
+    if ((threadIdx.x & 63) == 0 && threadIdx.x < kQABlock) red[threadIdx.x >> 6] = x;
+    __syncthreads();
+    const float r = red[0] + red[1];
+    __syncthreads();
+    return r;
 }
 
 __device__ __forceinline__ int frag_index(int row, int k) {  // [row tile][k step][lane]
@@ -442,26 +443,38 @@ struct AdamStep {
     }
 };
 
-// sum over the 256 threads of a workgroup in a fixed tree order (all threads get it)
-__device__ __forceinline__ float block_sum256(float x, float* red) {
-    const int t = threadIdx.x;
-    red[t] = x;
+// Sums over the 256 threads of a workgroup in a fixed order, so every launch (eager or
+// graph replay) gives the same bits: a butterfly of __shfl_xor within each wave (lane i
+// and lane i^m add the same two values, so the lanes stay identical), then the four
+// wave sums as (w0 + w1) + (w2 + w3) through LDS behind one barrier. K values reduce
+// side by side behind that one barrier: the W1 blocks' seven sums used to take seven
+// tree reductions of nine barriers each. `red` holds 4 * K floats.
+template <int K>
+__device__ __forceinline__ void block_sum(float (&x)[K], float* red) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) x[k] = wave_sum_f32(x[k]);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int k = 0; k < K; ++k) red[w * K + k] = x[k];
     __syncthreads();
 #pragma unroll
-    for (int s = 128; s > 0; s >>= 1) {
-        if (t < s) red[t] += red[t + s];
-        __syncthreads();
-    }
-    const float r = red[0];
-    __syncthreads();
-    return r;
+    for (int k = 0; k < K; ++k) x[k] = (red[k] + red[K + k]) + (red[2 * K + k] + red[3 * K + k]);
+    __syncthreads();  // red may be reused
+}
+
+__device__ __forceinline__ float block_sum256(float x, float* red) {
+    float v[1] = {x};
+    block_sum<1>(v, red);
+    return v[0];
 }
 
 // sum over the tiles of 64 consecutive floats (src + t * stride + e0): thread (grp, q) adds
 // float4 q of tiles grp, grp + 16, ... (skipping tiles without `bit` in present[] when
-// present is given), then a fixed tree over the 16 groups. Threads 0..15 return float4 q.
-__device__ __forceinline__ float4 tile_sum64(const float* src, int64_t stride, int64_t e0, int64_t tiles,
-                                             const uint32_t* present, uint32_t bit, float4* red) {
+// present is given); the 16 groups then combine in a fixed order (xor 16 and 32 inside a
+// wave, then the four waves). Thread t < 64 returns element t of the 64.
+__device__ __forceinline__ float tile_sum64(const float* src, int64_t stride, int64_t e0, int64_t tiles,
+                                            const uint32_t* present, uint32_t bit, float4* red) {
     const int t = threadIdx.x, q = t & 15, grp = t >> 4;
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     for (int64_t k0 = grp; k0 < tiles; k0 += 16 * 8) {  // 8 tiles per round, loads independent
@@ -484,21 +497,22 @@ __device__ __forceinline__ float4 tile_sum64(const float* src, int64_t stride, i
             acc.w += v[i].w;
         }
     }
-    red[t] = acc;
-    __syncthreads();
 #pragma unroll
-    for (int s = 8; s > 0; s >>= 1) {
-        if (grp < s) {
-            const float4 o = red[t + 16 * s];
-            red[t].x += o.x;
-            red[t].y += o.y;
-            red[t].z += o.z;
-            red[t].w += o.w;
-        }
-        __syncthreads();
+    for (int m = 16; m <= 32; m <<= 1) {
+        acc.x += __shfl_xor(acc.x, m);
+        acc.y += __shfl_xor(acc.y, m);
+        acc.z += __shfl_xor(acc.z, m);
+        acc.w += __shfl_xor(acc.w, m);
     }
-    const float4 r = red[q];
+    if ((t & 63) < 16) red[(t >> 6) * 16 + q] = acc;
     __syncthreads();
+    float r = 0.0f;
+    if (t < 64) {
+        const int j = t >> 2, c = t & 3;
+        const float* f = reinterpret_cast<const float*>(red);
+        r = (f[4 * j + c] + f[4 * (16 + j) + c]) + (f[4 * (32 + j) + c] + f[4 * (48 + j) + c]);
+    }
+    __syncthreads();  // red may be reused
     return r;
 }
 
@@ -526,11 +540,10 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             for (int c = 0; c < 6; ++c) x[c] += p[c];
             x[6] += A.W.part_b1[t * 128 + f];
         }
+        block_sum<7>(x, red);
+        if (tid == 0)  // every thread holds the sums; the row loop below indexes them by column
 #pragma unroll
-        for (int c = 0; c < 7; ++c) {
-            const float v = block_sum256(x[c], red);
-            if (tid == 0) sums[c] = v;
-        }
+            for (int c = 0; c < 7; ++c) sums[c] = x[c];
         __syncthreads();
         const float s1 = sums[6];
         float* w1row = A.on.w1 + (int64_t)f * in;
@@ -545,19 +558,8 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         __syncthreads();  // the new row and b1 are complete before the fold reads them
         const float b1 = sums[7];
         if (tid == 0) A.on.b1[f] = b1;
-        if (tid < kQABlock) {
-            float xf = 0.0f;  // fold_row's order (the pack kernel's), on the first 128 threads
-            for (int c = 6 + tid; c < in; c += kQABlock) xf += w1row[c] * A.W.portvec[c - 6];
-            red[tid] = xf;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int s = 64; s > 0; s >>= 1) {
-            if (tid < s) red[tid] += red[tid + s];
-            __syncthreads();
-        }
-        if (tid == 0) A.W.c1[0][f] = b1 + red[0];
-        __syncthreads();
+        const float xf = fold_row(w1row, in, A.W.portvec, red);  // the pack kernel's bits
+        if (tid == 0) A.W.c1[0][f] = b1 + xf;
         if (f == 0) {  // the loss: sum w d^2 / sum w
             float l = 0.0f;
             for (int64_t t = tid; t < A.tiles; t += kQRBlock) l += A.W.part_lw[2 * t];
@@ -566,10 +568,9 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         }
     } else if (b < 384) {  // W2 elements e0 .. e0 + 63 (row-major [f2][f1])
         const int64_t e0 = (int64_t)(b - 128) * 64;
-        tile_sum64(A.W.part_w2, 128 * 128, e0, A.tiles, nullptr, 0, red4);
+        const float g = tile_sum64(A.W.part_w2, 128 * 128, e0, A.tiles, nullptr, 0, red4);
         if (tid < 64) {
             const int e = (int)e0 + tid, f2 = e >> 7, f1 = e & 127;
-            const float g = comp(red4[tid >> 2], tid & 3);
             const float p = adam(A.on.w2[e], g * inv, A.m.w2[e], A.v.w2[e]);
             A.on.w2[e] = p;
             A.W.pw2[0][frag_index(f2, f1)] = p;
@@ -586,12 +587,11 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         const int k = b - 384, rt = k >> 6;
         const int64_t e0 = (int64_t)(k & 63) * 64;
         const uint32_t bit = 1u << rt;
-        tile_sum64(A.W.part_w3 + (int64_t)rt * 32 * 128, (int64_t)A.d.mt3 * 32 * 128, e0, A.tiles, A.W.present,
-                   bit, red4);
+        const float g = tile_sum64(A.W.part_w3 + (int64_t)rt * 32 * 128, (int64_t)A.d.mt3 * 32 * 128, e0,
+                                   A.tiles, A.W.present, bit, red4);
         if (tid < 64) {
             const int e = (int)e0 + tid, a = rt * 32 + (e >> 7), f = e & 127;
             if (a < A.d.A) {
-                const float g = comp(red4[tid >> 2], tid & 3);
                 const int64_t i = (int64_t)a * 128 + f;
                 A.on.w3[i] = adam(A.on.w3[i], g * inv, A.m.w3[i], A.v.w3[i]);
             }
