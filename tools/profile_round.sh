@@ -19,6 +19,9 @@ run() {  # name, timeout, rocprofv3 args..., -- program
 }
 cd /tmp
 rocprofv3 -L > "$OUT/counters_available.txt" 2>&1 || true
+run kt_bench 600 --kernel-trace --stats --output-format csv -d "$OUT" -o kt_bench -- python3 $R/bench.py --no-cpu &&
+rm -f "$OUT/kt_bench_kernel_trace.csv" &&
+grep '^{' "$OUT/kt_bench.log" > "$OUT/bench_under_rocprof.json" &&
 run kt_c3 240 --kernel-trace --stats --output-format csv -d "$OUT" -o kt_c3 -- $PY --config 3 --steps 200 &&
 run kt_c4 240 --kernel-trace --stats --output-format csv -d "$OUT" -o kt_c4 -- $PY --config 4 --steps 200 &&
 run kt_big 240 --kernel-trace --stats --output-format csv -d "$OUT" -o kt_big -- $PY --config 3 --n 16777216 --steps 40 &&

@@ -43,11 +43,14 @@ def main():
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     summary = {"tag": tag, "kernels": {}, "pmc": {}}
-    for name in ("kt_c3", "kt_c4", "kt_big", "kt_roll", "kt_pol", "kt_train"):
+    for name in ("kt_bench", "kt_c3", "kt_c4", "kt_big", "kt_roll", "kt_pol", "kt_train"):
         f = os.path.join(src, f"{name}_kernel_stats.csv")
         if os.path.exists(f):
             shutil.copy(f, os.path.join(dst, f"{name}_kernel_stats.csv"))
             summary["kernels"][name] = kstats(f)
+    b = os.path.join(src, "bench_under_rocprof.json")  # the bench's own line from the kt_bench run
+    if os.path.exists(b):
+        shutil.copy(b, os.path.join(dst, "bench_under_rocprof.json"))
     for name in ("fetch_c3", "write_c3", "fetch_big", "write_big", "fetch_c4", "write_c4", "sq_c3",
                  "sq2_c3"):
         summary["pmc"][name] = counters(os.path.join(src, f"pmc_{name}_counter_collection.csv"))
