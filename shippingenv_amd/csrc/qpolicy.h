@@ -444,12 +444,9 @@ int se_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, float* 
     if (env->n == 0) return SE_OK;
     DeviceGuard g(env->device);
     const size_t lds = (size_t)qn->q.bytes() + lds_bytes(env);
-    static bool attr_set = false;
-    if (!attr_set) {
-        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(policy_kernel),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr_set = true;
-    }
+    static std::atomic<uint64_t> lds_set{0};
+    rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(policy_kernel), 160 * 1024, env->device);
+    if (rc) return rc;
     if (lds > 160 * 1024) return fail(SE_EINVAL, "network + world image exceed the 160 KB LDS");
     int dev_cus = 256;
     if (hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, env->device) != hipSuccess)

@@ -727,12 +727,9 @@ int se_qtrain_step(se_qtrain* q, int64_t batch, const float* obs, const float* n
     const hipStream_t s = (hipStream_t)stream;
     const int64_t tiles = (batch + kQT - 1) / kQT;
     const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 5 * 32) * 4;
-    static bool attr_set = false;
-    if (!attr_set) {
-        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(qtrain_tile_kernel),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr_set = true;
-    }
+    static std::atomic<uint64_t> lds_set{0};
+    const int rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(qtrain_tile_kernel), (int)lds, q->device);
+    if (rc) return rc;
     QtStepArgs A{q->W, q->on, q->tg, q->d, batch, obs, next_obs, act, rew, done, weight, gamma};
     qtrain_tile_kernel<<<(unsigned)tiles, kQTBlock, lds, s>>>(A);
     HIP_TRY(hipGetLastError());

@@ -27,6 +27,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -1556,6 +1557,16 @@ int fail(int code, const std::string& msg) {
         if (e_ != hipSuccess)                                                                \
             return fail(SE_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));        \
     } while (0)
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) is per device: `done` holds, for one
+// kernel, a bit per device it has been set on (devices >= 64 set it on every call).
+int allow_dynamic_lds(std::atomic<uint64_t>& done, const void* kernel, int bytes, int device) {
+    const uint64_t bit = device >= 0 && device < 64 ? 1ull << device : 0ull;
+    if (bit && (done.load(std::memory_order_acquire) & bit)) return SE_OK;
+    HIP_TRY(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    done.fetch_or(bit, std::memory_order_acq_rel);
+    return SE_OK;
+}
 
 struct DeviceGuard {
     int prev = -1;
