@@ -1595,12 +1595,14 @@ int step_block_cap() {
     return c > 0 ? c : kStepBlocks;
 }
 
-// Nontemporal state loads when one step's traffic (~42-58 B per env) stays well
-// inside the 256 MiB Infinity Cache (measured: faster at N = 2^20, slower at 2^24).
+// Nontemporal state loads when one step's traffic (~42-58 B per env) stays
+// inside or near the 256 MiB Infinity Cache (measured on one box, forced on vs off:
+// 2% faster from 2^20 to 2^23 envs, equal for config 4 at 2^22, 15% slower at 2^24;
+// profiles/r01_v11/nt_sweep).
 bool step_nt_loads(const se_env* env) {
     const char* v = getenv("SHIPENV_NT_LOADS");
     if (v) return atoi(v) != 0;
-    return env->n * 64 <= (int64_t)128 << 20;
+    return env->n <= (int64_t)1 << 23;
 }
 
 size_t lds_bytes(const se_env* env) { return (size_t)env->dims.padded() * 4; }
