@@ -33,7 +33,13 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 constexpr int kQHidden = 128;     // DQNNetwork hidden_size (dqn.py:24, default 128)
-constexpr int kPolicyBlock = 768; // 12 waves (3 per SIMD, <= 170 VGPRs) share one LDS copy
+// 16 waves (4 per SIMD, <= 128 VGPRs, 28 B of scratch) share one LDS copy of the network.
+// Measured per launch at 2^20 envs: 512 threads 108.8 us, 768 (3 waves per SIMD, 165 VGPRs)
+// 92.5 us, 1024 87.2 us: the fourth wave covers the others' MFMA -> relu -> MFMA stalls.
+#ifndef SHIPENV_POLICY_BLOCK
+#define SHIPENV_POLICY_BLOCK 1024
+#endif
+constexpr int kPolicyBlock = SHIPENV_POLICY_BLOCK;
 constexpr int kPolicyWaves = kPolicyBlock / 64;
 
 // Packed network image (bytes). Fragments are 64 lanes x 8 bf16 = 1 KB.
