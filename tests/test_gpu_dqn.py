@@ -141,10 +141,14 @@ def _ref_adam(ref, lr, steps, exp_avg=None, exp_avg_sq=None):
 def _close_after_adam(got, want, lr, what):
     """Adam's first steps move a parameter by about lr * sign(g): a gradient element that
     cancels to near zero may flip sign under a different summation order. Allow rare
-    elements up to 2 lr apart; all others within f32 rounding."""
+    elements up to 2 lr apart; all others within f32 rounding. The share of such elements
+    is allowed up to 0.5%: torch's own update (the reference side) does not sum in a fixed
+    order from run to run on ROCm, and one full-suite run saw 36 of 16,384 W2 elements
+    (0.22%) apart by at most 3.9e-6 at step 3, with the same case passing on reruns. The
+    2.5 lr bound on every element is the guard against a wrong update."""
     d = (got - want).abs()
     far = d > 1e-6 + 1e-5 * want.abs()
-    assert far.float().mean().item() < 1e-3 and d.max().item() <= 2.5 * lr, (what, far.sum().item(), d.max().item())
+    assert far.float().mean().item() < 5e-3 and d.max().item() <= 2.5 * lr, (what, far.sum().item(), d.max().item())
 
 
 @pytest.mark.parametrize("n,ports64,batch", [(2048, False, 256), (4099, True, 300)])
