@@ -119,15 +119,15 @@ __global__ __launch_bounds__(256) void qnet_pack_kernel(PackArgs A) {
             continue;
         }
         int u = t - (n_w1 + n_w2 + n_w3);
-        const uint32_t* pos = A.world + A.dims.pos();
+        const LdsWorld wv = world_view(A.dims, A.world);  // the device image, read in place
+        const uint32_t* pos = wv.pos;
         const int P = q.P;
         if (u < kQHidden) {  // b1 + fc1 over the constant port block (x, y, fuel, cargo per port)
             double acc = (double)A.b1[u];
             for (int p = 0; p < P; ++p) {
                 const float* w = A.w1 + u * in1 + 6 + 4 * p;
-                acc += (double)w[0] * (double)(pos[p] & 0xffu) + (double)w[1] * (double)((pos[p] >> 8) & 0xffu) +
-                       (double)w[2] * (double)(int32_t)A.world[A.dims.pos() + P + p] +
-                       (double)w[3] * (double)(int32_t)A.world[A.dims.pos() + 2 * P + p];
+                acc += (double)w[0] * (double)wv.px(p) + (double)w[1] * (double)wv.py(p) +
+                       (double)w[2] * (double)wv.pfuel(p) + (double)w[3] * (double)wv.pcargo(p);
             }
             reinterpret_cast<float*>(A.img + q.b1())[u] = (float)acc;
         } else if ((u -= kQHidden) < kQHidden) {
@@ -147,8 +147,8 @@ __global__ __launch_bounds__(256) void qnet_pack_kernel(PackArgs A) {
             const int mt = u - P, base = mt * 32;
             int cmax = 0, fmax = 0;
             for (int p = 0; p < P; ++p) {
-                cmax = max(cmax, min((int)A.world[A.dims.pos() + 2 * P + p], 49));
-                fmax = max(fmax, min((int)A.world[A.dims.pos() + P + p], 199));
+                cmax = max(cmax, min(wv.pcargo(p), 49));
+                fmax = max(fmax, min(wv.pfuel(p), 199));
             }
             const int c_lo = 5 + P, c_hi = 4 + P + cmax, f_lo = 55 + P, f_hi = 54 + P + fmax;
             uint32_t rm = 0;
@@ -294,8 +294,8 @@ __global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
         // is_valid_action (dqn.py:125-175): moves always; SELECT p at the ship's cell
         // and != origin; TAKE_CARGO / TAKE_FUEL at a port with 0 < amount <= stock
         const int cur = w.port_at(x, y);
-        const int cst = cur >= 0 ? min(w.pcargo[max(cur, 0)], 49) : 0;
-        const int fst = cur >= 0 ? min(w.pfuel[max(cur, 0)], 199) : 0;
+        const int cst = cur >= 0 ? min(w.pcargo(max(cur, 0)), 49) : 0;
+        const int fst = cur >= 0 ? min(w.pfuel(max(cur, 0)), 199) : 0;
         const int c_lo = 5 + P, c_hi = 4 + P + cst, f_lo = 55 + P, f_hi = 54 + P + fst;
         float best = -INFINITY;
         int bidx = 0x7fffffff;

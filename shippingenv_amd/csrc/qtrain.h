@@ -161,13 +161,10 @@ __global__ __launch_bounds__(kQABlock) void qtrain_pack_kernel(QtPackArgs A) {
     __shared__ float red[kQABlock];
     __shared__ float port[4 * SE_MAX_PORTS];
     const int P = A.d.P, in = A.d.in;
+    const LdsWorld wv = world_view(A.wd, A.world);  // the device image, read in place
     for (int c = threadIdx.x; c < 4 * P; c += kQABlock) {
         const int p = c >> 2, f = c & 3;
-        const uint32_t pos = A.world[A.wd.pos() + p];
-        port[c] = f == 0 ? (float)(pos & 0xffu)
-                : f == 1 ? (float)((pos >> 8) & 0xffu)
-                : f == 2 ? (float)(int32_t)A.world[A.wd.pos() + P + p]
-                         : (float)(int32_t)A.world[A.wd.pos() + 2 * P + p];
+        port[c] = f == 0 ? (float)wv.px(p) : f == 1 ? (float)wv.py(p) : f == 2 ? (float)wv.pfuel(p) : (float)wv.pcargo(p);
         if (blockIdx.x == 0) A.W.portvec[c] = port[c];
     }
     __syncthreads();

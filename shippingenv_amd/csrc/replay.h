@@ -145,7 +145,7 @@ __device__ __forceinline__ float ship_col(uint32_t pos, float fuel, int c) {
 
 __device__ __forceinline__ float port_col(const LdsWorld& w, int c) {
     const int p = (c - 6) >> 2, f = (c - 6) & 3;
-    return f == 0 ? (float)w.px(p) : f == 1 ? (float)w.py(p) : f == 2 ? (float)w.pfuel[p] : (float)w.pcargo[p];
+    return f == 0 ? (float)w.px(p) : f == 1 ? (float)w.py(p) : f == 2 ? (float)w.pfuel(p) : (float)w.pcargo(p);
 }
 
 // kSampleRows transitions per workgroup: the first wave picks the slots, then all

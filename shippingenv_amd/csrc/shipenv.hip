@@ -70,147 +70,147 @@ constexpr double kMaxCargo = 50.0;
 
 // ------------------------------------------------------------------ world image
 // One device buffer of 32-bit words, staged as-is into LDS by every workgroup:
-//   [0, w)          ground bitmap  (bit = 1: np_game[x, y] == GROUND)
-//   [w, 2w)         port bitmap    (bit = 1: some port sits on the cell)
-//   [2w, 2w+w/4)    port-bit prefix counts, one byte per bitmap word (set bits in
-//                   the words before; at most P <= 254)
-//   [3w, 3w+P)      port position  (x | y << 8)
-//   [+P)            port fuel stock
-//   [+P)            port cargo stock
-//   [+P+1)          rank -> port: the FIRST port on the rank-th occupied cell
-//                   (_get_current_port_idx returns the first match, :150-152)
-//   [frac, +100)    f64 table fl(c / 50) for c in [0, 50) (8-byte aligned)
-//   [gate, +50)     u32 table floor(fl(c / 50) * 2^32): the gate on a Philox word
+//   [0, cw)         cell codes, one byte per cell c = x * W + y (x = map row, :65,
+//                   :293): 0 water, kCellGround ground (np_game[x, y] == GROUND),
+//                   k + 1 the FIRST port k on the cell (a port is never ground, :65;
+//                   _get_current_port_idx returns the first match, :150-152).
+//                   cw = H*W bytes rounded up to whole 16-byte units
+//   [pos, +P)       port position  x | y << 16 (the packed form of a ship position)
+//   [stk, +2P)      port stocks, (fuel, cargo) per port (8-byte aligned pairs)
+//   [gate, +51)     u32 table floor(fl(c / 50) * 2^32) for c in [0, 50), and
+//                   0xffffffff at 50: the gate on a Philox word (cargo >= 50 fires)
+//   [frac, +100)    f64 table fl(c / 50) for c in [0, 50) (8-byte aligned; replay)
 //   [rtab, +20)     f64 step rewards before cargo loss / arrival (8-byte aligned):
 //                   [0, 8) a move, index out_of_fuel*4 + ground*2 + closer, summed in
 //                   the reference's order (:288-315); [8] a take (0.05); [9] else 0
-// For the 100x100 map with 5 ports that is 4.5 KB.
-// kStepBlock-dword rows of the world image the step kernel stages unguarded: >= 1280
-// dwords, the 100x100 image with up to 98 ports (5 ports: ~900, 64 ports: ~1160)
-constexpr int kStageRows = (1280 + kStepBlock - 1) / kStepBlock;
+//   [moves, +4)     packed (dx, dy) of N, E, S, W (utils/preprocessing.py:126) as two
+//                   16-bit halves: v_pk_add_u16 moves a packed position
+// For the 100x100 map with 5 ports that is 10.8 KB: one byte lookup answers both
+// "is the target cell ground" (:293) and "which port is the ship on" (:145-153),
+// where bitmaps took a word read, bit arithmetic and a 3-read rank chain.
+constexpr int kCellGround = 255;
+// kStepBlock x 4-dword rows of the world image the step kernel stages unguarded
+// (one 16-byte load per thread and row): 3 rows = 12 KB hold the 100x100 image with
+// up to 130 ports
+constexpr int kStageRows = 3;
+constexpr int kStageWords = kStageRows * 4 * kStepBlock;
 
 struct WorldDims {
-    int32_t H, W, P, words;
-    __host__ __device__ int pos() const { return 2 * words + (words + 3) / 4; }
-    __host__ __device__ int rank2port() const { return pos() + 3 * P; }
-    __host__ __device__ int frac() const { return (rank2port() + P + 1 + 1) & ~1; }
-    __host__ __device__ int gate() const { return frac() + 2 * 50; }
-    __host__ __device__ int rtab() const { return (gate() + 50 + 1) & ~1; }
-    __host__ __device__ int total() const { return rtab() + 2 * 10; }
-    // device image / LDS size: whole kStepBlock-dword rows, at least the step
-    // kernel's unguarded staging window (kStageRows rows)
+    int32_t H, W, P, cw;  // cw: words of cell codes (a multiple of 4)
+    __host__ __device__ int pos() const { return cw; }
+    __host__ __device__ int stk() const { return (pos() + P + 1) & ~1; }
+    __host__ __device__ int gate() const { return stk() + 2 * P; }
+    __host__ __device__ int frac() const { return (gate() + 51 + 1) & ~1; }
+    __host__ __device__ int rtab() const { return frac() + 2 * 50; }
+    __host__ __device__ int moves() const { return rtab() + 2 * 10; }
+    __host__ __device__ int total() const { return moves() + 4; }
+    // device image / LDS size: whole 1024-dword rows, at least the step kernel's
+    // unguarded staging window
     __host__ __device__ int padded() const {
-        const int t = (total() + kStepBlock - 1) / kStepBlock * kStepBlock;
-        return t > kStepBlock * kStageRows ? t : kStepBlock * kStageRows;
+        const int t = (total() + 1023) / 1024 * 1024;
+        return t > kStageWords ? t : kStageWords;
     }
 };
 
 struct LdsWorld {
-    const uint32_t* ground;
-    const uint32_t* portbit;
-    const uint8_t* prefix;
+    const uint8_t* cell;
     const uint32_t* pos;
-    const int32_t* pfuel;
-    const int32_t* pcargo;
-    const int32_t* rank2port;
-    const double* frac;
+    const int2* stock;
     const uint32_t* gate_thr;
+    const double* frac;
     const double* rtab;
+    const uint32_t* moves;
     int32_t H, W, P;
 
     // cell index x * W + y: coordinates and W are below 256, so 24-bit multiplies
     // (full rate) are exact where a 32-bit one would be a 64-bit-product op
-    __device__ bool is_ground(int x, int y) const {
-        const uint32_t c = __umul24((uint32_t)x, (uint32_t)W) + (uint32_t)y;
-        return (ground[c >> 5] >> (c & 31)) & 1u;
+    __device__ int code(int x, int y) const { return cell[__umul24((uint32_t)x, (uint32_t)W) + (uint32_t)y]; }
+    __device__ bool is_ground(int x, int y) const { return code(x, y) == kCellGround; }
+    // _get_current_port_idx (:145-153): first port on the ship's cell, -1 if none
+    // (water 0 -> -1, ground 255 -> 254 >= P)
+    __device__ int port_at(int x, int y) const { return port_of_code(code(x, y)); }
+    __device__ int port_of_code(int c) const {
+        const int k = c - 1;
+        return (unsigned)k < (unsigned)P ? k : -1;
     }
-    // _get_current_port_idx (:145-153): first port on the ship's cell, -1 if none.
-    // O(1): rank of the cell among occupied cells -> first port index. The rank is
-    // at most P (rank2port has P + 1 entries), so the read is unconditional: no
-    // branch (and exec mask) around it.
-    __device__ int port_at(int x, int y) const {
-        const uint32_t c = __umul24((uint32_t)x, (uint32_t)W) + (uint32_t)y;
-        const uint32_t word = portbit[c >> 5], bit = c & 31;
-        const int rank = (int)prefix[c >> 5] + __popc(word & ((1u << bit) - 1u));
-        const int first = rank2port[rank];
-        return ((word >> bit) & 1u) ? first : -1;
-    }
-    __device__ int px(int i) const { return (int)(pos[i] & 0xffu); }
-    __device__ int py(int i) const { return (int)((pos[i] >> 8) & 0xffu); }
+    __device__ int px(int i) const { return (int)(pos[i] & 0xffffu); }
+    __device__ int py(int i) const { return (int)(pos[i] >> 16); }
+    __device__ int pfuel(int i) const { return stock[i].x; }
+    __device__ int pcargo(int i) const { return stock[i].y; }
     // normalize(cargo, 50, 0) (util.py:6-8), only read for 0 < cargo < 50
     __device__ double likelihood(int cargo) const { return frac[cargo]; }
 };
 
-// Staging in two halves. stage_issue puts every thread's share of the image in
-// flight at once (independent loads into registers); stage_finish writes it to LDS
-// and holds the barrier. A load -> wait -> ds_write loop would make each of the ~5
-// rounds a full L2 round trip behind whatever the wave loaded before it (its
-// s_waitcnt vmcnt(0) also waits for those). The step kernel issues its first
-// group's loads between the halves, so the image (first in the in-order vmcnt
-// queue) is written while the group's data is still on its way.
-struct Staged {
-    uint32_t r[kStageRows];
-};
-
-// The step kernel's half (kStepBlock threads): the image is padded to whole rows of at
-// least kStageRows (WorldDims::padded), so these loads need no guard and no branch.
-__device__ __forceinline__ Staged stage_issue(const uint32_t* __restrict__ g) {
-    Staged st;
-#pragma unroll
-    for (int k = 0; k < kStageRows; ++k) st.r[k] = g[threadIdx.x + kStepBlock * k];
-    return st;
-}
-
-__device__ __forceinline__ LdsWorld world_view(WorldDims d, const uint32_t* lds);
-
-__device__ __forceinline__ LdsWorld stage_finish(const uint32_t* __restrict__ g, WorldDims d,
-                                                 uint32_t* lds, const Staged& st) {
-#pragma unroll
-    for (int k = 0; k < kStageRows; ++k) lds[threadIdx.x + kStepBlock * k] = st.r[k];
-    for (int i = (int)threadIdx.x + kStepBlock * kStageRows; i < d.total(); i += kStepBlock)
-        lds[i] = g[i];  // larger maps / port tables: the remainder
-    __syncthreads();
-    return world_view(d, lds);
-}
-
-// Any block size (the other kernels): every thread's loads issued before any store.
-__device__ __forceinline__ LdsWorld stage_world(const uint32_t* __restrict__ g, WorldDims d,
-                                                uint32_t* lds) {
-    const int total = d.total();
-    constexpr int kR = 4;
-    for (int i0 = 0; i0 < total; i0 += kR * (int)blockDim.x) {
-        uint32_t r[kR];
-#pragma unroll
-        for (int k = 0; k < kR; ++k) {
-            const int i = i0 + (int)threadIdx.x + k * (int)blockDim.x;
-            r[k] = i < d.padded() ? g[i] : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < kR; ++k) {
-            const int i = i0 + (int)threadIdx.x + k * (int)blockDim.x;
-            if (i < d.padded()) lds[i] = r[k];
-        }
-    }
-    __syncthreads();
-    return world_view(d, lds);
-}
-
-__device__ __forceinline__ LdsWorld world_view(WorldDims d, const uint32_t* lds) {
+__host__ __device__ inline LdsWorld world_view(WorldDims d, const uint32_t* img) {
     LdsWorld w;
-    w.ground = lds;
-    w.portbit = lds + d.words;
-    w.prefix = reinterpret_cast<const uint8_t*>(lds + 2 * d.words);
-    w.pos = lds + d.pos();
-    w.pfuel = (const int32_t*)(lds + d.pos() + d.P);
-    w.pcargo = (const int32_t*)(lds + d.pos() + 2 * d.P);
-    w.rank2port = (const int32_t*)(lds + d.rank2port());
-    w.frac = (const double*)(lds + d.frac());
-    w.gate_thr = lds + d.gate();
-    w.rtab = (const double*)(lds + d.rtab());
+    w.cell = reinterpret_cast<const uint8_t*>(img);
+    w.pos = img + d.pos();
+    w.stock = reinterpret_cast<const int2*>(img + d.stk());
+    w.gate_thr = img + d.gate();
+    w.frac = reinterpret_cast<const double*>(img + d.frac());
+    w.rtab = reinterpret_cast<const double*>(img + d.rtab());
+    w.moves = img + d.moves();
     w.H = d.H;
     w.W = d.W;
     w.P = d.P;
     return w;
+}
+
+// Staging in two halves. stage_issue puts every thread's share of the image in
+// flight at once (independent 16-byte loads into registers); stage_finish writes it
+// to LDS and holds the barrier. A load -> wait -> ds_write loop would make each
+// round a full L2 round trip behind whatever the wave loaded before it (its
+// s_waitcnt vmcnt(0) also waits for those). The step kernel issues its first
+// group's loads between the halves, so the image (first in the in-order vmcnt
+// queue) is written while the group's data is still on its way.
+struct Staged {
+    uint4 r[kStageRows];
+};
+
+// The step kernel's half (kStepBlock threads): the image is padded to at least
+// kStageWords (WorldDims::padded), so these loads need no guard and no branch.
+__device__ __forceinline__ Staged stage_issue(const uint32_t* __restrict__ g) {
+    Staged st;
+    const uint4* g4 = reinterpret_cast<const uint4*>(g);
+#pragma unroll
+    for (int k = 0; k < kStageRows; ++k) st.r[k] = g4[threadIdx.x + kStepBlock * k];
+    return st;
+}
+
+__device__ __forceinline__ LdsWorld stage_finish(const uint32_t* __restrict__ g, WorldDims d,
+                                                 uint32_t* lds, const Staged& st) {
+    uint4* l4 = reinterpret_cast<uint4*>(lds);
+#pragma unroll
+    for (int k = 0; k < kStageRows; ++k) l4[threadIdx.x + kStepBlock * k] = st.r[k];
+    for (int i = (int)threadIdx.x + kStepBlock * kStageRows; i < (d.total() + 3) / 4; i += kStepBlock)
+        l4[i] = reinterpret_cast<const uint4*>(g)[i];  // larger maps / port tables: the remainder
+    __syncthreads();
+    return world_view(d, lds);
+}
+
+// Any block size (the other kernels): every thread's 16-byte loads issued before any
+// store (the image is padded to whole 1024-dword rows).
+__device__ __forceinline__ LdsWorld stage_world(const uint32_t* __restrict__ g, WorldDims d,
+                                                uint32_t* lds) {
+    const int total = (d.total() + 3) / 4;
+    const uint4* g4 = reinterpret_cast<const uint4*>(g);
+    uint4* l4 = reinterpret_cast<uint4*>(lds);
+    constexpr int kR = 4;
+    for (int i0 = 0; i0 < total; i0 += kR * (int)blockDim.x) {
+        uint4 r[kR];
+#pragma unroll
+        for (int k = 0; k < kR; ++k) {
+            const int i = i0 + (int)threadIdx.x + k * (int)blockDim.x;
+            if (i < total) r[k] = g4[i];
+        }
+#pragma unroll
+        for (int k = 0; k < kR; ++k) {
+            const int i = i0 + (int)threadIdx.x + k * (int)blockDim.x;
+            if (i < total) l4[i] = r[k];
+        }
+    }
+    __syncthreads();
+    return world_view(d, lds);
 }
 
 
@@ -318,8 +318,8 @@ __device__ __forceinline__ Pending env_begin(const LdsWorld& w, Ship& s, int e_i
     // --- TAKE_FUEL / TAKE_CARGO (:341-357)
     const int idx = w.port_at(s.x, s.y);
     const int sidx = idx < 0 ? 0 : idx;
-    const int cstock = w.pcargo[sidx], fstock = w.pfuel[sidx];
-    const int stock = type == 4 ? cstock : fstock;
+    const int2 st2 = w.stock[sidx];
+    const int stock = type == 4 ? st2.y : st2.x;
     const int e_amount = ((a <= 0) | (a > stock)) ? SE_ERR_AMOUNT : SE_ERR_OK;
     const int e_take = idx < 0 ? SE_ERR_NOT_AT_PORT : e_amount;
     const int e_oob = oob ? SE_ERR_OOB : SE_ERR_OK;
@@ -991,6 +991,304 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
 #endif
 }
 
+// ------------------------------------------------------------------ agent-index path
+// The production step for agent-index actions (se_step), written for VALU issue,
+// the bound at N = 2^20: the same semantics as env_begin +
+// env_finish with kUnitMoves (tests compare it bit for bit with the
+// oracle), in a packed form.
+//   * A ship position is one register x | y << 16: a move is one v_pk_add_u16 of
+//     the action's packed (dx, dy) from the world image, the bounds test one
+//     v_pk_min_u16 against (H-1, W-1), a cell index one v_dot2_u32_u16 with (W, 1),
+//     the squared distances of the closer/farther test (:307-315) one v_pk_sub_i16
+//     and one v_dot2_i32_i16 each, and the arrival test (:325) one compare.
+//   * One cell-code byte answers "ground?" for the target cell (:293) and "which
+//     port?" for the ship's cell (:145-153).
+//   * Fuel changes by one f64 add of a selected delta (-cost, +amount or -0.0, which
+//     leaves every fuel value as it is, -0.0 included).
+//   * Cargo loss and arrival arithmetic run inside the branches that draw their
+//     blocks, so waves without a firing gate / an arrival skip them.
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+typedef int16_t i16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
+}
+// squared euclidean distance of two packed positions (halves < 256)
+__device__ __forceinline__ int dist2(uint32_t a, uint32_t b) {
+    const i16x2 d = __builtin_bit_cast(i16x2, a) - __builtin_bit_cast(i16x2, b);
+    return __builtin_amdgcn_sdot2(d, d, 0, false);
+}
+// cell index x * W + y of a packed position; wh = W | 1 << 16
+__device__ __forceinline__ uint32_t cell_of(uint32_t p, uint32_t wh) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p), __builtin_bit_cast(u16x2, wh), 0u, false);
+}
+
+template <bool kAuto, bool kFull, bool kNt>
+__device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWorld& w,
+                                                 Group<false, kAuto, kNt>& G, At<kFull> at,
+                                                 BlockStats& bs, Finished& F) {
+    const int64_t n = A.n, base = at.base;
+    const int P = w.P;
+    const uint32_t lim = (uint32_t)(w.H - 1) | ((uint32_t)(w.W - 1) << 16);
+    const uint32_t wh = (uint32_t)w.W | (1u << 16);
+    const uint32_t pm1 = P > 0 ? (uint32_t)(P - 1) : 0u;  // clamp for table reads whose value an error discards
+    const Key qk = env_key(A.seed, (A.env_base + base) >> 2);
+    const uint32_t t = A.t;
+
+    // --- first half: everything that needs no optional draw (:359-376, :273-315)
+    uint32_t pos[4], pd16[4];
+    int val[4], dst[4], cg[4], err[4], ridx[4];
+    bool do_move[4], moved[4], tf_ok[4];
+    bool gate_needed = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        // utils/preprocessing.py:111-137: [0,4) moves N, E, S, W (-4..-1 wrap like a
+        // Python index), [4, 4+P) SELECT, [4+P, 54+P) TAKE_CARGO, then TAKE_FUEL
+        const int act = G.a[j];
+        const bool bad = act < -4, is_mv = act < 4, lt_sel = act < 4 + P, lt_tc = act < 54 + P;
+        val[j] = act - 4 - (lt_sel ? 0 : P) - (lt_tc ? 0 : 50);
+        const uint32_t dxy = w.moves[act & 3];
+        // packed position x | y << 16 from the group's x and y bytes
+        const uint32_t p = __builtin_amdgcn_perm(G.y, G.x, (uint32_t)j | 0x0c000c00u | ((uint32_t)(4 + j) << 16));
+        dst[j] = byte_of(G.dst, j);
+        cg[j] = G.c[j];
+        // MOVE (_move_ship :273-339)
+        const uint32_t np = pk_add_u16(p, dxy);
+        const bool inb = pk_min_u16(np, lim) == np;  // _is_within_map (:284); -1 wraps to 0xffff
+        const bool nodest = dst[j] == SE_NONE;       // :276
+        const uint32_t cp = (!nodest & inb) ? np : p;  // in-range cell for the lookups
+        const bool ground = w.cell[cell_of(cp, wh)] == kCellGround;  // :293
+        pd16[j] = w.pos[min((uint32_t)dst[j], pm1)];
+        const bool closer = dist2(p, pd16[j]) > dist2(cp, pd16[j]);  // old vs ATTEMPTED cell (:307-315)
+        // TAKE_* (:341-357) at the port on the ship's cell; SELECT_PORT (:265-271)
+        const int k = (int)w.cell[cell_of(p, wh)] - 1;
+        const bool atport = (uint32_t)k < (uint32_t)P;
+        const int2 st2 = w.stock[min((uint32_t)k, pm1)];
+        const int stock = lt_tc ? st2.y : st2.x;
+        const bool amount_bad = (val[j] <= 0) | (val[j] > stock);
+        const bool same = byte_of(G.org, j) == val[j];
+        const int e_move = nodest ? SE_ERR_NO_DEST : (inb ? SE_ERR_OK : SE_ERR_OOB);
+        const int e_sel = same ? SE_ERR_SAME_PORT : SE_ERR_OK;
+        const int e_amt = amount_bad ? SE_ERR_AMOUNT : SE_ERR_OK;
+        const int e_take = atport ? e_amt : SE_ERR_NOT_AT_PORT;
+        const int e_ns = lt_sel ? e_sel : e_take;
+        const int e_ty = is_mv ? e_move : e_ns;
+        const int e_p = P == 0 ? SE_ERR_NO_PORTS : e_ty;  // :360
+        err[j] = bad ? SE_ERR_BAD_INDEX : e_p;            // the decode runs before env.step
+        const bool ok = err[j] == SE_ERR_OK;
+        do_move[j] = ok & is_mv;
+        moved[j] = do_move[j] & !ground;
+        const bool take_ok = ok & !lt_sel;
+        tf_ok[j] = take_ok & !lt_tc;
+        const bool tc_ok = take_ok & lt_tc;
+        const bool sel_ok = ok & !is_mv & lt_sel;
+        pos[j] = moved[j] ? cp : p;
+        cg[j] = tc_ok ? cg[j] + val[j] : cg[j];
+        dst[j] = sel_ok ? val[j] : dst[j];
+        // reward row before loss / arrival: a move by (out_of_fuel, ground, closer),
+        // filled in once fuel is known; a take 0.05; anything else 0
+        const int r_rest = take_ok ? 8 : 9;
+        ridx[j] = do_move[j] ? (((int)ground << 1) | (int)closer) : r_rest;
+        gate_needed |= !bad & is_mv & !nodest & inb & (G.c[j] > 0) & (G.c[j] < 50);
+    }
+    const U4 fb = draw(qk, t, kSlotFuel);
+    U4 gb{{0u, 0u, 0u, 0u}};
+    if (gate_needed) gb = draw(qk, t, kSlotGate);
+    uint32_t fire = 0, arrive = 0, fin = 0, dead = 0;
+    double f[4], r[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        // fuel cost (:103-104): 1 * (1 + uniform(-0.1, 0.1)), uniform = -0.1 + 0.2 u
+        const double scale = 1.0 + (-0.1 + (double)fb.v[j] * kFifthPerWord);
+        const bool oof = G.f[j] < scale;  // :288-290 (the ship still moves)
+        const double take = tf_ok[j] ? (double)val[j] : -0.0;
+        f[j] = G.f[j] + (moved[j] ? -scale : take);
+        // the gate random() <= cargo / 50 (:318-323) as w <= floor(fl(c/50) 2^32); the
+        // table's entry 50 is all ones (cargo >= 50 always fires); cargo 0 loses nothing
+        const uint32_t thr = w.gate_thr[min(max(cg[j], 0), 50)];
+        const bool fires = do_move[j] & (cg[j] > 0) & (gb.v[j] <= thr);
+        r[j] = w.rtab[ridx[j] | ((int)(do_move[j] & oof) << 2)];
+        fire |= (uint32_t)fires << j;
+        arrive |= (uint32_t)(do_move[j] & (pos[j] == pd16[j])) << j;  // :325
+        dead |= (uint32_t)(do_move[j] & oof) << j;
+        fin |= (uint32_t)((kFull || base + j < n) & do_move[j] & oof) << j;
+    }
+#if SHIPENV_ABL4 & 8
+    fin = 0;
+#endif
+    // the flags travel as opaque VGPR bit masks (no lane masks live in SGPR pairs
+    // across the draw blocks below)
+    asm volatile("" : "+v"(fire), "+v"(arrive), "+v"(fin), "+v"(dead));
+    int org[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) org[j] = byte_of(G.org, j);
+
+    // auto-reset (:227-243) of the envs that ran out of fuel: position and fuel now,
+    // cargo / origin / dest after the second half (whose reward the finished episode
+    // still collects). Contract v5: the r-th finishing env of the quad takes RESET_r.
+    uint32_t reset_o = 0, reset_d = 0;
+    if constexpr (kAuto) {
+        if (fin) {
+            uint32_t ow[4], dw[4];
+            const uint32_t rk[4] = {0u, fin & 1u, (uint32_t)__popc(fin & 3u), (uint32_t)__popc(fin & 7u)};
+#if SHIPENV_ABL4 & 1
+            U4 rr{{qk.e0 ^ t, qk.e0 + t, 0u, 0u}};
+#else
+            U4 rr = draw(qk, t, reset_slot(0));
+#endif
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                ow[j] = rr.v[0];
+                dw[j] = rr.v[1];
+            }
+#pragma unroll
+            for (uint32_t q = 1; q < 4; ++q) {
+                if (__popc(fin) > q) {
+#if SHIPENV_ABL4 & 1
+                    rr = U4{{rr.v[1], rr.v[0] * 3u, 0u, 0u}};
+#else
+                    rr = draw(qk, t, reset_slot(q));
+#endif
+#pragma unroll
+                    for (int j = (int)q; j < 4; ++j) {
+                        ow[j] = rk[j] >= q ? rr.v[0] : ow[j];
+                        dw[j] = rk[j] >= q ? rr.v[1] : dw[j];
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int o = uniform_int(ow[j], (uint32_t)P);
+                const int d = pick_other(dw[j], P, o);
+                reset_o |= (uint32_t)o << (8 * j);
+                reset_d |= (uint32_t)d << (8 * j);
+                const bool fj = (fin >> j) & 1u;
+                pos[j] = fj ? w.pos[o] : pos[j];
+                f[j] = fj ? kFuelInit : f[j];
+            }
+        }
+        G.load_episode(late_args(), at);
+    }
+    // x, y, fuel, done and err are final here (cargo loss and arrival change none)
+    {
+        const uint32_t t01 = __builtin_amdgcn_perm(pos[1], pos[0], 0x06020400u);  // x0 x1 y0 y1
+        const uint32_t t23 = __builtin_amdgcn_perm(pos[3], pos[2], 0x06020400u);  // x2 x3 y2 y3
+        const uint32_t ox = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
+        const uint32_t oy = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
+        uint32_t dn = 0, ee = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            dn |= ((dead >> j) & 1u) << (8 * j);
+            ee |= (uint32_t)(err[j] & 0xff) << (8 * j);
+        }
+        const se_state& S = A.st;
+        __builtin_amdgcn_sched_barrier(0);  // the fuel halves back to back (store_moved)
+        store4u8(S.x, at, ox);
+        store4u8(S.y, at, oy);
+        store4(S.fuel, at, f);
+        store4u8(S.done, at, dn);
+        store4u8(reinterpret_cast<uint8_t*>(S.err), at, ee);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // --- second half: cargo loss (_calculate_cargo_loss :169-200), contract v5: the
+    // r-th env of the quad whose gate fired takes block LOSS_r (word 0 the loss type,
+    // words 1-3 the Beta(2, 2) uniforms); only waves with a firing gate run it
+    if (fire) {
+        uint32_t lt[4], v1[4], v2[4], v3[4];
+        const uint32_t rk[4] = {0u, fire & 1u, (uint32_t)__popc(fire & 3u), (uint32_t)__popc(fire & 7u)};
+        U4 rr = draw(qk, t, loss_slot(0));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            lt[j] = rr.v[0];
+            v1[j] = rr.v[1];
+            v2[j] = rr.v[2];
+            v3[j] = rr.v[3];
+        }
+#pragma unroll
+        for (uint32_t q = 1; q < 4; ++q) {
+            if (__popc(fire) > q) {
+                rr = draw(qk, t, loss_slot(q));
+#pragma unroll
+                for (int j = (int)q; j < 4; ++j) {
+                    const bool take = rk[j] >= q;
+                    lt[j] = take ? rr.v[0] : lt[j];
+                    v1[j] = take ? rr.v[1] : v1[j];
+                    v2[j] = take ? rr.v[2] : v2[j];
+                    v3[j] = take ? rr.v[3] : v3[j];
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            // beta = the median of the three words * 2^-32 (the conversion is monotone)
+            const uint32_t lo = min(v1[j], v2[j]), hi = max(v1[j], v2[j]);
+            const uint32_t med = max(lo, min(hi, v3[j]));  // v_med3_u32
+            const int part = beta_part(med, cg[j]);
+            const int some = lt[j] > kTypeHi ? cg[j] : part;
+            const int loss = lt[j] < kTypeLo ? 0 : some;
+            const bool fj = (fire >> j) & 1u;
+            const double rl = r[j] + (double)loss * -3.0;  // int(loss * -3) exactly, then += (:323)
+            r[j] = fj ? rl : r[j];
+            cg[j] = fj ? cg[j] - loss : cg[j];
+        }
+    }
+    // arrival (:325-337): +2 cargo, cargo 0, origin = dest, a new destination != origin
+    if (arrive) {
+        const U4 ab = draw(qk, t, kSlotArrive);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool aj = (arrive >> j) & 1u;
+            const double ra = (r[j] + (double)(2 * cg[j])) + 10.0;
+            const int nd = pick_other(ab.v[j], P, dst[j]);
+            r[j] = aj ? ra : r[j];
+            cg[j] = aj ? 0 : cg[j];
+            org[j] = aj ? dst[j] : org[j];
+            dst[j] = aj ? nd : dst[j];
+        }
+    }
+    float rw[4], epr[4];
+    int32_t epl[4];
+    uint32_t oo = 0, od = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        rw[j] = (float)r[j];  // one rounding of the reference's f64 reward
+        epr[j] = 0.0f;
+        epl[j] = 0;
+        if constexpr (kAuto) {
+            const bool fj = (fin >> j) & 1u;
+            F.ret[j] = G.e[j] + rw[j];
+            F.len[j] = G.l[j] + 1;
+            if ((SHIPENV_ABL4 & 4) == 0 && fj) {
+                bs.ret += (double)F.ret[j];
+                bs.eps += 1;
+                bs.len += F.len[j];
+            }
+            epr[j] = fj ? 0.0f : F.ret[j];
+            epl[j] = fj ? 0 : F.len[j];
+            cg[j] = fj ? 0 : cg[j];
+            org[j] = fj ? byte_of(reset_o, j) : org[j];
+            dst[j] = fj ? byte_of(reset_d, j) : dst[j];
+        }
+        oo |= (uint32_t)(org[j] & 0xff) << (8 * j);
+        od |= (uint32_t)(dst[j] & 0xff) << (8 * j);
+    }
+    if constexpr (kAuto) F.mask = fin;
+    const se_state& S = late_args().st;
+    store4u8(S.origin, at, oo);
+    store4u8(S.dest, at, od);
+    store4(S.cargo, at, cg);
+    store4(S.reward, at, rw);
+    if constexpr (kAuto) {
+        store4(S.ep_return, at, epr);
+        store4(S.ep_len, at, epl);
+    }
+}
+
 // Sum over the wave's 64 lanes in a fixed tree, so the result does not depend on
 // timing: within each row of 16 lanes, DPP exchanges with lane^1, lane^2, the
 // mirrored lane of the half row and of the row (every lane then holds its row's
@@ -1105,7 +1403,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
         // (Loading the next group before this group's compute instead measured
         // slower: the extra registers cost a wave per SIMD, which hid more.)
         if (g < full) {
-            step_group<kTyped, kReplay, kAuto, true, kNt>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F);
+            if constexpr (!kTyped && !kReplay && !SHIPENV_ABLATE)
+                step_group_agent<kAuto, true, kNt>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F);
+            else
+                step_group<kTyped, kReplay, kAuto, true, kNt>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F);
             if (k == 0) TRACE_STAMP(2);
             if (k + 1 < A.iters && g + kStepBlock < full) G.template load<true>(A, At<true>{g0 + kStepBlock, 0, A.n});
         }
@@ -1148,7 +1449,10 @@ __global__ __launch_bounds__(64) void step_tail_kernel(StepArgs A) {
     G.template load<false>(A, at);
     BlockStats bs;
     Finished F;
-    step_group<kTyped, kReplay, kAuto, false>(A, w, G, at, bs, F);
+    if constexpr (!kTyped && !kReplay && !SHIPENV_ABLATE)
+        step_group_agent<kAuto, false, false>(A, w, G, at, bs, F);
+    else
+        step_group<kTyped, kReplay, kAuto, false>(A, w, G, at, bs, F);
     if constexpr (kAuto) {
         const int64_t b = g >> 6;  // the (iteration, wave) segment that owns group g
         int32_t c = (g & 63) == 0 ? 0 : A.done_count[b];  // a fresh segment: step_kernel wrote none
@@ -1300,7 +1604,7 @@ __global__ __launch_bounds__(kBlock) void observe_kernel(ObsArgs A) {
             }
         } else {
             const int p = (c - 6) >> 2, f = (c - 6) & 3;
-            v = f == 0 ? (float)w.px(p) : f == 1 ? (float)w.py(p) : f == 2 ? (float)w.pfuel[p] : (float)w.pcargo[p];
+            v = f == 0 ? (float)w.px(p) : f == 1 ? (float)w.py(p) : f == 2 ? (float)w.pfuel(p) : (float)w.pcargo(p);
         }
         A.obs[i * A.ld + c] = v;
     }
@@ -1340,10 +1644,10 @@ __global__ __launch_bounds__(kBlock) void valid_mask_kernel(MaskArgs A) {
                 v = p != origin && w.px(p) == x && w.py(p) == y;
             } else if (a < 4 + P + 50) {
                 const int amt = a - (4 + P);
-                v = cur >= 0 && amt > 0 && amt <= w.pcargo[cur];
+                v = cur >= 0 && amt > 0 && amt <= w.pcargo(cur);
             } else {
                 const int amt = a - (4 + P + 50);
-                v = cur >= 0 && amt > 0 && amt <= w.pfuel[cur];
+                v = cur >= 0 && amt > 0 && amt <= w.pfuel(cur);
             }
             out |= (uint32_t)v << (7 - bit);
         }
@@ -1379,7 +1683,7 @@ __device__ __forceinline__ void sample_action(const LdsWorld& w, const Ship& s, 
         type = w.P < 2 ? SE_SAMPLE_NO_OTHER_PORT : 2;
         a = pick_other(r, w.P, cur);
     } else if (s.cargo == 0 && cur >= 0) {  // :255-257, randint(1, port_cargo[idx]) :160
-        const int stock = w.pcargo[cur];
+        const int stock = w.pcargo(cur);
         type = stock < 1 ? SE_SAMPLE_RAISES : 4;  // randint(1, 0): ValueError
         a = 1 + uniform_int(r, (uint32_t)max(stock, 1));
     } else if (s.fuel == 0.0 && cur >= 0) {  // :258-260: self.fuel[idx] raises TypeError (:163)
@@ -1616,32 +1920,17 @@ int upload_world(se_env* env, int32_t P, const int32_t* px, const int32_t* py, c
             return fail(SE_EINVAL, "Coordinates not within map");  // add_port, environment.py:59-60
         if (pf[i] < 0 || pc[i] < 0) return fail(SE_EINVAL, "port stocks must be >= 0");
     }
-    const int words = (H * W + 31) / 32;
-    WorldDims d{H, W, P, words};
-    std::vector<uint32_t> img((size_t)d.total(), 0u);
-    std::vector<uint8_t> nonground(env->water);
-    for (int i = 0; i < P; ++i) nonground[(size_t)px[i] * W + py[i]] = 1;  // Entity.PORT (:65)
-    for (int c = 0; c < H * W; ++c)
-        if (!nonground[c]) img[c >> 5] |= 1u << (c & 31);
+    const int cw = (H * W + 15) / 16 * 4;  // cell-code bytes in whole 16-byte units
+    WorldDims d{H, W, P, cw};
+    std::vector<uint32_t> img((size_t)d.padded(), 0u);
+    uint8_t* cell = reinterpret_cast<uint8_t*>(img.data());
+    for (int c = 0; c < H * W; ++c) cell[c] = env->water[c] ? 0 : (uint8_t)kCellGround;
+    for (int i = P - 1; i >= 0; --i)  // Entity.PORT (:65); the first port on a cell wins
+        cell[(size_t)px[i] * W + py[i]] = (uint8_t)(i + 1);
     for (int i = 0; i < P; ++i) {
-        const int c = px[i] * W + py[i];
-        img[words + (c >> 5)] |= 1u << (c & 31);
-        img[d.pos() + i] = (uint32_t)px[i] | ((uint32_t)py[i] << 8);
-        img[d.pos() + P + i] = (uint32_t)pf[i];
-        img[d.pos() + 2 * P + i] = (uint32_t)pc[i];
-    }
-    uint8_t* prefix = reinterpret_cast<uint8_t*>(&img[2 * words]);
-    uint32_t run = 0;
-    for (int k = 0; k < words; ++k) {
-        prefix[k] = (uint8_t)run;  // run <= P <= 254
-        run += (uint32_t)__builtin_popcount(img[words + k]);
-    }
-    // rank -> first port (in port order) on that cell
-    for (int i = P - 1; i >= 0; --i) {
-        const uint32_t c = (uint32_t)(px[i] * W + py[i]);
-        const uint32_t word = img[words + (c >> 5)];
-        const uint32_t rank = prefix[c >> 5] + (uint32_t)__builtin_popcount(word & ((1u << (c & 31)) - 1u));
-        img[d.rank2port() + rank] = (uint32_t)i;
+        img[d.pos() + i] = (uint32_t)px[i] | ((uint32_t)py[i] << 16);
+        img[d.stk() + 2 * i] = (uint32_t)pf[i];
+        img[d.stk() + 2 * i + 1] = (uint32_t)pc[i];
     }
     // normalize(cargo, 50, 0) = cargo / 50 (util.py:6-8): Python's int / int true
     // division is the correctly rounded quotient, which IEEE f64 division gives here.
@@ -1650,6 +1939,11 @@ int upload_world(se_env* env, int32_t P, const int32_t* px, const int32_t* py, c
         memcpy(&img[d.frac() + 2 * c], &q, sizeof q);
         img[d.gate() + c] = (uint32_t)floor(ldexp(q, 32));  // exact product, q < 1
     }
+    img[d.gate() + 50] = 0xffffffffu;  // cargo >= 50: random() < 1 <= cargo / 50
+    // N, E, S, W as packed 16-bit (dx, dy) (shipping/type.py:8-16)
+    const int mdx[4] = {0, -1, 0, 1}, mdy[4] = {-1, 0, 1, 0};
+    for (int k = 0; k < 4; ++k)
+        img[d.moves() + k] = ((uint32_t)mdx[k] & 0xffffu) | (((uint32_t)mdy[k] & 0xffffu) << 16);
     // step rewards before cargo loss / arrival, added in the reference's order:
     // out of fuel (:288-290), ground (:293-294) or fuel + water (:296-300), closer (:307-315)
     double rtab[10];
@@ -1668,7 +1962,6 @@ int upload_world(se_env* env, int32_t P, const int32_t* px, const int32_t* py, c
     rtab[8] = 0.05;  // TAKE_FUEL / TAKE_CARGO (:349, :357)
     rtab[9] = 0.0;
     memcpy(&img[d.rtab()], rtab, sizeof rtab);
-    img.resize((size_t)d.padded(), 0u);
     if (d.padded() > env->world_cap) {
         if (env->d_world) HIP_TRY(hipFree(env->d_world));
         env->d_world = nullptr;

@@ -58,13 +58,14 @@ static void* dev(size_t bytes) {
 
 int main(int argc, char** argv) {
     int64_t n = 1 << 20;
-    int config = 3, steps = 1000, rows = 0;  // rows > 0: cycle through that many action rows
+    int config = 3, steps = 1000, rows = 0, warm = 20;  // rows > 0: cycle through that many action rows
     std::vector<std::string> libs;
     for (int i = 1; i < argc; ++i) {
         if (!strcmp(argv[i], "--n")) n = atoll(argv[++i]);
         else if (!strcmp(argv[i], "--config")) config = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--steps")) steps = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--rows")) rows = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--warm")) warm = atoi(argv[++i]);
         else libs.push_back(argv[i]);
     }
     FILE* f = fopen("shippingenv_amd/data/mapa_mundi_binario.jpg", "rb");
@@ -145,25 +146,28 @@ int main(int argc, char** argv) {
         SE(a.bind(env, &st));
         hipStream_t s;
         CK(hipStreamCreate(&s));
-        int32_t* acts = (int32_t*)dev((size_t)steps * n * 4);
-        for (int t = 0; t < steps; ++t) SE(a.gen(env, acts + (size_t)t * n, (uint32_t)t, s));
+        // rows: warm-up rows first, then the timed ones (as bench.py: W warm-up steps,
+        // then K steps on fresh rows)
+        const int total = warm + steps;
+        int32_t* acts = (int32_t*)dev((size_t)total * n * 4);
+        for (int t = 0; t < total; ++t) SE(a.gen(env, acts + (size_t)t * n, (uint32_t)t, s));
         SE(a.reset(env, nullptr, s));
-        for (int t = 0; t < 20; ++t) SE(a.step(env, acts + (size_t)t * n, s));
+        for (int t = 0; t < warm; ++t) SE(a.step(env, acts + (size_t)t * n, s));
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0));
         CK(hipEventCreate(&e1));
         CK(hipStreamSynchronize(s));
         CK(hipEventRecord(e0, s));
         const int r = rows > 0 && rows < steps ? rows : steps;
-        for (int t = 0; t < steps; ++t) SE(a.step(env, acts + (size_t)(t % r) * n, s));
+        for (int t = 0; t < steps; ++t) SE(a.step(env, acts + (size_t)(warm + t % r) * n, s));
         CK(hipEventRecord(e1, s));
         CK(hipEventSynchronize(e1));
         float ms = 0.f;
         CK(hipEventElapsedTime(&ms, e0, e1));
         const char* base = strrchr(path.c_str(), '/');
         printf("{\"lib\": \"%s\", \"n\": %lld, \"config\": %d, \"steps\": %d, \"action_rows\": %d, "
-               "\"us_per_step\": %.3f}\n",
-               base ? base + 1 : path.c_str(), (long long)n, config, steps, r, 1000.0 * ms / steps);
+               "\"warm\": %d, \"us_per_step\": %.3f}\n",
+               base ? base + 1 : path.c_str(), (long long)n, config, steps, r, warm, 1000.0 * ms / steps);
         fflush(stdout);
         SE(a.destroy(env));
         for (void* p : {(void*)st.x, (void*)st.y, (void*)st.origin, (void*)st.dest, (void*)st.done,
