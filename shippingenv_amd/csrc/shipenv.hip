@@ -43,6 +43,9 @@
 // list, 4 no episode statistics, 8 no auto-reset at all (tools/build_ablation.sh)
 #define SHIPENV_ABL4 0
 #endif
+#ifndef SHIPENV_PREFETCH
+#define SHIPENV_PREFETCH 0  // 1 = load the next group before computing this one (step kernel)
+#endif
 #ifndef SHIPENV_ABLATE
 #define SHIPENV_ABLATE 0  // 0 = the product; 1 = timing-only memory-traffic build, 2 = also no staging (tools/build_ablation.sh, tools/ablate_libs.sh)
 #endif
@@ -90,9 +93,9 @@ constexpr double kMaxCargo = 50.0;
 // where bitmaps took a word read, bit arithmetic and a 3-read rank chain.
 constexpr int kCellGround = 255;
 // kStepBlock x 4-dword rows of the world image the step kernel stages unguarded
-// (one 16-byte load per thread and row): 3 rows = 12 KB hold the 100x100 image with
-// up to 130 ports
-constexpr int kStageRows = 3;
+// (one 16-byte load per thread and row), at least 12 KB: the 100x100 image with up
+// to 130 ports
+constexpr int kStageRows = (3072 + 4 * kStepBlock - 1) / (4 * kStepBlock);
 constexpr int kStageWords = kStageRows * 4 * kStepBlock;
 
 struct WorldDims {
@@ -1027,10 +1030,37 @@ __device__ __forceinline__ uint32_t cell_of(uint32_t p, uint32_t wh) {
     return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p), __builtin_bit_cast(u16x2, wh), 0u, false);
 }
 
+// The Philox blocks of a group that depend on no state (contract v5: FUEL every step;
+// GATE, whose words are the same whether or not an env consumes them; LOSS_0, the
+// block of the quad's first firing env, used by most waves): drawn right after the
+// group's loads are issued, so their VALU work overlaps the wait for the data
+// instead of following it.
+// LOSS_0 is drawn early with auto-reset (config 4 measured 12.71 -> 12.44 us at
+// 2^20) and on demand without (config 3: 8.48 vs 8.56 us); SHIPENV_SPEC_LOSS = 0 / 1
+// forces it off / on for both.
+#ifndef SHIPENV_SPEC_LOSS
+#define SHIPENV_SPEC_LOSS -1
+#endif
+struct Draws {
+    U4 fuel, gate, loss0;
+};
+template <bool kSpecLoss>
+__device__ __forceinline__ Draws early_draws(const StepArgs& A, int64_t base) {
+    const Key qk = env_key(A.seed, (A.env_base + base) >> 2);
+    Draws d;
+    d.fuel = draw(qk, A.t, kSlotFuel);
+    d.gate = draw(qk, A.t, kSlotGate);
+    d.loss0 = kSpecLoss ? draw(qk, A.t, loss_slot(0)) : U4{{0u, 0u, 0u, 0u}};
+    return d;
+}
+
+template <bool kAuto>
+constexpr bool spec_loss() { return SHIPENV_SPEC_LOSS < 0 ? kAuto : SHIPENV_SPEC_LOSS != 0; }
+
 template <bool kAuto, bool kFull, bool kNt>
 __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWorld& w,
                                                  Group<false, kAuto, kNt>& G, At<kFull> at,
-                                                 BlockStats& bs, Finished& F) {
+                                                 BlockStats& bs, Finished& F, const Draws& D) {
     const int64_t n = A.n, base = at.base;
     const int P = w.P;
     const uint32_t lim = (uint32_t)(w.H - 1) | ((uint32_t)(w.W - 1) << 16);
@@ -1038,7 +1068,11 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
     const uint32_t pm1 = P > 0 ? (uint32_t)(P - 1) : 0u;  // clamp for table reads whose value an error discards
     const Key qk = env_key(A.seed, (A.env_base + base) >> 2);
     const uint32_t t = A.t;
-
+    constexpr bool kSpecLoss = spec_loss<kAuto>();
+#if SHIPENV_TRACE
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the group's data has arrived
+    TRACE_STAMP(4);
+#endif
     // --- first half: everything that needs no optional draw (:359-376, :273-315)
     uint32_t pos[4], pd16[4];
     int val[4], dst[4], cg[4], err[4], ridx[4];
@@ -1095,9 +1129,9 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
         ridx[j] = do_move[j] ? (((int)ground << 1) | (int)closer) : r_rest;
         gate_needed |= !bad & is_mv & !nodest & inb & (G.c[j] > 0) & (G.c[j] < 50);
     }
-    const U4 fb = draw(qk, t, kSlotFuel);
-    U4 gb{{0u, 0u, 0u, 0u}};
-    if (gate_needed) gb = draw(qk, t, kSlotGate);
+    TRACE_STAMP(5);
+    (void)gate_needed;  // drawn early (early_draws) whether or not an env needs it
+    const U4 fb = D.fuel, gb = D.gate;
     uint32_t fire = 0, arrive = 0, fin = 0, dead = 0;
     double f[4], r[4];
 #pragma unroll
@@ -1194,6 +1228,7 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
         store4u8(reinterpret_cast<uint8_t*>(S.err), at, ee);
         __builtin_amdgcn_sched_barrier(0);
     }
+    TRACE_STAMP(6);
 
     // --- second half: cargo loss (_calculate_cargo_loss :169-200), contract v5: the
     // r-th env of the quad whose gate fired takes block LOSS_r (word 0 the loss type,
@@ -1201,7 +1236,7 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
     if (fire) {
         uint32_t lt[4], v1[4], v2[4], v3[4];
         const uint32_t rk[4] = {0u, fire & 1u, (uint32_t)__popc(fire & 3u), (uint32_t)__popc(fire & 7u)};
-        U4 rr = draw(qk, t, loss_slot(0));
+        U4 rr = kSpecLoss ? D.loss0 : draw(qk, t, loss_slot(0));
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             lt[j] = rr.v[0];
@@ -1379,6 +1414,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
     (void)lds;
 #else
     const Staged st = stage_issue(A.world);
+    // the image's loads first: the staging writes then wait for them alone
+    __builtin_amdgcn_sched_barrier(0);
 #endif
     // first group: an unconditional load (lanes past the end re-read the last full
     // group; the host launches this kernel only when there is one), so the staging
@@ -1388,6 +1425,14 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
         const int64_t last = full - 1 - first;  // block-uniform
         const uint32_t lane = last < (int64_t)threadIdx.x ? (uint32_t)(last < 0 ? 0 : last) : threadIdx.x;
         G.template load<true>(A, At<true>{last < 0 ? full - 1 : first, 0, A.n}, lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr bool kAgent = !kTyped && !kReplay && !SHIPENV_ABLATE;
+    Draws D;
+    if constexpr (kAgent) {
+        D = early_draws<spec_loss<kAuto>()>(A, (first + threadIdx.x) * 4);
+        // keep the draws ahead of the staging wait: they overlap the loads in flight
+        asm volatile("" : "+v"(D.fuel.v[0]), "+v"(D.gate.v[0]), "+v"(D.loss0.v[0]));
     }
 #if SHIPENV_ABLATE >= 2
     const LdsWorld w = world_view(A.dims, A.world);
@@ -1400,16 +1445,21 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
     for (int64_t k = 0; k < A.iters; ++k) {
         const int64_t g0 = first + k * kStepBlock, g = g0 + threadIdx.x;
         Finished F;
-        // (Loading the next group before this group's compute instead measured
-        // slower: the extra registers cost a wave per SIMD, which hid more.)
+        const bool more = k + 1 < A.iters && g + kStepBlock < full;
+        // SHIPENV_PREFETCH: the next group's loads go out before this group's compute
+        // (software pipelining; pays only with several groups per thread)
+        Group<kTyped, kAuto, kNt> Gn;
+        if (SHIPENV_PREFETCH && more) Gn.template load<true>(A, At<true>{g0 + kStepBlock, 0, A.n});
         if (g < full) {
-            if constexpr (!kTyped && !kReplay && !SHIPENV_ABLATE)
-                step_group_agent<kAuto, true, kNt>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F);
-            else
+            if constexpr (kAgent) {
+                if (k > 0) D = early_draws<spec_loss<kAuto>()>(A, g * 4);
+                step_group_agent<kAuto, true, kNt>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F, D);
+            } else
                 step_group<kTyped, kReplay, kAuto, true, kNt>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F);
             if (k == 0) TRACE_STAMP(2);
-            if (k + 1 < A.iters && g + kStepBlock < full) G.template load<true>(A, At<true>{g0 + kStepBlock, 0, A.n});
+            if (!SHIPENV_PREFETCH && more) G.template load<true>(A, At<true>{g0 + kStepBlock, 0, A.n});
         }
+        if (SHIPENV_PREFETCH) G = Gn;
         // done-list segment of this (iteration, wave): 64 groups, in env order
         if constexpr (kAuto && (SHIPENV_ABL4 & 2) == 0) wave_compact(late_args(), F, g * 4, __builtin_amdgcn_readfirstlane((int32_t)(g >> 6)));
     }
@@ -1450,7 +1500,7 @@ __global__ __launch_bounds__(64) void step_tail_kernel(StepArgs A) {
     BlockStats bs;
     Finished F;
     if constexpr (!kTyped && !kReplay && !SHIPENV_ABLATE)
-        step_group_agent<kAuto, false, false>(A, w, G, at, bs, F);
+        step_group_agent<kAuto, false, false>(A, w, G, at, bs, F, early_draws<spec_loss<kAuto>()>(A, at.base));
     else
         step_group<kTyped, kReplay, kAuto, false>(A, w, G, at, bs, F);
     if constexpr (kAuto) {

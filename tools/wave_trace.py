@@ -48,7 +48,9 @@ def main():
     half = (1 << 16) // 2
     both = buf.reshape(-1, 8)[:, :4].astype(np.int64)
     last = (a.steps - 1) & 1  # the last step's parity (t counts from the first step after reset)
+    allst = buf.reshape(-1, 8).astype(np.int64)
     tr = both[last * half:last * half + waves]
+    ex = allst[last * half:last * half + waves, 4:7]
     prev = both[(1 - last) * half:(1 - last) * half + waves]
     t0 = tr[:, 0].min()
     us = (tr - t0) / 100.0  # 100 MHz ticks -> us
@@ -57,6 +59,11 @@ def main():
            "start": pct(us[:, 0]), "staged": pct(us[:, 1]), "stepped": pct(us[:, 2]), "end": pct(us[:, 3]),
            "stage_dur": pct(us[:, 1] - us[:, 0]), "step_dur": pct(us[:, 2] - us[:, 1]),
            "drain_dur": pct(us[:, 3] - us[:, 2]), "life": pct(us[:, 3] - us[:, 0])}
+    if (ex > 0).all():  # agent path stamps: data arrived, first half computed, first stores issued
+        ue = (ex - t0) / 100.0
+        out.update({"arrived": pct(ue[:, 0]), "half1": pct(ue[:, 1]), "stored1": pct(ue[:, 2]),
+                    "wait_data": pct(ue[:, 0] - us[:, 1]), "half1_dur": pct(ue[:, 1] - ue[:, 0]),
+                    "draws_stores_dur": pct(ue[:, 2] - ue[:, 1]), "half2_dur": pct(us[:, 2] - ue[:, 2])})
     out["prev_end_to_start_us"] = round(float((t0 - prev[:, 3].max()) / 100.0), 2)
     out["prev_first_start_to_start_us"] = round(float((t0 - prev[:, 0].min()) / 100.0), 2)
     # waves alive over time (10 bins per us)
