@@ -33,9 +33,27 @@ def hipcc():
     raise RuntimeError("hipcc not found (ROCm is required to build libshipenv_hip.so)")
 
 
+STAMP = OUT + ".cmd"  # the flags that built OUT: options, defines and arch (no paths: the
+                      # tree travels to the GPU box under another root)
+
+
+def _flags():
+    extra = os.environ.get("SHIPENV_HIPCC_DEFINES", "").split()  # e.g. -DSHIPENV_POLICY_BLOCK=768
+    return FLAGS + extra
+
+
+def _command(out):
+    return [hipcc()] + _flags() + ["-o", out, SRC, MAPSRC]
+
+
 def up_to_date():
-    if not os.path.exists(OUT):
+    """OUT is newer than every source and was built by the same command line (an A/B build
+    with other defines or another SHIPENV_OFFLOAD_ARCH never reuses a stale library)."""
+    if not os.path.exists(OUT) or not os.path.exists(STAMP):
         return False
+    with open(STAMP) as f:
+        if f.read() != " ".join(_flags()):
+            return False
     t = os.path.getmtime(OUT)
     return all(os.path.getmtime(d) <= t for d in DEPS)
 
@@ -45,11 +63,13 @@ def build(force=False, verbose=True):
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     tmp = OUT + ".tmp"
-    cmd = [hipcc()] + FLAGS + ["-o", tmp, SRC, MAPSRC]
+    cmd = _command(tmp)
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, OUT)
+    with open(STAMP, "w") as f:
+        f.write(" ".join(_flags()))
     return OUT
 
 

@@ -20,8 +20,10 @@
 // argmax: each lane keeps the first maximum over the valid rows it holds, and the
 // two lane halves that share an env merge with one shuffle. Q never reaches HBM.
 //
-// LDS: the packed network (113 KB at P = 5) plus the world image, one 768-thread
-// workgroup (12 waves, 3 per SIMD) per CU for the whole launch.
+// LDS: the packed network (113 KB at P = 5) plus the world image, one 1024-thread
+// workgroup (16 waves, 4 per SIMD, <= 128 VGPRs) per CU for the whole launch. At 128
+// VGPRs the kernel spills 28 B per lane to scratch: check the spill count
+// (-Rpass-analysis=kernel-resource-usage) after any edit that adds register pressure.
 
 #ifndef SHIPENV_POLICY_ABL
 #define SHIPENV_POLICY_ABL 0  // timing-only ablations of the policy kernel (1: plain max epilogue, 2: no fc3)

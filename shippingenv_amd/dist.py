@@ -84,7 +84,10 @@ class ShardedVecEnv:
         self.env = VecEnv(count, env_id_base=first, device=self.device, **kw)
 
     def __getattr__(self, name):
-        return getattr(self.env, name)
+        env = self.__dict__.get("env")  # absent if VecEnv construction failed in __init__
+        if name == "env" or env is None:
+            raise AttributeError(name)
+        return getattr(env, name)
 
     def global_episode_stats(self):
         return reduce_episode_stats(self.env.episode_stats().clone())

@@ -210,11 +210,14 @@ class Environment:
 
     # ------------------------------------------------------------------ device
     def _world(self):
-        """The stepper follows assignments to np_game / port lists (agents/mcts.py:200-208)."""
-        key = (id(self.np_game), tuple(tuple(int(v) for v in p) for p in self.port_positions),
+        """The stepper follows assignments to np_game / port lists (agents/mcts.py:200-208)
+        and in-place edits of np_game: the reference reads the ground test live on every
+        move (environment.py:293), so the key holds the ground mask's bytes, not id()."""
+        ground = np.asarray(self.np_game) == Entity.GROUND
+        key = (ground.shape, ground.tobytes(), tuple(tuple(int(v) for v in p) for p in self.port_positions),
                tuple(self.port_fuel), tuple(self.port_cargo))
         if self._stepper is None or key != self._world_key:
-            water = (np.asarray(self.np_game) != Entity.GROUND).astype(np.uint8)
+            water = (~ground).astype(np.uint8)
             px = [int(p[0]) for p in self.port_positions]
             py = [int(p[1]) for p in self.port_positions]
             if self._stepper is None:

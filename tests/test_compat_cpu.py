@@ -55,3 +55,34 @@ def test_no_gpu_means_no_silent_fallback(monkeypatch):
     env.add_port([60, 22])
     with pytest.raises(_native.NativeLibraryError):
         env.reset()
+
+
+def test_in_place_np_game_edit_reaches_the_stepper(oracle_backend):
+    """The reference tests np_game[new] == GROUND live on every move
+    (shipping/environment.py:293): marking a water cell GROUND in place (no reassignment)
+    must block the next move into it."""
+    import random
+
+    from shippingenv_amd.maps import BUILTIN_MAP
+    from shippingenv_amd.shipping import Environment, ShipMove, environment
+
+    random.seed(5)
+    env = Environment(BUILTIN_MAP)
+    for p in ([41, 40], [60, 22], [78, 29], [49, 72], [62, 72]):
+        env.add_port(p)
+    env.reset()
+    x, y = env.ship_position
+    for move in (ShipMove.NORTH, ShipMove.SOUTH, ShipMove.EAST, ShipMove.WEST):
+        tx, ty = x + move[0], y + move[1]
+        if 0 <= tx < 100 and 0 <= ty < 100 and env.np_game[tx, ty] == 1:
+            break
+    else:
+        pytest.skip("no water neighbour")
+    env.step([environment.ActionType.MOVE_SHIP, move])  # stepper built and keyed on this map
+    env.step([environment.ActionType.MOVE_SHIP, (-move[0], -move[1])])  # back on the port
+    assert list(env.ship_position) == [x, y]
+    env.np_game[tx, ty] = 0  # in place: GROUND
+    fuel = env.fuel
+    _, reward, _, _ = env.step([environment.ActionType.MOVE_SHIP, move])
+    assert list(env.ship_position) == [x, y], "the edited cell did not block the move"
+    assert env.fuel == fuel and reward in (-3, -7)  # -5 blocked, then the +-2 distance term (:307-315)

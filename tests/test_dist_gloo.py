@@ -89,3 +89,13 @@ def test_shard_bounds_rules():
     assert shard_bounds(1 << 20, 8, 3) == (3 << 17, 1 << 17)
     with pytest.raises(ValueError):
         shard_bounds(4096 + 4, 2, 0)
+
+
+def test_sharded_env_attribute_lookup_without_env():
+    """A ShardedVecEnv whose __init__ failed before self.env was set answers attribute
+    lookups with AttributeError, not a RecursionError through __getattr__."""
+    from shippingenv_amd.dist import ShardedVecEnv
+
+    s = object.__new__(ShardedVecEnv)
+    assert not hasattr(s, "env") and not hasattr(s, "n")
+    repr(s)
