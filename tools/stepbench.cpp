@@ -59,6 +59,7 @@ static void* dev(size_t bytes) {
 int main(int argc, char** argv) {
     int64_t n = 1 << 20;
     int config = 3, steps = 1000, rows = 0, warm = 20;  // rows > 0: cycle through that many action rows
+    bool gen_late = false;  // generate the timed rows after the warm-up steps (right before timing)
     std::vector<std::string> libs;
     for (int i = 1; i < argc; ++i) {
         if (!strcmp(argv[i], "--n")) n = atoll(argv[++i]);
@@ -66,6 +67,7 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--steps")) steps = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--rows")) rows = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--warm")) warm = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--gen-late")) gen_late = true;
         else libs.push_back(argv[i]);
     }
     FILE* f = fopen("shippingenv_amd/data/mapa_mundi_binario.jpg", "rb");
@@ -150,9 +152,11 @@ int main(int argc, char** argv) {
         // then K steps on fresh rows)
         const int total = warm + steps;
         int32_t* acts = (int32_t*)dev((size_t)total * n * 4);
-        for (int t = 0; t < total; ++t) SE(a.gen(env, acts + (size_t)t * n, (uint32_t)t, s));
+        for (int t = 0; t < (gen_late ? warm : total); ++t) SE(a.gen(env, acts + (size_t)t * n, (uint32_t)t, s));
         SE(a.reset(env, nullptr, s));
         for (int t = 0; t < warm; ++t) SE(a.step(env, acts + (size_t)t * n, s));
+        if (gen_late)
+            for (int t = warm; t < total; ++t) SE(a.gen(env, acts + (size_t)t * n, (uint32_t)t, s));
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0));
         CK(hipEventCreate(&e1));
@@ -166,8 +170,9 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
         const char* base = strrchr(path.c_str(), '/');
         printf("{\"lib\": \"%s\", \"n\": %lld, \"config\": %d, \"steps\": %d, \"action_rows\": %d, "
-               "\"warm\": %d, \"us_per_step\": %.3f}\n",
-               base ? base + 1 : path.c_str(), (long long)n, config, steps, r, warm, 1000.0 * ms / steps);
+               "\"warm\": %d, \"gen_late\": %d, \"us_per_step\": %.3f}\n",
+               base ? base + 1 : path.c_str(), (long long)n, config, steps, r, warm, (int)gen_late,
+               1000.0 * ms / steps);
         fflush(stdout);
         SE(a.destroy(env));
         for (void* p : {(void*)st.x, (void*)st.y, (void*)st.origin, (void*)st.dest, (void*)st.done,
