@@ -60,6 +60,7 @@ def parse():
     p.add_argument("--train-steps", type=int, default=30,
                    help="timed vectorised DQN training iterations (policy, step, replay, update); 0 = skip")
     p.add_argument("--train-batch", type=int, default=8192, help="DQN minibatch per update")
+    p.add_argument("--config1", type=int, default=1, help="time BASELINE configs[0] (N = 1 drop-in API); 0 = skip")
     p.add_argument("--rollouts", type=int, default=20,
                    help="timed se_rollout launches (MCTS random rollouts, 2^20 x 100 steps); 0 = skip")
     return p.parse_args()
@@ -153,6 +154,45 @@ def run_config(n, ports, auto, args, dist, label):
     del acts
     torch.cuda.empty_cache()
     return wall, k_ms, stats
+
+
+def run_config1(args):
+    """BASELINE configs[0]: one env, 100 steps through the drop-in shipping.Environment
+    (N = 1 on the GPU: one launch and two copies per step), as the survey timed the
+    reference: random.seed(0), the five DEFAULT_PORTS, moves uniform over
+    N, E, S, W from random.Random(1), reset on done; median of 10 runs."""
+    import random
+    import statistics
+
+    from shippingenv_amd.shipping import ShipMove, environment
+
+    ports = [[41, 40], [60, 22], [78, 29], [49, 72], [62, 72]]  # utils/constants.py:57-63
+    moves = [ShipMove.NORTH, ShipMove.EAST, ShipMove.SOUTH, ShipMove.WEST]
+
+    def once():
+        random.seed(0)
+        env = environment.Environment("mapa_mundi_binario.jpg")
+        for p in ports:
+            env.add_port(list(p))
+        env.reset()
+        pick = random.Random(1)
+        t0 = time.perf_counter()
+        for _ in range(100):
+            try:
+                _, _, done, _ = env.step([environment.ActionType.MOVE_SHIP, moves[pick.randrange(4)]])
+            except ValueError:  # "Move is out of range" (:284)
+                continue
+            if done:
+                env.reset()
+        return (time.perf_counter() - t0) * 1e3
+
+    once()
+    ms = statistics.median(once() for _ in range(10))
+    return {"workload": "BASELINE configs[0]: 1 env x 100 steps through shipping.Environment "
+                        "(the reference's API, N = 1 on the GPU)",
+            "ms_per_100_steps": round(ms, 4),
+            "reference_python_ms_per_100_steps": 0.98,
+            "reference_note": "survey container, 1 core (BASELINE.md); the reference cannot run on the GPU box"}
 
 
 def run_rollouts(n, args, dist):
@@ -479,6 +519,9 @@ def main():
         if t4:
             out["config4"]["roofline"]["traffic"] = t4
             out["config4"]["roofline"]["traffic_source"] = src4
+
+    if args.config1 and dist.world == 1:
+        out["config1"] = run_config1(args)
 
     if args.rollouts:
         out["rollouts"] = run_rollouts(n, args, dist)

@@ -122,7 +122,9 @@ int se_create(se_env** out, int device, int64_t n, int64_t env_id_base, int32_t 
 int se_set_ports(se_env* env, int32_t P, const int32_t* port_x, const int32_t* port_y,
                  const int32_t* port_fuel, const int32_t* port_cargo);
 
-/* Bind the caller-owned SoA buffers (n entries each). */
+/* Bind the caller-owned SoA buffers (n entries each, 16-byte aligned): device memory,
+ * or pinned host memory, which ROCm maps into the GPU's address space (the N = 1
+ * shipping.Environment binds one pinned 256-byte block and reads results in place). */
 int se_bind(se_env* env, const se_state* state);
 
 /* reset() (environment.py:227-243) for every env with mask[i] != 0 (mask NULL = all):

@@ -126,6 +126,14 @@ def lib():
         raise NativeLibraryError(
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
             " (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    # torch's ROCm runtime loads first. It ships its own HIP and an HSA runtime with the
+    # soname libhsa-runtime64.so.1, the same soname as /opt/rocm's, which this library
+    # needs: whichever is loaded first serves both HIP runtimes in the process. Loaded
+    # before torch (shipping.Environment(<jpeg>) decodes the map through this library
+    # before anything touches the GPU, as the reference's MCTS agent does), the
+    # library's HIP later found no device once torch's runtime had initialised
+    # (tests/test_compat_gpu.py::test_library_loaded_before_torch).
+    import torch  # noqa: F401
     try:
         handle = C.CDLL(LIB_PATH)
     except OSError as e:

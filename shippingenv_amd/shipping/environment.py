@@ -254,13 +254,15 @@ class Environment:
         stepper = self._world()
         x, y = self._ship_xy()
         tape = [math.nan, math.nan, math.nan, math.nan, -1]
-        snap = None
-        if act_type == ActionType.MOVE_SHIP and hasattr(rs, "getstate"):
-            # an in-range MOVE draws uniform() then random() (:104, :320); draw them ahead and
-            # rewind if the kernel reports the step raised before drawing (:276, :284)
-            snap = rs.getstate()
-            tape[0] = rs.random()
-            tape[1] = rs.random()
+        ahead = False
+        if act_type == ActionType.MOVE_SHIP and self.destination_port_index is not None:
+            H, W = np.shape(self.np_game)[:2]
+            if 0 <= x + a < H and 0 <= y + b < W:
+                # a MOVE that raises neither at :276 nor at :284 draws uniform() then
+                # random() (:104, :320): draw them ahead, saving the kernel's request
+                ahead = True
+                tape[0] = rs.random()
+                tape[1] = rs.random()
         while True:
             res = stepper.step(x, y, float(self.fuel), int(self.cargo), self.origin_port_index,
                                self.destination_port_index, act_type, a, b, tape)
@@ -281,8 +283,8 @@ class Environment:
                 tape[4] = d
             else:
                 raise RuntimeError("step kernel asked for a variate the protocol cannot supply")
-        if snap is not None and not (res.used & N.USED_FUEL_GATE):
-            rs.setstate(snap)
+        if ahead and not (res.used & N.USED_FUEL_GATE):
+            raise RuntimeError("the step kernel raised a move the host expected to draw for")
         return res
 
     def step(self, action):

@@ -48,3 +48,27 @@ def test_steps_run_through_the_hip_library():
     dt = (time.perf_counter() - t0) / 200
     print(f"compat step: {dt * 1e6:.1f} us")
     assert dt < 5e-3
+
+
+def test_library_loaded_before_torch():
+    """The reference's MCTS agent imports shipping but not torch (agents/mcts.py:3-10)
+    and builds Environment("mapa_mundi_binario.jpg"), whose map decode loads the
+    library before torch: the steps must still run on the GPU (a fresh interpreter)."""
+    import os
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    code = (
+        "import sys; from shippingenv_amd.shipping import Environment\n"
+        "env = Environment('mapa_mundi_binario.jpg')\n"
+        "env.add_port([41, 40]); env.add_port([60, 22])\n"
+        "env.reset()\n"
+        "from shippingenv_amd.shipping._device import DeviceStepper\n"
+        "assert isinstance(env._stepper, DeviceStepper)\n"
+        "env.step([1, (0, 1)]) if env.np_game[41, 41] != 0 else env.step([1, (0, -1)])\n"
+        "print('ok')\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
