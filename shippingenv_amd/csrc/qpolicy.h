@@ -20,6 +20,10 @@
 // argmax: each lane keeps the first maximum over the valid rows it holds, and the
 // two lane halves that share an env merge with one shuffle. Q never reaches HBM.
 //
+// fc3 runs over the compact row layout (QnetDims): only the actions some env can
+// ever take, so at P = 5 two 32-row tiles where the full layout has three with a valid
+// row (of nine); the full layout serves q_out (every row's Q, for tests / inspection).
+//
 // LDS: the packed network (113 KB at P = 5) plus the world image, one 1024-thread
 // workgroup (16 waves, 4 per SIMD, <= 128 VGPRs) per CU for the whole launch. At 128
 // VGPRs the kernel spills 28 B per lane to scratch: check the spill count
@@ -45,9 +49,25 @@ constexpr int kPolicyBlock = SHIPENV_POLICY_BLOCK;
 constexpr int kPolicyWaves = kPolicyBlock / 64;
 
 // Packed network image (bytes). Fragments are 64 lanes x 8 bf16 = 1 KB.
+// Two layouts of fc3's rows:
+// * full: row r is action r (A = 4 + P + 250 rows), for the Q output (q_out);
+// * compact: only the actions some env can ever take, in ascending order: the moves and
+//   SELECT rows [0, 4 + P), then TAKE_CARGO amounts 1..cmax and TAKE_FUEL amounts
+//   1..fmax, cmax / fmax the largest stocks of the world's ports (add_port draws 5..20,
+//   so 49 rows and 2 tiles at P = 5 instead of 3 of the 9 full tiles with a valid row).
+//   The first maximum in compact rows is the first in actions (the map is increasing).
 struct QnetDims {
-    int32_t P, A, mt3;  // ports, actions, fc3 row tiles (A rounded up to 32)
+    int32_t P, A, rows, mt3;  // ports, actions, fc3 rows of this layout, its row tiles
+    int32_t compact, cmax;    // the layout; TAKE_CARGO rows in the compact one
     __host__ __device__ int in1() const { return 6 + 4 * P; }
+    // action of fc3 row r (utils/preprocessing.py:111-137)
+    __host__ __device__ int action_of_row(int r) const {
+        if (!compact || r < 4 + P) return r;
+        return r < 4 + P + cmax ? r + 1 : r + 51 - cmax;
+    }
+    // row of TAKE_CARGO amount 1 and of TAKE_FUEL amount 1
+    __host__ __device__ int cargo_row1() const { return compact ? 4 + P : 5 + P; }
+    __host__ __device__ int fuel_row1() const { return compact ? 4 + P + cmax : 55 + P; }
     __host__ __device__ int w1() const { return 0; }                    // 4 fc1 tiles
     __host__ __device__ int w2() const { return 4 * 1024; }              // 4 x 4 x 2 fc2 fragments
     __host__ __device__ int w3() const { return w2() + 32 * 1024; }      // mt3 x 4 x 2 fc3 fragments
@@ -59,11 +79,14 @@ struct QnetDims {
     __host__ __device__ int bytes() const { return (regm() + 4 * mt3 + 15) & ~15; }
 };
 
-QnetDims qnet_dims(int P) {
+QnetDims qnet_dims(int P, bool compact = false, int cmax = 0, int fmax = 0) {
     QnetDims q;
     q.P = P;
     q.A = 4 + P + 250;  // utils/preprocessing.py:93-108
-    q.mt3 = (q.A + 31) / 32;
+    q.compact = compact ? 1 : 0;
+    q.cmax = compact ? cmax : 49;
+    q.rows = compact ? 4 + P + cmax + fmax : q.A;
+    q.mt3 = (q.rows + 31) / 32;
     return q;
 }
 
@@ -111,10 +134,11 @@ __global__ __launch_bounds__(256) void qnet_pack_kernel(PackArgs A) {
                 const int s = f & 1, kt = (f >> 1) & 3, mt = f >> 3;
                 const int row = mt * 32 + r;
                 const float* W = second ? A.w2 : A.w3;
-                const bool in = second || row < q.A;
+                const bool in = second || row < q.rows;
+                const int wrow = second ? row : q.action_of_row(row);
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
-                    v[j] = in ? (__bf16)W[row * kQHidden + kt * 32 + acc_row(s, j, h)] : (__bf16)0.0f;
+                    v[j] = in ? (__bf16)W[wrow * kQHidden + kt * 32 + acc_row(s, j, h)] : (__bf16)0.0f;
                 dst = A.img + (second ? q.w2() : q.w3()) + f * 1024 + lane * 16;
             }
             *reinterpret_cast<bf16x8*>(dst) = v;
@@ -135,7 +159,7 @@ __global__ __launch_bounds__(256) void qnet_pack_kernel(PackArgs A) {
         } else if ((u -= kQHidden) < kQHidden) {
             reinterpret_cast<float*>(A.img + q.b2())[u] = A.b2[u];
         } else if ((u -= kQHidden) < q.mt3 * 32) {
-            reinterpret_cast<float*>(A.img + q.b3())[u] = u < q.A ? A.b3[u] : 0.0f;
+            reinterpret_cast<float*>(A.img + q.b3())[u] = u < q.rows ? A.b3[q.action_of_row(u)] : 0.0f;
         } else if ((u -= q.mt3 * 32) < P) {  // next port on the same cell, ascending (-1: none)
             int nx = -1;
             for (int p = u + 1; p < P && nx < 0; ++p)
@@ -157,8 +181,9 @@ __global__ __launch_bounds__(256) void qnet_pack_kernel(PackArgs A) {
             for (int reg = 0; reg < 16; ++reg)
                 for (int h = 0; h < 2; ++h) {
                     const int row = base + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-                    const bool ok = row < q.A && (row < 4 + P || (row >= c_lo && row <= c_hi) ||
-                                                  (row >= f_lo && row <= f_hi));
+                    const int a = q.action_of_row(row);
+                    const bool ok = row < q.rows && (a < 4 + P || (a >= c_lo && a <= c_hi) ||
+                                                     (a >= f_lo && a <= f_hi));
                     rm |= (uint32_t)ok << reg;
                 }
             reinterpret_cast<uint32_t*>(A.img + q.regm())[mt] = rm;
@@ -298,7 +323,8 @@ __global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
         const int cur = w.port_at(x, y);
         const int cst = cur >= 0 ? min(w.pcargo(max(cur, 0)), 49) : 0;
         const int fst = cur >= 0 ? min(w.pfuel(max(cur, 0)), 199) : 0;
-        const int c_lo = 5 + P, c_hi = 4 + P + cst, f_lo = 55 + P, f_hi = 54 + P + fst;
+        // valid TAKE rows of this env in the layout's row space
+        const int c_lo = q.cargo_row1(), c_hi = c_lo + cst - 1, f_lo = q.fuel_row1(), f_hi = f_lo + fst - 1;
         float best = -INFINITY;
         int bidx = 0x7fffffff;
 #if SHIPENV_POLICY_ABL == 2  // timing-only: no fc3
@@ -349,9 +375,9 @@ __global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
 #endif
             if (A.q_out && live) {
 #pragma unroll
-                for (int reg = 0; reg < 16; ++reg) {
+                for (int reg = 0; reg < 16; ++reg) {  // the full layout: row = action
                     const int row = base + 4 * h + (reg & 3) + 8 * (reg >> 2);
-                    if (row < q.A) A.q_out[e * A.ldq + row] = c[reg];
+                    if (row < q.rows) A.q_out[e * A.ldq + row] = c[reg];
                 }
             }
         }
@@ -363,7 +389,7 @@ __global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
             bidx = oi;
         }
         if (h == 0 && live) {
-            int act = bidx == 0x7fffffff ? 0 : bidx;  // no valid action: 0 (:188-189)
+            int act = bidx == 0x7fffffff ? 0 : q.action_of_row(bidx);  // no valid action: 0 (:188-189)
             if (A.eps > 0.0) {
                 const U4 d = draw(env_key(A.seed, A.env_base + e), A.t, kSlotPolicy);
                 if (u32(d.v[0]) <= A.eps) {  // np.random.rand() <= epsilon (:191)
@@ -378,7 +404,7 @@ __global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
                             if (p != origin && k-- == 0) act = 4 + p;
                     } else {
                         k -= nsel;
-                        act = k < cst ? c_lo + k : f_lo + (k - cst);
+                        act = k < cst ? 5 + P + k : 55 + P + (k - cst);  // amounts k + 1 (action space)
                     }
                 }
             }
@@ -393,7 +419,8 @@ __global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
 struct se_qnet {
     se_env* env = nullptr;  // must outlive the qnet (destroy the qnet first)
     int device = 0;
-    QnetDims q{};
+    QnetDims q{}, qc{};  // the full layout (q_out) and the compact one, whose image follows
+    size_t c_off = 0;    // byte offset of the compact image
     uint8_t* d_img = nullptr;
     int img_bytes = 0;
     uint64_t world_version = 0;
@@ -422,16 +449,24 @@ int se_qnet_set_weights(se_qnet* qn, const float* w1, const float* b1, const flo
     if (env->dims.P < 1) return fail(SE_EINVAL, "the policy needs at least one port");
     DeviceGuard g(env->device);
     const QnetDims q = qnet_dims(env->dims.P);
-    if (q.bytes() > qn->img_bytes) {
+    const QnetDims qc = qnet_dims(env->dims.P, true, env->cmax, env->fmax);
+    const size_t c_off = ((size_t)q.bytes() + 255) & ~(size_t)255;
+    const int total = (int)(c_off + (size_t)qc.bytes());
+    if (total > qn->img_bytes) {
         if (qn->d_img) HIP_TRY(hipFree(qn->d_img));
         qn->d_img = nullptr;
-        HIP_TRY(hipMalloc(&qn->d_img, (size_t)q.bytes()));
-        qn->img_bytes = q.bytes();
+        HIP_TRY(hipMalloc(&qn->d_img, (size_t)total));
+        qn->img_bytes = total;
     }
     qn->q = q;
-    PackArgs A{w1, b1, w2, b2, w3, b3, env->d_world, env->dims, q, qn->d_img};
-    qnet_pack_kernel<<<64, 256, 0, (hipStream_t)stream>>>(A);
-    HIP_TRY(hipGetLastError());
+    qn->qc = qc;
+    qn->c_off = c_off;
+    for (int layout = 0; layout < 2; ++layout) {
+        PackArgs A{w1, b1, w2, b2, w3, b3, env->d_world, env->dims, layout ? qc : q,
+                   qn->d_img + (layout ? c_off : 0)};
+        qnet_pack_kernel<<<64, 256, 0, (hipStream_t)stream>>>(A);
+        HIP_TRY(hipGetLastError());
+    }
     qn->world_version = env->world_version;
     qn->packed = true;
     return SE_OK;
@@ -451,7 +486,9 @@ int se_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, float* 
     if (!(epsilon >= 0.0)) return fail(SE_EINVAL, "epsilon must be >= 0");
     if (env->n == 0) return SE_OK;
     DeviceGuard g(env->device);
-    const size_t lds = (size_t)qn->q.bytes() + lds_bytes(env);
+    // the compact layout unless every row's Q is wanted
+    const QnetDims& q = q_out ? qn->q : qn->qc;
+    const size_t lds = (size_t)q.bytes() + lds_bytes(env);
     static std::atomic<uint64_t> lds_set{0};
     rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(policy_kernel), 160 * 1024, env->device);
     if (rc) return rc;
@@ -465,8 +502,8 @@ int se_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, float* 
     PolicyArgs A{};
     A.world = env->d_world;
     A.dims = env->dims;
-    A.qimg = reinterpret_cast<const uint4*>(qn->d_img);
-    A.q = qn->q;
+    A.qimg = reinterpret_cast<const uint4*>(qn->d_img + (q_out ? 0 : qn->c_off));
+    A.q = q;
     A.n = env->n;
     A.env_base = env->env_base;
     A.seed = env->seed;

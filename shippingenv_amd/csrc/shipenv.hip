@@ -27,6 +27,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <string>
 #include <vector>
@@ -1590,9 +1591,11 @@ struct ResetArgs {
     const int32_t* dest_in;
 };
 
+// The world is read in place (only the port positions, for the envs being reset): staged
+// per workgroup as the other kernels do, it cost 2048 x 10.8 KB of L2 reads per launch,
+// the whole launch when a mask selects a few envs (the training loop's episode cuts).
 __global__ __launch_bounds__(kBlock) void reset_kernel(ResetArgs A) {
-    extern __shared__ uint32_t lds[];
-    const LdsWorld w = stage_world(A.world, A.dims, lds);
+    const LdsWorld w = world_view(A.dims, A.world);
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < A.n;
          i += (int64_t)gridDim.x * kBlock) {
         if (A.mask && !A.mask[i]) continue;
@@ -1887,6 +1890,7 @@ struct se_env {
     int64_t iters = 1;  // groups per thread of the step kernel
     int world_cap = 0;  // words allocated
     uint64_t world_version = 0;  // bumped by every world upload (se_qnet folds the ports)
+    int32_t cmax = 0, fmax = 0;  // largest TAKE_CARGO / TAKE_FUEL amount any port allows (se_qnet)
     se_state st{};
     bool bound = false;
     double* d_slab = nullptr;       // [nslab][4]
@@ -2020,6 +2024,11 @@ int upload_world(se_env* env, int32_t P, const int32_t* px, const int32_t* py, c
     }
     HIP_TRY(hipMemcpy(env->d_world, img.data(), (size_t)d.padded() * 4, hipMemcpyHostToDevice));
     env->dims = d;
+    env->cmax = env->fmax = 0;
+    for (int i = 0; i < P; ++i) {  // amounts 1..49 / 1..199 exist (utils/preprocessing.py:93-108)
+        env->cmax = std::max(env->cmax, std::min(pc[i], 49));
+        env->fmax = std::max(env->fmax, std::min(pf[i], 199));
+    }
     env->world_version += 1;
     return SE_OK;
 }
@@ -2199,7 +2208,7 @@ int se_reset(se_env* env, const uint8_t* mask, void* stream) {
     ResetArgs A{env->d_world, env->dims, env->n, env->env_base, env->seed,
                 (uint32_t)env->epoch, env->st, mask, nullptr, nullptr};
     if (env->n > 0) {
-        reset_kernel<<<grid_for(env->n), kBlock, lds_bytes(env), (hipStream_t)stream>>>(A);
+        reset_kernel<<<grid_for(env->n), kBlock, 0, (hipStream_t)stream>>>(A);
         HIP_TRY(hipGetLastError());
     }
     env->epoch += 1;
@@ -2215,7 +2224,7 @@ int se_reset_to(se_env* env, const uint8_t* mask, const int32_t* origin, const i
     ResetArgs A{env->d_world, env->dims, env->n, env->env_base, env->seed,
                 (uint32_t)env->epoch, env->st, mask, origin, dest};
     if (env->n > 0) {
-        reset_kernel<<<grid_for(env->n), kBlock, lds_bytes(env), (hipStream_t)stream>>>(A);
+        reset_kernel<<<grid_for(env->n), kBlock, 0, (hipStream_t)stream>>>(A);
         HIP_TRY(hipGetLastError());
     }
     return SE_OK;

@@ -190,3 +190,23 @@ def test_shard_invariance():
     ppol = QPolicy(part, model)
     _OPEN.append(ppol)
     np.testing.assert_array_equal(ppol.act(0.5, 21).cpu().numpy(), full[2048:3072])
+
+
+@pytest.mark.parametrize("ports,steps", [(None, 0), (None, 40), ("64", 5), ("64", 30)])
+def test_compact_rows_choose_as_the_full_layout(ports, steps):
+    """Without q_out the kernel evaluates only the fc3 rows some env can ever take
+    (moves, SELECT, TAKE amounts up to the largest stock, in ascending action order);
+    with q_out it evaluates all of them. The two choose the same action for every env,
+    greedy and exploring."""
+    from conftest import golden_water
+    from shippingenv_amd.vec import random_water_ports
+
+    pp = random_water_ports(golden_water(), 64, seed=5) if ports else None
+    env, model, pol = make(8192 + 5, ports=pp, steps=steps, scale=20.0)
+    q_out = torch.empty((env.n, env.action_space_size), dtype=torch.float32, device=env.device)
+    for eps, t in ((0.0, 7), (0.3, 8)):
+        a_compact = pol.act(eps, t).clone()
+        a_full = pol.act(eps, t, q_out=q_out).clone()
+        assert torch.equal(a_compact, a_full), (eps, int((a_compact != a_full).sum()))
+    if not ports:
+        assert int((a_compact >= 4).sum()) > 0  # TAKE / SELECT rows were chosen
