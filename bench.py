@@ -298,6 +298,11 @@ def run_dqn(n, args, dist):
     torch_ms = e0.elapsed_time(e1) / 5
     flop_env = 2 * (env.obs_size * 128 + 128 * 128 + 128 * A)  # the reference network's MACs x 2
     achieved = flop_env * n / (pol_ms * 1e-3) / 1e12
+    # what the kernel issues per 32 envs at most: fc1 (the port block folded into the bias,
+    # one k-step per row tile), fc2, and fc3 over the compact rows
+    cmax = min(max(int(v) for v in env.port_cargo), 49)
+    fmax = min(max(int(v) for v in env.port_fuel), 199)
+    mfma_tile = 4 + 32 + 8 * ((4 + env.P + cmax + fmax + 31) // 32)
     pol.close()
     env.close()
     return {
@@ -311,7 +316,12 @@ def run_dqn(n, args, dist):
         "torch_unfused_policy_ms": round(torch_ms, 4),
         "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": BF16_DENSE_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4),
-                     "flop_per_env": flop_env, "traffic": None},
+                     "flop_per_env": flop_env, "traffic": None,
+                     "executed_mfma_per_32_envs": mfma_tile,
+                     "executed_tflops": round(mfma_tile * 32768 / 32 * n / (pol_ms * 1e-3) / 1e12, 1),
+                     "note": "achieved is on the reference network's FLOPs (all of fc3's rows, fc1's 26 "
+                             "inputs); the kernel issues at most executed_mfma_per_32_envs "
+                             "v_mfma_f32_32x32x16_bf16 per 32 envs"},
     }
 
 

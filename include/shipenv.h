@@ -219,6 +219,10 @@ int se_qnet_set_weights(se_qnet* q, const float* w1, const float* b1, const floa
  * the Q rows as computed, [n][ldq] f32, ldq >= A. */
 int se_policy(se_qnet* q, int32_t* actions, double epsilon, uint32_t t, float* q_out, int64_t ldq,
               void* stream);
+/* Repack from the device weights of the last se_qnet_set_weights (same tensors, new values:
+ * after an optimizer step). bump (optional, device int32): incremented once on the stream
+ * (a training loop's update counter, advanced where the new weights take effect). */
+int se_qnet_repack(se_qnet* q, int32_t* bump, void* stream);
 int se_qnet_destroy(se_qnet* q);  /* destroy a qnet before the env it was created on */
 
 /* DQN experience replay on the device (agents/dqn.py): remember (:117-123) into a ring of
@@ -236,6 +240,13 @@ int se_replay_begin(se_replay* r, const int32_t* actions, void* stream);
  * restart, i.e. the step raised or ep_len >= max_steps (max_steps > 0 needs an auto-reset
  * env, :281); pass it to se_reset. */
 int se_replay_end(se_replay* r, uint8_t* cut, int32_t max_steps, void* stream);
+/* The training loop's fused forms (one launch each instead of two):
+ * se_policy_record = se_policy (q_out NULL) + se_replay_begin with the chosen actions
+ * (remember's state and action, agents/dqn.py:117-123 and :285-291);
+ * se_replay_end_reset = se_replay_end + se_reset(cut): the cut episodes restart in the
+ * same pass, with the draws se_reset would make (the env's reset epoch advances). */
+int se_policy_record(se_qnet* q, se_replay* r, int32_t* actions, double epsilon, uint32_t t, void* stream);
+int se_replay_end_reset(se_replay* r, uint8_t* cut, int32_t max_steps, void* stream);
 int se_replay_size(se_replay* r, int64_t* size, int64_t* capacity);
 /* A minibatch of `batch` distinct transitions: batch position j takes logical index
  * perm(j) of a 4-round Feistel permutation of [0, size) keyed by Philox(seed, 2^64 - 1) at

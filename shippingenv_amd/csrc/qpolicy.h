@@ -100,8 +100,9 @@ struct PackArgs {
     const float *w1, *b1, *w2, *b2, *w3, *b3;
     const uint32_t* world;
     WorldDims dims;
-    QnetDims q;
-    uint8_t* img;
+    QnetDims q[2];  // blockIdx.y: the full layout, the compact one
+    uint8_t* img[2];
+    int32_t* bump;  // se_qnet_repack: a device counter advanced once, or null
 };
 
 // fc1 input column of fragment element j: x, y, fuel (hi), fuel (lo), "cargo" = fuel
@@ -113,7 +114,9 @@ __device__ __forceinline__ int fc1_col(int j) {
 __device__ __forceinline__ int acc_row(int s, int j, int h) { return 16 * s + 8 * (j >> 2) + 4 * h + (j & 3); }
 
 __global__ __launch_bounds__(256) void qnet_pack_kernel(PackArgs A) {
-    const QnetDims q = A.q;
+    const QnetDims q = A.q[blockIdx.y];
+    uint8_t* const img = A.img[blockIdx.y];
+    if (A.bump && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *A.bump += 1;
     const int in1 = q.in1();
     const int n_w1 = 4 * 64, n_w2 = 32 * 64, n_w3 = q.mt3 * 8 * 64;
     for (int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -127,7 +130,7 @@ __global__ __launch_bounds__(256) void qnet_pack_kernel(PackArgs A) {
                 const int row = f * 32 + r;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) v[j] = h == 0 ? (__bf16)A.w1[row * in1 + fc1_col(j)] : (__bf16)0.0f;
-                dst = A.img + q.w1() + f * 1024 + lane * 16;
+                dst = img + q.w1() + f * 1024 + lane * 16;
             } else {
                 const bool second = t < n_w1 + n_w2;
                 f -= second ? 4 : 4 + 32;  // fragment index ((mt*4 + kt)*2 + s)
@@ -139,7 +142,7 @@ __global__ __launch_bounds__(256) void qnet_pack_kernel(PackArgs A) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
                     v[j] = in ? (__bf16)W[wrow * kQHidden + kt * 32 + acc_row(s, j, h)] : (__bf16)0.0f;
-                dst = A.img + (second ? q.w2() : q.w3()) + f * 1024 + lane * 16;
+                dst = img + (second ? q.w2() : q.w3()) + f * 1024 + lane * 16;
             }
             *reinterpret_cast<bf16x8*>(dst) = v;
             continue;
@@ -155,16 +158,16 @@ __global__ __launch_bounds__(256) void qnet_pack_kernel(PackArgs A) {
                 acc += (double)w[0] * (double)wv.px(p) + (double)w[1] * (double)wv.py(p) +
                        (double)w[2] * (double)wv.pfuel(p) + (double)w[3] * (double)wv.pcargo(p);
             }
-            reinterpret_cast<float*>(A.img + q.b1())[u] = (float)acc;
+            reinterpret_cast<float*>(img + q.b1())[u] = (float)acc;
         } else if ((u -= kQHidden) < kQHidden) {
-            reinterpret_cast<float*>(A.img + q.b2())[u] = A.b2[u];
+            reinterpret_cast<float*>(img + q.b2())[u] = A.b2[u];
         } else if ((u -= kQHidden) < q.mt3 * 32) {
-            reinterpret_cast<float*>(A.img + q.b3())[u] = u < q.rows ? A.b3[q.action_of_row(u)] : 0.0f;
+            reinterpret_cast<float*>(img + q.b3())[u] = u < q.rows ? A.b3[q.action_of_row(u)] : 0.0f;
         } else if ((u -= q.mt3 * 32) < P) {  // next port on the same cell, ascending (-1: none)
             int nx = -1;
             for (int p = u + 1; p < P && nx < 0; ++p)
                 if (pos[p] == pos[u]) nx = p;
-            reinterpret_cast<int32_t*>(A.img + q.next())[u] = nx;
+            reinterpret_cast<int32_t*>(img + q.next())[u] = nx;
         } else {
             // fc3 tile mt = u - P: bit reg set when accumulator register reg (rows
             // base + (reg & 3) + 8 (reg >> 2) + 4h, h = 0, 1) can hold a valid action of
@@ -186,7 +189,7 @@ __global__ __launch_bounds__(256) void qnet_pack_kernel(PackArgs A) {
                                                      (a >= f_lo && a <= f_hi));
                     rm |= (uint32_t)ok << reg;
                 }
-            reinterpret_cast<uint32_t*>(A.img + q.regm())[mt] = rm;
+            reinterpret_cast<uint32_t*>(img + q.regm())[mt] = rm;
         }
     }
 }
@@ -205,6 +208,12 @@ struct PolicyArgs {
     int32_t* actions;
     float* q_out;
     int64_t ldq;
+    // remember's state and action (se_policy_record): the replay ring's s / a columns
+    // at slot (rec_head + env) mod rec_cap, or null
+    uint32_t* rec_pos;
+    float* rec_fuel;
+    int32_t* rec_act;
+    int64_t rec_head, rec_cap;
 };
 
 // accumulator initial value: bias rows (reg & 3) + 8 (reg >> 2) + 4h of a 32-row tile
@@ -409,6 +418,13 @@ __global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
                 }
             }
             A.actions[e] = act;
+            if (A.rec_pos) {  // replay_begin_kernel's record, from the state already in registers
+                int64_t slot = A.rec_head + e;
+                slot -= slot >= A.rec_cap ? A.rec_cap : 0;
+                A.rec_pos[slot] = cur_in.x | cur_in.y << 8 | cur_in.o8 << 16 | cur_in.d8 << 24;
+                A.rec_fuel[slot] = ff;
+                A.rec_act[slot] = act;
+            }
         }
         (void)dest;
     }
@@ -420,6 +436,7 @@ struct se_qnet {
     se_env* env = nullptr;  // must outlive the qnet (destroy the qnet first)
     int device = 0;
     QnetDims q{}, qc{};  // the full layout (q_out) and the compact one, whose image follows
+    const float* w[6] = {};  // the device weights of the last se_qnet_set_weights (se_qnet_repack)
     size_t c_off = 0;    // byte offset of the compact image
     uint8_t* d_img = nullptr;
     int img_bytes = 0;
@@ -461,19 +478,29 @@ int se_qnet_set_weights(se_qnet* qn, const float* w1, const float* b1, const flo
     qn->q = q;
     qn->qc = qc;
     qn->c_off = c_off;
-    for (int layout = 0; layout < 2; ++layout) {
-        PackArgs A{w1, b1, w2, b2, w3, b3, env->d_world, env->dims, layout ? qc : q,
-                   qn->d_img + (layout ? c_off : 0)};
-        qnet_pack_kernel<<<64, 256, 0, (hipStream_t)stream>>>(A);
-        HIP_TRY(hipGetLastError());
-    }
+    PackArgs A{w1, b1, w2, b2, w3, b3, env->d_world, env->dims, {q, qc}, {qn->d_img, qn->d_img + c_off},
+               nullptr};
+    qnet_pack_kernel<<<dim3(64, 2), 256, 0, (hipStream_t)stream>>>(A);  // both layouts, one launch
+    HIP_TRY(hipGetLastError());
+    const float* wp[6] = {w1, b1, w2, b2, w3, b3};
+    for (int i = 0; i < 6; ++i) qn->w[i] = wp[i];
     qn->world_version = env->world_version;
     qn->packed = true;
     return SE_OK;
 }
 
-int se_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, float* q_out, int64_t ldq,
-              void* stream) {
+}  // extern "C"
+
+namespace {
+struct PolicyRecord {
+    uint32_t* pos;
+    float* fuel;
+    int32_t* act;
+    int64_t head, cap;
+};
+
+int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, float* q_out, int64_t ldq,
+                  const PolicyRecord* rec, void* stream) {
     if (!qn) return fail(SE_EINVAL, "null qnet");
     se_env* env = qn->env;
     int rc = check_ready(env);
@@ -513,10 +540,40 @@ int se_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, float* 
     A.actions = actions;
     A.q_out = q_out;
     A.ldq = ldq;
+    if (rec) {
+        A.rec_pos = rec->pos;
+        A.rec_fuel = rec->fuel;
+        A.rec_act = rec->act;
+        A.rec_head = rec->head;
+        A.rec_cap = rec->cap;
+    }
     policy_kernel<<<grid, kPolicyBlock, lds, (hipStream_t)stream>>>(A);
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }
+}  // namespace
+
+extern "C" {
+
+int se_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, float* q_out, int64_t ldq,
+              void* stream) {
+    return launch_policy(qn, actions, epsilon, t, q_out, ldq, nullptr, stream);
+}
+
+int se_qnet_repack(se_qnet* qn, int32_t* bump, void* stream) {
+    if (!qn) return fail(SE_EINVAL, "null qnet");
+    if (!qn->packed) return fail(SE_ESTATE, "se_qnet_set_weights has not been called");
+    se_env* env = qn->env;
+    if (qn->world_version != env->world_version)
+        return fail(SE_ESTATE, "ports changed: call se_qnet_set_weights (the port block is folded into fc1)");
+    DeviceGuard g(env->device);
+    PackArgs A{qn->w[0], qn->w[1], qn->w[2], qn->w[3], qn->w[4], qn->w[5], env->d_world, env->dims,
+               {qn->q, qn->qc}, {qn->d_img, qn->d_img + qn->c_off}, bump};
+    qnet_pack_kernel<<<dim3(64, 2), 256, 0, (hipStream_t)stream>>>(A);
+    HIP_TRY(hipGetLastError());
+    return SE_OK;
+}
+
 
 int se_qnet_destroy(se_qnet* qn) {
     if (!qn) return SE_OK;

@@ -55,6 +55,13 @@ struct RecordArgs {
     Ring ring;
     uint8_t* cut;
     int32_t max_steps;
+    // se_replay_end_reset: reset() the cut envs in the same pass, exactly as se_reset(cut)
+    // would (reset_kernel: Philox(seed, env) at (epoch, slot 5)); world null otherwise
+    const uint32_t* world;
+    WorldDims dims;
+    uint64_t seed;
+    int64_t env_base;
+    uint32_t epoch;
 };
 
 // s and a of every env, before se_step (remember's state, action)
@@ -80,7 +87,26 @@ __global__ __launch_bounds__(kBlock) void replay_end_kernel(RecordArgs A) {
         A.ring.flags[slot] = (uint8_t)((A.st.done[i] ? kRecDone : 0) | (raised ? kRecInvalid : 0));
         A.ring.n_pos[slot] = pack_pos(A.st, i);
         A.ring.n_fuel[slot] = (float)A.st.fuel[i];
-        if (A.cut) A.cut[i] = (uint8_t)(raised | (A.max_steps > 0 && A.st.ep_len[i] >= A.max_steps));
+        if (!A.cut) continue;
+        const bool cut = raised | (A.max_steps > 0 && A.st.ep_len[i] >= A.max_steps);
+        A.cut[i] = (uint8_t)cut;
+        if (A.world && cut) {  // reset_kernel's body for this env
+            const LdsWorld w = world_view(A.dims, A.world);
+            const U4 o = draw(env_key(A.seed, A.env_base + i), A.epoch, kSlotExplicitReset);
+            Ship s;
+            reset_ship(w, s, o.v[0], o.v[1]);
+            A.st.x[i] = (uint8_t)s.x;
+            A.st.y[i] = (uint8_t)s.y;
+            A.st.fuel[i] = s.fuel;
+            A.st.cargo[i] = s.cargo;
+            A.st.origin[i] = (uint8_t)s.origin;
+            A.st.dest[i] = (uint8_t)s.dest;
+            if (A.st.ep_return) A.st.ep_return[i] = 0.0f;
+            if (A.st.ep_len) A.st.ep_len[i] = 0;
+            A.st.done[i] = 0;
+            A.st.err[i] = 0;
+            A.st.reward[i] = 0.0f;
+        }
     }
 }
 
@@ -256,7 +282,7 @@ int se_replay_begin(se_replay* r, const int32_t* actions, void* stream) {
     if (r->open) return fail(SE_ESTATE, "se_replay_begin twice without se_replay_end");
     se_env* env = r->env;
     DeviceGuard g(env->device);
-    RecordArgs A{env->n, r->cap, r->head, 0, env->st, actions, r->ring, nullptr, 0};
+    RecordArgs A{env->n, r->cap, r->head, 0, env->st, actions, r->ring, nullptr, 0, nullptr, {}, 0, 0, 0};
     if (env->n > 0) {
         replay_begin_kernel<<<grid_for(env->n), kBlock, 0, (hipStream_t)stream>>>(A);
         HIP_TRY(hipGetLastError());
@@ -265,7 +291,10 @@ int se_replay_begin(se_replay* r, const int32_t* actions, void* stream) {
     return SE_OK;
 }
 
-int se_replay_end(se_replay* r, uint8_t* cut, int32_t max_steps, void* stream) {
+}  // extern "C"
+
+namespace {
+int replay_end(se_replay* r, uint8_t* cut, int32_t max_steps, bool reset_cut, void* stream) {
     if (!r) return fail(SE_EINVAL, "null replay");
     int rc = check_ready(r->env);
     if (rc) return rc;
@@ -273,14 +302,41 @@ int se_replay_end(se_replay* r, uint8_t* cut, int32_t max_steps, void* stream) {
     se_env* env = r->env;
     if (max_steps > 0 && (!cut || !env->st.ep_len))
         return fail(SE_EINVAL, "max_steps needs a cut buffer and an auto-reset env (ep_len)");
+    if (reset_cut && !cut) return fail(SE_EINVAL, "se_replay_end_reset needs a cut buffer");
+    if (reset_cut && env->dims.P < 2) return fail(SE_EINVAL, "reset needs at least two ports");
     DeviceGuard g(env->device);
     const int64_t new_size = std::min(r->size + env->n, r->cap);
-    RecordArgs A{env->n, r->cap, r->head, new_size, env->st, nullptr, r->ring, cut, max_steps};
+    RecordArgs A{env->n, r->cap, r->head, new_size, env->st, nullptr, r->ring, cut, max_steps,
+                 reset_cut ? env->d_world : nullptr, env->dims, env->seed, env->env_base,
+                 (uint32_t)env->epoch};
     replay_end_kernel<<<grid_for(std::max<int64_t>(env->n, 1)), kBlock, 0, (hipStream_t)stream>>>(A);
     HIP_TRY(hipGetLastError());
+    if (reset_cut) env->epoch += 1;  // as se_reset
     r->head = (r->head + env->n) % r->cap;
     r->size = new_size;
     r->open = false;
+    return SE_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int se_replay_end(se_replay* r, uint8_t* cut, int32_t max_steps, void* stream) {
+    return replay_end(r, cut, max_steps, false, stream);
+}
+
+int se_replay_end_reset(se_replay* r, uint8_t* cut, int32_t max_steps, void* stream) {
+    return replay_end(r, cut, max_steps, true, stream);
+}
+
+int se_policy_record(se_qnet* qn, se_replay* r, int32_t* actions, double epsilon, uint32_t t, void* stream) {
+    if (!qn || !r) return fail(SE_EINVAL, "null qnet / replay");
+    if (qn->env != r->env) return fail(SE_EINVAL, "the qnet and the replay belong to different envs");
+    if (r->open) return fail(SE_ESTATE, "se_replay_begin twice without se_replay_end");
+    const PolicyRecord rec{r->ring.s_pos, r->ring.s_fuel, r->ring.act, r->head, r->cap};
+    const int rc = launch_policy(qn, actions, epsilon, t, nullptr, 0, &rec, stream);
+    if (rc) return rc;
+    r->open = true;
     return SE_OK;
 }
 

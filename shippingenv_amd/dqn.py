@@ -91,9 +91,12 @@ class ReplayBuffer:
         self._act = actions  # kept alive until the launch has run
         N.check(N.lib().se_replay_begin(self._h, _ptr(actions), self.env._stream()))
 
-    def end(self, cut: torch.Tensor | None = None, max_steps: int = 0):
-        """reward, done and next_state, after env.step; cut[i] = 1 where the episode must restart."""
-        N.check(N.lib().se_replay_end(self._h, _ptr(cut), int(max_steps), self.env._stream()))
+    def end(self, cut: torch.Tensor | None = None, max_steps: int = 0, reset: bool = False):
+        """reward, done and next_state, after env.step; cut[i] = 1 where the episode must restart.
+        reset: also restart those episodes in the same pass (se_replay_end_reset: what
+        env.reset(cut) would do, one launch instead of two)."""
+        fn = N.lib().se_replay_end_reset if reset else N.lib().se_replay_end
+        N.check(fn(self._h, _ptr(cut), int(max_steps), self.env._stream()))
 
     def sample(self, out: MiniBatch, t: int = 0, t_dev: torch.Tensor | None = None) -> MiniBatch:
         """update()'s minibatch (agents/dqn.py:213-224) into `out`; the sampler key is t, or
@@ -251,8 +254,8 @@ class VecDQNAgent:
             loss.backward()
             self.optimizer.step()
             self._loss.copy_(loss.detach())
-        self._ctr.add_(1)
-        self.policy.set_weights()  # the next choose_action sees the new weights
+        # the next choose_action sees the new weights; the update counter advances in the same launch
+        self.policy.repack(bump=self._ctr)
 
     def _capture(self):
         for p in self.model.parameters():  # static gradient buffers for the graph (torch path)
@@ -292,11 +295,12 @@ class VecDQNAgent:
     def step(self):
         """One training-loop iteration for every env; returns the last update's loss (or None)."""
         env = self.env
-        a = self.choose_actions()
-        self.memory.begin(a)
+        # choose_action + remember(state, action): one launch (se_policy_record)
+        a = self.policy.act_record(self.memory, self.epsilon, self.t)
         env.step(a)
-        self.memory.end(self.cut, self.max_steps)
-        env.reset(self.cut)  # episodes that raised or reached max_steps start over
+        # remember's reward / next_state, and the episodes that raised or reached max_steps
+        # start over (env.reset(cut)): one launch (se_replay_end_reset)
+        self.memory.end(self.cut, self.max_steps, reset=True)
         loss = None
         for _ in range(self.updates_per_step):
             loss = self.update()

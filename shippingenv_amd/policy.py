@@ -63,6 +63,19 @@ class QPolicy:
             m.fc1.weight, m.fc1.bias, m.fc2.weight, m.fc2.bias, m.fc3.weight, m.fc3.bias)]
         N.check(N.lib().se_qnet_set_weights(self._h, *[_ptr(t) for t in self._w], self.env._stream()))
 
+    def repack(self, bump: torch.Tensor | None = None):
+        """Repack the same weight tensors after their values changed in place (an optimizer
+        step); bump (device int32 [1]) is advanced by one on the stream (se_qnet_repack)."""
+        N.check(N.lib().se_qnet_repack(self._h, _ptr(bump) if bump is not None else None, self.env._stream()))
+
+    def act_record(self, replay, epsilon: float = 0.0, t: int = 0):
+        """act() plus the replay ring's remember(state, action) in the same launch
+        (se_policy_record; replay: shippingenv_amd.dqn.ReplayBuffer)."""
+        N.check(N.lib().se_policy_record(self._h, replay._h, _ptr(self.actions), float(epsilon),
+                                         int(t) & 0xFFFFFFFF, self.env._stream()))
+        replay._act = self.actions
+        return self.actions
+
     def act(self, epsilon: float = 0.0, t: int = 0, q_out: torch.Tensor | None = None):
         """int32 actions [n] in the agent-index encoding (VecEnv.step input).
         q_out: optional f32 [n, >= A] to receive the Q rows (testing / inspection)."""

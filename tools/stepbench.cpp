@@ -60,6 +60,7 @@ int main(int argc, char** argv) {
     int64_t n = 1 << 20;
     int config = 3, steps = 1000, rows = 0, warm = 20;  // rows > 0: cycle through that many action rows
     bool gen_late = false;  // generate the timed rows after the warm-up steps (right before timing)
+    bool per_launch = false;  // also print every timed launch's own event-pair duration
     std::vector<std::string> libs;
     for (int i = 1; i < argc; ++i) {
         if (!strcmp(argv[i], "--n")) n = atoll(argv[++i]);
@@ -68,6 +69,7 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--rows")) rows = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--warm")) warm = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--gen-late")) gen_late = true;
+        else if (!strcmp(argv[i], "--per-launch")) per_launch = true;
         else libs.push_back(argv[i]);
     }
     FILE* f = fopen("shippingenv_amd/data/mapa_mundi_binario.jpg", "rb");
@@ -161,11 +163,27 @@ int main(int argc, char** argv) {
         CK(hipEventCreate(&e0));
         CK(hipEventCreate(&e1));
         CK(hipStreamSynchronize(s));
+        std::vector<hipEvent_t> ev(per_launch ? steps + 1 : 0);
+        for (auto& e : ev) CK(hipEventCreate(&e));
         CK(hipEventRecord(e0, s));
         const int r = rows > 0 && rows < steps ? rows : steps;
-        for (int t = 0; t < steps; ++t) SE(a.step(env, acts + (size_t)(warm + t % r) * n, s));
+        for (int t = 0; t < steps; ++t) {
+            if (per_launch) CK(hipEventRecord(ev[t], s));
+            SE(a.step(env, acts + (size_t)(warm + t % r) * n, s));
+        }
+        if (per_launch) CK(hipEventRecord(ev[steps], s));
         CK(hipEventRecord(e1, s));
         CK(hipEventSynchronize(e1));
+        if (per_launch) {
+            printf("{\"per_launch_us\": [");
+            for (int t = 0; t < steps; ++t) {
+                float m = 0.f;
+                CK(hipEventElapsedTime(&m, ev[t], ev[t + 1]));
+                printf("%s%.2f", t ? ", " : "", 1000.0 * m);
+            }
+            printf("]}\n");
+            for (auto& e : ev) CK(hipEventDestroy(e));
+        }
         float ms = 0.f;
         CK(hipEventElapsedTime(&ms, e0, e1));
         const char* base = strrchr(path.c_str(), '/');

@@ -3,7 +3,8 @@
     python tools/time_train.py [--n N] [--batch B] [--iters K] [--eager]
 
 Prints one JSON line: HIP-event ms per iteration of each part on the launch stream
-(policy, replay begin, step, replay end, reset of cut envs, update) and the whole loop.
+(the fused launches VecDQNAgent.step makes, or with --separate the policy, replay begin,
+step, replay end and reset of cut envs), the update, and the whole loop.
 """
 import argparse
 import json
@@ -22,6 +23,9 @@ def main():
     p.add_argument("--batch", type=int, default=8192)
     p.add_argument("--iters", type=int, default=30)
     p.add_argument("--eager", action="store_true", help="no graph capture of the update")
+    p.add_argument("--separate", action="store_true",
+                   help="time the separate launches (policy, begin, step, end, reset) instead of the "
+                        "fused ones VecDQNAgent.step uses (policy + begin, step, end + reset)")
     a = p.parse_args()
     from shippingenv_amd.dqn import VecDQNAgent
     from shippingenv_amd.vec import VecEnv
@@ -34,7 +38,8 @@ def main():
         agent.step()
     torch.cuda.synchronize()
     s = torch.cuda.current_stream()
-    parts = ("policy", "begin", "step", "end", "reset", "update")
+    parts = ("policy", "begin", "step", "end", "reset", "update") if a.separate else \
+        ("policy_record", "step", "end_reset", "update")
     ev = {k: [] for k in parts}
 
     def mark(name, fn):
@@ -48,11 +53,16 @@ def main():
     g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     g0.record(s)
     for _ in range(a.iters):
-        act = mark("policy", agent.choose_actions)
-        mark("begin", lambda: agent.memory.begin(act))
-        mark("step", lambda: env.step(act))
-        mark("end", lambda: agent.memory.end(agent.cut, agent.max_steps))
-        mark("reset", lambda: env.reset(agent.cut))
+        if a.separate:
+            act = mark("policy", agent.choose_actions)
+            mark("begin", lambda: agent.memory.begin(act))
+            mark("step", lambda: env.step(act))
+            mark("end", lambda: agent.memory.end(agent.cut, agent.max_steps))
+            mark("reset", lambda: env.reset(agent.cut))
+        else:
+            act = mark("policy_record", lambda: agent.policy.act_record(agent.memory, agent.epsilon, agent.t))
+            mark("step", lambda: env.step(act))
+            mark("end_reset", lambda: agent.memory.end(agent.cut, agent.max_steps, reset=True))
         mark("update", agent.update)
         agent.t += 1
     g1.record(s)
