@@ -45,7 +45,14 @@ constexpr int kQHidden = 128;     // DQNNetwork hidden_size (dqn.py:24, default 
 #ifndef SHIPENV_POLICY_BLOCK
 #define SHIPENV_POLICY_BLOCK 1024
 #endif
+#ifndef SHIPENV_POLICY_WG_PER_CU
+#define SHIPENV_POLICY_WG_PER_CU 1  // resident workgroups per CU (each stages its own network copy)
+#endif
+#ifndef SHIPENV_POLICY_WAVES_PER_EU
+#define SHIPENV_POLICY_WAVES_PER_EU 0  // 0: the compiler's choice from the block size
+#endif
 constexpr int kPolicyBlock = SHIPENV_POLICY_BLOCK;
+constexpr int kPolicyWgPerCu = SHIPENV_POLICY_WG_PER_CU;
 constexpr int kPolicyWaves = kPolicyBlock / 64;
 
 // Packed network image (bytes). Fragments are 64 lanes x 8 bf16 = 1 KB.
@@ -244,7 +251,11 @@ __device__ __forceinline__ uint32_t range_bits(int lo, int hi) {
     return lo > hi ? 0u : (top & ~low);
 }
 
-__global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
+__global__ __launch_bounds__(kPolicyBlock)
+#if SHIPENV_POLICY_WAVES_PER_EU
+__attribute__((amdgpu_waves_per_eu(SHIPENV_POLICY_WAVES_PER_EU)))
+#endif
+void policy_kernel(PolicyArgs A) {
     extern __shared__ uint4 smem[];
     const QnetDims q = A.q;
     const int qwords = q.bytes() / 16;
@@ -307,24 +318,33 @@ __global__ __launch_bounds__(kPolicyBlock) void policy_kernel(PolicyArgs A) {
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(W1f[mt * 64 + lane], ob, c, 0, 0, 0);
             relu_pack(c, h1[mt]);
         }
-        {  // fc2 + relu: the 4 row tiles advance together, so consecutive MFMAs are
-           // independent and each k-step's 4 fragments are read in one batch
-            f32x16 c2[4];
+#ifndef SHIPENV_FC2_SPLIT
+#define SHIPENV_FC2_SPLIT 4  // one pass per row tile: no spills at 128 VGPRs (2 passes spill 7, 1 spills 14)
+#endif
+        // fc2 + relu in SHIPENV_FC2_SPLIT passes over the 4 row tiles: the tiles of a pass
+        // advance together (consecutive MFMAs independent, a k-step's fragments read in one
+        // batch); with two passes the accumulators take 32 VGPRs instead of 64 and the
+        // first pass's relu can issue in the shadow of the second pass's MFMAs
+        constexpr int kFc2Tiles = 4 / SHIPENV_FC2_SPLIT;
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt) c2[mt] = bias_frag(B2 + mt * 32 + 4 * h);
+        for (int pass = 0; pass < SHIPENV_FC2_SPLIT; ++pass) {
+            f32x16 c2[kFc2Tiles];
+#pragma unroll
+            for (int i = 0; i < kFc2Tiles; ++i) c2[i] = bias_frag(B2 + (pass * kFc2Tiles + i) * 32 + 4 * h);
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
-                    bf16x8 wf[4];
+                    bf16x8 wf[kFc2Tiles];
 #pragma unroll
-                    for (int mt = 0; mt < 4; ++mt) wf[mt] = W2f[((mt * 4 + kt) * 2 + s) * 64 + lane];
+                    for (int i = 0; i < kFc2Tiles; ++i)
+                        wf[i] = W2f[(((pass * kFc2Tiles + i) * 4 + kt) * 2 + s) * 64 + lane];
 #pragma unroll
-                    for (int mt = 0; mt < 4; ++mt)
-                        c2[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[mt], h1[kt][s], c2[mt], 0, 0, 0);
+                    for (int i = 0; i < kFc2Tiles; ++i)
+                        c2[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i], h1[kt][s], c2[i], 0, 0, 0);
                 }
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt) relu_pack(c2[mt], h2[mt]);
+            for (int i = 0; i < kFc2Tiles; ++i) relu_pack(c2[i], h2[pass * kFc2Tiles + i]);
         }
 
         // is_valid_action (dqn.py:125-175): moves always; SELECT p at the ship's cell
@@ -525,7 +545,8 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
         dev_cus = 256;
     const int64_t tiles = (env->n + 31) / 32;
     const int64_t want = (tiles + kPolicyWaves - 1) / kPolicyWaves;
-    const int grid = (int)(want < dev_cus ? want : dev_cus);  // one resident workgroup per CU
+    const int64_t resident = (int64_t)dev_cus * kPolicyWgPerCu;  // workgroups resident at once
+    const int grid = (int)(want < resident ? want : resident);
     PolicyArgs A{};
     A.world = env->d_world;
     A.dims = env->dims;
