@@ -1663,6 +1663,70 @@ __global__ __launch_bounds__(kBlock) void observe_kernel(ObsArgs A) {
     }
 }
 
+// Rows of a 256-row tile are contiguous in a dense [n][W] output, so a workgroup
+// builds its tile's values once and writes them with 16-byte stores in address order
+// (every wave store a full 1 KB run). The generic kernels above / below (one thread per
+// output element or byte) serve any other row stride; they measured 117 us (observe,
+// P = 5) and 321 us (mask) at 2^20 envs against 22 us and 7 us of HBM writes.
+constexpr int kTileRows = 256;  // = kBlock: one row per thread in the per-row phase
+
+// x / W for x < kTileRows * W, W <= 1022, as one multiply-high (exact: checked for every
+// such x and W)
+__device__ __forceinline__ uint32_t div_tile(uint32_t x, uint32_t magic) { return __umulhi(x, magic); }
+
+// preprocess_state rows, dense ld == W = 6 + 4P: the tile's ship columns (6 floats a row)
+// and the constant port block (4P floats) in LDS, then float4 stores
+__global__ __launch_bounds__(kBlock) void observe_tiled_kernel(ObsArgs A, uint32_t magic) {
+    extern __shared__ float olds[];
+    const LdsWorld w = world_view(A.dims, A.world);  // only the port table is read
+    const int W = 6 + 4 * w.P;
+    float* ship = olds;                  // [kTileRows][6]
+    float* pblk = olds + kTileRows * 6;  // [4P]
+    for (int c = threadIdx.x; c < 4 * w.P; c += kBlock) {
+        const int p = c >> 2, f = c & 3;
+        pblk[c] = f == 0 ? (float)w.px(p) : f == 1 ? (float)w.py(p) : f == 2 ? (float)w.pfuel(p) : (float)w.pcargo(p);
+    }
+    for (int64_t r0 = (int64_t)blockIdx.x * kTileRows; r0 < A.n; r0 += (int64_t)gridDim.x * kTileRows) {
+        const int rows = (int)min((int64_t)kTileRows, A.n - r0);
+        __syncthreads();  // the previous tile's reads of `ship` are done
+        if ((int)threadIdx.x < rows) {
+            const int64_t i = r0 + threadIdx.x;
+            const float fuel = (float)A.st.fuel[i];  // "cargo" is self.fuel (environment.py:206)
+            const uint8_t o = A.st.origin[i], d = A.st.dest[i];
+            float* sr = ship + threadIdx.x * 6;
+            sr[0] = (float)A.st.x[i];
+            sr[1] = (float)A.st.y[i];
+            sr[2] = fuel;
+            sr[3] = fuel;
+            sr[4] = o == SE_NONE ? -1.0f : (float)o;
+            sr[5] = d == SE_NONE ? -1.0f : (float)d;
+        }
+        __syncthreads();
+        const uint32_t nf = (uint32_t)(rows * W);  // W is even: whole float4 runs when rows is
+        float4* out = reinterpret_cast<float4*>(A.obs + r0 * W);
+        for (uint32_t q = threadIdx.x; 4 * q < nf; q += kBlock) {
+            const uint32_t j = 4 * q;
+            uint32_t r = div_tile(j, magic);
+            int c = (int)(j - r * W);
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                v[e] = c < 6 ? ship[r * 6 + c] : pblk[c - 6];
+                if (++c == W) {
+                    c = 0;
+                    ++r;
+                }
+            }
+            if (j + 4 <= nf) {
+                out[q] = make_float4(v[0], v[1], v[2], v[3]);
+            } else {  // the last run of a ragged tile: 2 floats (rows * W is even)
+                A.obs[r0 * W + j] = v[0];
+                A.obs[r0 * W + j + 1] = v[1];
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ DQN validity mask
 // agents/dqn.py:125-175, one thread per output byte (8 agent indices).
 struct MaskArgs {
@@ -1705,6 +1769,65 @@ __global__ __launch_bounds__(kBlock) void valid_mask_kernel(MaskArgs A) {
             out |= (uint32_t)v << (7 - bit);
         }
         A.bits[k] = (uint8_t)out;
+    }
+}
+
+// bits i of [0, 32) with lo <= i <= hi (lo, hi any ints)
+__device__ __forceinline__ uint32_t bits_in(int lo, int hi) {
+    lo = max(lo, 0);
+    hi = min(hi, 31);
+    if (lo > hi) return 0u;
+    const uint32_t top = hi >= 31 ? 0xffffffffu : ((1u << (hi + 1)) - 1u);
+    return top & ~((1u << lo) - 1u);
+}
+
+// is_valid_action bits, dense rows of S bytes: each thread builds its row 32 actions at a
+// time (a word whose bit o is action 32k + o, then bit-reversed and byte-swapped into the
+// MSB-first byte order of np.packbits), writes its S bytes into the LDS tile, then the
+// workgroup stores the tile with 16-byte writes.
+__global__ __launch_bounds__(kBlock) void valid_mask_tiled_kernel(MaskArgs A) {
+    extern __shared__ uint8_t mlds[];  // [kTileRows][S] (+ pad to 16 bytes)
+    const LdsWorld w = world_view(A.dims, A.world);
+    const int P = w.P, S = A.stride, nw = (S + 3) / 4;
+    const int c_lo = 5 + P, f_lo = 55 + P;  // TAKE_CARGO / TAKE_FUEL amount 1
+    for (int64_t r0 = (int64_t)blockIdx.x * kTileRows; r0 < A.n; r0 += (int64_t)gridDim.x * kTileRows) {
+        const int rows = (int)min((int64_t)kTileRows, A.n - r0);
+        __syncthreads();  // the previous tile's stores have read the LDS tile
+        if ((int)threadIdx.x < rows) {
+            const int64_t i = r0 + threadIdx.x;
+            const int x = A.st.x[i], y = A.st.y[i];
+            const int origin = A.st.origin[i] == SE_NONE ? -1 : A.st.origin[i];
+            const int cur = w.port_at(x, y);  // the first port on the ship's cell
+            const int cst = cur >= 0 ? w.pcargo(cur) : 0, fst = cur >= 0 ? w.pfuel(cur) : 0;
+            const uint32_t spos = (uint32_t)x | ((uint32_t)y << 16);
+            uint8_t* row = mlds + threadIdx.x * S;
+            for (int k = 0; k < nw; ++k) {
+                const int b = 32 * k;
+                uint32_t m = bits_in(-b, 3 - b);  // moves: always
+                if (cur >= 0) {
+                    m |= bits_in(c_lo - b, c_lo + min(cst, 49) - 1 - b) | bits_in(f_lo - b, f_lo + min(fst, 199) - 1 - b);
+                    // SELECT p: every port on the ship's cell but the origin (dqn.py:152-161)
+                    const int p0 = max(cur, b - 4), p1 = min(P, b + 28);
+                    for (int p = p0; p < p1; ++p)
+                        if (w.pos[p] == spos && p != origin) m |= 1u << (4 + p - b);
+                }
+                const uint32_t word = __builtin_amdgcn_perm(0u, __builtin_bitreverse32(m), 0x00010203u);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (4 * k + j < S) row[4 * k + j] = (uint8_t)(word >> (8 * j));
+            }
+        }
+        __syncthreads();
+        const uint32_t nb = (uint32_t)(rows * S);
+        uint8_t* out = A.bits + r0 * S;
+        const uint4* src = reinterpret_cast<const uint4*>(mlds);
+        for (uint32_t q = threadIdx.x; 16 * q < nb; q += kBlock) {
+            if (16 * q + 16 <= nb) {
+                reinterpret_cast<uint4*>(out)[q] = src[q];
+            } else {
+                for (uint32_t b = 16 * q; b < nb; ++b) out[b] = mlds[b];
+            }
+        }
     }
 }
 
@@ -2250,11 +2373,17 @@ int se_observe(se_env* env, float* obs, int64_t ld, void* stream) {
     if (!obs || ld < 6 + 4 * (int64_t)env->dims.P) return fail(SE_EINVAL, "bad obs buffer / ld");
     DeviceGuard g(env->device);
     ObsArgs A{env->d_world, env->dims, env->n, ld, env->st, obs};
-    const int64_t total = env->n * (6 + 4 * (int64_t)env->dims.P);
-    if (total > 0) {
+    const int64_t W = 6 + 4 * (int64_t)env->dims.P;
+    const int64_t total = env->n * W;
+    if (total == 0) return SE_OK;
+    if (ld == W && aligned16(obs) && W <= 1022) {  // dense rows: the tiled kernel
+        const uint32_t magic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)W - 1) / (uint64_t)W);
+        const size_t lds = (size_t)(kTileRows * 6 + 4 * env->dims.P) * sizeof(float);
+        observe_tiled_kernel<<<grid_for(env->n), kBlock, lds, (hipStream_t)stream>>>(A, magic);
+    } else {
         observe_kernel<<<grid_for(total), kBlock, lds_bytes(env), (hipStream_t)stream>>>(A);
-        HIP_TRY(hipGetLastError());
     }
+    HIP_TRY(hipGetLastError());
     return SE_OK;
 }
 
@@ -2266,10 +2395,14 @@ int se_valid_mask(se_env* env, uint8_t* bits, void* stream) {
     const int32_t stride = (4 + env->dims.P + 250 + 7) / 8;
     MaskArgs A{env->d_world, env->dims, env->n, stride, env->st, bits};
     const int64_t total = env->n * stride;
-    if (total > 0) {
+    if (total == 0) return SE_OK;
+    if (aligned16(bits)) {  // the tiled kernel (rows are always dense here)
+        const size_t lds = ((size_t)kTileRows * stride + 15) & ~(size_t)15;
+        valid_mask_tiled_kernel<<<grid_for(env->n), kBlock, lds, (hipStream_t)stream>>>(A);
+    } else {
         valid_mask_kernel<<<grid_for(total), kBlock, lds_bytes(env), (hipStream_t)stream>>>(A);
-        HIP_TRY(hipGetLastError());
     }
+    HIP_TRY(hipGetLastError());
     return SE_OK;
 }
 

@@ -258,6 +258,38 @@ def test_observe_and_valid_mask_vs_oracle(oracle_mod):
     env.close()
 
 
+@pytest.mark.parametrize("ports64", [False, True])
+def test_tiled_and_generic_observe_and_mask_agree(oracle_mod, water, ports64):
+    """Dense, 16-byte aligned outputs take the tiled kernels (a 256-row tile built in LDS,
+    written with 16-byte stores); any other row stride or alignment the generic ones. Both
+    equal the oracle, with ragged last tiles (n = 2 * 256 + 77) and at P = 64."""
+    from shippingenv_amd.vec import random_water_ports
+
+    O = oracle_mod
+    n, seed = 2 * 256 + 77, 9
+    ports = random_water_ports(water, 64, seed=4) if ports64 else None
+    env = VecEnv(n, seed=seed, ports=ports)
+    world, st = _oracle_pair(O, env)
+    env.reset()
+    O.reset(world, st, seed=seed, epoch=0)
+    for t in range(12):
+        env.step(env.gen_actions(t))
+        O.step(world, st, actions=O.gen_actions(n, env.P, seed, 0, t), seed=seed, t=t)
+    want_obs, want_bits = O.observe(world, st), O.valid_mask(world, st)
+    W, S = env.obs_size, want_bits.shape[1]
+    np.testing.assert_array_equal(env.observe().cpu().numpy(), want_obs)  # tiled
+    wide = torch.full((n, W + 2), -7.0, dtype=torch.float32, device=env.device)
+    env.observe(wide)  # ld = W + 2: the generic kernel
+    np.testing.assert_array_equal(wide[:, :W].cpu().numpy(), want_obs)
+    assert bool((wide[:, W:] == -7.0).all())
+    np.testing.assert_array_equal(env.valid_mask().cpu().numpy(), want_bits)  # tiled
+    raw = torch.zeros(n * S + 16, dtype=torch.uint8, device=env.device)
+    odd = raw[1:1 + n * S].view(n, S)  # not 16-byte aligned: the generic kernel
+    env.valid_mask(odd)
+    np.testing.assert_array_equal(odd.cpu().numpy(), want_bits)
+    env.close()
+
+
 def test_observe_and_valid_mask_vs_golden(water):
     z = load_golden(os.path.join(GOLDEN, "tape_seed0.npz"))
     k = len(z["valid_bits"])
