@@ -23,10 +23,15 @@ def main():
     p.add_argument("--batch", type=int, default=8192)
     p.add_argument("--iters", type=int, default=30)
     p.add_argument("--eager", action="store_true", help="no graph capture of the update")
+    p.add_argument("--lib", default=None)
     p.add_argument("--separate", action="store_true",
                    help="time the separate launches (policy, begin, step, end, reset) instead of the "
                         "fused ones VecDQNAgent.step uses (policy + begin, step, end + reset)")
     a = p.parse_args()
+    if a.lib:
+        from shippingenv_amd import _native
+
+        _native.LIB_PATH = os.path.abspath(a.lib)
     from shippingenv_amd.dqn import VecDQNAgent
     from shippingenv_amd.vec import VecEnv
 
@@ -67,7 +72,7 @@ def main():
         agent.t += 1
     g1.record(s)
     torch.cuda.synchronize()
-    out = {"n": a.n, "batch": a.batch, "graph": not a.eager,
+    out = {"lib": os.path.basename(a.lib or "default"), "n": a.n, "batch": a.batch, "graph": not a.eager,
            "loop_ms": round(g0.elapsed_time(g1) / a.iters, 4)}
     for k in parts:
         out[k + "_ms"] = round(sum(x.elapsed_time(y) for x, y in ev[k]) / a.iters, 4)
