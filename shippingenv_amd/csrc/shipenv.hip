@@ -1888,9 +1888,18 @@ struct SampleArgs {
     int32_t* b;
 };
 
+#ifndef SHIPENV_SAMPLE_STAGE
+#define SHIPENV_SAMPLE_STAGE 0  // 1: stage the world image per workgroup (the round-1 form)
+#endif
+// One cell-code byte and one stock per env: read in place through L1 / L2 instead of
+// staging the 10.8 KB image into every one of up to 2048 workgroups.
 __global__ __launch_bounds__(kBlock) void sample_kernel(SampleArgs A) {
+#if SHIPENV_SAMPLE_STAGE
     extern __shared__ uint32_t lds[];
     const LdsWorld w = stage_world(A.world, A.dims, lds);
+#else
+    const LdsWorld w = world_view(A.dims, A.world);
+#endif
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < A.n;
          i += (int64_t)gridDim.x * kBlock) {
         const Ship s{A.st.x[i], A.st.y[i], A.st.fuel[i], A.st.cargo[i], A.st.origin[i], A.st.dest[i]};
@@ -2426,7 +2435,7 @@ int se_sample_actions(se_env* env, int32_t* type, int32_t* a, int32_t* b, uint32
     if (env->n == 0) return SE_OK;
     DeviceGuard g(env->device);
     SampleArgs A{env->d_world, env->dims, env->n, env->env_base, env->seed, t, env->st, type, a, b};
-    sample_kernel<<<grid_for(env->n), kBlock, lds_bytes(env), (hipStream_t)stream>>>(A);
+    sample_kernel<<<grid_for(env->n), kBlock, SHIPENV_SAMPLE_STAGE ? lds_bytes(env) : 0, (hipStream_t)stream>>>(A);
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }

@@ -1,5 +1,6 @@
-"""Time the observation gather (se_observe: preprocess_state rows) and the DQN validity
-mask (se_valid_mask) at N envs, against the HBM bytes each writes.
+"""Time the observation gather (se_observe: preprocess_state rows), the DQN validity
+mask (se_valid_mask) and the random policy (se_sample_actions) at N envs, against the
+HBM bytes each writes.
 
     python tools/time_obs.py [--n N] [--ports 5|64] [--reps K] [--lib path]
 """
@@ -35,10 +36,12 @@ def main():
         env.step(env.gen_actions(t))
     obs = env.observe()
     bits = env.valid_mask()
+    smp = env.sample_actions(7)
     s = torch.cuda.current_stream()
     out = {"lib": os.path.basename(a.lib or "default"), "n": a.n, "P": env.P}
     for name, fn, nbytes in (("observe", lambda: env.observe(obs), obs.numel() * 4),
-                             ("valid_mask", lambda: env.valid_mask(bits), bits.numel())):
+                             ("valid_mask", lambda: env.valid_mask(bits), bits.numel()),
+                             ("sample_actions", lambda: env.sample_actions(7, smp), 12 * env.n)):
         fn()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
