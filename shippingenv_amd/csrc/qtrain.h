@@ -206,6 +206,24 @@ struct QtStepArgs {
     float gamma;
 };
 
+#ifndef SHIPENV_QTRACE
+#define SHIPENV_QTRACE 0  // 1 = diagnostic build: per-wave phase stamps of T1 (tools/qtrain_trace.py)
+#endif
+#if SHIPENV_QTRACE
+constexpr int kQTraceWg = 1024, kQTraceStamps = 16;
+__device__ uint64_t g_qtrace[kQTraceWg * 8 * kQTraceStamps];
+#define QSTAMP(k)                                                                              \
+    do {                                                                                       \
+        const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                                  \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < kQTraceWg)                                 \
+            g_qtrace[(blockIdx.x * 8 + (threadIdx.x >> 6)) * kQTraceStamps + (k)] = t_;        \
+    } while (0)
+#else
+#define QSTAMP(k) \
+    do {          \
+    } while (0)
+#endif
+
 // 8 waves: 0-3 the online net's feature tiles, 4-7 the target net's, concurrently; fc3
 // of the target net and the dW3 tiles over all 8; then dH1 (waves 0-3) beside dW2 (4-7).
 __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
@@ -228,6 +246,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     const bool tgt = wave >= 4;
     const int64_t r0 = (int64_t)blockIdx.x * kQT;
     const int in = A.d.in;
+    QSTAMP(0);
 
     for (int e = tid; e < 2 * 8 * 32; e += kQTBlock) {
         const int which = e >> 8, c = (e >> 5) & 7, j = e & 31;
@@ -242,7 +261,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         ACT[tid] = live ? (int)A.act[row] : 0;
         WT[tid] = live ? A.weight[row] : 0.0f;
     }
-    __syncthreads();
+    __syncthreads(); QSTAMP(1);
 
     // this thread's slice of W3[a_j] (q_j and dZ2 below): sample j = tid >> 4, features
     // 8 (tid & 15) .. + 7
@@ -265,14 +284,14 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         acc = gemm_lds(f1, tgt ? XN : X, acc, lane);
         store_relu(tgt ? TA : HA, wt, acc, lane);
     }
-    __syncthreads();
+    __syncthreads(); QSTAMP(2);
     if (wave < A.d.mt3) fb.load(A.W.pw3t + wave * 64 * 64, lane);
     {
         f32x16 acc = bias_init(tgt ? A.tg.b2 : A.on.b2, wt, lane, 128);
         acc = gemm_lds(fa, tgt ? TA : HA, acc, lane);
         store_relu(tgt ? TB : HB, wt, acc, lane);
     }
-    __syncthreads();
+    __syncthreads(); QSTAMP(3);
     // target fc3 over all A rows and the max over actions: tiles wave, wave + 8
     {
         const bool second = wave + 8 < A.d.mt3;
@@ -297,14 +316,14 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         m = fmaxf(m, __shfl_xor(m, 32));
         if (lane < 32) QM[wave * 32 + lane] = m;
     }
-    __syncthreads();
+    __syncthreads(); QSTAMP(4);
     if (tid < 32) {
         const int64_t row = r0 + tid;
         float mx = QM[tid];
         for (int w = 1; w < 8; ++w) mx = fmaxf(mx, QM[w * 32 + tid]);
         Y[tid] = row < A.B ? A.rew[row] + (A.gamma * mx) * (1.0f - A.done[row]) : 0.0f;
     }
-    __syncthreads();
+    __syncthreads(); QSTAMP(5);
 
     // q_j = W3[a_j] . h2_j + b3[a_j]; g_j = 2 w_j (q_j - y_j): 16 threads per sample
     {
@@ -321,7 +340,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             LW[qj] = WT[qj] * d * d;
         }
     }
-    __syncthreads();
+    __syncthreads(); QSTAMP(6);
     // dZ2 = (h2 > 0) g_j W3[a_j] (into the target's dead h1 buffer)
     {
         const float g = G[qj];
@@ -331,7 +350,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             DZ2[f * kLS + qj] = HB[f * kLS + qj] > 0.0f ? g * w3s[k] : 0.0f;
         }
     }
-    __syncthreads();
+    __syncthreads(); QSTAMP(7);
 
     const int h = lane >> 5, c = lane & 31;
     if (!tgt) {  // dH1 = W2^T dZ2 -> dZ1 = (h1 > 0) dH1
@@ -383,7 +402,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         }
         if (tid == 0) A.W.present[blockIdx.x] = present;
     }
-    __syncthreads();  // dZ1 complete
+    __syncthreads(); QSTAMP(8);  // dZ1 complete
     // partial dW1 (dynamic columns), db1, db2, loss and weight sums
     if (tid < 256) {
         const int f = tid >> 1, c0 = (tid & 1) * 3;
@@ -409,6 +428,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             A.W.part_lw[2 * blockIdx.x + 1] = w;
         }
     }
+    QSTAMP(9);
 }
 
 struct QtAdamArgs {
@@ -748,3 +768,9 @@ int se_qtrain_destroy(se_qtrain* q) {
 }
 
 }  // extern "C"
+
+#if SHIPENV_QTRACE
+extern "C" int se_qtrace_read(void* host, size_t bytes) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_qtrace), bytes) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -1,0 +1,63 @@
+"""Phase timeline of the DQN update's T1 kernel (diagnostic; needs a build with
+-DSHIPENV_QTRACE=1): s_memrealtime (100 MHz) stamps per wave at kernel start and after
+each of its barriers (1 inputs staged, 2 fc1, 3 fc2, 4 target fc3 + max, 5 targets y,
+6 q and g, 7 dZ2, 8 dH1 / dW2 / dW3), then 9 at the end. Runs a few training steps
+and prints, for the last T1 launch, per-phase medians over workgroups (us) and the
+launch span.
+
+    bash -c 'hipcc ... -DSHIPENV_QTRACE=1 -o /tmp/qt.so ...'; python tools/qtrain_trace.py --lib /tmp/qt.so
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--lib", required=True)
+    p.add_argument("--n", type=int, default=1 << 20)
+    p.add_argument("--batch", type=int, default=8192)
+    a = p.parse_args()
+    from shippingenv_amd import _native
+
+    _native.LIB_PATH = os.path.abspath(a.lib)
+    from shippingenv_amd.dqn import VecDQNAgent
+    from shippingenv_amd.vec import VecEnv
+
+    env = VecEnv(a.n, seed=2026, auto_reset=True, device="cuda:0")
+    env.reset()
+    torch.manual_seed(2026)
+    agent = VecDQNAgent(env, batch_size=a.batch, memory_size=4 * a.n, graph=False)
+    for _ in range(8):
+        agent.step()
+    torch.cuda.synchronize()
+    wg, stamps = 1024, 16
+    buf = np.zeros(wg * 8 * stamps, np.uint64)
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    assert lib.se_qtrace_read(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes)) == 0
+    tiles = (a.batch + 31) // 32
+    t = buf.reshape(wg, 8, stamps)[:tiles, :, :10].astype(np.int64)
+    t0 = t[:, :, 0].min()
+    rel = (t - t0) / 100.0  # 100 MHz -> us
+    wgmax = rel.max(axis=1)  # per workgroup: the slowest wave at each stamp
+    out = {"tiles": tiles, "span_us": float(rel[:, :, 9].max()),
+           "wg_alone_median_us": float(np.median(wgmax[:, 9] - rel[:, :, 0].min(axis=1)))}
+    phases = ["start", "inputs", "fc1", "fc2", "fc3_max", "targets", "q_g", "dZ2", "dH1_dW2_dW3", "end"]
+    d = np.diff(wgmax, axis=1)
+    out["phase_median_us"] = {phases[k + 1]: round(float(np.median(d[:, k])), 3) for k in range(9)}
+    out["start_spread_us"] = float(np.percentile(rel[:, :, 0].min(axis=1), 99))
+    print(json.dumps(out))
+    agent.close()
+    env.close()
+
+
+if __name__ == "__main__":
+    main()
