@@ -49,6 +49,8 @@ constexpr int kQTBlock = 512; // T1: 8 waves
 constexpr int kQABlock = 128; // fold / pack workgroups
 constexpr int kQRBlock = 256; // T2 workgroups
 
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
 struct QtDims {
     int32_t P, in, A, mt3;  // in = 6 + 4P; mt3 = fc3 row tiles (A rounded up to 32)
 };
@@ -248,6 +250,15 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     const int in = A.d.in;
     QSTAMP(0);
 
+    // fc1's operands and fc2's fragments do not depend on the batch: their loads are in
+    // flight while the inputs are staged
+    const int net = tgt ? 1 : 0;
+    Frags<64> fa, fb;  // fc2, then fc3 / W2^T: each loaded one layer ahead
+    Frags<3> f1;
+    f1.load(A.W.pw1[net] + wt * 3 * 64, lane);
+    fa.load(A.W.pw2[net] + wt * 64 * 64, lane);
+    f32x16 acc1 = bias_init(A.W.c1[net], wt, lane, 128);
+
     for (int e = tid; e < 2 * 8 * 32; e += kQTBlock) {
         const int which = e >> 8, c = (e >> 5) & 7, j = e & 31;
         const int64_t row = r0 + j;
@@ -274,16 +285,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     }
 
     // fc1, fc2 of both networks: online on states, target on next_states
-    const int net = tgt ? 1 : 0;
-    Frags<64> fa, fb;  // fc2, then fc3 / W2^T: each loaded one layer ahead
-    {
-        Frags<3> f1;
-        f1.load(A.W.pw1[net] + wt * 3 * 64, lane);
-        fa.load(A.W.pw2[net] + wt * 64 * 64, lane);
-        f32x16 acc = bias_init(A.W.c1[net], wt, lane, 128);
-        acc = gemm_lds(f1, tgt ? XN : X, acc, lane);
-        store_relu(tgt ? TA : HA, wt, acc, lane);
-    }
+    store_relu(tgt ? TA : HA, wt, gemm_lds(f1, tgt ? XN : X, acc1, lane), lane);
     __syncthreads(); QSTAMP(2);
     if (wave < A.d.mt3) fb.load(A.W.pw3t + wave * 64 * 64, lane);
     {
@@ -292,10 +294,23 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         store_relu(tgt ? TB : HB, wt, acc, lane);
     }
     __syncthreads(); QSTAMP(3);
-    // target fc3 over all A rows and the max over actions: tiles wave, wave + 8
+    // target fc3 over all A rows and the max over actions: tile `wave` on each wave, and the
+    // mt3 - 8 (at most 2) tiles beyond the eighth in 16 x 16 quadrants, so every SIMD gets the
+    // same MFMA cycles: tile 8 on waves 4-7, tile 9 on waves 0-3, quadrant wt = (row half
+    // rh, sample half sh) on v_mfma_f32_16x16x4_f32 (32 steps of K = 4, 32 cycles each; a
+    // quarter of a 32-row tile's 64 x 64 cycles). Before, waves 0 and 1 took the extra tiles
+    // whole and their SIMDs ran 1.5x the others' MFMA cycles.
     {
-        const bool second = wave + 8 < A.d.mt3;
-        if (second) fa.load(A.W.pw3t + (wave + 8) * 64 * 64, lane);
+        const int xt = tgt ? 8 : 9, rh = wt >> 1, sh = wt & 1;
+        const bool extra = xt < A.d.mt3;  // wave-uniform
+        float xa[32];  // quadrant A operands: rows 16 rh + (lane & 15), k = 4 t + (lane >> 4)
+        if (extra) {
+#pragma unroll
+            for (int t = 0; t < 32; ++t) {
+                const int k = 4 * t + (lane >> 4);
+                xa[t] = A.W.pw3t[(xt * 64 + (k >> 1)) * 64 + rh * 16 + (lane & 15) + 32 * (k & 1)];
+            }
+        }
         float m = -INFINITY;
         if (wave < A.d.mt3) {
             f32x16 acc = bias_init(A.tg.b3, wave, lane, A.d.A);
@@ -305,15 +320,31 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
                 if (wave * 32 + acc_r(r, lane) < A.d.A) m = fmaxf(m, acc[r]);
         }
         if (!tgt) fb.load(A.W.pw2t + wt * 64 * 64, lane);  // dH1's operands
-        if (second) {
-            const int t = wave + 8;
-            f32x16 acc = bias_init(A.tg.b3, t, lane, A.d.A);
-            acc = gemm_lds(fa, TB, acc, lane);
+        m = fmaxf(m, __shfl_xor(m, 32));  // lane & 31 = sample
+        if (extra) {
+            f32x4 acc;
 #pragma unroll
-            for (int r = 0; r < 16; ++r)
-                if (t * 32 + acc_r(r, lane) < A.d.A) m = fmaxf(m, acc[r]);
+            for (int r = 0; r < 4; ++r) {
+                const int row = xt * 32 + rh * 16 + 4 * (lane >> 4) + r;
+                acc[r] = row < A.d.A ? A.tg.b3[row] : 0.0f;
+            }
+            const float* hb = TB + (lane >> 4) * kLS + sh * 16 + (lane & 15);
+#pragma unroll
+            for (int t0 = 0; t0 < 32; t0 += 8) {
+                float bv[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) bv[i] = hb[4 * (t0 + i) * kLS];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[t0 + i], bv[i], acc, 0, 0, 0);
+            }
+            float qm = -INFINITY;  // over this lane's 4 rows, then the 16 rows of the quadrant
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (xt * 32 + rh * 16 + 4 * (lane >> 4) + r < A.d.A) qm = fmaxf(qm, acc[r]);
+            qm = fmaxf(qm, __shfl_xor(qm, 16));
+            qm = fmaxf(qm, __shfl_xor(qm, 32));  // every lane with lane & 15 = i: sample 16 sh + i
+            if (((lane & 31) >> 4) == sh) m = fmaxf(m, qm);
         }
-        m = fmaxf(m, __shfl_xor(m, 32));
         if (lane < 32) QM[wave * 32 + lane] = m;
     }
     __syncthreads(); QSTAMP(4);
@@ -373,31 +404,47 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         }
     }
     // partial dW3[a][f] = sum_j (a_j == a) g_j h2[f][j] over the action tiles present:
-    // (row tile, column tile) pairs round-robin over the 8 waves; db3 alike
-    uint32_t present = 0;
-    for (int j = 0; j < 32; ++j)
-        if (r0 + j < A.B) present |= 1u << (ACT[j] >> 5);
+    // (row tile, column tile) pairs round-robin over the 8 waves; db3 by the wave of a row
+    // tile's first pair. Each lane holds the action and g of its 16 k-step samples
+    // j = 2s + h in registers, so an A operand is a compare and a select, and a pair's 16
+    // B operands are read from LDS in one batch ahead of its MFMA chain (reading ACT and G
+    // per MFMA put two dependent LDS round trips in front of every MFMA).
     {
+        int aj[16];
+        float gj[16];
+        uint32_t pres = 0;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            const int j = 2 * s + h;
+            aj[s] = ACT[j];
+            gj[s] = G[j];
+            pres |= r0 + j < A.B ? 1u << (aj[s] >> 5) : 0u;
+        }
+        const uint32_t present = __builtin_amdgcn_readfirstlane(pres | (uint32_t)__shfl_xor((int)pres, 32));
         int k = 0;
         for (int rt = 0; rt < A.d.mt3; ++rt) {
             if (!((present >> rt) & 1u)) continue;  // block-uniform
+            const int a = rt * 32 + c;
             for (int ct = 0; ct < 4; ++ct, ++k) {
                 if ((k & 7) != wave) continue;  // wave-uniform
-                const int a = rt * 32 + c;
+                float bv[16], av[16];
+#pragma unroll
+                for (int s = 0; s < 16; ++s) bv[s] = HB[(ct * 32 + c) * kLS + 2 * s + h];
+#pragma unroll
+                for (int s = 0; s < 16; ++s) av[s] = aj[s] == a ? gj[s] : 0.0f;
                 f32x16 acc = {};
 #pragma unroll
-                for (int s = 0; s < 16; ++s) {
-                    const int j = 2 * s + h;
-                    acc = mfma_f32(ACT[j] == a ? G[j] : 0.0f, HB[(ct * 32 + c) * kLS + j], acc);
-                }
+                for (int s = 0; s < 16; ++s) acc = mfma_f32(av[s], bv[s], acc);
                 float* out = A.W.part_w3 + (((int64_t)blockIdx.x * A.d.mt3 + rt) * 32) * 128;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) out[acc_r(r, lane) * 128 + ct * 32 + c] = acc[r];
-            }
-            if (tid < 32) {
-                float s3 = 0.0f;
-                for (int j = 0; j < 32; ++j) s3 += ACT[j] == rt * 32 + tid ? G[j] : 0.0f;
-                A.W.part_b3[((int64_t)blockIdx.x * A.d.mt3 + rt) * 32 + tid] = s3;
+                if (ct == 0) {  // db3[a]: the even samples' sum plus the odd samples' sum
+                    float s3 = 0.0f;
+#pragma unroll
+                    for (int s = 0; s < 16; ++s) s3 += av[s];
+                    const float o3 = __shfl_xor(s3, 32);
+                    if (h == 0) A.W.part_b3[((int64_t)blockIdx.x * A.d.mt3 + rt) * 32 + c] = s3 + o3;
+                }
             }
         }
         if (tid == 0) A.W.present[blockIdx.x] = present;
