@@ -448,6 +448,9 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             }
         }
         if (tid == 0) A.W.present[blockIdx.x] = present;
+        // db3 of the absent action tiles is 0: stored, so T2 sums part_b3 with no presence test
+        if (tid < 32 * A.d.mt3 && !((present >> (tid >> 5)) & 1u))
+            A.W.part_b3[(int64_t)blockIdx.x * A.d.mt3 * 32 + tid] = 0.0f;
     }
     __syncthreads(); QSTAMP(8);  // dZ1 complete
     // partial dW1 (dynamic columns), db1, db2, loss and weight sums
@@ -537,24 +540,29 @@ __device__ __forceinline__ float block_sum256(float x, float* red) {
 // float4 q of tiles grp, grp + 16, ... (skipping tiles without `bit` in present[] when
 // present is given); the 16 groups then combine in a fixed order (xor 16 and 32 inside a
 // wave, then the four waves). Thread t < 64 returns element t of the 64.
+template <int kU>  // tiles per group and round (a round: presence words, then the loads)
 __device__ __forceinline__ float tile_sum64(const float* src, int64_t stride, int64_t e0, int64_t tiles,
                                             const uint32_t* present, uint32_t bit, float4* red) {
     const int t = threadIdx.x, q = t & 15, grp = t >> 4;
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    for (int64_t k0 = grp; k0 < tiles; k0 += 16 * 8) {  // 8 tiles per round, loads independent
-        uint32_t pm[8];
-        float4 v[8];
+    for (int64_t k0 = grp; k0 < tiles; k0 += 16 * kU) {  // kU tiles per round, loads independent
+        uint32_t pm[kU];
+        float4 v[kU];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < kU; ++i) {
             const int64_t k = k0 + 16 * i;
             pm[i] = k < tiles ? (present ? present[k] & bit : 1u) : 0u;
         }
+        // every load issues: an absent tile reads tile 0's line (cached) and is dropped, so
+        // the loads need no branch around each one
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-            v[i] = pm[i] ? *reinterpret_cast<const float4*>(src + (k0 + 16 * i) * stride + e0 + 4 * q)
-                         : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        for (int i = 0; i < kU; ++i)
+            v[i] = *reinterpret_cast<const float4*>(src + (pm[i] ? (k0 + 16 * i) * stride : 0) + e0 + 4 * q);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < kU; ++i)
+            if (!pm[i]) v[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+        for (int i = 0; i < kU; ++i) {
             acc.x += v[i].x;
             acc.y += v[i].y;
             acc.z += v[i].z;
@@ -583,17 +591,21 @@ __device__ __forceinline__ float tile_sum64(const float* src, int64_t stride, in
 __device__ __forceinline__ float comp(const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
 
 // Workgroups: [0, 128) W1 row f (+ b1, the fold, the loss at f = 0); [128, 384) W2 64-element
-// blocks (+ b2 on a row's first block); then mt3 x 64 W3 blocks of the [rt][32][128] layout
-// (+ b3 of tile rt on its first block).
+// blocks (+ b2 on a row's first block); then mt3 x 64 W3 blocks of the [rt][32][128] layout;
+// then mt3 b3 blocks (tile rt's 32 biases).
 __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
     __shared__ float red[kQRBlock];
     __shared__ float4 red4[kQRBlock];
     __shared__ float sums[8];
     const int tid = threadIdx.x, in = A.d.in;
+    QSTAMP(10);  // T2's stamps: slots 10-13 of the same rows (4 waves)
     const AdamStep adam(A);
+    // sum(w): this thread's share loads now, and the workgroup reduces it after its own
+    // sum (inv is first needed by the Adam step), so the two round trips overlap
     float wsum = 0.0f;
     for (int64_t t = tid; t < A.tiles; t += kQRBlock) wsum += A.W.part_lw[2 * t + 1];
-    const float inv = 1.0f / fmaxf(block_sum256(wsum, red), 1.0f);
+    auto weight_inv = [&]() { return 1.0f / fmaxf(block_sum256(wsum, red), 1.0f); };
+    QSTAMP(11);
     const int b = blockIdx.x;
     if (b < 128) {  // W1 row f: 6 dynamic columns + db1 reduced over the tiles, the port columns
         const int f = b;
@@ -605,6 +617,8 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             x[6] += A.W.part_b1[t * 128 + f];
         }
         block_sum<7>(x, red);
+        const float inv = weight_inv();
+        QSTAMP(12);
         if (tid == 0)  // every thread holds the sums; the row loop below indexes them by column
 #pragma unroll
             for (int c = 0; c < 7; ++c) sums[c] = x[c];
@@ -632,7 +646,9 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         }
     } else if (b < 384) {  // W2 elements e0 .. e0 + 63 (row-major [f2][f1])
         const int64_t e0 = (int64_t)(b - 128) * 64;
-        const float g = tile_sum64(A.W.part_w2, 128 * 128, e0, A.tiles, nullptr, 0, red4);
+        const float g = tile_sum64<16>(A.W.part_w2, 128 * 128, e0, A.tiles, nullptr, 0, red4);
+        const float inv = weight_inv();
+        QSTAMP(12);
         if (tid < 64) {
             const int e = (int)e0 + tid, f2 = e >> 7, f1 = e & 127;
             const float p = adam(A.on.w2[e], g * inv, A.m.w2[e], A.v.w2[e]);
@@ -647,12 +663,14 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             const float s2 = block_sum256(x, red);
             if (tid == 0) A.on.b2[f2] = adam(A.on.b2[f2], s2 * inv, A.m.b2[f2], A.v.b2[f2]);
         }
-    } else {  // W3 block: tile rt, elements e0 .. e0 + 63 of its [32][128]
+    } else if (b < 384 + 64 * A.d.mt3) {  // W3 block: tile rt, elements e0 .. e0 + 63 of its [32][128]
         const int k = b - 384, rt = k >> 6;
         const int64_t e0 = (int64_t)(k & 63) * 64;
         const uint32_t bit = 1u << rt;
-        const float g = tile_sum64(A.W.part_w3 + (int64_t)rt * 32 * 128, (int64_t)A.d.mt3 * 32 * 128, e0,
+        const float g = tile_sum64<16>(A.W.part_w3 + (int64_t)rt * 32 * 128, (int64_t)A.d.mt3 * 32 * 128, e0,
                                    A.tiles, A.W.present, bit, red4);
+        const float inv = weight_inv();
+        QSTAMP(12);
         if (tid < 64) {
             const int e = (int)e0 + tid, a = rt * 32 + (e >> 7), f = e & 127;
             if (a < A.d.A) {
@@ -660,11 +678,25 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                 A.on.w3[i] = adam(A.on.w3[i], g * inv, A.m.w3[i], A.v.w3[i]);
             }
         }
-        if (e0 == 0) {  // b3 of rows 32 rt .. 32 rt + 31: 32 rows x 8 tile groups
+    } else {  // b3 of rows 32 rt .. 32 rt + 31: 32 rows x 8 tile groups
+        // its own workgroup: behind a W3 block's sum it was the kernel's critical path.
+        // Tiles grp, grp + 8, ... in order, kU independent loads per round (T1 stores 0 for
+        // an absent action tile, so no presence test: a conditional load per tile kept these
+        // blocks busy 3x as long as the rest of the kernel)
+        const int rt = b - 384 - 64 * A.d.mt3;
+        {
             const int r = tid & 31, grp = tid >> 5;
             float x = 0.0f;
-            for (int64_t t = grp; t < A.tiles; t += 8)
-                if (A.W.present[t] & bit) x += A.W.part_b3[(t * A.d.mt3 + rt) * 32 + r];
+            constexpr int kU = 32;  // 256 tiles (B = 8192) in one round
+            for (int64_t t0 = grp; t0 < A.tiles; t0 += 8 * kU) {
+                float v[kU];
+#pragma unroll
+                for (int i = 0; i < kU; ++i)
+                    v[i] = t0 + 8 * i < A.tiles ? A.W.part_b3[((t0 + 8 * i) * A.d.mt3 + rt) * 32 + r] : 0.0f;
+#pragma unroll
+                for (int i = 0; i < kU; ++i) x += v[i];
+            }
+            QSTAMP(12);
             __syncthreads();
             red[tid] = x;
             __syncthreads();
@@ -673,10 +705,14 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                 if (grp < s) red[tid] += red[tid + 32 * s];
                 __syncthreads();
             }
+            const float s3 = red[tid & 31];
+            __syncthreads();  // weight_inv reuses red
+            const float inv = weight_inv();
             const int a = rt * 32 + r;
-            if (tid < 32 && a < A.d.A) A.on.b3[a] = adam(A.on.b3[a], red[tid] * inv, A.m.b3[a], A.v.b3[a]);
+            if (tid < 32 && a < A.d.A) A.on.b3[a] = adam(A.on.b3[a], s3 * inv, A.m.b3[a], A.v.b3[a]);
         }
     }
+    QSTAMP(13);
 }
 
 }  // namespace
@@ -798,7 +834,7 @@ int se_qtrain_step(se_qtrain* q, int64_t batch, const float* obs, const float* n
     qtrain_tile_kernel<<<(unsigned)tiles, kQTBlock, lds, s>>>(A);
     HIP_TRY(hipGetLastError());
     QtAdamArgs B{q->W, q->on, q->m, q->v, q->d, batch, tiles, act, lr, beta1, beta2, eps, step_dev, loss_out};
-    qtrain_adam_kernel<<<384 + 64 * q->d.mt3, kQRBlock, 0, s>>>(B);
+    qtrain_adam_kernel<<<384 + 65 * q->d.mt3, kQRBlock, 0, s>>>(B);
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }
