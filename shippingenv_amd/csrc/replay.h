@@ -110,6 +110,74 @@ __global__ __launch_bounds__(kBlock) void replay_end_kernel(RecordArgs A) {
     }
 }
 
+// replay_end_kernel for four consecutive envs per thread, when the ring slots of a group
+// are consecutive too (head, cap and n multiples of 4): every field moves as one 4-byte
+// (u8 fields) or 16-byte (f32 / i32 / f64 pair) lane access, as in the step kernel, where one
+// env per thread issued a 1-byte access per u8 field. Same stores, same bits.
+__device__ __forceinline__ uint32_t byte_at(uint32_t w, int j) { return (w >> (8 * j)) & 0xffu; }
+
+__global__ __launch_bounds__(kBlock) void replay_end4_kernel(RecordArgs A) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *A.ring.d_size = A.new_size;
+    const int64_t groups = A.n >> 2;
+    for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < groups; g += (int64_t)gridDim.x * kBlock) {
+        const int64_t i0 = g * 4;
+        int64_t slot = A.head + i0;
+        slot -= slot >= A.cap ? A.cap : 0;
+        const uint32_t err4 = *reinterpret_cast<const uint32_t*>(A.st.err + i0);
+        const uint32_t done4 = *reinterpret_cast<const uint32_t*>(A.st.done + i0);
+        const uint32_t x4 = *reinterpret_cast<const uint32_t*>(A.st.x + i0);
+        const uint32_t y4 = *reinterpret_cast<const uint32_t*>(A.st.y + i0);
+        const uint32_t o4 = *reinterpret_cast<const uint32_t*>(A.st.origin + i0);
+        const uint32_t d4 = *reinterpret_cast<const uint32_t*>(A.st.dest + i0);
+        const float4 rew = *reinterpret_cast<const float4*>(A.st.reward + i0);
+        const double2 f01 = *reinterpret_cast<const double2*>(A.st.fuel + i0);
+        const double2 f23 = *reinterpret_cast<const double2*>(A.st.fuel + i0 + 2);
+        uint32_t flags4 = 0, cut4 = 0;
+        uint4 pos;
+        uint32_t* pw = &pos.x;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool raised = byte_at(err4, j) != 0;
+            flags4 |= ((byte_at(done4, j) ? kRecDone : 0u) | (raised ? kRecInvalid : 0u)) << (8 * j);
+            pw[j] = byte_at(x4, j) | byte_at(y4, j) << 8 | byte_at(o4, j) << 16 | byte_at(d4, j) << 24;
+            cut4 |= (uint32_t)raised << (8 * j);
+        }
+        *reinterpret_cast<float4*>(A.ring.rew + slot) = rew;
+        *reinterpret_cast<uint32_t*>(A.ring.flags + slot) = flags4;
+        *reinterpret_cast<uint4*>(A.ring.n_pos + slot) = pos;
+        *reinterpret_cast<float4*>(A.ring.n_fuel + slot) =
+            make_float4((float)f01.x, (float)f01.y, (float)f23.x, (float)f23.y);
+        if (!A.cut) continue;
+        if (A.max_steps > 0) {
+            const int4 len = *reinterpret_cast<const int4*>(A.st.ep_len + i0);
+            cut4 |= (uint32_t)(len.x >= A.max_steps) | (uint32_t)(len.y >= A.max_steps) << 8 |
+                    (uint32_t)(len.z >= A.max_steps) << 16 | (uint32_t)(len.w >= A.max_steps) << 24;
+        }
+        *reinterpret_cast<uint32_t*>(A.cut + i0) = cut4;
+        if (!A.world || !cut4) continue;
+        const LdsWorld w = world_view(A.dims, A.world);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (!byte_at(cut4, j)) continue;
+            const int64_t i = i0 + j;  // reset_kernel's body for this env
+            const U4 o = draw(env_key(A.seed, A.env_base + i), A.epoch, kSlotExplicitReset);
+            Ship sh;
+            reset_ship(w, sh, o.v[0], o.v[1]);
+            A.st.x[i] = (uint8_t)sh.x;
+            A.st.y[i] = (uint8_t)sh.y;
+            A.st.fuel[i] = sh.fuel;
+            A.st.cargo[i] = sh.cargo;
+            A.st.origin[i] = (uint8_t)sh.origin;
+            A.st.dest[i] = (uint8_t)sh.dest;
+            if (A.st.ep_return) A.st.ep_return[i] = 0.0f;
+            if (A.st.ep_len) A.st.ep_len[i] = 0;
+            A.st.done[i] = 0;
+            A.st.err[i] = 0;
+            A.st.reward[i] = 0.0f;
+        }
+    }
+}
+
 __host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {  // lowbias32 finaliser
     x ^= x >> 16;
     x *= 0x7feb352du;
@@ -309,7 +377,10 @@ int replay_end(se_replay* r, uint8_t* cut, int32_t max_steps, bool reset_cut, vo
     RecordArgs A{env->n, r->cap, r->head, new_size, env->st, nullptr, r->ring, cut, max_steps,
                  reset_cut ? env->d_world : nullptr, env->dims, env->seed, env->env_base,
                  (uint32_t)env->epoch};
-    replay_end_kernel<<<grid_for(std::max<int64_t>(env->n, 1)), kBlock, 0, (hipStream_t)stream>>>(A);
+    if (env->n % 4 == 0 && r->head % 4 == 0 && r->cap % 4 == 0 && ((uintptr_t)cut & 3u) == 0)
+        replay_end4_kernel<<<grid_for(std::max<int64_t>(env->n / 4, 1)), kBlock, 0, (hipStream_t)stream>>>(A);
+    else
+        replay_end_kernel<<<grid_for(std::max<int64_t>(env->n, 1)), kBlock, 0, (hipStream_t)stream>>>(A);
     HIP_TRY(hipGetLastError());
     if (reset_cut) env->epoch += 1;  // as se_reset
     r->head = (r->head + env->n) % r->cap;
