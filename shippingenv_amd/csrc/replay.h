@@ -237,18 +237,26 @@ __device__ __forceinline__ float ship_col(uint32_t pos, float fuel, int c) {
     return c == 2 || c == 3 ? fuel : v;
 }
 
-__device__ __forceinline__ float port_col(const LdsWorld& w, int c) {
-    const int p = (c - 6) >> 2, f = (c - 6) & 3;
-    return f == 0 ? (float)w.px(p) : f == 1 ? (float)w.py(p) : f == 2 ? (float)w.pfuel(p) : (float)w.pcargo(p);
-}
 
-// kSampleRows transitions per workgroup: the first wave picks the slots, then all
-// threads write the two [rows][width] f32 blocks with coalesced row-major stores.
+// kSampleRows transitions per workgroup. The first wave picks the slots, loading each
+// candidate's flags and its transition together (a flagged one is then dropped), and
+// writes its row's six ship columns; all threads then write the constant port block from
+// a small LDS copy of the port table, which the other threads load while the picks run.
+// Three dependent memory steps (size, transition, stores) where staging the whole world
+// image, a flags-only probe and a second gather behind a barrier made five.
 __global__ __launch_bounds__(kBlock) void replay_sample_kernel(SampleBatchArgs A) {
-    extern __shared__ uint32_t lds[];
     __shared__ int64_t slot_of[kSampleRows];
-    const LdsWorld w = stage_world(A.world, A.dims, lds);
+    __shared__ float port[4 * SE_MAX_PORTS];
+    const int P = A.dims.P, width = A.width;
     const int64_t r0 = (int64_t)blockIdx.x * kSampleRows;
+    {
+        const LdsWorld wv = world_view(A.dims, A.world);  // the port table only, in place
+        for (int c = (int)threadIdx.x - kSampleRows; c < 4 * P; c += kBlock - kSampleRows) {
+            if (c < 0) continue;
+            const int p = c >> 2, f = c & 3;
+            port[c] = f == 0 ? (float)wv.px(p) : f == 1 ? (float)wv.py(p) : f == 2 ? (float)wv.pfuel(p) : (float)wv.pcargo(p);
+        }
+    }
     if (threadIdx.x < kSampleRows) {
         const int64_t size = *A.ring.d_size;
         const uint32_t t = A.t_dev ? *A.t_dev : A.t;
@@ -256,41 +264,48 @@ __global__ __launch_bounds__(kBlock) void replay_sample_kernel(SampleBatchArgs A
         const uint32_t h = feistel_half((uint32_t)size);
         const int64_t j = r0 + threadIdx.x;
         int64_t slot = -1;
+        uint32_t sp = 0, np = 0;
+        float sf = 0.0f, nf = 0.0f, rw = 0.0f;
+        int32_t ac = 0;
+        uint8_t fl = 0;
         if (j < A.B) {
             for (int k = 0; k < kReplayTries; ++k) {
                 const int64_t pos = j + (int64_t)k * A.B;
                 if (pos >= size) break;
                 const uint32_t l = feistel_perm((uint32_t)pos, (uint32_t)size, h, key.v);
-                if (!(A.ring.flags[l] & kRecInvalid)) {
+                fl = A.ring.flags[l];
+                sp = A.ring.s_pos[l];
+                sf = A.ring.s_fuel[l];
+                np = A.ring.n_pos[l];
+                nf = A.ring.n_fuel[l];
+                ac = A.ring.act[l];
+                rw = A.ring.rew[l];
+                if (!(fl & kRecInvalid)) {
                     slot = l;
                     break;
                 }
             }
             const bool ok = slot >= 0;
-            A.act[j] = ok ? (int64_t)A.ring.act[slot] : 0;
-            A.rew[j] = ok ? A.ring.rew[slot] : 0.0f;
-            A.done[j] = ok && (A.ring.flags[slot] & kRecDone) ? 1.0f : 0.0f;
+            A.act[j] = ok ? (int64_t)ac : 0;
+            A.rew[j] = ok ? rw : 0.0f;
+            A.done[j] = ok && (fl & kRecDone) ? 1.0f : 0.0f;
             A.weight[j] = ok ? 1.0f : 0.0f;
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                A.obs[j * width + c] = ok ? ship_col(sp, sf, c) : 0.0f;
+                A.next_obs[j * width + c] = ok ? ship_col(np, nf, c) : 0.0f;
+            }
         }
         slot_of[threadIdx.x] = slot;
     }
     __syncthreads();
     const int64_t rows = min((int64_t)kSampleRows, A.B - r0);
-    const int width = A.width;
-    for (int e = threadIdx.x; e < rows * width; e += kBlock) {
-        const int r = e / width, c = e - r * width;
-        const int64_t slot = slot_of[r];
-        float a = 0.0f, b = 0.0f;
-        if (slot >= 0) {
-            if (c < 6) {
-                a = ship_col(A.ring.s_pos[slot], A.ring.s_fuel[slot], c);
-                b = ship_col(A.ring.n_pos[slot], A.ring.n_fuel[slot], c);
-            } else {
-                a = b = port_col(w, c);
-            }
-        }
-        A.obs[(r0 + r) * width + c] = a;
-        A.next_obs[(r0 + r) * width + c] = b;
+    const int pw = width - 6;
+    for (int e = threadIdx.x; e < rows * pw; e += kBlock) {
+        const int r = e / pw, c = e - r * pw;
+        const float v = slot_of[r] >= 0 ? port[c] : 0.0f;
+        A.obs[(r0 + r) * width + 6 + c] = v;
+        A.next_obs[(r0 + r) * width + 6 + c] = v;
     }
 }
 
@@ -432,7 +447,7 @@ int se_replay_sample(se_replay* r, int64_t batch, const uint32_t* t_dev, uint32_
     SampleBatchArgs A{env->d_world, env->dims, r->ring, batch, 6 + 4 * env->dims.P, env->seed, t_dev, t,
                       obs, next_obs, actions, rewards, dones, weights};
     const int grid = (int)((batch + kSampleRows - 1) / kSampleRows);
-    replay_sample_kernel<<<grid, kBlock, lds_bytes(env), (hipStream_t)stream>>>(A);
+    replay_sample_kernel<<<grid, kBlock, 0, (hipStream_t)stream>>>(A);
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }
