@@ -220,8 +220,18 @@ __device__ uint64_t g_qtrace[kQTraceWg * 8 * kQTraceStamps];
         if ((threadIdx.x & 63) == 0 && blockIdx.x < kQTraceWg)                                 \
             g_qtrace[(blockIdx.x * 8 + (threadIdx.x >> 6)) * kQTraceStamps + (k)] = t_;        \
     } while (0)
+// the shader clock (s_memtime) beside the 100 MHz stamps, in slots 14 and 15
+#define QCLOCK(k)                                                                              \
+    do {                                                                                       \
+        const uint64_t c_ = __builtin_readcyclecounter();                                      \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < kQTraceWg)                                 \
+            g_qtrace[(blockIdx.x * 8 + (threadIdx.x >> 6)) * kQTraceStamps + (k)] = c_;        \
+    } while (0)
 #else
 #define QSTAMP(k) \
+    do {          \
+    } while (0)
+#define QCLOCK(k) \
     do {          \
     } while (0)
 #endif
@@ -286,7 +296,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
 
     // fc1, fc2 of both networks: online on states, target on next_states
     store_relu(tgt ? TA : HA, wt, gemm_lds(f1, tgt ? XN : X, acc1, lane), lane);
-    __syncthreads(); QSTAMP(2);
+    __syncthreads(); QSTAMP(2); QCLOCK(14);
     if (wave < A.d.mt3) fb.load(A.W.pw3t + wave * 64 * 64, lane);
     {
         f32x16 acc = bias_init(tgt ? A.tg.b2 : A.on.b2, wt, lane, 128);
@@ -347,7 +357,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         }
         if (lane < 32) QM[wave * 32 + lane] = m;
     }
-    __syncthreads(); QSTAMP(4);
+    __syncthreads(); QSTAMP(4); QCLOCK(15);
     if (tid < 32) {
         const int64_t row = r0 + tid;
         float mx = QM[tid];

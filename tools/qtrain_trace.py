@@ -77,6 +77,10 @@ def main():
                     "end": [round(float(v), 2) for v in wb[:, 3]]}
     out["t2_w3_sum_by_tile_p50"] = [round(float(np.median(np.diff(w2[384 + k * 64:384 + (k + 1) * 64], axis=1)[:, 1])), 2)
                                     for k in range(mt3)]
+    cyc = buf.reshape(wg, 8, stamps)[:tiles, :, 14:16].astype(np.int64)
+    rt = buf.reshape(wg, 8, stamps)[:tiles, :, [2, 4]].astype(np.int64)
+    ghz = (cyc[:, :, 1] - cyc[:, :, 0]) / ((rt[:, :, 1] - rt[:, :, 0]) * 10.0)  # cycles per ns
+    out["t1_shader_clock_ghz_fc2_fc3"] = [round(float(np.percentile(ghz, q)), 3) for q in (10, 50, 90)]
     print(json.dumps(out))
     agent.close()
     env.close()
