@@ -1471,9 +1471,26 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
 #endif
     if (kAuto && (SHIPENV_ABL4 & 4) == 0) {
         // per-wave statistics: a fixed-order tree (wave_sum), added to this wave's own
-        // slab entry
-        const double ret = wave_sum(bs.ret), len = wave_sum((double)bs.len);
-        const int eps = wave_sum_int(bs.eps);
+        // slab entry. With episodes ending about once per 240 steps, most waves have one
+        // lane with a finished episode or none: then that lane's values are the sums
+        // (every other lane adds +0.0, which the tree's f64 adds leave exact), read
+        // with three readlanes instead of three trees.
+        const uint64_t ended = __ballot(bs.eps != 0);
+        if (ended == 0) return;
+        double ret, len;
+        int eps;
+        if ((ended & (ended - 1)) == 0) {
+            const int src = __builtin_ctzll(ended);
+            const uint64_t rb = __builtin_bit_cast(uint64_t, bs.ret);
+            ret = __builtin_bit_cast(double, (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(rb >> 32), src) << 32 |
+                                                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rb, src));
+            len = (double)__builtin_amdgcn_readlane(bs.len, src);
+            eps = __builtin_amdgcn_readlane(bs.eps, src);
+        } else {
+            ret = wave_sum(bs.ret);
+            len = wave_sum((double)bs.len);
+            eps = wave_sum_int(bs.eps);
+        }
         if (eps != 0 && (threadIdx.x & 63) == 0) {
             double* sl = late_args().slab + 4 * (blockIdx.x * (kStepBlock / 64) + (threadIdx.x >> 6));
             slab_add(sl + 0, ret);
