@@ -110,12 +110,16 @@ def timed_loop(env, acts, first, steps, dist, reduce_every=0):
     stream = torch.cuda.current_stream(env.device)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     stats = torch.zeros(3, dtype=torch.float64, device=env.device)
+    # the step's action rows as views made before the clock starts: indexing the
+    # [steps, n] table inside the loop is harness work (1.4 us of host time per step,
+    # tools/diag/host_step_cost.py), not the step's
+    rows = [acts[first + k] for k in range(steps)]
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     e0.record(stream)
     for k in range(steps):
-        env.step(acts[first + k])
+        env.step(rows[k])
         if reduce_every and (k + 1) % reduce_every == 0:
             # episode-return aggregation over the GPUs (RCCL all-reduce of 3 doubles)
             stats.copy_(env.episode_stats())
