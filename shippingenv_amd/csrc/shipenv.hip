@@ -1508,9 +1508,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
 // as in the main kernel).
 template <bool kTyped, bool kReplay, bool kAuto>
 __global__ __launch_bounds__(64) void step_tail_kernel(StepArgs A) {
-    extern __shared__ uint32_t lds[];
-    const LdsWorld w = stage_world(A.world, A.dims, lds);
+    // at most 3 envs: the world is read in place (L2), not staged, so the step starts
+    // without the staging round trips (the N = 1 drop-in path is this kernel alone)
     if (threadIdx.x != 0) return;
+    const LdsWorld w = world_view(A.dims, A.world);
     const int64_t g = A.n >> 2;
     const At<false> at{0, g * 4, A.n};
     Group<kTyped, kAuto> G;
@@ -2238,11 +2239,11 @@ int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const 
         HIP_TRY(hipGetLastError());
     }
     if (env->n & 3) {
-        if (!typed && !autoreset) step_tail_kernel<false, false, false><<<1, 64, lds, s>>>(A);
-        else if (!typed && autoreset) step_tail_kernel<false, false, true><<<1, 64, lds, s>>>(A);
-        else if (typed && replay) step_tail_kernel<true, true, false><<<1, 64, lds, s>>>(A);
-        else if (typed && !autoreset) step_tail_kernel<true, false, false><<<1, 64, lds, s>>>(A);
-        else step_tail_kernel<true, false, true><<<1, 64, lds, s>>>(A);
+        if (!typed && !autoreset) step_tail_kernel<false, false, false><<<1, 64, 0, s>>>(A);
+        else if (!typed && autoreset) step_tail_kernel<false, false, true><<<1, 64, 0, s>>>(A);
+        else if (typed && replay) step_tail_kernel<true, true, false><<<1, 64, 0, s>>>(A);
+        else if (typed && !autoreset) step_tail_kernel<true, false, false><<<1, 64, 0, s>>>(A);
+        else step_tail_kernel<true, false, true><<<1, 64, 0, s>>>(A);
         HIP_TRY(hipGetLastError());
     }
     if (!replay) env->step_t += 1;

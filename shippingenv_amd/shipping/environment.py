@@ -118,6 +118,8 @@ class Environment:
         self.destination_port_index = None
         self._stepper = None
         self._world_key = None
+        self._g_ref = self._ground = None
+        self._pp = self._pf = self._pc = None
         self._initialize_map(map_path)
 
     # ------------------------------------------------------------------ setup
@@ -209,11 +211,22 @@ class Environment:
             return [ActionType.MOVE_SHIP, self._sample_random_move()]
 
     # ------------------------------------------------------------------ device
-    def _world(self):
+    def _world(self, cell=None):
         """The stepper follows assignments to np_game / port lists (agents/mcts.py:200-208)
         and in-place edits of np_game: the reference reads the ground test live on every
-        move (environment.py:293), so the key holds the ground mask's bytes, not id()."""
-        ground = np.asarray(self.np_game) == Entity.GROUND
+        move (environment.py:293). The full check keys the device world on the ground
+        mask's bytes and the port lists; it runs when np_game is another object, a port
+        list changed, or the one cell this step's kernel reads (a move's target, `cell`)
+        disagrees with the mask the device holds. A step reads no other cell, so the
+        fast path (no pass over the grid: the full key cost ~15 us of a ~30 us step) is
+        exact for every read the kernel makes."""
+        g = self.np_game
+        if (self._stepper is not None and g is self._g_ref and type(g) is np.ndarray
+                and self.port_positions == self._pp
+                and self.port_fuel == self._pf and self.port_cargo == self._pc
+                and (cell is None or (g.item(cell) == Entity.GROUND) == self._ground.item(cell))):
+            return self._stepper
+        ground = np.asarray(g) == Entity.GROUND
         key = (ground.shape, ground.tobytes(), tuple(tuple(int(v) for v in p) for p in self.port_positions),
                tuple(self.port_fuel), tuple(self.port_cargo))
         if self._stepper is None or key != self._world_key:
@@ -225,6 +238,9 @@ class Environment:
             else:
                 self._stepper.set_world(water, px, py, self.port_fuel, self.port_cargo)
             self._world_key = key
+        self._g_ref, self._ground = g, ground
+        self._pp = [list(p) for p in self.port_positions]
+        self._pf, self._pc = list(self.port_fuel), list(self.port_cargo)
         return self._stepper
 
     def _ship_xy(self):
@@ -251,13 +267,17 @@ class Environment:
     def _run(self, act_type, a, b):
         """Step on the device, drawing the reference's variates as the kernel asks for them."""
         rs = random
-        stepper = self._world()
         x, y = self._ship_xy()
+        cell = None  # the one grid cell this step reads: a move's target (:293)
+        if act_type == ActionType.MOVE_SHIP:
+            H, W = np.shape(self.np_game)[:2]
+            if 0 <= x + a < H and 0 <= y + b < W:
+                cell = (x + a, y + b)
+        stepper = self._world(cell)
         tape = [math.nan, math.nan, math.nan, math.nan, -1]
         ahead = False
         if act_type == ActionType.MOVE_SHIP and self.destination_port_index is not None:
-            H, W = np.shape(self.np_game)[:2]
-            if 0 <= x + a < H and 0 <= y + b < W:
+            if cell is not None:
                 # a MOVE that raises neither at :276 nor at :284 draws uniform() then
                 # random() (:104, :320): draw them ahead, saving the kernel's request
                 ahead = True
