@@ -287,6 +287,15 @@ int se_qtrain_step(se_qtrain* q, int64_t batch, const float* obs, const float* n
                    const float* rew, const float* done, const float* weight, float gamma, float lr,
                    float beta1, float beta2, float eps, const int32_t* step_dev, float* loss_out,
                    void* stream);
+/* se_qtrain_step, then what se_qnet_repack(qn, step_dev) would do, in the same two launches:
+ * the first kernel advances step_dev (the second's bias correction then uses it as is),
+ * and the second writes the policy's bf16 images (both layouts) from the parameters it
+ * has just updated. qn must be packed (se_qnet_set_weights) from the very tensors bound
+ * as `online` in se_qtrain_bind, on the same env. Same bits as the two calls. */
+int se_qtrain_step_policy(se_qtrain* q, se_qnet* qn, int64_t batch, const float* obs,
+                          const float* next_obs, const int64_t* act, const float* rew,
+                          const float* done, const float* weight, float gamma, float lr, float beta1,
+                          float beta2, float eps, int32_t* step_dev, float* loss_out, void* stream);
 int se_qtrain_destroy(se_qtrain* q);  /* destroy before the env it was created on */
 
 /* Episode statistics accumulated by the auto-reset path since the last clear:

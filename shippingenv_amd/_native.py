@@ -37,7 +37,7 @@ EXPORTS = (
     "se_qnet_destroy", "se_replay_create", "se_replay_begin", "se_replay_end", "se_replay_end_reset",
     "se_replay_size",
     "se_replay_sample", "se_replay_destroy", "se_qtrain_create", "se_qtrain_bind", "se_qtrain_pack",
-    "se_qtrain_step", "se_qtrain_destroy",
+    "se_qtrain_step", "se_qtrain_step_policy", "se_qtrain_destroy",
     "se_episode_stats", "se_clear_stats", "se_done_layout", "se_done_list", "se_done_compact",
     "se_get_counters", "se_set_counters",
     "se_map_decode_luma", "se_map_area_threshold", "se_map_from_jpeg",
@@ -100,6 +100,7 @@ def _declare(lib):
         "se_qtrain_bind": [P, P, P, P, P, P],
         "se_qtrain_pack": [P, C.c_int32, P],
         "se_qtrain_step": [P, i64, P, P, P, P, P, P] + [C.c_float] * 5 + [P, P, P],
+        "se_qtrain_step_policy": [P, P, i64, P, P, P, P, P, P] + [C.c_float] * 5 + [P, P, P],
         "se_qtrain_destroy": [P],
         "se_episode_stats": [P, P, P],
         "se_clear_stats": [P, P],

@@ -206,6 +206,7 @@ struct QtStepArgs {
     const int64_t* act;
     const float *rew, *done, *weight;
     float gamma;
+    int32_t* bump;  // se_qtrain_step_policy: the update counter, advanced once here (T2 reads it after)
 };
 
 #ifndef SHIPENV_QTRACE
@@ -259,6 +260,8 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     const int64_t r0 = (int64_t)blockIdx.x * kQT;
     const int in = A.d.in;
     QSTAMP(0);
+    if (A.bump && blockIdx.x == 0 && tid == 0)  // no return value: the wave does not wait on it
+        __hip_atomic_fetch_add(A.bump, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
     // fc1's operands and fc2's fragments do not depend on the batch: their loads are in
     // flight while the inputs are staged
@@ -498,16 +501,39 @@ struct QtAdamArgs {
     int64_t B, tiles;
     const int64_t* act;
     float lr, beta1, beta2, eps;
-    const int32_t* step_dev;  // Adam steps taken before this one
+    const int32_t* step_dev;  // Adam steps taken before this one (this one included when bumped)
     float* loss_out;
+    // se_qtrain_step_policy: the policy's bf16 images (full, compact), rewritten from the new
+    // parameters as qnet_pack_kernel would write them; img[0] null otherwise
+    uint8_t* img[2];
+    QnetDims q[2];
+    int32_t bumped;  // T1 advanced step_dev already
 };
+
+// byte offset of W[row][k] within a packed policy image's fc2 / fc3 fragments: fragment
+// ((row / 32) * 4 + k / 32) * 2 + s, lane row % 32 + 32 h, element j, where
+// k % 32 = 16 s + 8 (j >> 2) + 4 h + (j & 3) (qnet_pack_kernel's acc_row map)
+__device__ __forceinline__ int pol_offset(int row, int k) {
+    const int kk = k & 31, s = kk >> 4, h = (kk >> 2) & 1, j = 4 * ((kk >> 3) & 1) + (kk & 3);
+    return ((((row >> 5) * 4 + (k >> 5)) * 2 + s) * 64 + (row & 31) + 32 * h) * 16 + 2 * j;
+}
+
+__device__ __forceinline__ void put_bf16(uint8_t* p, float v) { *reinterpret_cast<__bf16*>(p) = (__bf16)v; }
+
+// the row of action a in a layout (QnetDims::action_of_row inverted), -1 if it has none
+__device__ __forceinline__ int row_of_action(const QnetDims& q, int a) {
+    if (!q.compact || a < 4 + q.P) return a < q.rows ? a : -1;
+    if (a >= 5 + q.P && a <= 4 + q.P + q.cmax) return a - 1;
+    const int r = a - 51 + q.cmax;
+    return a >= 55 + q.P && r < q.rows ? r : -1;
+}
 
 // torch.optim.Adam (foreach, capturable) for one element: m lerps to g, v = v b2 + (1 - b2) g g,
 // p += m / ((sqrt(v) / sqrt(1 - b2^t) + eps) / (-lr / (1 - b1^t)))
 struct AdamStep {
     float b1, b2, eps, step_size, bc2_sqrt;
     __device__ AdamStep(const QtAdamArgs& A) : b1(A.beta1), b2(A.beta2), eps(A.eps) {
-        const float t = (float)(*A.step_dev + 1);
+        const float t = (float)(*A.step_dev + (A.bumped ? 0 : 1));
         step_size = 1.0f / ((powf(A.beta1, t) - 1.0f) / A.lr);
         bc2_sqrt = sqrtf(-(powf(A.beta2, t) - 1.0f));
     }
@@ -640,7 +666,15 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             const int64_t i = (int64_t)f * in + c;
             const float p = adam(w1row[c], g, A.m.w1[i], A.v.w1[i]);
             w1row[c] = p;
-            if (c < 6) A.W.pw1[0][((f >> 5) * 3 + (c >> 1)) * 64 + (f & 31) + 32 * (c & 1)] = p;
+            if (c < 6) {
+                A.W.pw1[0][((f >> 5) * 3 + (c >> 1)) * 64 + (f & 31) + 32 * (c & 1)] = p;
+                if (A.img[0])  // the policy's fc1 fragment: element j holds column fc1_col(j)
+#pragma unroll
+                    for (int l = 0; l < 2; ++l)
+#pragma unroll
+                        for (int j = 0; j < 8; ++j)
+                            if (fc1_col(j) == c) put_bf16(A.img[l] + A.q[l].w1() + ((f >> 5) * 64 + (f & 31)) * 16 + 2 * j, p);
+            }
         }
         if (tid == 0) sums[7] = adam(A.on.b1[f], s1 * inv, A.m.b1[f], A.v.b1[f]);
         __syncthreads();  // the new row and b1 are complete before the fold reads them
@@ -648,6 +682,17 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         if (tid == 0) A.on.b1[f] = b1;
         const float xf = fold_row(w1row, in, A.W.portvec, red);  // the pack kernel's bits
         if (tid == 0) A.W.c1[0][f] = b1 + xf;
+        if (A.img[0] && tid == 0) {  // the policy's b1: qnet_pack_kernel's f64 fold, same order
+            double acc = (double)b1;
+            for (int p = 0; p < A.d.P; ++p) {
+                const float* wp = w1row + 6 + 4 * p;
+                const float* pv = A.W.portvec + 4 * p;
+                acc += (double)wp[0] * (double)pv[0] + (double)wp[1] * (double)pv[1] +
+                       (double)wp[2] * (double)pv[2] + (double)wp[3] * (double)pv[3];
+            }
+#pragma unroll
+            for (int l = 0; l < 2; ++l) reinterpret_cast<float*>(A.img[l] + A.q[l].b1())[f] = (float)acc;
+        }
         if (f == 0) {  // the loss: sum w d^2 / sum w
             float l = 0.0f;
             for (int64_t t = tid; t < A.tiles; t += kQRBlock) l += A.W.part_lw[2 * t];
@@ -665,13 +710,22 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             A.on.w2[e] = p;
             A.W.pw2[0][frag_index(f2, f1)] = p;
             A.W.pw2t[frag_index(f1, f2)] = p;
+            if (A.img[0])
+#pragma unroll
+                for (int l = 0; l < 2; ++l) put_bf16(A.img[l] + A.q[l].w2() + pol_offset(f2, f1), p);
         }
         if ((e0 & 127) == 0) {
             const int f2 = (int)(e0 >> 7);
             float x = 0.0f;
             for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[t * 128 + f2];
             const float s2 = block_sum256(x, red);
-            if (tid == 0) A.on.b2[f2] = adam(A.on.b2[f2], s2 * inv, A.m.b2[f2], A.v.b2[f2]);
+            if (tid == 0) {
+                const float p = adam(A.on.b2[f2], s2 * inv, A.m.b2[f2], A.v.b2[f2]);
+                A.on.b2[f2] = p;
+                if (A.img[0])
+#pragma unroll
+                    for (int l = 0; l < 2; ++l) reinterpret_cast<float*>(A.img[l] + A.q[l].b2())[f2] = p;
+            }
         }
     } else if (b < 384 + 64 * A.d.mt3) {  // W3 block: tile rt, elements e0 .. e0 + 63 of its [32][128]
         const int k = b - 384, rt = k >> 6;
@@ -685,7 +739,14 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             const int e = (int)e0 + tid, a = rt * 32 + (e >> 7), f = e & 127;
             if (a < A.d.A) {
                 const int64_t i = (int64_t)a * 128 + f;
-                A.on.w3[i] = adam(A.on.w3[i], g * inv, A.m.w3[i], A.v.w3[i]);
+                const float p = adam(A.on.w3[i], g * inv, A.m.w3[i], A.v.w3[i]);
+                A.on.w3[i] = p;
+                if (A.img[0])
+#pragma unroll
+                    for (int l = 0; l < 2; ++l) {
+                        const int row = row_of_action(A.q[l], a);
+                        if (row >= 0) put_bf16(A.img[l] + A.q[l].w3() + pol_offset(row, f), p);
+                    }
             }
         }
     } else {  // b3 of rows 32 rt .. 32 rt + 31: 32 rows x 8 tile groups
@@ -719,7 +780,16 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             __syncthreads();  // weight_inv reuses red
             const float inv = weight_inv();
             const int a = rt * 32 + r;
-            if (tid < 32 && a < A.d.A) A.on.b3[a] = adam(A.on.b3[a], s3 * inv, A.m.b3[a], A.v.b3[a]);
+            if (tid < 32 && a < A.d.A) {
+                const float p = adam(A.on.b3[a], s3 * inv, A.m.b3[a], A.v.b3[a]);
+                A.on.b3[a] = p;
+                if (A.img[0])
+#pragma unroll
+                    for (int l = 0; l < 2; ++l) {
+                        const int row = row_of_action(A.q[l], a);
+                        if (row >= 0) reinterpret_cast<float*>(A.img[l] + A.q[l].b3())[row] = p;
+                    }
+            }
         }
     }
     QSTAMP(13);
@@ -823,9 +893,13 @@ int se_qtrain_pack(se_qtrain* q, int32_t which, void* stream) {
     return qtrain_pack(q, which, (hipStream_t)stream);
 }
 
-int se_qtrain_step(se_qtrain* q, int64_t batch, const float* obs, const float* next_obs, const int64_t* act,
-                   const float* rew, const float* done, const float* weight, float gamma, float lr, float beta1,
-                   float beta2, float eps, const int32_t* step_dev, float* loss_out, void* stream) {
+}  // extern "C"
+
+namespace {
+int qtrain_step(se_qtrain* q, se_qnet* qn, int64_t batch, const float* obs, const float* next_obs,
+                const int64_t* act, const float* rew, const float* done, const float* weight, float gamma,
+                float lr, float beta1, float beta2, float eps, int32_t* step_dev, float* loss_out,
+                void* stream) {
     if (!q) return fail(SE_EINVAL, "null qtrain");
     if (!q->bound) return fail(SE_ESTATE, "se_qtrain_bind has not been called");
     if (q->world_version != q->env->world_version)
@@ -833,6 +907,15 @@ int se_qtrain_step(se_qtrain* q, int64_t batch, const float* obs, const float* n
     if (batch < 1 || batch > q->max_batch) return fail(SE_EINVAL, "batch must be in [1, max_batch]");
     if (!obs || !next_obs || !act || !rew || !done || !weight || !step_dev || !loss_out)
         return fail(SE_EINVAL, "null batch / counter / loss pointer");
+    if (qn) {  // the policy must be packed from the very tensors this update changes
+        if (!qn->packed) return fail(SE_ESTATE, "se_qnet_set_weights has not been called");
+        if (qn->env != q->env) return fail(SE_EINVAL, "qnet and qtrain belong to different envs");
+        if (qn->world_version != q->env->world_version)
+            return fail(SE_ESTATE, "ports changed: call se_qnet_set_weights (the port block is folded into fc1)");
+        const float* on[6] = {q->on.w1, q->on.b1, q->on.w2, q->on.b2, q->on.w3, q->on.b3};
+        for (int k = 0; k < 6; ++k)
+            if (qn->w[k] != on[k]) return fail(SE_EINVAL, "the qnet is not packed from the online parameters");
+    }
     DeviceGuard g(q->device);
     const hipStream_t s = (hipStream_t)stream;
     const int64_t tiles = (batch + kQT - 1) / kQT;
@@ -840,13 +923,35 @@ int se_qtrain_step(se_qtrain* q, int64_t batch, const float* obs, const float* n
     static std::atomic<uint64_t> lds_set{0};
     const int rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(qtrain_tile_kernel), (int)lds, q->device);
     if (rc) return rc;
-    QtStepArgs A{q->W, q->on, q->tg, q->d, batch, obs, next_obs, act, rew, done, weight, gamma};
+    QtStepArgs A{q->W, q->on, q->tg, q->d, batch, obs, next_obs, act, rew, done, weight, gamma,
+                 qn ? step_dev : nullptr};
     qtrain_tile_kernel<<<(unsigned)tiles, kQTBlock, lds, s>>>(A);
     HIP_TRY(hipGetLastError());
-    QtAdamArgs B{q->W, q->on, q->m, q->v, q->d, batch, tiles, act, lr, beta1, beta2, eps, step_dev, loss_out};
+    QtAdamArgs B{q->W, q->on, q->m, q->v, q->d, batch, tiles, act, lr, beta1, beta2, eps, step_dev, loss_out,
+                 {qn ? qn->d_img : nullptr, qn ? qn->d_img + qn->c_off : nullptr},
+                 {qn ? qn->q : QnetDims{}, qn ? qn->qc : QnetDims{}}, qn ? 1 : 0};
     qtrain_adam_kernel<<<384 + 65 * q->d.mt3, kQRBlock, 0, s>>>(B);
     HIP_TRY(hipGetLastError());
     return SE_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int se_qtrain_step(se_qtrain* q, int64_t batch, const float* obs, const float* next_obs, const int64_t* act,
+                   const float* rew, const float* done, const float* weight, float gamma, float lr, float beta1,
+                   float beta2, float eps, const int32_t* step_dev, float* loss_out, void* stream) {
+    return qtrain_step(q, nullptr, batch, obs, next_obs, act, rew, done, weight, gamma, lr, beta1, beta2, eps,
+                       const_cast<int32_t*>(step_dev), loss_out, stream);
+}
+
+int se_qtrain_step_policy(se_qtrain* q, se_qnet* qn, int64_t batch, const float* obs, const float* next_obs,
+                          const int64_t* act, const float* rew, const float* done, const float* weight,
+                          float gamma, float lr, float beta1, float beta2, float eps, int32_t* step_dev,
+                          float* loss_out, void* stream) {
+    if (!qn) return fail(SE_EINVAL, "null qnet");
+    return qtrain_step(q, qn, batch, obs, next_obs, act, rew, done, weight, gamma, lr, beta1, beta2, eps,
+                       step_dev, loss_out, stream);
 }
 
 int se_qtrain_destroy(se_qtrain* q) {

@@ -165,6 +165,15 @@ class FusedUpdate:
                                        self.lr, self.betas[0], self.betas[1], self.eps,
                                        _ptr(step_dev), _ptr(loss_out), self.env._stream()))
 
+    def step_policy(self, b: MiniBatch, gamma: float, step_dev: torch.Tensor, loss_out: torch.Tensor, policy):
+        """step(), then policy.repack(bump=step_dev), in the same two launches
+        (se_qtrain_step_policy): the policy's images are written by the Adam kernel and the
+        counter is advanced by the first kernel. policy: a QPolicy packed from `model`."""
+        N.check(N.lib().se_qtrain_step_policy(self._h, policy._h, b.batch, _ptr(b.obs), _ptr(b.next_obs),
+                                              _ptr(b.act), _ptr(b.rew), _ptr(b.done), _ptr(b.weight),
+                                              float(gamma), self.lr, self.betas[0], self.betas[1], self.eps,
+                                              _ptr(step_dev), _ptr(loss_out), self.env._stream()))
+
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
             torch.cuda.synchronize(self.env.device)
@@ -247,13 +256,14 @@ class VecDQNAgent:
     def _update_body(self):
         self.memory.sample(self.batch, t_dev=self._ctr)
         if self.fused:  # _ctr = Adam steps taken so far
-            self.trainer.step(self.batch, self.gamma, self._ctr, self._loss)
-        else:
-            loss = dqn_loss(self.model, self.target_model, self.batch, self.gamma)
-            self.optimizer.zero_grad(set_to_none=False)
-            loss.backward()
-            self.optimizer.step()
-            self._loss.copy_(loss.detach())
+            # the update, the policy's new images and the counter's advance: two launches
+            self.trainer.step_policy(self.batch, self.gamma, self._ctr, self._loss, self.policy)
+            return
+        loss = dqn_loss(self.model, self.target_model, self.batch, self.gamma)
+        self.optimizer.zero_grad(set_to_none=False)
+        loss.backward()
+        self.optimizer.step()
+        self._loss.copy_(loss.detach())
         # the next choose_action sees the new weights; the update counter advances in the same launch
         self.policy.repack(bump=self._ctr)
 

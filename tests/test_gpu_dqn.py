@@ -299,6 +299,14 @@ def test_graph_replay_matches_eager():
     assert agents[1]._graph is not None
     for p, q in zip(agents[0].model.parameters(), agents[1].model.parameters()):
         assert torch.equal(p, q)
+    qs, acts = [], []
+    for a in agents:
+        q = torch.full((a.env.n, a.env.action_space_size), float("nan"), device=a.env.device)
+        acts.append(a.policy.act(0.0, 0, q_out=q).clone())
+        qs.append(q)
+        acts.append(a.policy.act(0.0, 0).clone())  # the compact image
+    assert torch.equal(qs[0], qs[1])
+    assert torch.equal(acts[0], acts[2]) and torch.equal(acts[1], acts[3]) and torch.equal(acts[0], acts[1])
 
 
 def test_training_loop_bookkeeping():
@@ -326,9 +334,11 @@ def test_training_loop_bookkeeping():
 
 def test_fused_launches_equal_the_unfused_loop():
     """The training loop's fused launches (se_policy_record = policy + remember(s, a);
-    se_replay_end_reset = remember(r, s') + reset of the cut episodes; se_qnet_repack with
-    the counter bump) give, bit for bit, what the separate launches give: actions, env
-    state, losses, the update counter and the weights."""
+    se_replay_end_reset = remember(r, s') + reset of the cut episodes; se_qtrain_step_policy
+    = the update + the policy's repack + the counter's advance) give, bit for bit, what the
+    separate launches give: actions, env state, losses, the update counter, the weights,
+    and the Q rows of both policy images (the compact one through the greedy actions, the
+    full one through q_out)."""
     from shippingenv_amd.dqn import VecDQNAgent
 
     class Unfused(VecDQNAgent):
@@ -373,3 +383,11 @@ def test_fused_launches_equal_the_unfused_loop():
     assert int(agents[0]._ctr.item()) > 0 and int(agents[0].cut.sum()) >= 0
     for p, q in zip(agents[0].model.parameters(), agents[1].model.parameters()):
         assert torch.equal(p, q)
+    qs, acts = [], []
+    for a in agents:
+        q = torch.full((a.env.n, a.env.action_space_size), float("nan"), device=a.env.device)
+        acts.append(a.policy.act(0.0, 0, q_out=q).clone())
+        qs.append(q)
+        acts.append(a.policy.act(0.0, 0).clone())  # the compact image
+    assert torch.equal(qs[0], qs[1])
+    assert torch.equal(acts[0], acts[2]) and torch.equal(acts[1], acts[3]) and torch.equal(acts[0], acts[1])
