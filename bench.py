@@ -383,7 +383,7 @@ def run_dqn_train(n, args, dist):
         "update_roofline": {"bound": "mfma (f32)", "achieved": round(upd_tf, 2), "peak": F32_MFMA_PEAK_TFLOPS,
                             "unit": "TFLOP/s", "frac": round(upd_tf / F32_MFMA_PEAK_TFLOPS, 4),
                             "flop_per_sample": flop,
-                            "note": "whole update (sample + 2 kernels + policy repack + counter), graph replay"},
+                            "note": "whole update (sample + 2 kernels: T1 also advances the counter, T2 also rewrites the policy images), graph replay"},
         "batch": args.train_batch,
         "replay_capacity": agent.memory.capacity,
         "final_loss": float(loss),
