@@ -391,3 +391,31 @@ def test_fused_launches_equal_the_unfused_loop():
         acts.append(a.policy.act(0.0, 0).clone())  # the compact image
     assert torch.equal(qs[0], qs[1])
     assert torch.equal(acts[0], acts[2]) and torch.equal(acts[1], acts[3]) and torch.equal(acts[0], acts[1])
+
+
+def test_update_with_policy_refuses_a_foreign_qnet():
+    """se_qtrain_step_policy writes the policy's images from the parameters it updates, so it
+    refuses a qnet packed from other tensors (another model, or a copy)."""
+    from shippingenv_amd import _native as N
+    from shippingenv_amd.dqn import VecDQNAgent
+    from shippingenv_amd.policy import DQNNetwork, QPolicy
+
+    env = make_env(1024, seed=5)
+    torch.manual_seed(0)
+    agent = VecDQNAgent(env, graph=False, batch_size=64)
+    _OPEN.append(agent)
+    for _ in range(3):
+        agent.step()
+    other = QPolicy(env, DQNNetwork(env.obs_size, env.action_space_size))
+    _OPEN.append(other)
+    before = [p.detach().clone() for p in agent.model.parameters()]
+    ctr = int(agent._ctr.item())
+    with pytest.raises(N.ShipEnvError, match="not packed from the online parameters"):
+        agent.trainer.step_policy(agent.batch, agent.gamma, agent._ctr, agent._loss, other)
+    torch.cuda.synchronize()
+    assert int(agent._ctr.item()) == ctr  # refused before any launch
+    for p, q in zip(agent.model.parameters(), before):
+        assert torch.equal(p, q)
+    agent.trainer.step_policy(agent.batch, agent.gamma, agent._ctr, agent._loss, agent.policy)
+    torch.cuda.synchronize()
+    assert int(agent._ctr.item()) == ctr + 1
