@@ -25,9 +25,9 @@
 // row (of nine); the full layout serves q_out (every row's Q, for tests / inspection).
 //
 // LDS: the packed network (113 KB at P = 5) plus the world image, one 1024-thread
-// workgroup (16 waves, 4 per SIMD, <= 128 VGPRs) per CU for the whole launch. At 128
-// VGPRs the kernel spills 28 B per lane to scratch: check the spill count
-// (-Rpass-analysis=kernel-resource-usage) after any edit that adds register pressure.
+// workgroup (16 waves, 4 per SIMD, <= 128 VGPRs) per CU for the whole launch. It fits
+// 128 VGPRs with no spills and no scratch: check (-Rpass-analysis=kernel-resource-usage)
+// after any edit that adds register pressure.
 
 #ifndef SHIPENV_POLICY_ABL
 #define SHIPENV_POLICY_ABL 0  // timing-only ablations of the policy kernel (1: plain max epilogue, 2: no fc3)

@@ -201,12 +201,11 @@ __device__ __forceinline__ LdsWorld stage_world(const uint32_t* __restrict__ g, 
     uint4* l4 = reinterpret_cast<uint4*>(lds);
     constexpr int kR = 4;
     for (int i0 = 0; i0 < total; i0 += kR * (int)blockDim.x) {
+        // unconditional loads (past the end: the last word again), so r stays in VGPRs: a
+        // conditionally assigned array was placed in scratch
         uint4 r[kR];
 #pragma unroll
-        for (int k = 0; k < kR; ++k) {
-            const int i = i0 + (int)threadIdx.x + k * (int)blockDim.x;
-            if (i < total) r[k] = g4[i];
-        }
+        for (int k = 0; k < kR; ++k) r[k] = g4[min(i0 + (int)threadIdx.x + k * (int)blockDim.x, total - 1)];
 #pragma unroll
         for (int k = 0; k < kR; ++k) {
             const int i = i0 + (int)threadIdx.x + k * (int)blockDim.x;
