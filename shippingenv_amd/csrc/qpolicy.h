@@ -81,8 +81,8 @@ struct QnetDims {
     __host__ __device__ int b1() const { return w3() + mt3 * 8 * 1024; } // 128 f32, port block folded
     __host__ __device__ int b2() const { return b1() + 4 * kQHidden; }
     __host__ __device__ int b3() const { return b2() + 4 * kQHidden; }   // mt3 * 32 f32 (0 beyond A)
-    __host__ __device__ int next() const { return b3() + mt3 * 128; }    // P int32: next port on the cell
-    __host__ __device__ int regm() const { return next() + 4 * P; }      // mt3 uint32: fc3 epilogue regs
+    __host__ __device__ int same() const { return b3() + mt3 * 128; }    // P uint64: ports on port p's cell
+    __host__ __device__ int regm() const { return same() + 8 * P; }      // mt3 uint32: fc3 epilogue regs
     __host__ __device__ int bytes() const { return (regm() + 4 * mt3 + 15) & ~15; }
 };
 
@@ -170,11 +170,11 @@ __global__ __launch_bounds__(256) void qnet_pack_kernel(PackArgs A) {
             reinterpret_cast<float*>(img + q.b2())[u] = A.b2[u];
         } else if ((u -= kQHidden) < q.mt3 * 32) {
             reinterpret_cast<float*>(img + q.b3())[u] = u < q.rows ? A.b3[q.action_of_row(u)] : 0.0f;
-        } else if ((u -= q.mt3 * 32) < P) {  // next port on the same cell, ascending (-1: none)
-            int nx = -1;
-            for (int p = u + 1; p < P && nx < 0; ++p)
-                if (pos[p] == pos[u]) nx = p;
-            reinterpret_cast<int32_t*>(img + q.next())[u] = nx;
+        } else if ((u -= q.mt3 * 32) < P) {  // bit p: port p stands on port u's cell (u included)
+            uint64_t same = 0;
+            for (int p = 0; p < P; ++p)
+                if (pos[p] == pos[u]) same |= 1ull << p;
+            reinterpret_cast<uint64_t*>(img + q.same())[u] = same;
         } else {
             // fc3 tile mt = u - P: bit reg set when accumulator register reg (rows
             // base + (reg & 3) + 8 (reg >> 2) + 4h, h = 0, 1) can hold a valid action of
@@ -280,7 +280,7 @@ void policy_kernel(PolicyArgs A) {
     const float* B1 = reinterpret_cast<const float*>(qb + q.b1());
     const float* B2 = reinterpret_cast<const float*>(qb + q.b2());
     const float* B3 = reinterpret_cast<const float*>(qb + q.b3());
-    const int32_t* NEXT = reinterpret_cast<const int32_t*>(qb + q.next());
+    const uint64_t* SAME = reinterpret_cast<const uint64_t*>(qb + q.same());
     const uint32_t* REGM = reinterpret_cast<const uint32_t*>(qb + q.regm());
 
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -366,6 +366,8 @@ void policy_kernel(PolicyArgs A) {
         const int fst = cur >= 0 ? min(w.pfuel(max(cur, 0)), 199) : 0;
         // valid TAKE rows of this env in the layout's row space
         const int c_lo = q.cargo_row1(), c_hi = c_lo + cst - 1, f_lo = q.fuel_row1(), f_hi = f_lo + fst - 1;
+        // SELECT: bit p for each port on the ship's cell other than the origin (P <= 64)
+        const uint64_t sel = cur >= 0 ? SAME[max(cur, 0)] & ~(origin >= 0 ? 1ull << origin : 0ull) : 0ull;
         float best = -INFINITY;
         int bidx = 0x7fffffff;
 #if SHIPENV_POLICY_ABL == 2  // timing-only: no fc3
@@ -383,11 +385,9 @@ void policy_kernel(PolicyArgs A) {
             if (!A.q_out && !__any(maybe)) continue;
             uint32_t m = range_bits(-base, 3 - base) | range_bits(c_lo - base, c_hi - base) |
                          range_bits(f_lo - base, f_hi - base);
-            if (base < 4 + P) {  // SELECT rows live in this tile (uniform)
-                for (int p = cur; p >= 0; p = NEXT[p]) {
-                    const int i = 4 + p - base;
-                    if (p != origin && i >= 0 && i < 32) m |= 1u << i;
-                }
+            if (base < 4 + P) {  // SELECT rows 4 + p live in this tile (uniform): sel shifted by 4 - base
+                const int sh = base - 4;
+                m |= (uint32_t)(sh < 0 ? sel << -sh : (sh < 64 ? sel >> sh : 0ull));
             }
             // registers that hold no valid action for any env are skipped (wave-uniform)
             const uint32_t rm = __builtin_amdgcn_readfirstlane(REGM[mt]);
@@ -435,14 +435,14 @@ void policy_kernel(PolicyArgs A) {
                 const U4 d = draw(env_key(A.seed, A.env_base + e), A.t, kSlotPolicy);
                 if (u32(d.v[0]) <= A.eps) {  // np.random.rand() <= epsilon (:191)
                     // random.choice(valid_actions) (:192): the k-th valid action, ascending
-                    int nsel = 0;
-                    for (int p = cur; p >= 0; p = NEXT[p]) nsel += p != origin;
+                    const int nsel = __popcll(sel);
                     int k = uniform_int(d.v[1], (uint32_t)(4 + nsel + cst + fst));
                     if (k < 4) {
                         act = k;
-                    } else if ((k -= 4) < nsel) {
-                        for (int p = cur; p >= 0; p = NEXT[p])
-                            if (p != origin && k-- == 0) act = 4 + p;
+                    } else if ((k -= 4) < nsel) {  // the k-th port of sel, ascending
+                        uint64_t b = sel;
+                        for (; k > 0; --k) b &= b - 1;
+                        act = 4 + __builtin_ctzll(b);
                     } else {
                         k -= nsel;
                         act = k < cst ? 5 + P + k : 55 + P + (k - cst);  // amounts k + 1 (action space)

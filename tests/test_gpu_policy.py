@@ -112,9 +112,13 @@ def test_q_values_vs_torch(n, ports, steps):
     assert float((qk - q32).abs().max()) <= 0.03 * float(q32.abs().max())
 
 
-@pytest.mark.parametrize("steps", [0, 40])
-def test_greedy_is_first_masked_argmax(steps):
-    env, model, pol = make(8192 + 7, steps=steps, scale=20.0)
+# three ports on one cell (add_port appends duplicates): SELECT is valid for the others
+SHARED = [[41, 40], [41, 40], [60, 22], [41, 40], [78, 29]]
+
+
+@pytest.mark.parametrize("steps,ports", [(0, None), (40, None), (0, SHARED), (30, SHARED)])
+def test_greedy_is_first_masked_argmax(steps, ports):
+    env, model, pol = make(8192 + 7, ports=ports, steps=steps, scale=20.0)
     A = env.action_space_size
     q_out = torch.empty((env.n, A), dtype=torch.float32, device=env.device)
     act = pol.act(0.0, 5, q_out=q_out).cpu().numpy()
@@ -124,6 +128,8 @@ def test_greedy_is_first_masked_argmax(steps):
     assert valid[np.arange(env.n), act].all()
     if steps == 0:  # at ports: non-move actions are chosen too
         assert (act >= 4).any()
+    if ports is SHARED and steps == 0:  # ships on the shared cell can select its other ports
+        assert valid[:, 4:9].sum(axis=1).max() >= 2
     # fp32 agreement wherever the fp32 decision is not within the bf16 tolerance
     q32 = model(env.observe()).detach().double().cpu().numpy()
     m32 = np.where(valid, q32, -np.inf)
@@ -146,9 +152,9 @@ def explore_expected(env, valid, t):
     return out, u
 
 
-@pytest.mark.parametrize("steps", [0, 25])
-def test_explore_is_uniform_over_valid_actions(steps):
-    env, model, pol = make(3000, steps=steps)
+@pytest.mark.parametrize("steps,ports", [(0, None), (25, None), (0, SHARED)])
+def test_explore_is_uniform_over_valid_actions(steps, ports):
+    env, model, pol = make(3000, ports=ports, steps=steps)
     valid = valid_bool(env)
     act = pol.act(1.0, 9).cpu().numpy()
     want, _ = explore_expected(env, valid, 9)
