@@ -1804,9 +1804,16 @@ __device__ __forceinline__ uint32_t bits_in(int lo, int hi) {
 // workgroup stores the tile with 16-byte writes.
 __global__ __launch_bounds__(kBlock) void valid_mask_tiled_kernel(MaskArgs A) {
     extern __shared__ uint8_t mlds[];  // [kTileRows][S] (+ pad to 16 bytes)
+    __shared__ uint64_t same[64];  // P <= 64: bit q of same[p] = port q stands on port p's cell
     const LdsWorld w = world_view(A.dims, A.world);
     const int P = w.P, S = A.stride, nw = (S + 3) / 4;
     const int c_lo = 5 + P, f_lo = 55 + P;  // TAKE_CARGO / TAKE_FUEL amount 1
+    const bool masks = P <= 64;  // the SELECT rows as one shifted mask per env (else a scan)
+    if (masks && (int)threadIdx.x < P) {
+        uint64_t m = 0;
+        for (int q = 0; q < P; ++q) m |= (uint64_t)(w.pos[q] == w.pos[threadIdx.x]) << q;
+        same[threadIdx.x] = m;
+    }
     for (int64_t r0 = (int64_t)blockIdx.x * kTileRows; r0 < A.n; r0 += (int64_t)gridDim.x * kTileRows) {
         const int rows = (int)min((int64_t)kTileRows, A.n - r0);
         __syncthreads();  // the previous tile's stores have read the LDS tile
@@ -1817,16 +1824,22 @@ __global__ __launch_bounds__(kBlock) void valid_mask_tiled_kernel(MaskArgs A) {
             const int cur = w.port_at(x, y);  // the first port on the ship's cell
             const int cst = cur >= 0 ? w.pcargo(cur) : 0, fst = cur >= 0 ? w.pfuel(cur) : 0;
             const uint32_t spos = (uint32_t)x | ((uint32_t)y << 16);
+            // SELECT p: every port on the ship's cell but the origin (dqn.py:152-161)
+            const uint64_t sel = masks && cur >= 0 ? same[cur] & ~(origin >= 0 ? 1ull << origin : 0ull) : 0ull;
             uint8_t* row = mlds + threadIdx.x * S;
             for (int k = 0; k < nw; ++k) {
                 const int b = 32 * k;
                 uint32_t m = bits_in(-b, 3 - b);  // moves: always
                 if (cur >= 0) {
                     m |= bits_in(c_lo - b, c_lo + min(cst, 49) - 1 - b) | bits_in(f_lo - b, f_lo + min(fst, 199) - 1 - b);
-                    // SELECT p: every port on the ship's cell but the origin (dqn.py:152-161)
-                    const int p0 = max(cur, b - 4), p1 = min(P, b + 28);
-                    for (int p = p0; p < p1; ++p)
-                        if (w.pos[p] == spos && p != origin) m |= 1u << (4 + p - b);
+                    if (masks) {  // rows 4 + p: sel shifted by 4 - b
+                        const int sh = b - 4;
+                        m |= (uint32_t)(sh < 0 ? sel << -sh : (sh < 64 ? sel >> sh : 0ull));
+                    } else {
+                        const int p0 = max(cur, b - 4), p1 = min(P, b + 28);
+                        for (int p = p0; p < p1; ++p)
+                            if (w.pos[p] == spos && p != origin) m |= 1u << (4 + p - b);
+                    }
                 }
                 const uint32_t word = __builtin_amdgcn_perm(0u, __builtin_bitreverse32(m), 0x00010203u);
 #pragma unroll
