@@ -280,9 +280,12 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         (which ? XN : X)[c * kLS + j] = v;
     }
     if (tid < 32) {
+        // an action outside [0, A) (the reference's gather would raise) takes no part in the
+        // update (weight 0), and its W3 row gather reads row 0 instead of past the matrix
         const int64_t row = r0 + tid;
-        const bool live = row < A.B;
-        ACT[tid] = live ? (int)A.act[row] : 0;
+        const int64_t a = row < A.B ? A.act[row] : -1;
+        const bool live = a >= 0 && a < A.d.A;
+        ACT[tid] = live ? (int)a : 0;
         WT[tid] = live ? A.weight[row] : 0.0f;
     }
     __syncthreads(); QSTAMP(1);
