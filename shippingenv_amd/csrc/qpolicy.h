@@ -39,9 +39,10 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 constexpr int kQHidden = 128;     // DQNNetwork hidden_size (dqn.py:24, default 128)
-// 16 waves (4 per SIMD, <= 128 VGPRs, 28 B of scratch) share one LDS copy of the network.
-// Measured per launch at 2^20 envs: 512 threads 108.8 us, 768 (3 waves per SIMD, 165 VGPRs)
-// 92.5 us, 1024 87.2 us: the fourth wave covers the others' MFMA -> relu -> MFMA stalls.
+// 16 waves (4 per SIMD, <= 128 VGPRs, no scratch) share one LDS copy of the network.
+// Measured per launch at 2^20 envs when it was chosen (round 1 kernel): 512 threads
+// 108.8 us, 768 (3 waves per SIMD, 165 VGPRs) 92.5 us, 1024 87.2 us: the fourth wave
+// covers the others' MFMA -> relu -> MFMA stalls.
 #ifndef SHIPENV_POLICY_BLOCK
 #define SHIPENV_POLICY_BLOCK 1024
 #endif
