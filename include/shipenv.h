@@ -247,6 +247,12 @@ int se_replay_end(se_replay* r, uint8_t* cut, int32_t max_steps, void* stream);
  * same pass, with the draws se_reset would make (the env's reset epoch advances). */
 int se_policy_record(se_qnet* q, se_replay* r, int32_t* actions, double epsilon, uint32_t t, void* stream);
 int se_replay_end_reset(se_replay* r, uint8_t* cut, int32_t max_steps, void* stream);
+/* se_step_record = se_step + se_replay_end_reset in one launch: the step kernel writes the
+ * ring's reward / done / s' record and restarts the cut envs from the state it holds
+ * (env.step + remember + env.reset of the training loop, agents/dqn.py:281-309). Needs an
+ * auto-reset env; when n, the ring head / capacity are not multiples of 4 or cut is not
+ * 4-byte aligned it makes the two launches instead. Results are identical either way. */
+int se_step_record(se_replay* r, const int32_t* actions, uint8_t* cut, int32_t max_steps, void* stream);
 int se_replay_size(se_replay* r, int64_t* size, int64_t* capacity);
 /* A minibatch of `batch` distinct transitions: batch position j takes logical index
  * perm(j) of a 4-round Feistel permutation of [0, size) keyed by Philox(seed, 2^64 - 1) at

@@ -34,7 +34,7 @@ EXPORTS = (
     "se_step_typed", "se_step_replay", "se_observe", "se_valid_mask", "se_gen_actions",
     "se_sample_actions", "se_rollout", "se_qnet_create", "se_qnet_set_weights", "se_policy",
     "se_qnet_repack", "se_policy_record",
-    "se_qnet_destroy", "se_replay_create", "se_replay_begin", "se_replay_end", "se_replay_end_reset",
+    "se_qnet_destroy", "se_replay_create", "se_replay_begin", "se_replay_end", "se_replay_end_reset", "se_step_record",
     "se_replay_size",
     "se_replay_sample", "se_replay_destroy", "se_qtrain_create", "se_qtrain_bind", "se_qtrain_pack",
     "se_qtrain_step", "se_qtrain_step_policy", "se_qtrain_destroy",
@@ -93,6 +93,7 @@ def _declare(lib):
         "se_replay_begin": [P, P, P],
         "se_replay_end": [P, P, C.c_int32, P],
         "se_replay_end_reset": [P, P, C.c_int32, P],
+        "se_step_record": [P, P, P, C.c_int32, P],
         "se_replay_size": [P, P, P],
         "se_replay_sample": [P, i64, P, u32, P, P, P, P, P, P, P],
         "se_replay_destroy": [P],

@@ -28,7 +28,6 @@
 
 namespace {
 
-constexpr uint8_t kRecDone = 1, kRecInvalid = 2;  // flags byte
 constexpr int kReplayTries = 4;
 constexpr int kSampleRows = 64;                   // transitions per sample workgroup
 constexpr int64_t kReplayKeyId = -1;              // Philox key (seed, 2^64 - 1): no env has this id
@@ -413,6 +412,36 @@ int se_replay_end(se_replay* r, uint8_t* cut, int32_t max_steps, void* stream) {
 
 int se_replay_end_reset(se_replay* r, uint8_t* cut, int32_t max_steps, void* stream) {
     return replay_end(r, cut, max_steps, true, stream);
+}
+
+int se_step_record(se_replay* r, const int32_t* actions, uint8_t* cut, int32_t max_steps, void* stream) {
+    if (!r) return fail(SE_EINVAL, "null replay");
+    int rc = check_ready(r->env);
+    if (rc) return rc;
+    if (!r->open) return fail(SE_ESTATE, "se_step_record without se_replay_begin / se_policy_record");
+    if (!cut) return fail(SE_EINVAL, "se_step_record needs a cut buffer");
+    se_env* env = r->env;
+    if (!(env->flags & SE_FLAG_AUTO_RESET) || !env->st.ep_len)
+        return fail(SE_EINVAL, "se_step_record needs an auto-reset env");
+    if (env->dims.P < 2) return fail(SE_EINVAL, "reset needs at least two ports");
+    if (!actions || !aligned16(actions)) return fail(SE_EINVAL, "actions must be a 16-byte aligned buffer");
+    // one launch where every group's ring slots are consecutive; otherwise the two
+    // launches it replaces, with the same results
+    if (env->n == 0 || env->n % 4 != 0 || r->head % 4 != 0 || r->cap % 4 != 0 || ((uintptr_t)cut & 3u) != 0 ||
+        env->iters > kRecMaxIters) {
+        rc = se_step(env, actions, stream);
+        return rc ? rc : replay_end(r, cut, max_steps, true, stream);
+    }
+    const int64_t new_size = std::min(r->size + env->n, r->cap);
+    const StepRecord rec{r->ring.rew, r->ring.flags, r->ring.n_pos, r->ring.n_fuel, r->ring.d_size,
+                         r->head, r->cap, new_size, cut, max_steps, (uint32_t)env->epoch};
+    rc = launch_step(env, false, false, actions, nullptr, nullptr, nullptr, stream, &rec);
+    if (rc) return rc;
+    env->epoch += 1;  // as se_reset
+    r->head = (r->head + env->n) % r->cap;
+    r->size = new_size;
+    r->open = false;
+    return SE_OK;
 }
 
 int se_policy_record(se_qnet* qn, se_replay* r, int32_t* actions, double epsilon, uint32_t t, void* stream) {

@@ -450,6 +450,25 @@ __device__ uint64_t g_trace[kTraceWaves * 8];
     } while (0)
 #endif
 
+constexpr uint8_t kRecDone = 1, kRecInvalid = 2;  // replay ring flags byte (csrc/replay.h)
+
+constexpr int64_t kRecMaxIters = 8;  // se_step_record's cut bits: 4 per group, <= 32 per thread
+
+// se_step_record: the replay ring's end-of-step record (replay_end4_kernel's stores,
+// csrc/replay.h) written by the step kernel from the state it holds in registers, and
+// the cut envs restarted there (se_replay_end_reset). Null rew outside se_step_record.
+struct StepRecord {
+    float* rew;
+    uint8_t* flags;
+    uint32_t* n_pos;
+    float* n_fuel;
+    int64_t* d_size;
+    int64_t head, cap, new_size;  // head, cap multiples of 4 (a group's slots are consecutive)
+    uint8_t* cut;
+    int32_t max_steps;
+    uint32_t epoch;
+};
+
 struct StepArgs {
     const uint32_t* world;
     WorldDims dims;
@@ -467,6 +486,7 @@ struct StepArgs {
     int64_t seg;             // segment stride (records) of one workgroup
     int64_t iters;           // groups per thread (each workgroup owns iters * 256 groups)
     double* slab;            // per-wave {sum_ret, n_eps, sum_len, pad}
+    StepRecord rec;          // step_kernel<..., kRec = true> only
 };
 
 // The kernel's StepArgs re-read from the kernarg segment where a late phase needs
@@ -678,6 +698,7 @@ struct Finished {
     uint32_t mask = 0;
     float ret[4];
     int32_t len[4];
+    uint32_t cut = 0;  // se_step_record: bit j = env j of the group restarts (cut)
 };
 
 // x, y, fuel, done, err of a group's 4 envs: final once the first half has run
@@ -1057,7 +1078,71 @@ __device__ __forceinline__ Draws early_draws(const StepArgs& A, int64_t base) {
 template <bool kAuto>
 constexpr bool spec_loss() { return SHIPENV_SPEC_LOSS < 0 ? kAuto : SHIPENV_SPEC_LOSS != 0; }
 
-template <bool kAuto, bool kFull, bool kNt>
+// se_step_record, per group of 4 envs at env index base (a full group; head and cap
+// multiples of 4, so its ring slots are consecutive): the stores of replay_end4_kernel
+// (csrc/replay.h) from the post-step values this thread just computed. After the
+// thread's last group, record_restart runs se_replay_end_reset's restart of the cut envs
+// (reset_kernel's body, at most one bit per env of the thread's <= 8 groups). Their
+// fields were stored by this thread earlier in program order; the restart stores the same
+// addresses again, as the separate replay-end launch would after the step. Deferred past
+// the loop, the restart's registers do not overlap the group's (inline there it spilled).
+__device__ __forceinline__ void record_restart(const StepArgs& A, const LdsWorld& w, uint32_t cuts) {
+    const se_state& S = A.st;
+    const int64_t first = (int64_t)blockIdx.x * A.iters * kStepBlock;  // step_kernel's first group
+    while (cuts) {
+        const int b = __builtin_ctz(cuts);
+        cuts &= cuts - 1;
+        const int64_t i = (first + (int64_t)(b >> 2) * kStepBlock + threadIdx.x) * 4 + (b & 3);
+        const U4 o = draw(env_key(A.seed, A.env_base + i), A.rec.epoch, kSlotExplicitReset);
+        Ship sh;
+        reset_ship(w, sh, o.v[0], o.v[1]);
+        S.x[i] = (uint8_t)sh.x;
+        S.y[i] = (uint8_t)sh.y;
+        S.fuel[i] = sh.fuel;
+        S.cargo[i] = sh.cargo;
+        S.origin[i] = (uint8_t)sh.origin;
+        S.dest[i] = (uint8_t)sh.dest;
+        S.ep_return[i] = 0.0f;
+        S.ep_len[i] = 0;
+        S.done[i] = 0;
+        S.err[i] = 0;
+        S.reward[i] = 0.0f;
+    }
+}
+
+__device__ __forceinline__ int64_t record_slot(const StepRecord& R, int64_t base) {
+    const int64_t slot = R.head + base;
+    return slot - (slot >= R.cap ? R.cap : 0);
+}
+
+__device__ __forceinline__ void record_early(const StepArgs& A, int64_t base, uint32_t flags4, const float (&fuel)[4]) {
+    const StepRecord& R = A.rec;
+    const int64_t slot = record_slot(R, base);
+    *reinterpret_cast<uint32_t*>(R.flags + slot) = flags4;
+    *reinterpret_cast<float4*>(R.n_fuel + slot) = make_float4(fuel[0], fuel[1], fuel[2], fuel[3]);
+}
+
+// returns the cut envs as bits 0-3
+__device__ __forceinline__ uint32_t record_group(const StepArgs& A, int64_t base, const float (&rw)[4],
+                                                 uint32_t x4, uint32_t y4, uint32_t o4, uint32_t d4,
+                                                 uint32_t cut4, const int32_t (&len)[4]) {
+    const StepRecord& R = A.rec;
+    const int64_t slot = record_slot(R, base);
+    uint4 pos;
+    uint32_t* pw = &pos.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        pw[j] = ((x4 >> (8 * j)) & 0xffu) | ((y4 >> (8 * j)) & 0xffu) << 8 | ((o4 >> (8 * j)) & 0xffu) << 16 |
+                ((d4 >> (8 * j)) & 0xffu) << 24;
+        if (R.max_steps > 0) cut4 |= (uint32_t)(len[j] >= R.max_steps) << (8 * j);
+    }
+    *reinterpret_cast<float4*>(R.rew + slot) = make_float4(rw[0], rw[1], rw[2], rw[3]);
+    *reinterpret_cast<uint4*>(R.n_pos + slot) = pos;
+    *reinterpret_cast<uint32_t*>(R.cut + base) = cut4;
+    return (cut4 & 1u) | ((cut4 >> 7) & 2u) | ((cut4 >> 14) & 4u) | ((cut4 >> 21) & 8u);
+}
+
+template <bool kAuto, bool kFull, bool kNt, bool kRec = false>
 __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWorld& w,
                                                  Group<false, kAuto, kNt>& G, At<kFull> at,
                                                  BlockStats& bs, Finished& F, const Draws& D) {
@@ -1208,6 +1293,7 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
         G.load_episode(late_args(), at);
     }
     // x, y, fuel, done and err are final here (cargo loss and arrival change none)
+    uint32_t rec_x = 0, rec_y = 0, rec_cut = 0;
     {
         const uint32_t t01 = __builtin_amdgcn_perm(pos[1], pos[0], 0x06020400u);  // x0 x1 y0 y1
         const uint32_t t23 = __builtin_amdgcn_perm(pos[3], pos[2], 0x06020400u);  // x2 x3 y2 y3
@@ -1218,6 +1304,20 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
         for (int j = 0; j < 4; ++j) {
             dn |= ((dead >> j) & 1u) << (8 * j);
             ee |= (uint32_t)(err[j] & 0xff) << (8 * j);
+        }
+        if constexpr (kRec) {  // replay_end4_kernel's flags and s' fuel now; x / y held to the end
+            rec_x = ox;
+            rec_y = oy;
+            uint32_t flags4 = 0;
+            float nf[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool raised = err[j] != SE_ERR_OK;
+                nf[j] = (float)f[j];
+                flags4 |= (((dead >> j) & 1u ? (uint32_t)kRecDone : 0u) | (raised ? (uint32_t)kRecInvalid : 0u)) << (8 * j);
+                rec_cut |= (uint32_t)raised << (8 * j);
+            }
+            record_early(late_args(), base, flags4, nf);
         }
         const se_state& S = A.st;
         __builtin_amdgcn_sched_barrier(0);  // the fuel halves back to back (store_moved)
@@ -1322,6 +1422,7 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
         store4(S.ep_return, at, epr);
         store4(S.ep_len, at, epl);
     }
+    if constexpr (kRec) F.cut = record_group(late_args(), base, rw, rec_x, rec_y, oo, od, rec_cut, epl);
 }
 
 // Sum over the wave's 64 lanes in a fixed tree, so the result does not depend on
@@ -1403,8 +1504,9 @@ __device__ __forceinline__ void wave_compact(const StepArgs& A, const Finished& 
 // step_tail_kernel, so this loop carries no guarded scalar path. The world image's
 // loads, then the first group's, are all in flight before the LDS writes; each
 // iteration loads the next group after storing the current one.
-template <bool kTyped, bool kReplay, bool kAuto, bool kNt = false>
+template <bool kTyped, bool kReplay, bool kAuto, bool kNt = false, bool kRec = false>
 __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4))) void step_kernel(StepArgs A) {
+    static_assert(!kRec || (kAuto && !kTyped && !kReplay), "se_step_record: agent actions, auto-reset");
     extern __shared__ uint32_t lds[];
     const int64_t full = A.n >> 2;
     const int64_t first = (int64_t)blockIdx.x * A.iters * kStepBlock;  // block-uniform first group
@@ -1442,6 +1544,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
     TRACE_STAMP(1);
 
     BlockStats bs;
+    uint32_t cuts = 0;  // kRec: bit 4k + j = env j of this thread's group k restarts
     for (int64_t k = 0; k < A.iters; ++k) {
         const int64_t g0 = first + k * kStepBlock, g = g0 + threadIdx.x;
         Finished F;
@@ -1453,7 +1556,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
         if (g < full) {
             if constexpr (kAgent) {
                 if (k > 0) D = early_draws<spec_loss<kAuto>()>(A, g * 4);
-                step_group_agent<kAuto, true, kNt>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F, D);
+                step_group_agent<kAuto, true, kNt, kRec>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F, D);
+                if constexpr (kRec) cuts |= F.cut << (4 * k);
             } else
                 step_group<kTyped, kReplay, kAuto, true, kNt>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F);
             if (k == 0) TRACE_STAMP(2);
@@ -1468,6 +1572,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
     __builtin_amdgcn_s_waitcnt(0);  // stores acknowledged
     TRACE_STAMP(3);
 #endif
+    if constexpr (kRec) {  // the ring's stored count, read by the sampler (replay_end4_kernel)
+        if (blockIdx.x == 0 && threadIdx.x == 0) *late_args().rec.d_size = late_args().rec.new_size;
+        if (cuts) record_restart(late_args(), w, cuts);
+    }
     if (kAuto && (SHIPENV_ABL4 & 4) == 0) {
         // per-wave statistics: a fixed-order tree (wave_sum), added to this wave's own
         // slab entry. With episodes ending about once per 240 steps, most waves have one
@@ -2204,7 +2312,7 @@ int check_ready(se_env* env) {
 }
 
 int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const int32_t* a,
-                const int32_t* b, se_tape* tape, void* stream) {
+                const int32_t* b, se_tape* tape, void* stream, const StepRecord* rec = nullptr) {
     int rc = check_ready(env);
     if (rc) return rc;
     if (!act || (typed && (!a || !b)) || (replay && !tape))
@@ -2240,7 +2348,12 @@ int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const 
     const size_t lds = lds_bytes(env);
     const int grid = env->grid;
     const bool ntl = step_nt_loads(env);
-    if (env->n >= kEnvsPerThread) {  // at least one full group (step_kernel's first load assumes it)
+    if (rec) {  // se_step_record: the caller checked agent actions, auto-reset, n % 4 == 0, n > 0
+        A.rec = *rec;
+        if (ntl) step_kernel<false, false, true, true, true><<<grid, kStepBlock, lds, s>>>(A);
+        else step_kernel<false, false, true, false, true><<<grid, kStepBlock, lds, s>>>(A);
+        HIP_TRY(hipGetLastError());
+    } else if (env->n >= kEnvsPerThread) {  // at least one full group (step_kernel's first load assumes it)
         if (!typed && !autoreset && ntl) step_kernel<false, false, false, true><<<grid, kStepBlock, lds, s>>>(A);
         else if (!typed && autoreset && ntl) step_kernel<false, false, true, true><<<grid, kStepBlock, lds, s>>>(A);
         else if (!typed && !autoreset) step_kernel<false, false, false><<<grid, kStepBlock, lds, s>>>(A);

@@ -98,6 +98,17 @@ class ReplayBuffer:
         fn = N.lib().se_replay_end_reset if reset else N.lib().se_replay_end
         N.check(fn(self._h, _ptr(cut), int(max_steps), self.env._stream()))
 
+    def step_end(self, actions: torch.Tensor, cut: torch.Tensor, max_steps: int = 0):
+        """env.step(actions) then end(cut, max_steps, reset=True) in one launch
+        (se_step_record: the step kernel writes the record and restarts the cut envs)."""
+        env = self.env
+        a = actions
+        if not (type(a) is torch.Tensor and a.dtype is torch.int32 and a.is_cuda and a.is_contiguous()
+                and a.numel() == env.n and a.data_ptr() % 16 == 0):
+            a = env._dev(actions, torch.int32)
+        N.check(N.lib().se_step_record(self._h, _ptr(a), _ptr(cut), int(max_steps), env._stream()))
+        env._keep = a
+
     def sample(self, out: MiniBatch, t: int = 0, t_dev: torch.Tensor | None = None) -> MiniBatch:
         """update()'s minibatch (agents/dqn.py:213-224) into `out`; the sampler key is t, or
         the device counter t_dev (uint32 viewed as int32) when given."""
@@ -304,13 +315,11 @@ class VecDQNAgent:
 
     def step(self):
         """One training-loop iteration for every env; returns the last update's loss (or None)."""
-        env = self.env
         # choose_action + remember(state, action): one launch (se_policy_record)
         a = self.policy.act_record(self.memory, self.epsilon, self.t)
-        env.step(a)
-        # remember's reward / next_state, and the episodes that raised or reached max_steps
-        # start over (env.reset(cut)): one launch (se_replay_end_reset)
-        self.memory.end(self.cut, self.max_steps, reset=True)
+        # env.step, remember's reward / next_state, and the episodes that raised or reached
+        # max_steps start over (env.reset(cut)): one launch (se_step_record)
+        self.memory.step_end(a, self.cut, self.max_steps)
         loss = None
         for _ in range(self.updates_per_step):
             loss = self.update()

@@ -393,6 +393,62 @@ def test_fused_launches_equal_the_unfused_loop():
     assert torch.equal(acts[0], acts[2]) and torch.equal(acts[1], acts[3]) and torch.equal(acts[0], acts[1])
 
 
+@pytest.mark.parametrize("n,cap", [(4096, 20000), (4096, 10000), (4100, 10002), (4098, 20000)])
+def test_step_record_equals_step_then_end_reset(n, cap):
+    """se_step_record (one launch: the step kernel writes the ring's record and restarts the
+    cut envs) against se_step + se_replay_end_reset, bit for bit: env state, cut mask, episode
+    statistics and the ring, read through minibatches of every stored transition. The first
+    two cases take the one-launch path (the second wraps the ring); n or the capacity not a
+    multiple of 4 take the two-launch path inside se_step_record."""
+    from shippingenv_amd.dqn import MiniBatch, ReplayBuffer
+
+    envs, rbs, cuts = [], [], []
+    for _ in range(2):
+        env = make_env(n, seed=13)
+        rb = ReplayBuffer(env, cap)
+        _OPEN.append(rb)
+        envs.append(env)
+        rbs.append(rb)
+        cuts.append(torch.zeros(n, dtype=torch.uint8, device=env.device))
+    max_steps = 4
+    n_cut = 0
+    for t in range(9):
+        a = envs[0].gen_actions(t)
+        rbs[0].begin(a)
+        rbs[0].step_end(a, cuts[0], max_steps)
+        rbs[1].begin(a)
+        envs[1].step(a)
+        rbs[1].end(cuts[1], max_steps, reset=True)
+        torch.cuda.synchronize()
+        assert torch.equal(cuts[0], cuts[1]), t
+        n_cut += int(cuts[0].sum())
+        for f in ("x", "y", "fuel", "cargo", "origin", "dest", "ep_len", "ep_return", "done", "err", "reward"):
+            assert torch.equal(getattr(envs[0], f), getattr(envs[1], f)), (t, f)
+    assert n_cut > 0
+    assert torch.equal(envs[0].episode_stats(), envs[1].episode_stats())
+    assert rbs[0].size == rbs[1].size == min(9 * n, cap)
+    B = rbs[0].size
+    for t in (0, 5):
+        outs = [MiniBatch(B, envs[0].obs_size, envs[0].device) for _ in range(2)]
+        for rb, out in zip(rbs, outs):
+            rb.sample(out, t=t)
+        torch.cuda.synchronize()
+        for name in ("obs", "next_obs", "act", "rew", "done", "weight"):
+            assert torch.equal(getattr(outs[0], name), getattr(outs[1], name)), (t, name)
+
+
+def test_step_record_refuses_without_begin():
+    from shippingenv_amd import _native as N
+    from shippingenv_amd.dqn import ReplayBuffer
+
+    env = make_env(64, seed=1)
+    rb = ReplayBuffer(env, 256)
+    _OPEN.append(rb)
+    cut = torch.zeros(64, dtype=torch.uint8, device=env.device)
+    with pytest.raises(N.ShipEnvError, match="se_replay_begin"):
+        rb.step_end(env.gen_actions(0), cut, 4)
+
+
 def test_update_with_policy_refuses_a_foreign_qnet():
     """se_qtrain_step_policy writes the policy's images from the parameters it updates, so it
     refuses a qnet packed from other tensors (another model, or a copy)."""

@@ -3,8 +3,9 @@
     python tools/time_train.py [--n N] [--batch B] [--iters K] [--eager]
 
 Prints one JSON line: HIP-event ms per iteration of each part on the launch stream
-(the fused launches VecDQNAgent.step makes, or with --separate the policy, replay begin,
-step, replay end and reset of cut envs), the update, and the whole loop.
+(the fused launches VecDQNAgent.step makes: policy + begin, step + end + reset; with --pair the
+step and the end + reset as two launches; with --separate the policy, replay begin, step, replay
+end and reset of cut envs), the update, and the whole loop.
 """
 import argparse
 import json
@@ -27,6 +28,8 @@ def main():
     p.add_argument("--separate", action="store_true",
                    help="time the separate launches (policy, begin, step, end, reset) instead of the "
                         "fused ones VecDQNAgent.step uses (policy + begin, step, end + reset)")
+    p.add_argument("--pair", action="store_true",
+                   help="the step and the replay end + reset as two launches (se_step, se_replay_end_reset)")
     a = p.parse_args()
     if a.lib:
         from shippingenv_amd import _native
@@ -44,7 +47,7 @@ def main():
     torch.cuda.synchronize()
     s = torch.cuda.current_stream()
     parts = ("policy", "begin", "step", "end", "reset", "update") if a.separate else \
-        ("policy_record", "step", "end_reset", "update")
+        ("policy_record", "step", "end_reset", "update") if a.pair else ("policy_record", "step_record", "update")
     ev = {k: [] for k in parts}
 
     def mark(name, fn):
@@ -64,15 +67,19 @@ def main():
             mark("step", lambda: env.step(act))
             mark("end", lambda: agent.memory.end(agent.cut, agent.max_steps))
             mark("reset", lambda: env.reset(agent.cut))
-        else:
+        elif a.pair:
             act = mark("policy_record", lambda: agent.policy.act_record(agent.memory, agent.epsilon, agent.t))
             mark("step", lambda: env.step(act))
             mark("end_reset", lambda: agent.memory.end(agent.cut, agent.max_steps, reset=True))
+        else:
+            act = mark("policy_record", lambda: agent.policy.act_record(agent.memory, agent.epsilon, agent.t))
+            mark("step_record", lambda: agent.memory.step_end(act, agent.cut, agent.max_steps))
         mark("update", agent.update)
         agent.t += 1
     g1.record(s)
     torch.cuda.synchronize()
-    out = {"lib": os.path.basename(a.lib or "default"), "n": a.n, "batch": a.batch, "graph": not a.eager,
+    mode = "separate" if a.separate else "pair" if a.pair else "fused"
+    out = {"lib": os.path.basename(a.lib or "default"), "mode": mode, "n": a.n, "batch": a.batch, "graph": not a.eager,
            "loop_ms": round(g0.elapsed_time(g1) / a.iters, 4)}
     for k in parts:
         out[k + "_ms"] = round(sum(x.elapsed_time(y) for x, y in ev[k]) / a.iters, 4)
