@@ -302,6 +302,20 @@ int se_qtrain_step_policy(se_qtrain* q, se_qnet* qn, int64_t batch, const float*
                           const float* next_obs, const int64_t* act, const float* rew,
                           const float* done, const float* weight, float gamma, float lr, float beta1,
                           float beta2, float eps, int32_t* step_dev, float* loss_out, void* stream);
+/* Data-parallel update (one learner per GPU, the same parameters on every rank): se_qtrain_step
+ * split at the exchange. se_qtrain_grad writes this rank's gradient sums (before the division
+ * by sum w) and {sum w (q - y)^2, sum w} into grad, a device f32 vector of
+ * se_qtrain_grad_size(q) floats, and changes no parameter. After an all-reduce(SUM) of grad
+ * over the ranks, se_qtrain_apply takes one Adam step from it: the update on the union of
+ * the ranks' minibatches (loss = global sum w d^2 / global sum w). Same bias-correction
+ * counter as se_qtrain_step (step_dev + 1; the caller increments it). qn (nullable): also
+ * write that policy's bf16 images, as se_qtrain_step_policy does. Both capturable. */
+int64_t se_qtrain_grad_size(const se_qtrain* q);
+int se_qtrain_grad(se_qtrain* q, int64_t batch, const float* obs, const float* next_obs, const int64_t* act,
+                   const float* rew, const float* done, const float* weight, float gamma, float* grad,
+                   void* stream);
+int se_qtrain_apply(se_qtrain* q, se_qnet* qn, const float* grad, float lr, float beta1, float beta2,
+                    float eps, const int32_t* step_dev, float* loss_out, void* stream);
 int se_qtrain_destroy(se_qtrain* q);  /* destroy before the env it was created on */
 
 /* Episode statistics accumulated by the auto-reset path since the last clear:

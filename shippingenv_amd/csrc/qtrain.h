@@ -511,6 +511,23 @@ struct QtAdamArgs {
     uint8_t* img[2];
     QnetDims q[2];
     int32_t bumped;  // T1 advanced step_dev already
+    // data-parallel split (se_qtrain_grad / se_qtrain_apply): mode 0 sums the tile partials
+    // and steps Adam; mode 1 stores the sums (unscaled) in grad and stops; mode 2 steps Adam
+    // from grad (summed over the ranks in between) instead of the partials
+    int32_t mode;
+    float* grad;  // [grad_floats(d)], layout of the Grad offsets below
+};
+
+// The data-parallel gradient: the sums T2 forms before dividing by sum(w), in a flat f32
+// vector that an all-reduce(SUM) over the ranks turns into the global minibatch's sums.
+// dW1's port columns are db1 (x) port (the port block is the same on every rank), so only
+// the six dynamic columns travel. [128][6] dW1 dynamic, [128] db1, [128][128] dW2, [128] db2,
+// [mt3 * 32][128] dW3, [mt3 * 32] db3, then {sum w d^2, sum w}.
+struct Grad {
+    static constexpr int64_t w1d = 0, b1 = 768, w2 = 896, b2 = 896 + 128 * 128, w3 = b2 + 128;
+    __host__ __device__ static int64_t b3(const QtDims& d) { return w3 + (int64_t)d.mt3 * 32 * 128; }
+    __host__ __device__ static int64_t lw(const QtDims& d) { return b3(d) + (int64_t)d.mt3 * 32; }
+    __host__ __device__ static int64_t size(const QtDims& d) { return lw(d) + 2; }
 };
 
 // byte offset of W[row][k] within a packed policy image's fc2 / fc3 fragments: fragment
@@ -536,7 +553,8 @@ __device__ __forceinline__ int row_of_action(const QnetDims& q, int a) {
 struct AdamStep {
     float b1, b2, eps, step_size, bc2_sqrt;
     __device__ AdamStep(const QtAdamArgs& A) : b1(A.beta1), b2(A.beta2), eps(A.eps) {
-        const float t = (float)(*A.step_dev + (A.bumped ? 0 : 1));
+        // (no counter in mode 1, which stops before any Adam step)
+        const float t = A.step_dev ? (float)(*A.step_dev + (A.bumped ? 0 : 1)) : 1.0f;
         step_size = 1.0f / ((powf(A.beta1, t) - 1.0f) / A.lr);
         bc2_sqrt = sqrtf(-(powf(A.beta2, t) - 1.0f));
     }
@@ -641,21 +659,50 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
     const AdamStep adam(A);
     // sum(w): this thread's share loads now, and the workgroup reduces it after its own
     // sum (inv is first needed by the Adam step), so the two round trips overlap
+    const int mode = A.mode;  // block-uniform
+    float* G = A.grad;
     float wsum = 0.0f;
-    for (int64_t t = tid; t < A.tiles; t += kQRBlock) wsum += A.W.part_lw[2 * t + 1];
-    auto weight_inv = [&]() { return 1.0f / fmaxf(block_sum256(wsum, red), 1.0f); };
+    if (mode == 0 || (mode == 1 && blockIdx.x == 0))
+        for (int64_t t = tid; t < A.tiles; t += kQRBlock) wsum += A.W.part_lw[2 * t + 1];
+    auto weight_inv = [&]() {
+        return 1.0f / fmaxf(mode == 2 ? G[Grad::lw(A.d) + 1] : block_sum256(wsum, red), 1.0f);
+    };
     QSTAMP(11);
     const int b = blockIdx.x;
     if (b < 128) {  // W1 row f: 6 dynamic columns + db1 reduced over the tiles, the port columns
         const int f = b;
         float x[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        for (int64_t t = tid; t < A.tiles; t += kQRBlock) {
-            const float* p = A.W.part_w1d + (t * 128 + f) * 6;
+        if (mode == 2) {
 #pragma unroll
-            for (int c = 0; c < 6; ++c) x[c] += p[c];
-            x[6] += A.W.part_b1[t * 128 + f];
+            for (int c = 0; c < 6; ++c) x[c] = G[Grad::w1d + f * 6 + c];
+            x[6] = G[Grad::b1 + f];
+        } else {
+            for (int64_t t = tid; t < A.tiles; t += kQRBlock) {
+                const float* p = A.W.part_w1d + (t * 128 + f) * 6;
+#pragma unroll
+                for (int c = 0; c < 6; ++c) x[c] += p[c];
+                x[6] += A.W.part_b1[t * 128 + f];
+            }
+            block_sum<7>(x, red);
+            if (mode == 1) {
+                if (tid == 0) {
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) G[Grad::w1d + f * 6 + c] = x[c];
+                    G[Grad::b1 + f] = x[6];
+                }
+                if (f == 0) {  // the loss and weight sums
+                    float l = 0.0f;
+                    for (int64_t t = tid; t < A.tiles; t += kQRBlock) l += A.W.part_lw[2 * t];
+                    const float ls = block_sum256(l, red);
+                    const float ws = block_sum256(wsum, red);
+                    if (tid == 0) {
+                        G[Grad::lw(A.d)] = ls;
+                        G[Grad::lw(A.d) + 1] = ws;
+                    }
+                }
+                return;
+            }
         }
-        block_sum<7>(x, red);
         const float inv = weight_inv();
         QSTAMP(12);
         if (tid == 0)  // every thread holds the sums; the row loop below indexes them by column
@@ -697,14 +744,35 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             for (int l = 0; l < 2; ++l) reinterpret_cast<float*>(A.img[l] + A.q[l].b1())[f] = (float)acc;
         }
         if (f == 0) {  // the loss: sum w d^2 / sum w
-            float l = 0.0f;
-            for (int64_t t = tid; t < A.tiles; t += kQRBlock) l += A.W.part_lw[2 * t];
-            const float loss = block_sum256(l, red);
+            float loss;
+            if (mode == 2) {
+                loss = G[Grad::lw(A.d)];
+            } else {
+                float l = 0.0f;
+                for (int64_t t = tid; t < A.tiles; t += kQRBlock) l += A.W.part_lw[2 * t];
+                loss = block_sum256(l, red);
+            }
             if (tid == 0) *A.loss_out = loss * inv;
         }
     } else if (b < 384) {  // W2 elements e0 .. e0 + 63 (row-major [f2][f1])
         const int64_t e0 = (int64_t)(b - 128) * 64;
-        const float g = tile_sum64<16>(A.W.part_w2, 128 * 128, e0, A.tiles, nullptr, 0, red4);
+        float g;
+        if (mode == 2) {
+            g = tid < 64 ? G[Grad::w2 + e0 + tid] : 0.0f;
+        } else {
+            g = tile_sum64<16>(A.W.part_w2, 128 * 128, e0, A.tiles, nullptr, 0, red4);
+            if (mode == 1) {
+                if (tid < 64) G[Grad::w2 + e0 + tid] = g;
+                if ((e0 & 127) == 0) {
+                    const int f2 = (int)(e0 >> 7);
+                    float x = 0.0f;
+                    for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[t * 128 + f2];
+                    const float s2 = block_sum256(x, red);
+                    if (tid == 0) G[Grad::b2 + f2] = s2;
+                }
+                return;
+            }
+        }
         const float inv = weight_inv();
         QSTAMP(12);
         if (tid < 64) {
@@ -719,9 +787,14 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         }
         if ((e0 & 127) == 0) {
             const int f2 = (int)(e0 >> 7);
-            float x = 0.0f;
-            for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[t * 128 + f2];
-            const float s2 = block_sum256(x, red);
+            float s2;
+            if (mode == 2) {
+                s2 = G[Grad::b2 + f2];
+            } else {
+                float x = 0.0f;
+                for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[t * 128 + f2];
+                s2 = block_sum256(x, red);
+            }
             if (tid == 0) {
                 const float p = adam(A.on.b2[f2], s2 * inv, A.m.b2[f2], A.v.b2[f2]);
                 A.on.b2[f2] = p;
@@ -734,8 +807,17 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         const int k = b - 384, rt = k >> 6;
         const int64_t e0 = (int64_t)(k & 63) * 64;
         const uint32_t bit = 1u << rt;
-        const float g = tile_sum64<16>(A.W.part_w3 + (int64_t)rt * 32 * 128, (int64_t)A.d.mt3 * 32 * 128, e0,
-                                   A.tiles, A.W.present, bit, red4);
+        float g;
+        if (mode == 2) {
+            g = tid < 64 ? G[Grad::w3 + (int64_t)rt * 32 * 128 + e0 + tid] : 0.0f;
+        } else {
+            g = tile_sum64<16>(A.W.part_w3 + (int64_t)rt * 32 * 128, (int64_t)A.d.mt3 * 32 * 128, e0, A.tiles,
+                               A.W.present, bit, red4);
+            if (mode == 1) {
+                if (tid < 64) G[Grad::w3 + (int64_t)rt * 32 * 128 + e0 + tid] = g;
+                return;
+            }
+        }
         const float inv = weight_inv();
         QSTAMP(12);
         if (tid < 64) {
@@ -758,7 +840,10 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         // an absent action tile, so no presence test: a conditional load per tile kept these
         // blocks busy 3x as long as the rest of the kernel)
         const int rt = b - 384 - 64 * A.d.mt3;
-        {
+        float s3;
+        if (mode == 2) {
+            s3 = G[Grad::b3(A.d) + rt * 32 + (tid & 31)];
+        } else {
             const int r = tid & 31, grp = tid >> 5;
             float x = 0.0f;
             constexpr int kU = 32;  // 256 tiles (B = 8192) in one round
@@ -779,10 +864,16 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                 if (grp < s) red[tid] += red[tid + 32 * s];
                 __syncthreads();
             }
-            const float s3 = red[tid & 31];
+            s3 = red[tid & 31];
             __syncthreads();  // weight_inv reuses red
+            if (mode == 1) {
+                if (tid < 32) G[Grad::b3(A.d) + rt * 32 + tid] = s3;
+                return;
+            }
+        }
+        {
             const float inv = weight_inv();
-            const int a = rt * 32 + r;
+            const int a = rt * 32 + (tid & 31);
             if (tid < 32 && a < A.d.A) {
                 const float p = adam(A.on.b3[a], s3 * inv, A.m.b3[a], A.v.b3[a]);
                 A.on.b3[a] = p;
@@ -899,40 +990,60 @@ int se_qtrain_pack(se_qtrain* q, int32_t which, void* stream) {
 }  // extern "C"
 
 namespace {
-int qtrain_step(se_qtrain* q, se_qnet* qn, int64_t batch, const float* obs, const float* next_obs,
-                const int64_t* act, const float* rew, const float* done, const float* weight, float gamma,
-                float lr, float beta1, float beta2, float eps, int32_t* step_dev, float* loss_out,
-                void* stream) {
+int qtrain_check_bound(se_qtrain* q) {
     if (!q) return fail(SE_EINVAL, "null qtrain");
     if (!q->bound) return fail(SE_ESTATE, "se_qtrain_bind has not been called");
     if (q->world_version != q->env->world_version)
         return fail(SE_ESTATE, "ports changed since se_qtrain_bind (the port block is folded into fc1)");
+    return SE_OK;
+}
+
+// the policy must be packed from the very tensors the update changes (null: no policy)
+int qtrain_check_qnet(se_qtrain* q, se_qnet* qn) {
+    if (!qn) return SE_OK;
+    if (!qn->packed) return fail(SE_ESTATE, "se_qnet_set_weights has not been called");
+    if (qn->env != q->env) return fail(SE_EINVAL, "qnet and qtrain belong to different envs");
+    if (qn->world_version != q->env->world_version)
+        return fail(SE_ESTATE, "ports changed: call se_qnet_set_weights (the port block is folded into fc1)");
+    const float* on[6] = {q->on.w1, q->on.b1, q->on.w2, q->on.b2, q->on.w3, q->on.b3};
+    for (int k = 0; k < 6; ++k)
+        if (qn->w[k] != on[k]) return fail(SE_EINVAL, "the qnet is not packed from the online parameters");
+    return SE_OK;
+}
+
+QtAdamArgs adam_args(se_qtrain* q, se_qnet* qn, int64_t batch, const int64_t* act, float lr, float beta1,
+                     float beta2, float eps, const int32_t* step_dev, float* loss_out, int32_t bumped,
+                     int32_t mode, float* grad) {
+    const int64_t tiles = (batch + kQT - 1) / kQT;
+    return QtAdamArgs{q->W, q->on, q->m, q->v, q->d, batch, tiles, act, lr, beta1, beta2, eps, step_dev, loss_out,
+                      {qn ? qn->d_img : nullptr, qn ? qn->d_img + qn->c_off : nullptr},
+                      {qn ? qn->q : QnetDims{}, qn ? qn->qc : QnetDims{}}, bumped, mode, grad};
+}
+
+// T1, then T2 in mode 0 (grad null: sums + Adam) or mode 1 (the sums into grad)
+int qtrain_step(se_qtrain* q, se_qnet* qn, int64_t batch, const float* obs, const float* next_obs,
+                const int64_t* act, const float* rew, const float* done, const float* weight, float gamma,
+                float lr, float beta1, float beta2, float eps, int32_t* step_dev, float* loss_out,
+                void* stream, float* grad = nullptr) {
+    if (int rc0 = qtrain_check_bound(q)) return rc0;
     if (batch < 1 || batch > q->max_batch) return fail(SE_EINVAL, "batch must be in [1, max_batch]");
-    if (!obs || !next_obs || !act || !rew || !done || !weight || !step_dev || !loss_out)
+    if (!obs || !next_obs || !act || !rew || !done || !weight || (!grad && (!step_dev || !loss_out)))
         return fail(SE_EINVAL, "null batch / counter / loss pointer");
-    if (qn) {  // the policy must be packed from the very tensors this update changes
-        if (!qn->packed) return fail(SE_ESTATE, "se_qnet_set_weights has not been called");
-        if (qn->env != q->env) return fail(SE_EINVAL, "qnet and qtrain belong to different envs");
-        if (qn->world_version != q->env->world_version)
-            return fail(SE_ESTATE, "ports changed: call se_qnet_set_weights (the port block is folded into fc1)");
-        const float* on[6] = {q->on.w1, q->on.b1, q->on.w2, q->on.b2, q->on.w3, q->on.b3};
-        for (int k = 0; k < 6; ++k)
-            if (qn->w[k] != on[k]) return fail(SE_EINVAL, "the qnet is not packed from the online parameters");
-    }
+    int rc = qtrain_check_qnet(q, qn);
+    if (rc) return rc;
     DeviceGuard g(q->device);
     const hipStream_t s = (hipStream_t)stream;
     const int64_t tiles = (batch + kQT - 1) / kQT;
     const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 5 * 32) * 4;
     static std::atomic<uint64_t> lds_set{0};
-    const int rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(qtrain_tile_kernel), (int)lds, q->device);
+    rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(qtrain_tile_kernel), (int)lds, q->device);
     if (rc) return rc;
     QtStepArgs A{q->W, q->on, q->tg, q->d, batch, obs, next_obs, act, rew, done, weight, gamma,
                  qn ? step_dev : nullptr};
     qtrain_tile_kernel<<<(unsigned)tiles, kQTBlock, lds, s>>>(A);
     HIP_TRY(hipGetLastError());
-    QtAdamArgs B{q->W, q->on, q->m, q->v, q->d, batch, tiles, act, lr, beta1, beta2, eps, step_dev, loss_out,
-                 {qn ? qn->d_img : nullptr, qn ? qn->d_img + qn->c_off : nullptr},
-                 {qn ? qn->q : QnetDims{}, qn ? qn->qc : QnetDims{}}, qn ? 1 : 0};
+    const QtAdamArgs B = adam_args(q, qn, batch, act, lr, beta1, beta2, eps, step_dev, loss_out, qn ? 1 : 0,
+                                   grad ? 1 : 0, grad);
     qtrain_adam_kernel<<<384 + 65 * q->d.mt3, kQRBlock, 0, s>>>(B);
     HIP_TRY(hipGetLastError());
     return SE_OK;
@@ -955,6 +1066,29 @@ int se_qtrain_step_policy(se_qtrain* q, se_qnet* qn, int64_t batch, const float*
     if (!qn) return fail(SE_EINVAL, "null qnet");
     return qtrain_step(q, qn, batch, obs, next_obs, act, rew, done, weight, gamma, lr, beta1, beta2, eps,
                        step_dev, loss_out, stream);
+}
+
+int64_t se_qtrain_grad_size(const se_qtrain* q) { return q ? Grad::size(q->d) : 0; }
+
+int se_qtrain_grad(se_qtrain* q, int64_t batch, const float* obs, const float* next_obs, const int64_t* act,
+                   const float* rew, const float* done, const float* weight, float gamma, float* grad,
+                   void* stream) {
+    if (!grad) return fail(SE_EINVAL, "null grad");
+    return qtrain_step(q, nullptr, batch, obs, next_obs, act, rew, done, weight, gamma, 0.0f, 0.0f, 0.0f, 0.0f,
+                       nullptr, nullptr, stream, grad);
+}
+
+int se_qtrain_apply(se_qtrain* q, se_qnet* qn, const float* grad, float lr, float beta1, float beta2, float eps,
+                    const int32_t* step_dev, float* loss_out, void* stream) {
+    if (int rc = qtrain_check_bound(q)) return rc;
+    if (!grad || !step_dev || !loss_out) return fail(SE_EINVAL, "null grad / counter / loss pointer");
+    if (int rc = qtrain_check_qnet(q, qn)) return rc;
+    DeviceGuard g(q->device);
+    const QtAdamArgs B = adam_args(q, qn, 0, nullptr, lr, beta1, beta2, eps, step_dev, loss_out, 0, 2,
+                                   const_cast<float*>(grad));
+    qtrain_adam_kernel<<<384 + 65 * q->d.mt3, kQRBlock, 0, (hipStream_t)stream>>>(B);
+    HIP_TRY(hipGetLastError());
+    return SE_OK;
 }
 
 int se_qtrain_destroy(se_qtrain* q) {

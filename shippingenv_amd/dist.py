@@ -8,6 +8,8 @@ shard's trajectories are identical to the same ids in a single-GPU run
 (tests/test_gpu_parity.py::test_shard_invariance). The one collective is a
 SUM all-reduce of three doubles {sum of returns, episodes, sum of lengths}
 (backend "nccl", which is RCCL on ROCm): latency-bound, off the step path.
+Data-parallel DQN training (shippingenv_amd.dqn.VecDQNAgent with several ranks) adds the
+one exchange its update has: a SUM all-reduce of the gradient vector per update.
 """
 from __future__ import annotations
 
@@ -63,6 +65,21 @@ def reduce_episode_stats(stats, group=None):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.SUM, group=group)
     return stats
+
+
+def allreduce_gradient(grad, group=None):
+    """SUM-all-reduce a data-parallel DQN gradient vector in place (se_qtrain_grad's sums
+    and {sum w d^2, sum w}; shippingenv_amd.dqn.grad_layout). Summing, not averaging: the
+    update divides by the global weight sum, so ranks may hold different numbers of valid
+    transitions. One 200-odd-KB message per update: on xGMI that is latency, not link
+    bandwidth."""
+    import torch.distributed as dist
+
+    if grad.dtype != torch.float32 or grad.dim() != 1:
+        raise ValueError("the gradient vector is a 1-D float32 tensor")
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
+    return grad
 
 
 def summarize(stats):

@@ -185,6 +185,28 @@ class FusedUpdate:
                                               float(gamma), self.lr, self.betas[0], self.betas[1], self.eps,
                                               _ptr(step_dev), _ptr(loss_out), self.env._stream()))
 
+    # ---- data parallel (one learner per GPU): the update split at the gradient exchange
+    def grad_size(self) -> int:
+        """Floats in the gradient vector of grad() / apply() (layout: grad_layout)."""
+        return int(N.lib().se_qtrain_grad_size(self._h))
+
+    def grad(self, b: MiniBatch, gamma: float, out: torch.Tensor):
+        """This rank's gradient sums and {sum w d^2, sum w} into `out` (se_qtrain_grad);
+        no parameter changes."""
+        if out.dtype != torch.float32 or not out.is_contiguous() or out.numel() < self.grad_size():
+            raise ValueError("out must be a contiguous float32 device tensor of grad_size() floats")
+        N.check(N.lib().se_qtrain_grad(self._h, b.batch, _ptr(b.obs), _ptr(b.next_obs), _ptr(b.act),
+                                       _ptr(b.rew), _ptr(b.done), _ptr(b.weight), float(gamma), _ptr(out),
+                                       self.env._stream()))
+
+    def apply(self, grad: torch.Tensor, step_dev: torch.Tensor, loss_out: torch.Tensor, policy=None):
+        """One Adam step from `grad` summed over the ranks (se_qtrain_apply); with `policy`,
+        its bf16 images are rewritten too. step_dev: Adam steps taken before this one (the
+        caller advances it)."""
+        N.check(N.lib().se_qtrain_apply(self._h, None if policy is None else policy._h, _ptr(grad),
+                                        self.lr, self.betas[0], self.betas[1], self.eps, _ptr(step_dev),
+                                        _ptr(loss_out), self.env._stream()))
+
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
             torch.cuda.synchronize(self.env.device)
@@ -196,6 +218,20 @@ class FusedUpdate:
             self.close()
         except Exception:  # noqa: BLE001 - interpreter shutdown
             pass
+
+
+def grad_layout(action_size: int, in_size: int) -> dict:
+    """Offsets (floats) of the data-parallel gradient vector (csrc/qtrain.h Grad): the
+    six dynamic columns of dW1 ([128][6]; the port columns are db1 x port on every rank),
+    db1, dW2, db2, dW3 and db3 (rows padded to a multiple of 32), then {sum w d^2, sum w}."""
+    rows3 = (action_size + 31) // 32 * 32
+    lay = {"w1d": 0, "b1": 768, "w2": 896, "b2": 896 + 128 * 128}
+    lay["w3"] = lay["b2"] + 128
+    lay["b3"] = lay["w3"] + rows3 * 128
+    lay["lw"] = lay["b3"] + rows3
+    lay["size"] = lay["lw"] + 2
+    lay["rows3"] = rows3
+    return lay
 
 
 def dqn_loss(model, target_model, b: MiniBatch, gamma: float) -> torch.Tensor:
@@ -219,7 +255,8 @@ class VecDQNAgent:
                  batch_size: int = DQN_BATCH_SIZE, target_update_every: int = 1000,
                  hidden_size: int = HIDDEN, max_steps: int = MAX_STEPS_PER_EPISODE,
                  updates_per_step: int = 1, graph: bool = True, graph_warmup: int = 3,
-                 fused: bool = True, model: DQNNetwork | None = None):
+                 fused: bool = True, model: DQNNetwork | None = None,
+                 data_parallel: bool | None = None, process_group=None):
         if not env.auto_reset:
             raise ValueError("VecDQNAgent needs an auto-reset VecEnv (finished episodes restart in se_step)")
         self.env = env
@@ -254,6 +291,21 @@ class VecDQNAgent:
         self.use_graph, self.graph_warmup = bool(graph), int(graph_warmup)
         self._graph = None
         self._loss = torch.zeros((), dtype=torch.float32, device=dev)
+        # data parallel: every rank steps its own envs into its own ring; the update sums the
+        # ranks' gradients (all-reduce, RCCL) and takes the same Adam step everywhere
+        self.group = process_group
+        if data_parallel is None:
+            import torch.distributed as dist
+
+            data_parallel = dist.is_available() and dist.is_initialized() and dist.get_world_size(process_group) > 1
+        self.data_parallel = bool(data_parallel)
+        self._grad = None
+        self._graphs = None
+        if self.data_parallel:
+            if not self.fused:
+                raise ValueError("data_parallel needs the fused update (fused=True)")
+            self._grad = torch.zeros(self.trainer.grad_size(), dtype=torch.float32, device=dev)
+            self._broadcast_params()
 
     def update_target_model(self):
         """agents/dqn.py:109-111 (an in-place copy: the graph keeps the same tensors)."""
@@ -263,7 +315,32 @@ class VecDQNAgent:
         if self.trainer is not None:
             self.trainer.pack(1)
 
+    def _broadcast_params(self):
+        """Rank 0's initial weights on every rank (DDP's start), then the kernel images."""
+        import torch.distributed as dist
+
+        src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
+        with torch.no_grad():
+            for p in self.model.parameters():
+                dist.broadcast(p.data, src, group=self.group)
+        self.update_target_model()
+        self.trainer.pack(0)
+        self.policy.repack()
+
     # ------------------------------------------------------------------ update
+    def _grad_body(self):  # data parallel, before the exchange
+        self.memory.sample(self.batch, t_dev=self._ctr)
+        self.trainer.grad(self.batch, self.gamma, self._grad)
+
+    def _apply_body(self):  # data parallel, after the exchange
+        self.trainer.apply(self._grad, self._ctr, self._loss, self.policy)
+        self._ctr.add_(1)
+
+    def _exchange(self):
+        from .dist import allreduce_gradient
+
+        allreduce_gradient(self._grad, self.group)
+
     def _update_body(self):
         self.memory.sample(self.batch, t_dev=self._ctr)
         if self.fused:  # _ctr = Adam steps taken so far
@@ -278,17 +355,24 @@ class VecDQNAgent:
         # the next choose_action sees the new weights; the update counter advances in the same launch
         self.policy.repack(bump=self._ctr)
 
-    def _capture(self):
-        for p in self.model.parameters():  # static gradient buffers for the graph (torch path)
-            if p.grad is None and not self.fused:
-                p.grad = torch.zeros_like(p)
+    def _capture_one(self, body):
         g = torch.cuda.CUDAGraph()
         side = torch.cuda.Stream(self.env.device)
         side.wait_stream(torch.cuda.current_stream(self.env.device))
         with torch.cuda.stream(side), torch.cuda.graph(g, stream=side):
-            self._update_body()
+            body()
         torch.cuda.current_stream(self.env.device).wait_stream(side)
-        self._graph = g
+        return g
+
+    def _capture(self):
+        for p in self.model.parameters():  # static gradient buffers for the graph (torch path)
+            if p.grad is None and not self.fused:
+                p.grad = torch.zeros_like(p)
+        if self.data_parallel:  # two graphs; the all-reduce runs eagerly between them
+            self._graphs = (self._capture_one(self._grad_body), self._capture_one(self._apply_body))
+            self._graph = self._graphs
+        else:
+            self._graph = self._capture_one(self._update_body)
 
     def update(self):
         """agents/dqn.py:206-245. Returns the loss as a device scalar (no host sync), or
@@ -297,7 +381,16 @@ class VecDQNAgent:
             return None
         if self.use_graph and self._graph is None and self.updates >= self.graph_warmup:
             self._capture()  # capturing records the update; it runs on replay below
-        if self._graph is not None:
+        if self.data_parallel:
+            if self._graphs is not None:
+                self._graphs[0].replay()
+                self._exchange()
+                self._graphs[1].replay()
+            else:
+                self._grad_body()
+                self._exchange()
+                self._apply_body()
+        elif self._graph is not None:
             self._graph.replay()
         else:
             self._update_body()
@@ -340,4 +433,4 @@ class VecDQNAgent:
                 obj.close()
 
 
-__all__ = ["DQNNetwork", "FusedUpdate", "MiniBatch", "ReplayBuffer", "VecDQNAgent", "dqn_loss"]
+__all__ = ["DQNNetwork", "FusedUpdate", "MiniBatch", "ReplayBuffer", "VecDQNAgent", "dqn_loss", "grad_layout"]

@@ -505,3 +505,206 @@ def test_out_of_range_action_is_weight_zero():
         assert torch.equal(a, b)
     for a, b in zip(agents[0].trainer.exp_avg_sq, agents[1].trainer.exp_avg_sq):
         assert torch.equal(a, b)
+
+
+# ---------------------------------------------------------------- data parallel (§8e x §8f row 3)
+def _one_rank_dp():
+    """VecDQNAgent's data-parallel path with a world of one: the exchange is the identity."""
+    from shippingenv_amd.dqn import VecDQNAgent
+
+    class OneRank(VecDQNAgent):
+        def _broadcast_params(self):
+            self.exchanges = 0
+
+        def _exchange(self):
+            self.exchanges += 1
+
+    return OneRank
+
+
+def test_grad_then_apply_is_the_fused_step_bit_for_bit():
+    """se_qtrain_grad + se_qtrain_apply (the update split at the all-reduce) against
+    se_qtrain_step_policy, one rank: the same sums reach the same Adam step, so losses,
+    weights, Adam moments, the update counter and both policy images agree bit for bit,
+    eager and from the two captured graphs."""
+    from shippingenv_amd.dqn import VecDQNAgent
+
+    agents, envs = [], []
+    for cls in (VecDQNAgent, _one_rank_dp()):
+        env = make_env(4096, seed=13)
+        torch.manual_seed(2)
+        kw = dict(data_parallel=True) if cls is not VecDQNAgent else {}
+        agent = cls(env, graph=True, graph_warmup=3, batch_size=512, epsilon=0.4, target_update_every=4,
+                    max_steps=9, **kw)
+        _OPEN.append(agent)
+        agents.append(agent)
+        envs.append(env)
+    assert agents[1].data_parallel and not agents[0].data_parallel
+    for k in range(10):
+        la, lb = (a.step() for a in agents)
+        assert (la is None) == (lb is None), k
+        if la is not None:
+            assert la.item() == lb.item(), k
+        assert torch.equal(agents[0].policy.actions, agents[1].policy.actions), k
+        assert int(agents[0]._ctr.item()) == int(agents[1]._ctr.item()), k
+    assert agents[1]._graphs is not None and agents[1].exchanges == 10
+    for p, q in zip(agents[0].model.parameters(), agents[1].model.parameters()):
+        assert torch.equal(p, q)
+    for a, b in zip(agents[0].trainer.exp_avg + agents[0].trainer.exp_avg_sq,
+                    agents[1].trainer.exp_avg + agents[1].trainer.exp_avg_sq):
+        assert torch.equal(a, b)
+    qs = []
+    for a in agents:
+        q = torch.full((a.env.n, a.env.action_space_size), float("nan"), device=a.env.device)
+        a.policy.act(0.0, 0, q_out=q)
+        qs.append(q)
+    assert torch.equal(qs[0], qs[1])
+
+
+class _Batch:
+    def __init__(self, parts):
+        for f in ("obs", "next_obs", "act", "rew", "done", "weight"):
+            setattr(self, f, torch.cat([getattr(p, f) for p in parts]))
+        self.batch = sum(p.batch for p in parts)
+
+
+def _grad_sums64(model, target, b, gamma, lay):
+    """float64 autograd of sum w (q - y)^2 (undivided) in se_qtrain_grad's layout."""
+    import copy
+
+    m = copy.deepcopy(model).double()
+    tg = copy.deepcopy(target).double()
+    q = m(b.obs.double()).gather(1, b.act.unsqueeze(1)).squeeze(1)
+    with torch.no_grad():
+        y = b.rew.double() + gamma * tg(b.next_obs.double()).max(1)[0] * (1 - b.done.double())
+    w = b.weight.double()
+    ls = (w * (q - y) ** 2).sum()
+    ls.backward()
+    v = torch.zeros(lay["size"], dtype=torch.float64, device=b.obs.device)
+    A = m.fc3.out_features
+    v[lay["w1d"]:lay["w1d"] + 768] = m.fc1.weight.grad[:, :6].reshape(-1)
+    v[lay["b1"]:lay["b1"] + 128] = m.fc1.bias.grad
+    v[lay["w2"]:lay["w2"] + 128 * 128] = m.fc2.weight.grad.reshape(-1)
+    v[lay["b2"]:lay["b2"] + 128] = m.fc2.bias.grad
+    v[lay["w3"]:lay["w3"] + A * 128] = m.fc3.weight.grad.reshape(-1)
+    v[lay["b3"]:lay["b3"] + A] = m.fc3.bias.grad
+    v[lay["lw"]] = ls.detach()
+    v[lay["lw"] + 1] = w.sum()
+    return v
+
+
+def test_rank_gradients_sum_to_the_union_update():
+    """Two ranks' minibatches, exchanged as se_qtrain_grad vectors: each vector equals the
+    float64 autograd sums of its minibatch (5e-3 of the segment's rms), grad() changes no
+    parameter, and se_qtrain_apply on their sum is the reference update (nn.MSELoss + Adam,
+    _Ref64) on the union of the two minibatches."""
+    import copy
+
+    from shippingenv_amd.dqn import MiniBatch, VecDQNAgent, grad_layout
+
+    env = make_env(4096, seed=5)
+    agent = VecDQNAgent(env, graph=False, batch_size=256, epsilon=0.5, target_update_every=0)
+    _OPEN.append(agent)
+    for _ in range(3):
+        agent.step()
+    tr = agent.trainer
+    lay = grad_layout(env.action_space_size, env.obs_size)
+    assert tr.grad_size() == lay["size"]
+    parts, grads = [], []
+    for t in (77, 78):
+        b = agent.memory.sample(MiniBatch(256, env.obs_size, env.device), t=t)
+        g = torch.full((lay["size"],), float("nan"), dtype=torch.float32, device=env.device)
+        before = [p.clone() for p in agent.model.parameters()] + [m.clone() for m in tr.exp_avg]
+        tr.grad(b, agent.gamma, g)
+        torch.cuda.synchronize()
+        for x, y in zip(before, list(agent.model.parameters()) + tr.exp_avg):
+            assert torch.equal(x, y)
+        assert b.weight.min().item() == 1.0
+        want = _grad_sums64(agent.model, agent.target_model, b, agent.gamma, lay)
+        A = env.action_space_size
+        segs = [("w1d", 768), ("b1", 128), ("w2", 128 * 128), ("b2", 128), ("w3", A * 128), ("b3", A), ("lw", 2)]
+        for name, n in segs:
+            got, ref = g[lay[name]:lay[name] + n].double(), want[lay[name]:lay[name] + n]
+            tol = 5e-3 * ref.pow(2).mean().sqrt() + 1e-5 * ref.abs()
+            assert bool(((got - ref).abs() <= tol).all()), (name, float((got - ref).abs().max()))
+        parts.append(b)
+        grads.append(g)
+    k = int(agent._ctr.item())
+    before = copy.deepcopy(agent.model)
+    target = copy.deepcopy(agent.target_model)
+    m0 = [t.clone() for t in tr.exp_avg]
+    v0 = [t.clone() for t in tr.exp_avg_sq]
+    tr.apply(grads[0] + grads[1], agent._ctr, agent._loss, agent.policy)
+    torch.cuda.synchronize()
+    ref = _Ref64(before, target, _Batch(parts), agent.gamma, agent.learning_rate, k, m0, v0)
+    ref.check(agent._loss, list(agent.model.parameters()), tr.exp_avg, tr.exp_avg_sq, what="union")
+    # the policy's images now hold the new weights: the same Q as a fresh packing
+    from shippingenv_amd.policy import QPolicy
+
+    fresh = QPolicy(env, agent.model)
+    _OPEN.append(fresh)
+    qa, qb = (torch.empty((env.n, env.action_space_size), device=env.device) for _ in range(2))
+    agent.policy.act(0.0, 0, q_out=qa)
+    fresh.act(0.0, 0, q_out=qb)
+    assert torch.equal(qa, qb)
+
+
+def _dp_worker(rank, world, port, out):
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), SHIPENV_SHARE_GPUS="1")
+    import torch.distributed as dist
+
+    from shippingenv_amd import dist as D
+    from shippingenv_amd.dqn import DQNNetwork, VecDQNAgent
+    from shippingenv_amd.vec import VecEnv
+
+    r, w, _, dev = D.init_from_env(backend="gloo")
+    n = 2048
+    env = VecEnv(n, seed=9, env_id_base=r * n, device=dev, auto_reset=True)
+    env.reset()
+    torch.manual_seed(100 + r)  # different initial weights: the broadcast must align them
+    model = DQNNetwork(env.obs_size, env.action_space_size)
+    init = torch.cat([p.detach().flatten() for p in model.parameters()]).cpu()
+    agent = VecDQNAgent(env, graph=True, graph_warmup=2, batch_size=256, epsilon=0.5, target_update_every=3,
+                        max_steps=8, model=model)
+    assert agent.data_parallel
+    losses = []
+    for _ in range(7):
+        loss = agent.step()
+        losses.append(None if loss is None else loss.item())
+    flat = torch.cat([p.detach().flatten() for p in agent.model.parameters()]).cpu()
+    got = [None] * w
+    dist.all_gather_object(got, (flat, losses, init))
+    out[rank] = (got, agent._graphs is not None)
+    agent.close()
+    env.close()
+    dist.destroy_process_group()
+
+
+def test_data_parallel_ranks_stay_in_step():
+    """Two ranks (gloo here, sharing this box's GPU; RCCL on a node) train on their own
+    envs and rings: after rank 0's weights are broadcast, the summed gradients keep every
+    rank's weights and losses identical, bit for bit, through eager and graph updates."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    mp.start_processes(_dp_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    got, graphs = out[0]
+    (f0, l0, i0), (f1, l1, i1) = got
+    assert graphs
+    assert not torch.equal(i0, i1)        # the ranks started from different weights
+    assert torch.equal(f0, f1)            # and train as one model
+    assert not torch.equal(f0, i0)
+    assert l0 == l1 and all(v is not None for v in l0[1:])

@@ -11,7 +11,7 @@ from conftest import ROOT
 
 def header_symbols():
     text = open(os.path.join(ROOT, "include", "shipenv.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(se_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(se_\w+)\s*\(", text, re.M)))
 
 
 @pytest.fixture(scope="module")
