@@ -335,7 +335,10 @@ def run_dqn_train(n, args, dist):
     replay end and cut, reset of cut envs, then one update. The update is captured as
     one HIP graph: minibatch sample, DQNNetwork forward and backward at batch B, Adam,
     and the policy repack. Random-init weights; the reference's hyperparameters
-    (gamma 0.95, lr 1e-3, epsilon decay 0.995), with B = --train-batch."""
+    (gamma 0.95, lr 1e-3, epsilon decay 0.995), with B = --train-batch per GPU.
+    Several GPUs: data parallel, one learner per rank on its own envs and ring; each
+    update is graph 1 (sample + gradient sums), a SUM all-reduce of the gradient vector
+    (RCCL), graph 2 (Adam + policy images), so the global minibatch is B x ranks."""
     from shippingenv_amd.dqn import VecDQNAgent
     from shippingenv_amd.vec import VecEnv
 
@@ -385,6 +388,9 @@ def run_dqn_train(n, args, dist):
                             "flop_per_sample": flop,
                             "note": "whole update (sample + 2 kernels: T1 also advances the counter, T2 also rewrites the policy images), graph replay"},
         "batch": args.train_batch,
+        "global_batch": args.train_batch * dist.world,
+        "data_parallel": (f"dp{dist.world}: gradient SUM all-reduce of {agent._grad.numel()} f32 per update"
+                          if agent.data_parallel else None),
         "replay_capacity": agent.memory.capacity,
         "final_loss": float(loss),
         "epsilon": agent.epsilon,
@@ -543,7 +549,7 @@ def main():
     if args.dqn_steps:
         out["config5_dqn"] = run_dqn(n, args, dist)
 
-    if args.train_steps and dist.world == 1:  # one learner per GPU; no gradient exchange is built
+    if args.train_steps:  # N > 1: data parallel (gradient all-reduce per update)
         out["dqn_train"] = run_dqn_train(n, args, dist)
 
     if args.large_n and dist.world == 1:
