@@ -62,7 +62,11 @@ constexpr int kBlock = 256;       // 4 waves
 constexpr int kStepBlock = SHIPENV_STEP_BLOCK;  // step kernel workgroup (one LDS world copy each)
 constexpr int kEnvsPerThread = 4; // one 4-byte / 16-byte lane access per field
 constexpr int kMaxBlocks = 2048;  // 256 CUs x 8; grid-stride beyond
-constexpr int kStepBlocks = 2048; // step kernel default cap (SHIPENV_STEP_BLOCKS overrides)
+// step kernel default workgroup cap (SHIPENV_STEP_BLOCKS overrides): one group of 4 envs per
+// thread up to 2^25 envs. Measured against 2048 (iters = 8 at 2^24; tools/blk_sweep.sh,
+// profiles/r02h/blk_sweep): 2^24 129 -> 123 us, 2^25 293 -> 253 us, config 4 at 2^24
+// 200 -> 182 us; 2^20 (grid 1024 either way) unchanged
+constexpr int kStepBlocks = 32768;
 
 // se_tape.used bits (replay): which of the reference's draws this step consumed
 constexpr uint32_t kUsedFuelGate = SE_USED_FUEL_GATE, kUsedLossType = SE_USED_LOSS_TYPE,
@@ -2123,10 +2127,16 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs A) {
 }
 
 // ------------------------------------------------------------------ stats reduce
-__global__ __launch_bounds__(64) void stats_kernel(const double* __restrict__ slab, int blocks,
-                                                   double* __restrict__ out) {
+// One workgroup sums the per-wave slab entries in a fixed order (thread t takes entries
+// t, t + 1024, ... in turn; then a shuffle butterfly per wave and the 16 wave sums in
+// wave order), so the result does not depend on timing. The slab has one entry per wave
+// of the step grid: 4096 at 2^20 envs, 131072 at 2^25 with one group per thread.
+constexpr int kStatsBlock = 1024;
+__global__ __launch_bounds__(kStatsBlock) void stats_kernel(const double* __restrict__ slab, int blocks,
+                                                            double* __restrict__ out) {
+    __shared__ double part[3][kStatsBlock / 64];
     double a = 0.0, b = 0.0, c = 0.0;
-    for (int i = threadIdx.x; i < blocks; i += 64) {
+    for (int i = threadIdx.x; i < blocks; i += kStatsBlock) {
         a += slab[4 * i];
         b += slab[4 * i + 1];
         c += slab[4 * i + 2];
@@ -2137,10 +2147,17 @@ __global__ __launch_bounds__(64) void stats_kernel(const double* __restrict__ sl
         b += __shfl_xor(b, off);
         c += __shfl_xor(c, off);
     }
-    if (threadIdx.x == 0) {
-        out[0] = a;
-        out[1] = b;
-        out[2] = c;
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        part[0][w] = a;
+        part[1][w] = b;
+        part[2][w] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        double s = 0.0;
+        for (int k = 0; k < kStatsBlock / 64; ++k) s += part[threadIdx.x][k];
+        out[threadIdx.x] = s;
     }
 }
 
@@ -2614,7 +2631,7 @@ int se_rollout(se_env* env, const int32_t* src, int64_t m, int32_t max_steps, in
 int se_episode_stats(se_env* env, double* out, void* stream) {
     if (!env || !out) return fail(SE_EINVAL, "null argument");
     DeviceGuard g(env->device);
-    stats_kernel<<<1, 64, 0, (hipStream_t)stream>>>(env->d_slab, (int)env->nslab, out);
+    stats_kernel<<<1, kStatsBlock, 0, (hipStream_t)stream>>>(env->d_slab, (int)env->nslab, out);
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }
