@@ -2240,13 +2240,17 @@ int step_block_cap() {
     return c > 0 ? c : kStepBlocks;
 }
 
-// Nontemporal state loads when one step's traffic (~42-58 B per env) stays
-// inside or near the 256 MiB Infinity Cache (measured on one box, forced on vs off:
-// 2% faster from 2^20 to 2^23 envs, equal for config 4 at 2^22, 15% slower at 2^24;
-// profiles/r01_v11/nt_sweep).
+// Nontemporal state loads for the kernels without auto-reset while one step's traffic
+// (~42 B per env) stays inside or near the 256 MiB Infinity Cache. Forced on vs off at
+// the 32768-workgroup cap (profiles/r02h/nt_sweep, two runs each): config 3 at 2^20
+// 8.5-8.8 vs 9.1-9.2 us, at 2^24 131-134 vs 123 us. The auto-reset kernels (which also
+// read and write the episode counters) are faster without them: config 4 at 2^20
+// 11.6 vs 12.5-12.7 us, equal from 2^21 to 2^24; the training loop's step + record
+// 16.0-16.3 vs 17.5-17.9 us.
 bool step_nt_loads(const se_env* env) {
     const char* v = getenv("SHIPENV_NT_LOADS");
     if (v) return atoi(v) != 0;
+    if (env->flags & SE_FLAG_AUTO_RESET) return false;
     return env->n <= (int64_t)1 << 23;
 }
 

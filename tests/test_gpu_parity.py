@@ -174,10 +174,12 @@ def test_config2_move_only_vs_oracle(oracle_mod, n):
     env.close()
 
 
-@pytest.mark.parametrize("blocks", [None, "3"])
-def test_config3_full_mix_vs_oracle(oracle_mod, monkeypatch, blocks):
+@pytest.mark.parametrize("blocks,nt", [(None, None), ("3", None), (None, "0")])
+def test_config3_full_mix_vs_oracle(oracle_mod, monkeypatch, blocks, nt):
     if blocks:  # several groups per thread, partial last workgroup
         monkeypatch.setenv("SHIPENV_STEP_BLOCKS", blocks)
+    if nt:  # the kernel variant with temporal loads (the default above 2^23 envs)
+        monkeypatch.setenv("SHIPENV_NT_LOADS", nt)
     O = oracle_mod
     seed, n = 77, 8192
     env = VecEnv(n, seed=seed)
@@ -201,14 +203,17 @@ def test_config3_full_mix_vs_oracle(oracle_mod, monkeypatch, blocks):
     env.close()
 
 
-@pytest.mark.parametrize("n,blocks", [(8192, None), (8195, "3")])
-def test_config4_autoreset_64_ports_vs_oracle(oracle_mod, water, monkeypatch, n, blocks):
+@pytest.mark.parametrize("n,blocks,nt", [(8192, None, None), (8195, "3", None), (8192, None, "1")])
+def test_config4_autoreset_64_ports_vs_oracle(oracle_mod, water, monkeypatch, n, blocks, nt):
     """blocks="3": 3 workgroups, several groups per thread (double-buffered loads),
-    a partial last workgroup and a tail group appended to its done segment."""
+    a partial last workgroup and a tail group appended to its done segment. nt="1": the
+    variant with nontemporal loads (off by default with auto-reset)."""
     from shippingenv_amd.vec import random_water_ports
 
     if blocks:
         monkeypatch.setenv("SHIPENV_STEP_BLOCKS", blocks)
+    if nt:
+        monkeypatch.setenv("SHIPENV_NT_LOADS", nt)
     O = oracle_mod
     seed = 4242
     ports = random_water_ports(water, 64, seed=3)
