@@ -316,9 +316,18 @@ class VecDQNAgent:
             self.trainer.pack(1)
 
     def _broadcast_params(self):
-        """Rank 0's initial weights on every rank (DDP's start), then the kernel images."""
+        """Rank 0's initial weights on every rank (DDP's start), then the kernel images.
+        Every rank must hold as many envs and ring slots: the rings then fill in step, so all
+        ranks begin updating (and all-reducing) at the same iteration."""
         import torch.distributed as dist
 
+        shape = torch.tensor([self.env.n, self.memory.capacity, self.batch_size], dtype=torch.int64,
+                             device=self.env.device)
+        lo, hi = -shape.clone(), shape.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MAX, group=self.group)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
+        if not torch.equal(-lo, hi):
+            raise ValueError("data-parallel ranks need the same env count, memory size and batch size")
         src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
         with torch.no_grad():
             for p in self.model.parameters():

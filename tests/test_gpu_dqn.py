@@ -708,3 +708,44 @@ def test_data_parallel_ranks_stay_in_step():
     assert torch.equal(f0, f1)            # and train as one model
     assert not torch.equal(f0, i0)
     assert l0 == l1 and all(v is not None for v in l0[1:])
+
+
+def _dp_mismatch_worker(rank, world, port, out):
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), SHIPENV_SHARE_GPUS="1")
+    import torch.distributed as dist
+
+    from shippingenv_amd import dist as D
+    from shippingenv_amd.dqn import VecDQNAgent
+    from shippingenv_amd.vec import VecEnv
+
+    r, w, _, dev = D.init_from_env(backend="gloo")
+    env = VecEnv(2048 * (1 + r), seed=9, env_id_base=r * 4096, device=dev, auto_reset=True)
+    env.reset()
+    try:
+        VecDQNAgent(env, graph=False, batch_size=256)
+        out[rank] = "built"
+    except ValueError as e:
+        out[rank] = str(e)
+    env.close()
+    dist.destroy_process_group()
+
+
+def test_data_parallel_refuses_unequal_ranks():
+    """Ranks with different env counts would reach their first update at different
+    iterations and leave an all-reduce waiting: construction refuses them on every rank."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = mp.get_context("spawn").Manager().dict()
+    mp.start_processes(_dp_mismatch_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    assert all("same env count" in out[r] for r in range(2)), dict(out)
