@@ -660,11 +660,10 @@ def _dp_worker(rank, world, port, out):
 
     from shippingenv_amd import dist as D
     from shippingenv_amd.dqn import DQNNetwork, VecDQNAgent
-    from shippingenv_amd.vec import VecEnv
 
     r, w, _, dev = D.init_from_env(backend="gloo")
-    n = 2048
-    env = VecEnv(n, seed=9, env_id_base=r * n, device=dev, auto_reset=True)
+    env = D.ShardedVecEnv(2048, seed=9, auto_reset=True)  # the INTEGRATION.md recipe
+    assert env.first == r * 2048
     env.reset()
     torch.manual_seed(100 + r)  # different initial weights: the broadcast must align them
     model = DQNNetwork(env.obs_size, env.action_space_size)
@@ -679,7 +678,8 @@ def _dp_worker(rank, world, port, out):
     flat = torch.cat([p.detach().flatten() for p in agent.model.parameters()]).cpu()
     got = [None] * w
     dist.all_gather_object(got, (flat, losses, init))
-    out[rank] = (got, agent._graphs is not None)
+    stats = env.global_episode_stats().cpu().tolist()
+    out[rank] = (got, agent._graphs is not None, stats)
     agent.close()
     env.close()
     dist.destroy_process_group()
@@ -701,7 +701,8 @@ def test_data_parallel_ranks_stay_in_step():
     mgr = ctx.Manager()
     out = mgr.dict()
     mp.start_processes(_dp_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
-    got, graphs = out[0]
+    got, graphs, stats = out[0]
+    assert stats == out[1][2]  # the episode statistics all-reduced over both shards
     (f0, l0, i0), (f1, l1, i1) = got
     assert graphs
     assert not torch.equal(i0, i1)        # the ranks started from different weights
