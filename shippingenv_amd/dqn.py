@@ -203,6 +203,8 @@ class FusedUpdate:
         """One Adam step from `grad` summed over the ranks (se_qtrain_apply); with `policy`,
         its bf16 images are rewritten too. step_dev: Adam steps taken before this one (the
         caller advances it)."""
+        if grad.dtype != torch.float32 or not grad.is_contiguous() or grad.numel() < self.grad_size():
+            raise ValueError("grad must be a contiguous float32 device tensor of grad_size() floats")
         N.check(N.lib().se_qtrain_apply(self._h, None if policy is None else policy._h, _ptr(grad),
                                         self.lr, self.betas[0], self.betas[1], self.eps, _ptr(step_dev),
                                         _ptr(loss_out), self.env._stream()))
