@@ -1,0 +1,59 @@
+"""Where the driver's short run (5 warm-up + 20 timed steps) spends its wall time beyond the
+kernels: the host cost of a timing event record, of the first step call after a synchronise,
+and the synchronise itself, at N = 2^20 (config 3).
+
+    python tools/diag/short_run_overhead.py
+"""
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+
+def main():
+    from shippingenv_amd.vec import VecEnv
+
+    env = VecEnv(1 << 20, seed=0, device="cuda:0")
+    acts = torch.empty((25, env.n), dtype=torch.int32, device="cuda:0")
+    for t in range(25):
+        env.gen_actions(t, out=acts[t])
+    env.reset()
+    rows = [acts[k] for k in range(25)]
+    for k in range(5):
+        env.step(rows[k])
+    torch.cuda.synchronize()
+    out = {}
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(200)]
+    s = torch.cuda.current_stream()
+    t0 = time.perf_counter()
+    for e in ev:
+        e.record(s)
+    out["event_record_us"] = (time.perf_counter() - t0) / len(ev) * 1e6
+    torch.cuda.synchronize()
+    firsts, rest, syncs, walls = [], [], [], []
+    for rep in range(20):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        env.step(rows[5])
+        t1 = time.perf_counter()
+        for k in range(6, 25):
+            env.step(rows[k])
+        t2 = time.perf_counter()
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        firsts.append((t1 - t0) * 1e6)
+        rest.append((t2 - t1) / 19 * 1e6)
+        syncs.append((t3 - t2) * 1e6)
+        walls.append((t3 - t0) / 20 * 1e6)
+    med = lambda v: sorted(v)[len(v) // 2]
+    out.update(first_step_call_us=med(firsts), later_step_call_us=med(rest), final_sync_us=med(syncs),
+               wall_us_per_step_20=med(walls))
+    print(json.dumps({k: round(v, 2) for k, v in out.items()}))
+
+
+if __name__ == "__main__":
+    main()
