@@ -35,6 +35,10 @@
 // * Takes one Adam step on the parameters in place (torch nn.Linear layout).
 // * Rewrites the online net's MFMA fragment images, and refolds fc1's bias for the
 //   next update.
+// * Data parallel (se_qtrain_grad / se_qtrain_apply): mode 1 stops after the sums and
+//   stores them in a flat gradient vector (struct Grad); the ranks all-reduce it; mode 2
+//   reads the summed vector instead of the partials and runs the rest unchanged, so one
+//   rank's grad + apply gives the bits of mode 0.
 //
 // The weight operands are pre-permuted into A-fragment order, [row tile][k step][lane],
 // one coalesced 256-byte load per MFMA per wave. Activations are [feature][sample]
