@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-config4", action="store_true")
+    p.add_argument("--preroll4", type=int, default=1000,
+                   help="config 4 workload setup: untimed steps from reset to the steady episode mix "
+                        "(episodes of ~240 steps end in every step), before the warm-up")
     p.add_argument("--large-n", type=int, default=1 << 24,
                    help="extra HBM-resident run (working set beyond the 256 MiB MALL); 0 = skip")
     p.add_argument("--dqn-steps", type=int, default=50,
@@ -103,7 +106,7 @@ def make_actions(env, steps):
     return acts
 
 
-def timed_loop(env, acts, first, steps, dist, reduce_every=0):
+def timed_loop(env, acts, first, steps, dist, reduce_every=0, counter=None):
     """K back-to-back launches bracketed by barrier + synchronize on both sides; wall
     time is the max over ranks. HIP events on the launch stream give the GPU time per
     launch (roofline.kernel_ms): from the end of launch 1 to the end of launch K, over
@@ -129,6 +132,8 @@ def timed_loop(env, acts, first, steps, dist, reduce_every=0):
             # episode-return aggregation over the GPUs (RCCL all-reduce of 3 doubles)
             stats.copy_(env.episode_stats())
             dist.D.reduce_episode_stats(stats)
+            if counter is not None:
+                counter[0] += 1
     e1.record(stream)
     torch.cuda.synchronize()
     dist.barrier()
@@ -137,15 +142,24 @@ def timed_loop(env, acts, first, steps, dist, reduce_every=0):
     return wall, (ef.elapsed_time(e1) / (steps - 1) if steps > 1 else incl), incl
 
 
-def run_config(n, ports, auto, args, dist, label):
+def run_config(n, ports, auto, args, dist, label, preroll=0):
+    """One leg: reset, `preroll` untimed steps of workload setup (actions generated one row
+    at a time), W warm-up steps, then the K timed steps from rows resident in HBM.
+    Auto-reset legs all-reduce the episode statistics (RCCL) every min(100, K // 2) steps
+    inside the timed region; the count is returned in `info`."""
     from shippingenv_amd.vec import VecEnv
 
     env = VecEnv(n, seed=args.seed, ports=ports, env_id_base=dist.rank * n, device=dist.dev,
                  auto_reset=auto)
     total = args.warmup + args.steps
-    log(f"[{label}] rank {dist.rank}: n={n} P={env.P} auto_reset={auto}; generating {total} action rows")
+    log(f"[{label}] rank {dist.rank}: n={n} P={env.P} auto_reset={auto}; pre-roll {preroll}, "
+        f"generating {total} action rows")
     acts = make_actions(env, total)
     env.reset()
+    if preroll:
+        row = torch.empty(n, dtype=torch.int32, device=env.device)
+        for t in range(preroll):  # action rows of their own (t offset past the timed rows)
+            env.step(env.gen_actions(1_000_000 + t, out=row))
     for k in range(args.warmup):
         env.step(acts[k])
     if auto:  # the stats path runs inside the timed region: load its kernels now
@@ -153,8 +167,10 @@ def run_config(n, ports, auto, args, dist, label):
     torch.cuda.synchronize()
     if auto:
         env.clear_stats()
-    wall, k_ms, k_incl = timed_loop(env, acts, args.warmup, args.steps, dist,
-                                    reduce_every=100 if auto else 0)
+    every = max(1, min(100, args.steps // 2)) if auto else 0
+    count = [0]
+    wall, k_ms, k_incl = timed_loop(env, acts, args.warmup, args.steps, dist, reduce_every=every,
+                                    counter=count)
     stats = None
     if auto:
         s = env.episode_stats().clone()
@@ -163,7 +179,8 @@ def run_config(n, ports, auto, args, dist, label):
     env.close()
     del acts
     torch.cuda.empty_cache()
-    return wall, k_ms, stats, k_incl
+    info = {"preroll_steps": preroll, "allreduce_every": every, "allreduces_in_timed_region": count[0]}
+    return wall, k_ms, stats, k_incl, info
 
 
 def run_config1(args):
@@ -351,7 +368,8 @@ def run_dqn_train(n, args, dist):
     env = VecEnv(n, seed=args.seed, env_id_base=dist.rank * n, device=dist.dev, auto_reset=True)
     env.reset()
     torch.manual_seed(args.seed)
-    agent = VecDQNAgent(env, batch_size=args.train_batch, memory_size=4 * n, graph=True)
+    agent = VecDQNAgent(env, batch_size=args.train_batch, memory_size=4 * n, graph=True,
+                        data_parallel=dist.world > 1)
     for _ in range(6):  # eager warm-up updates, then the graph capture
         agent.step()
     stream = torch.cuda.current_stream(env.device)
@@ -406,7 +424,14 @@ def run_dqn_train(n, args, dist):
     return out
 
 
+KERNEL_MS_BASIS = "HIP events on the launch stream, end of launch 1 to end of launch K, over K - 1 launches"
+
+
 def roofline(bytes_per_step, n, k_ms, canonical, k_incl=None):
+    """The roofline object of one leg. achieved = this build's algorithmic bytes per
+    env-step (42 / 58 B) x n / the per-launch kernel time; the
+    survey's canonical field widths (66 / 82 B) are given as a byte count only: the
+    kernel does not move them, so no rate is derived from them."""
     achieved = bytes_per_step * n / (k_ms * 1e-3) / 1e9
     extra = {}
     if k_incl is not None:  # HIP events from before launch 1: includes its idle-queue start
@@ -421,9 +446,8 @@ def roofline(bytes_per_step, n, k_ms, canonical, k_incl=None):
         "traffic": None,
         "bytes_per_env_step": bytes_per_step,
         "canonical_bytes_per_env_step": canonical,
-        "canonical_achieved": round(canonical * n / (k_ms * 1e-3) / 1e9, 1),
         "kernel_ms": round(k_ms, 5),
-        "kernel_ms_basis": "HIP events, end of launch 1 to end of launch K, over K - 1 launches",
+        "kernel_ms_basis": KERNEL_MS_BASIS,
     } | extra
 
 
@@ -503,7 +527,7 @@ def main():
     from shippingenv_amd.vec import random_water_ports
 
     n = args.n
-    el3, k3, _, k3i = run_config(n, None, False, args, dist, "config3")
+    el3, k3, _, k3i, _ = run_config(n, None, False, args, dist, "config3")
     value = n * dist.world * args.steps / el3
     out = {
         "metric": "env-steps/sec at N=2^20 parallel envs per GPU (config 3: full step, 5 default ports)",
@@ -519,7 +543,8 @@ def main():
         "dtype": "f64+int (fuel/reward f64, positions/cargo int)",
         "data": "synthetic (Philox agent actions resident in HBM; reference map and ports)",
         "config": {
-            "workload": "BASELINE configs[2]: N=2^20 envs/GPU, full step, default 5 ports",
+            "workload": "BASELINE configs[2]: N=2^20 envs/GPU, full step, default 5 ports, from reset; "
+                        f"roofline.kernel_ms: {KERNEL_MS_BASIS}",
             "envs_per_gpu": n,
             "global_envs": n * dist.world,
             "ports": 5,
@@ -534,19 +559,22 @@ def main():
 
     if not args.no_config4:
         ports64 = random_water_ports(builtin_water(), 64, seed=3)
-        el4, k4, stats, k4i = run_config(n, ports64, True, args, dist, "config4")
+        el4, k4, stats, k4i, info4 = run_config(n, ports64, True, args, dist, "config4",
+                                                preroll=args.preroll4)
         t4, src4 = pmc_traffic("step_kernel_auto_bytes_per_launch")
         out["config4"] = {
             "workload": "BASELINE configs[3]: N=2^20 envs/GPU, 64 random ports, auto-reset, "
                         "ballot-compacted done list (per-wave segments), per-wave return reduction, RCCL all-reduce "
-                        "of the stats every 100 steps (inside the timed region)",
+                        "of the stats every min(100, steps // 2) steps inside the timed region; steady episode "
+                        f"mix: {args.preroll4} untimed pre-roll steps from reset before the warm-up; "
+                        f"roofline.kernel_ms: {KERNEL_MS_BASIS}",
             "value": round(n * dist.world * args.steps / el4, 1),
             "ms_per_step": round(el4 / args.steps * 1e3, 5),
             "roofline": roofline(BYTES_STEP_AUTO, n, k4, CANONICAL_STEP_AUTO, k4i),
             "episodes": stats[1],
             "mean_return": stats[0] / stats[1] if stats and stats[1] else None,
             "mean_len": stats[2] / stats[1] if stats and stats[1] else None,
-        }
+        } | info4
         if t4:
             out["config4"]["roofline"]["traffic"] = t4
             out["config4"]["roofline"]["traffic_source"] = src4
@@ -561,12 +589,16 @@ def main():
         out["config5_dqn"] = run_dqn(n, args, dist)
 
     if args.train_steps:  # N > 1: data parallel (gradient all-reduce per update)
-        out["dqn_train"] = run_dqn_train(n, args, dist)
+        try:
+            out["dqn_train"] = run_dqn_train(n, args, dist)
+        except Exception as e:  # noqa: BLE001 - keep the headline line whatever this leg does
+            log(f"[dqn_train] failed: {type(e).__name__}: {e}")
+            out["dqn_train"] = {"error": f"{type(e).__name__}: {e}"[:400]}
 
     if args.large_n and dist.world == 1:
         small = argparse.Namespace(**vars(args))
         small.steps, small.warmup = 100, 5
-        el, k, _, ki = run_config(args.large_n, None, False, small, dist, "large-n")
+        el, k, _, ki, _ = run_config(args.large_n, None, False, small, dist, "large-n")
         out["large_n"] = {
             "envs": args.large_n,
             "note": "working set beyond the 256 MiB Infinity Cache: traffic reaches HBM",

@@ -6,7 +6,12 @@ reset) as gfx950 HIP kernels behind a C-ABI (include/shipenv.h):
 * ``shippingenv_amd.vec.VecEnv`` — N environments per GPU on torch tensors;
 * ``shippingenv_amd.shipping`` — the reference's ``shipping`` package surface
   (Environment, add_port, reset, step, sample_action, ...) on the same kernels;
-* ``shippingenv_amd.utils`` — the reference's ``utils.preprocessing`` layout;
+  the directory ``shippingenv_amd/dropin`` on ``sys.path`` makes it ``import shipping``;
+* ``VecEnv.observe`` / ``VecEnv.valid_mask`` — the reference's
+  ``utils.preprocessing`` row layout and DQN validity, batched;
+* ``shippingenv_amd.policy`` / ``shippingenv_amd.dqn`` — the fused DQN policy and
+  the vectorised DQN training loop;
+* ``shippingenv_amd.maps`` — the map loader (``_initialize_map``);
 * ``shippingenv_amd.dist`` — one process per GPU, env sharding, RCCL stats.
 """
 

@@ -258,7 +258,7 @@ class VecDQNAgent:
                  hidden_size: int = HIDDEN, max_steps: int = MAX_STEPS_PER_EPISODE,
                  updates_per_step: int = 1, graph: bool = True, graph_warmup: int = 3,
                  fused: bool = True, model: DQNNetwork | None = None,
-                 data_parallel: bool | None = None, process_group=None):
+                 data_parallel: bool = False, process_group=None):
         if not env.auto_reset:
             raise ValueError("VecDQNAgent needs an auto-reset VecEnv (finished episodes restart in se_step)")
         self.env = env
@@ -293,13 +293,12 @@ class VecDQNAgent:
         self.use_graph, self.graph_warmup = bool(graph), int(graph_warmup)
         self._graph = None
         self._loss = torch.zeros((), dtype=torch.float32, device=dev)
-        # data parallel: every rank steps its own envs into its own ring; the update sums the
-        # ranks' gradients (all-reduce, RCCL) and takes the same Adam step everywhere
+        # data parallel (opt-in): every rank steps its own envs into its own ring; the update
+        # sums the ranks' gradients (all-reduce, RCCL) and takes the same Adam step everywhere.
+        # Every rank of the group must construct its agent and update in lockstep (the
+        # construction and every update issue collectives), so it is never switched on
+        # implicitly: independent per-rank learners stay collective-free.
         self.group = process_group
-        if data_parallel is None:
-            import torch.distributed as dist
-
-            data_parallel = dist.is_available() and dist.is_initialized() and dist.get_world_size(process_group) > 1
         self.data_parallel = bool(data_parallel)
         self._grad = None
         self._graphs = None
@@ -323,13 +322,21 @@ class VecDQNAgent:
         ranks begin updating (and all-reducing) at the same iteration."""
         import torch.distributed as dist
 
-        shape = torch.tensor([self.env.n, self.memory.capacity, self.batch_size], dtype=torch.int64,
-                             device=self.env.device)
-        lo, hi = -shape.clone(), shape.clone()
-        dist.all_reduce(lo, op=dist.ReduceOp.MAX, group=self.group)
-        dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
-        if not torch.equal(-lo, hi):
-            raise ValueError("data-parallel ranks need the same env count, memory size and batch size")
+        def agree(vals):
+            t = torch.tensor(vals, dtype=torch.int64, device=self.env.device)
+            lo, hi = -t.clone(), t.clone()
+            dist.all_reduce(lo, op=dist.ReduceOp.MAX, group=self.group)
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
+            return torch.equal(-lo, hi)
+
+        if not agree([self.env.n, self.memory.capacity, self.batch_size, self.env.P]):
+            raise ValueError("data-parallel ranks need the same env count, memory size, batch size "
+                             "and port count")
+        # the exchanged gradient leaves out dW1's port columns: every rank rebuilds them as
+        # db1 x its own port block, so the ports (positions and stocks) must be the same too
+        e = self.env
+        if not agree([int(v) for v in (*e.port_x, *e.port_y, *e.port_fuel, *e.port_cargo)]):
+            raise ValueError("data-parallel ranks need the same ports (positions and stocks)")
         src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
         with torch.no_grad():
             for p in self.model.parameters():

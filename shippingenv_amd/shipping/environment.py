@@ -90,6 +90,12 @@ def _new_stepper(water, px, py, pf, pc):
     return DeviceStepper(water, px, py, pf, pc)
 
 
+def _port_key(positions):
+    """Port positions as int tuples: add_port keeps `pos` as given (:57-65), and a list,
+    tuple or numpy array must key the same way (ndarray == ndarray has no truth value)."""
+    return tuple(tuple(int(v) for v in p) for p in positions)
+
+
 def _category(c):
     """`match action_category` compares by equality (:364-374)."""
     for t in (ActionType.MOVE_SHIP, ActionType.SELECT_PORT, ActionType.TAKE_FUEL,
@@ -222,13 +228,13 @@ class Environment:
         exact for every read the kernel makes."""
         g = self.np_game
         if (self._stepper is not None and g is self._g_ref and type(g) is np.ndarray
-                and self.port_positions == self._pp
+                and _port_key(self.port_positions) == self._pp
                 and self.port_fuel == self._pf and self.port_cargo == self._pc
                 and (cell is None or (g.item(cell) == Entity.GROUND) == self._ground.item(cell))):
             return self._stepper
         ground = np.asarray(g) == Entity.GROUND
-        key = (ground.shape, ground.tobytes(), tuple(tuple(int(v) for v in p) for p in self.port_positions),
-               tuple(self.port_fuel), tuple(self.port_cargo))
+        ports = _port_key(self.port_positions)
+        key = (ground.shape, ground.tobytes(), ports, tuple(self.port_fuel), tuple(self.port_cargo))
         if self._stepper is None or key != self._world_key:
             water = (~ground).astype(np.uint8)
             px = [int(p[0]) for p in self.port_positions]
@@ -239,7 +245,7 @@ class Environment:
                 self._stepper.set_world(water, px, py, self.port_fuel, self.port_cargo)
             self._world_key = key
         self._g_ref, self._ground = g, ground
-        self._pp = [list(p) for p in self.port_positions]
+        self._pp = ports
         self._pf, self._pc = list(self.port_fuel), list(self.port_cargo)
         return self._stepper
 

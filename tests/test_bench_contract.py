@@ -25,3 +25,15 @@ def test_roofline_object_has_the_contract_keys():
     assert r["kernel_ms"] == 0.0085 and r["kernel_ms_incl_start"] == 0.009
     assert r["frac_incl_start"] < r["frac"]
     assert "kernel_ms_incl_start" not in b.roofline(b.BYTES_STEP, 1 << 20, 0.0085, b.CANONICAL_STEP)
+
+
+def test_no_roofline_rate_above_its_peak():
+    """Every GB/s figure in the object is a rate the kernel moves: the survey's canonical
+    widths appear as a byte count only (canonical_achieved exceeded 8 TB/s)."""
+    b = _bench()
+    for k_ms in (0.0085, 0.004):  # the second would put a 66 B rate above the peak
+        r = b.roofline(b.BYTES_STEP, 1 << 20, k_ms, b.CANONICAL_STEP)
+        assert "canonical_achieved" not in r
+        assert r["canonical_bytes_per_env_step"] == 66
+        assert [key for key in r if key.endswith("achieved")] == ["achieved"]
+    assert b.KERNEL_MS_BASIS in b.roofline(b.BYTES_STEP, 1, 1.0, 66)["kernel_ms_basis"]

@@ -86,3 +86,38 @@ def test_in_place_np_game_edit_reaches_the_stepper(oracle_backend):
     _, reward, _, _ = env.step([environment.ActionType.MOVE_SHIP, move])
     assert list(env.ship_position) == [x, y], "the edited cell did not block the move"
     assert env.fuel == fuel and reward in (-3, -7)  # -5 blocked, then the +-2 distance term (:307-315)
+
+
+@pytest.mark.parametrize("kind", ["ndarray", "tuple"])
+def test_port_positions_of_any_indexable_type(oracle_backend, kind):
+    """add_port keeps `pos` as given (shipping/environment.py:57-65): numpy-array or tuple
+    port positions must step like lists, step after step (list equality on
+    ndarrays has no truth value)."""
+    import random
+
+    import numpy as np
+
+    from shippingenv_amd.maps import BUILTIN_MAP
+    from shippingenv_amd.shipping import Environment, ShipMove
+
+    ports = ([41, 40], [60, 22], [78, 29], [49, 72], [62, 72])
+    traces = []
+    for conv in (list, np.array if kind == "ndarray" else tuple):
+        random.seed(11)
+        env = Environment(BUILTIN_MAP)
+        for p in ports:
+            env.add_port(conv(p))
+        env.reset()
+        pick, out = random.Random(3), []
+        for _ in range(60):
+            move = (ShipMove.NORTH, ShipMove.EAST, ShipMove.SOUTH, ShipMove.WEST)[pick.randrange(4)]
+            try:
+                state, reward, done, _ = env.step([1, move])
+            except ValueError:
+                continue
+            out.append((tuple(int(v) for v in state["ship"]["position"]), float(state["ship"]["fuel"]),
+                        reward, done))
+            if done:
+                env.reset()
+        traces.append(out)
+    assert len(traces[0]) > 40 and traces[0] == traces[1]

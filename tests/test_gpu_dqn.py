@@ -669,7 +669,7 @@ def _dp_worker(rank, world, port, out):
     model = DQNNetwork(env.obs_size, env.action_space_size)
     init = torch.cat([p.detach().flatten() for p in model.parameters()]).cpu()
     agent = VecDQNAgent(env, graph=True, graph_warmup=2, batch_size=256, epsilon=0.5, target_update_every=3,
-                        max_steps=8, model=model)
+                        max_steps=8, model=model, data_parallel=True)
     assert agent.data_parallel
     losses = []
     for _ in range(7):
@@ -711,7 +711,7 @@ def test_data_parallel_ranks_stay_in_step():
     assert l0 == l1 and all(v is not None for v in l0[1:])
 
 
-def _dp_mismatch_worker(rank, world, port, out):
+def _dp_mismatch_worker(rank, world, port, out, what="n"):
     import os
     import sys
 
@@ -725,10 +725,14 @@ def _dp_mismatch_worker(rank, world, port, out):
     from shippingenv_amd.vec import VecEnv
 
     r, w, _, dev = D.init_from_env(backend="gloo")
-    env = VecEnv(2048 * (1 + r), seed=9, env_id_base=r * 4096, device=dev, auto_reset=True)
+    if what == "n":  # different env counts
+        env = VecEnv(2048 * (1 + r), seed=9, env_id_base=r * 4096, device=dev, auto_reset=True)
+    else:  # the same count and port positions, different port stocks
+        env = VecEnv(2048, seed=9, env_id_base=r * 2048, device=dev, auto_reset=True,
+                     port_fuel=[5 + r, 6, 7, 8, 9], port_cargo=[10, 11, 12, 13, 14])
     env.reset()
     try:
-        VecDQNAgent(env, graph=False, batch_size=256)
+        VecDQNAgent(env, graph=False, batch_size=256, data_parallel=True)
         out[rank] = "built"
     except ValueError as e:
         out[rank] = str(e)
@@ -750,3 +754,21 @@ def test_data_parallel_refuses_unequal_ranks():
     out = mp.get_context("spawn").Manager().dict()
     mp.start_processes(_dp_mismatch_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
     assert all("same env count" in out[r] for r in range(2)), dict(out)
+
+
+def test_data_parallel_refuses_unequal_ports():
+    """The exchanged gradient leaves out dW1's port columns (each rank rebuilds them from
+    its own port block), so ranks whose ports differ would drift apart silently:
+    construction refuses them on every rank."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = mp.get_context("spawn").Manager().dict()
+    mp.start_processes(_dp_mismatch_worker, args=(2, port, out, "ports"), nprocs=2, join=True,
+                       start_method="spawn")
+    assert all("same ports" in out[r] for r in range(2)), dict(out)
