@@ -184,10 +184,12 @@ def run_config(n, ports, auto, args, dist, label, preroll=0):
 
 
 def run_config1(args):
-    """BASELINE configs[0]: one env, 100 steps through the drop-in shipping.Environment
-    (N = 1 on the GPU: one launch and two copies per step), as the survey timed the
-    reference: random.seed(0), the five DEFAULT_PORTS, moves uniform over
-    N, E, S, W from random.Random(1), reset on done; median of 10 runs."""
+    """BASELINE configs[0]: one env, 100 steps through the drop-in shipping.Environment, as
+    the survey timed the reference: random.seed(0), the five DEFAULT_PORTS,
+    moves uniform over N, E, S, W from random.Random(1), reset on done; median of 10 runs.
+    Timed on the drop-in's default stepper (the step kernels' per-env code compiled for the
+    host: one C call per step) and on SHIPENV_STEPPER=gpu (one launch and one stream
+    synchronise per step)."""
     import random
     import statistics
 
@@ -213,13 +215,25 @@ def run_config1(args):
                 env.reset()
         return (time.perf_counter() - t0) * 1e3
 
-    once()
-    ms = statistics.median(once() for _ in range(10))
+    ms = {}
+    prev = os.environ.get("SHIPENV_STEPPER")
+    try:
+        for kind in ("host", "gpu"):
+            os.environ["SHIPENV_STEPPER"] = kind
+            once()
+            ms[kind] = statistics.median(once() for _ in range(10))
+    finally:
+        if prev is None:
+            os.environ.pop("SHIPENV_STEPPER", None)
+        else:
+            os.environ["SHIPENV_STEPPER"] = prev
     return {"workload": "BASELINE configs[0]: 1 env x 100 steps through shipping.Environment "
-                        "(the reference's API, N = 1 on the GPU)",
-            "ms_per_100_steps": round(ms, 4),
+                        "(the reference's API) on its default host stepper",
+            "ms_per_100_steps": round(ms["host"], 4),
+            "ms_per_100_steps_gpu_stepper": round(ms["gpu"], 4),
             "reference_python_ms_per_100_steps": 0.98,
-            "reference_note": "survey container, 1 core (BASELINE.md); the reference cannot run on the GPU box"}
+            "reference_note": "survey container, 1 core (BASELINE.md); the reference cannot run on the GPU box. "
+                              "Same-host comparison in the build container: profiles/r03/config1_vs_reference.json"}
 
 
 def run_rollouts(n, args, dist):

@@ -153,6 +153,28 @@ int se_step_typed(se_env* env, const int32_t* type, const int32_t* a, const int3
 int se_step_replay(se_env* env, const int32_t* type, const int32_t* a, const int32_t* b,
                    se_tape* tape, void* stream);
 
+/* Host-resident environments (no device, no HIP call): the N = 1 drop-in
+ * shipping.Environment steps here by default (shippingenv_amd/shipping/_host.py), with the
+ * step kernels' own per-env code compiled for the host (replay_env in shipenv.hip), so a
+ * reference step() costs one C call instead of a kernel launch and a stream synchronise.
+ * The state buffers are host memory; no alignment is required.
+ *   se_host_create / se_host_set_ports   Environment.__init__ + add_port (:29-65)
+ *   se_host_step_replay                  step() (:359-376) with the reference's draws from
+ *                                        tape[i], exactly as se_step_replay
+ *   se_host_reset_to                     reset() (:227-243) to given origin / dest
+ */
+typedef struct se_host se_host;
+int se_host_create(se_host** out, int32_t H, int32_t W, const uint8_t* water, int32_t P,
+                   const int32_t* port_x, const int32_t* port_y, const int32_t* port_fuel,
+                   const int32_t* port_cargo);
+int se_host_set_ports(se_host* h, int32_t P, const int32_t* port_x, const int32_t* port_y,
+                      const int32_t* port_fuel, const int32_t* port_cargo);
+int se_host_step_replay(se_host* h, int64_t n, const se_state* st, const int32_t* type,
+                        const int32_t* a, const int32_t* b, se_tape* tape);
+int se_host_reset_to(se_host* h, int64_t n, const se_state* st, const uint8_t* mask,
+                     const int32_t* origin, const int32_t* dest);
+int se_host_destroy(se_host* h);
+
 /* utils.preprocessing.preprocess_state rows (:25-62) as f32, row stride ld >= 6+4P:
  * [x, y, fuel, fuel ("cargo" is self.fuel, environment.py:206), origin, dest, (px,py,pfuel,pcargo)*P],
  * None -> -1. */

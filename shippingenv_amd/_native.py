@@ -42,6 +42,7 @@ EXPORTS = (
     "se_episode_stats", "se_clear_stats", "se_done_layout", "se_done_list", "se_done_compact",
     "se_get_counters", "se_set_counters",
     "se_map_decode_luma", "se_map_area_threshold", "se_map_from_jpeg",
+    "se_host_create", "se_host_set_ports", "se_host_step_replay", "se_host_reset_to", "se_host_destroy",
     "se_destroy", "se_last_error", "se_abi_version",
 )
 
@@ -117,6 +118,11 @@ def _declare(lib):
         "se_map_decode_luma": [C.c_char_p, C.c_size_t, P, C.c_size_t, C.POINTER(i32), C.POINTER(i32)],
         "se_map_area_threshold": [P, i32, i32, i32, i32, i32, i32, i32, i32, C.c_uint8, P, P],
         "se_map_from_jpeg": [C.c_char_p, C.c_size_t, i32, i32, P],
+        "se_host_create": [C.POINTER(P), i32, i32, P, i32, P, P, P, P],
+        "se_host_set_ports": [P, i32, P, P, P, P],
+        "se_host_step_replay": [P, i64, P, P, P, P, P],
+        "se_host_reset_to": [P, i64, P, P, P, P],
+        "se_host_destroy": [P],
         "se_destroy": [P],
         "se_last_error": [],
         "se_abi_version": [],

@@ -120,6 +120,33 @@ struct WorldDims {
     }
 };
 
+// The per-env step core (env_begin / env_finish, the replayed step) is compiled for the
+// host too: se_host_step_replay steps host-resident envs with the same source (the N = 1
+// drop-in). The two helpers below are the only operations that differ between the
+// targets; both are exact for the operand ranges used (< 2^24, correctly rounded sqrt).
+__host__ __device__ inline uint32_t mul24u(uint32_t a, uint32_t b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __umul24(a, b);
+#else
+    return a * b;
+#endif
+}
+__host__ __device__ inline int mul24i(int a, int b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __mul24(a, b);
+#else
+    return a * b;
+#endif
+}
+// IEEE square root, correctly rounded on both targets (np.sqrt, shipping/util.py:4)
+__host__ __device__ inline double sqrt_rn(double v) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __dsqrt_rn(v);
+#else
+    return sqrt(v);
+#endif
+}
+
 struct LdsWorld {
     const uint8_t* cell;
     const uint32_t* pos;
@@ -132,21 +159,21 @@ struct LdsWorld {
 
     // cell index x * W + y: coordinates and W are below 256, so 24-bit multiplies
     // (full rate) are exact where a 32-bit one would be a 64-bit-product op
-    __device__ int code(int x, int y) const { return cell[__umul24((uint32_t)x, (uint32_t)W) + (uint32_t)y]; }
-    __device__ bool is_ground(int x, int y) const { return code(x, y) == kCellGround; }
+    __host__ __device__ int code(int x, int y) const { return cell[mul24u((uint32_t)x, (uint32_t)W) + (uint32_t)y]; }
+    __host__ __device__ bool is_ground(int x, int y) const { return code(x, y) == kCellGround; }
     // _get_current_port_idx (:145-153): first port on the ship's cell, -1 if none
     // (water 0 -> -1, ground 255 -> 254 >= P)
-    __device__ int port_at(int x, int y) const { return port_of_code(code(x, y)); }
-    __device__ int port_of_code(int c) const {
+    __host__ __device__ int port_at(int x, int y) const { return port_of_code(code(x, y)); }
+    __host__ __device__ int port_of_code(int c) const {
         const int k = c - 1;
         return (unsigned)k < (unsigned)P ? k : -1;
     }
-    __device__ int px(int i) const { return (int)(pos[i] & 0xffffu); }
-    __device__ int py(int i) const { return (int)(pos[i] >> 16); }
-    __device__ int pfuel(int i) const { return stock[i].x; }
-    __device__ int pcargo(int i) const { return stock[i].y; }
+    __host__ __device__ int px(int i) const { return (int)(pos[i] & 0xffffu); }
+    __host__ __device__ int py(int i) const { return (int)(pos[i] >> 16); }
+    __host__ __device__ int pfuel(int i) const { return stock[i].x; }
+    __host__ __device__ int pcargo(int i) const { return stock[i].y; }
     // normalize(cargo, 50, 0) (util.py:6-8), only read for 0 < cargo < 50
-    __device__ double likelihood(int cargo) const { return frac[cargo]; }
+    __host__ __device__ double likelihood(int cargo) const { return frac[cargo]; }
 };
 
 __host__ __device__ inline LdsWorld world_view(WorldDims d, const uint32_t* img) {
@@ -250,8 +277,8 @@ enum LossKind : int { kLossNone = 0, kLossPartial = 1, kLossTotal = 2 };
 
 // sqrt of a non-negative integer, correctly rounded (np.sqrt on the int sum of
 // squares, shipping/util.py:4). Unit moves take the exact fast path.
-__device__ __forceinline__ double int_sqrt_rn(int v) {
-    return v == 1 ? 1.0 : __dsqrt_rn((double)v);
+__host__ __device__ __forceinline__ double int_sqrt_rn(int v) {
+    return v == 1 ? 1.0 : sqrt_rn((double)v);
 }
 
 // Does this env's step draw a gate that can change anything? (a MOVE that passes
@@ -295,7 +322,7 @@ constexpr double kFifthPerWord = 0x1.999999999999ap-35;  // fl(0.2) * 2^-32
 static_assert(kFifthPerWord * 4294967296.0 == 0.2, "0.2 * 2^-32 must be exact");
 
 template <bool kUnitMoves, bool kReplay>
-__device__ __forceinline__ Pending env_begin(const LdsWorld& w, Ship& s, int e_in, int type, int a,
+__host__ __device__ __forceinline__ Pending env_begin(const LdsWorld& w, Ship& s, int e_in, int type, int a,
                                              int b, double u_fuel, double u_gate, uint32_t gw) {
     // --- MOVE (_move_ship :273-339)
     const bool no_dest = s.dest == SE_NONE;                                      // :276
@@ -315,8 +342,8 @@ __device__ __forceinline__ Pending env_begin(const LdsWorld& w, Ship& s, int e_i
     // distances are small integers, so comparing them is exact
     const int dcl = no_dest ? 0 : s.dest;
     const int px = w.px(dcl), py = w.py(dcl);
-    const int d_old = __mul24(s.x - px, s.x - px) + __mul24(s.y - py, s.y - py);  // |d| < 256
-    const int d_new = __mul24(cx - px, cx - px) + __mul24(cy - py, cy - py);
+    const int d_old = mul24i(s.x - px, s.x - px) + mul24i(s.y - py, s.y - py);  // |d| < 256
+    const int d_new = mul24i(cx - px, cx - px) + mul24i(cy - py, cy - py);
     const bool closer = d_old > d_new;
 
     // --- SELECT_PORT (_select_port :265-271); an agent index always names a port in range
@@ -388,7 +415,7 @@ __device__ __forceinline__ int beta_part(uint32_t m, int cargo) {
 // Second half: cargo loss (_calculate_cargo_loss :169-200) of kind none / partial
 // (part = int(beta * cargo), :195-197) / total, then arrival (:325-337) with the
 // redrawn destination. Selects only.
-__device__ __forceinline__ void env_finish(Ship& s, Pending& p, int kind, int part, int new_dest,
+__host__ __device__ __forceinline__ void env_finish(Ship& s, Pending& p, int kind, int part, int new_dest,
                                            bool fires, bool arrive) {
     const int some = kind == kLossTotal ? s.cargo : part;
     const int loss = kind == kLossNone ? 0 : some;
@@ -418,6 +445,46 @@ __device__ __forceinline__ int decode_agent(int P, int act, int& type, int& a, i
     a = move ? dx : val;
     b = move * (1 - odd) * (k - 1);  // NORTH = (0, -1), SOUTH = (0, 1)
     return act < -4 ? SE_ERR_BAD_INDEX : SE_ERR_OK;
+}
+
+// One env's replayed step (se_step_replay; se_host_step_replay runs the same code on the
+// host): the reference's draws come from the tape record tp (uf / ug its u_fuel / u_gate,
+// read by the caller). Returns the SE_USED_* bits of the draws the reference made. A
+// variate the step needs but the record lacks (NaN, arrive_dest < 0) leaves the env
+// untouched with SE_ERR_NEED_DRAW, reward 0 and done 0.
+__host__ __device__ __forceinline__ uint32_t replay_env(const LdsWorld& w, Ship& s, Pending& p, int er, int ty,
+                                                        int va, int vb, double uf, double ug,
+                                                        const se_tape* tp) {
+    const Ship s0 = s;
+    p = env_begin<false, true>(w, s, er, ty, va, vb, uf, ug, 0u);
+    uint32_t used = p.mv ? (kUsedFuelGate | (p.moved ? kUsedMoved : 0u)) : 0u;
+    bool need = p.mv && (uf != uf || ug != ug);
+    int kind = kLossNone, nd = 0;
+    double beta = 0.0;
+    if (p.fires) {
+        used |= kUsedLossType;
+        const double lt = tp->u_type;
+        const bool partial = s.cargo != 0 && lt >= 0.1 && lt <= 0.9;
+        if (partial) {
+            used |= kUsedBeta;
+            beta = tp->beta;
+        }
+        need = need || lt != lt || (partial && beta != beta);
+        kind = lt < 0.1 ? kLossNone : (lt > 0.9 ? kLossTotal : kLossPartial);
+    }
+    if (p.arrive) {
+        used |= kUsedArrive;
+        nd = tp->arrive_dest;
+        need = need || nd < 0;
+    }
+    env_finish(s, p, kind, (int)(beta * (double)s.cargo), nd, p.fires, p.arrive);
+    if (need) {  // ask the caller for the next variate; change nothing
+        s = s0;
+        p.r = 0.0;
+        p.dead = false;
+        p.e = SE_ERR_NEED_DRAW;
+    }
+    return used;
 }
 
 // reset (:227-243) from two Philox words
@@ -824,36 +891,8 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
             const int64_t i = base + j;
             const bool live = kFull || i < n;
             se_tape* tp = A.tape + (live ? i : 0);
-            const Ship s0 = s[j];
             const double uf = live ? tp->u_fuel : 0.0, ug = live ? tp->u_gate : 0.0;
-            p[j] = env_begin<false, true>(w, s[j], er[j], ty[j], va[j], vb[j], uf, ug, 0u);
-            uint32_t used = p[j].mv ? (kUsedFuelGate | (p[j].moved ? kUsedMoved : 0u)) : 0u;
-            bool need = p[j].mv && (uf != uf || ug != ug);
-            int kind = kLossNone, nd = 0;
-            double beta = 0.0;
-            if (p[j].fires) {
-                used |= kUsedLossType;
-                const double lt = tp->u_type;
-                const bool partial = s[j].cargo != 0 && lt >= 0.1 && lt <= 0.9;
-                if (partial) {
-                    used |= kUsedBeta;
-                    beta = tp->beta;
-                }
-                need = need || lt != lt || (partial && beta != beta);
-                kind = lt < 0.1 ? kLossNone : (lt > 0.9 ? kLossTotal : kLossPartial);
-            }
-            if (p[j].arrive) {
-                used |= kUsedArrive;
-                nd = tp->arrive_dest;
-                need = need || nd < 0;
-            }
-            env_finish(s[j], p[j], kind, (int)(beta * (double)s[j].cargo), nd, p[j].fires, p[j].arrive);
-            if (need) {  // ask the caller for the next variate; change nothing
-                s[j] = s0;
-                p[j].r = 0.0;
-                p[j].dead = false;
-                p[j].e = SE_ERR_NEED_DRAW;
-            }
+            const uint32_t used = replay_env(w, s[j], p[j], er[j], ty[j], va[j], vb[j], uf, ug, tp);
             if (live) {
                 tp->used = (int32_t)used;
                 if (S.reward64) S.reward64[i] = p[j].r;
@@ -2187,6 +2226,14 @@ struct se_env {
     int64_t nslab = 0;  // stats slab entries: one per step-kernel wave
 };
 
+// A host-resident world (se_host_*): no device, no HIP call. It steps envs whose SoA
+// state lives in host memory with the kernels' own per-env code (replay_env).
+struct se_host {
+    WorldDims dims{};
+    std::vector<uint8_t> water;  // H*W, 0 = ground
+    std::vector<uint32_t> img;   // the world image, as staged into LDS on the device
+};
+
 namespace {
 
 thread_local std::string g_err;
@@ -2256,10 +2303,12 @@ bool step_nt_loads(const se_env* env) {
 
 size_t lds_bytes(const se_env* env) { return (size_t)env->dims.padded() * 4; }
 
-int upload_world(se_env* env, int32_t P, const int32_t* px, const int32_t* py, const int32_t* pf,
-                 const int32_t* pc) {
+// The world image (layout above WorldDims) of an H x W map and P ports, built on the
+// host: uploaded by se_create / se_set_ports, kept as is by the host handles.
+int build_world_image(int H, int W, const std::vector<uint8_t>& water, int32_t P, const int32_t* px,
+                      const int32_t* py, const int32_t* pf, const int32_t* pc, WorldDims& dims,
+                      std::vector<uint32_t>& img) {
     if (P < 0 || P > SE_MAX_PORTS) return fail(SE_EINVAL, "P must be in [0, 254]");
-    const int H = env->dims.H, W = env->dims.W;
     for (int i = 0; i < P; ++i) {
         if (px[i] < 0 || px[i] >= H || py[i] < 0 || py[i] >= W)
             return fail(SE_EINVAL, "Coordinates not within map");  // add_port, environment.py:59-60
@@ -2267,9 +2316,9 @@ int upload_world(se_env* env, int32_t P, const int32_t* px, const int32_t* py, c
     }
     const int cw = (H * W + 15) / 16 * 4;  // cell-code bytes in whole 16-byte units
     WorldDims d{H, W, P, cw};
-    std::vector<uint32_t> img((size_t)d.padded(), 0u);
+    img.assign((size_t)d.padded(), 0u);
     uint8_t* cell = reinterpret_cast<uint8_t*>(img.data());
-    for (int c = 0; c < H * W; ++c) cell[c] = env->water[c] ? 0 : (uint8_t)kCellGround;
+    for (int c = 0; c < H * W; ++c) cell[c] = water[c] ? 0 : (uint8_t)kCellGround;
     for (int i = P - 1; i >= 0; --i)  // Entity.PORT (:65); the first port on a cell wins
         cell[(size_t)px[i] * W + py[i]] = (uint8_t)(i + 1);
     for (int i = 0; i < P; ++i) {
@@ -2307,6 +2356,16 @@ int upload_world(se_env* env, int32_t P, const int32_t* px, const int32_t* py, c
     rtab[8] = 0.05;  // TAKE_FUEL / TAKE_CARGO (:349, :357)
     rtab[9] = 0.0;
     memcpy(&img[d.rtab()], rtab, sizeof rtab);
+    dims = d;
+    return SE_OK;
+}
+
+int upload_world(se_env* env, int32_t P, const int32_t* px, const int32_t* py, const int32_t* pf,
+                 const int32_t* pc) {
+    WorldDims d{};
+    std::vector<uint32_t> img;
+    int rc = build_world_image(env->dims.H, env->dims.W, env->water, P, px, py, pf, pc, d, img);
+    if (rc) return rc;
     if (d.padded() > env->world_cap) {
         if (env->d_world) HIP_TRY(hipFree(env->d_world));
         env->d_world = nullptr;
@@ -2706,6 +2765,94 @@ int se_destroy(se_env* env) {
     if (env->d_slab) (void)hipFree(env->d_slab);
     if (env->d_offsets) (void)hipFree(env->d_offsets);
     delete env;
+    return SE_OK;
+}
+
+// ---------------------------------------------------------------- host-resident envs
+int se_host_create(se_host** out, int32_t H, int32_t W, const uint8_t* water, int32_t P,
+                   const int32_t* port_x, const int32_t* port_y, const int32_t* port_fuel,
+                   const int32_t* port_cargo) {
+    if (!out) return fail(SE_EINVAL, "null out");
+    *out = nullptr;
+    if (H < 1 || W < 1 || H > SE_MAX_SIDE || W > SE_MAX_SIDE)
+        return fail(SE_EINVAL, "map sides must be in [1, 256]");
+    if (!water) return fail(SE_EINVAL, "null water map");
+    if (P > 0 && (!port_x || !port_y || !port_fuel || !port_cargo)) return fail(SE_EINVAL, "null port arrays");
+    se_host* h = new se_host();
+    h->dims.H = H;
+    h->dims.W = W;
+    h->water.assign(water, water + (size_t)H * W);
+    for (auto& v : h->water) v = v ? 1 : 0;
+    const int rc = build_world_image(H, W, h->water, P, port_x, port_y, port_fuel, port_cargo, h->dims, h->img);
+    if (rc) {
+        delete h;
+        return rc;
+    }
+    *out = h;
+    return SE_OK;
+}
+
+int se_host_set_ports(se_host* h, int32_t P, const int32_t* port_x, const int32_t* port_y,
+                      const int32_t* port_fuel, const int32_t* port_cargo) {
+    if (!h) return fail(SE_EINVAL, "null host world");
+    if (P > 0 && (!port_x || !port_y || !port_fuel || !port_cargo)) return fail(SE_EINVAL, "null port arrays");
+    return build_world_image(h->dims.H, h->dims.W, h->water, P, port_x, port_y, port_fuel, port_cargo, h->dims,
+                             h->img);
+}
+
+int se_host_step_replay(se_host* h, int64_t n, const se_state* st, const int32_t* type, const int32_t* a,
+                        const int32_t* b, se_tape* tape) {
+    if (!h || !st || n < 0) return fail(SE_EINVAL, "null argument or n < 0");
+    if (n == 0) return SE_OK;
+    if (!type || !a || !b || !tape || !st->x || !st->y || !st->fuel || !st->cargo || !st->origin || !st->dest ||
+        !st->reward || !st->done || !st->err)
+        return fail(SE_EINVAL, "null state, action or tape buffer");
+    const LdsWorld w = world_view(h->dims, h->img.data());
+    for (int64_t i = 0; i < n; ++i) {
+        Ship s{st->x[i], st->y[i], st->fuel[i], st->cargo[i], st->origin[i], st->dest[i]};
+        Pending p;
+        se_tape* tp = tape + i;
+        tp->used = (int32_t)replay_env(w, s, p, SE_ERR_OK, type[i], a[i], b[i], tp->u_fuel, tp->u_gate, tp);
+        st->x[i] = (uint8_t)s.x;
+        st->y[i] = (uint8_t)s.y;
+        st->fuel[i] = s.fuel;
+        st->cargo[i] = s.cargo;
+        st->origin[i] = (uint8_t)s.origin;
+        st->dest[i] = (uint8_t)s.dest;
+        st->reward[i] = (float)p.r;  // one rounding of the reference's f64 reward
+        st->done[i] = (uint8_t)p.dead;
+        st->err[i] = (int8_t)p.e;
+        if (st->reward64) st->reward64[i] = p.r;
+    }
+    return SE_OK;
+}
+
+int se_host_reset_to(se_host* h, int64_t n, const se_state* st, const uint8_t* mask, const int32_t* origin,
+                     const int32_t* dest) {
+    if (!h || !st || n < 0 || (n > 0 && (!origin || !dest))) return fail(SE_EINVAL, "null argument or n < 0");
+    const LdsWorld w = world_view(h->dims, h->img.data());
+    for (int64_t i = 0; i < n; ++i)
+        if ((!mask || mask[i]) && (origin[i] < 0 || origin[i] >= w.P || dest[i] < 0 || dest[i] >= w.P))
+            return fail(SE_EINVAL, "origin / dest must name ports");
+    for (int64_t i = 0; i < n; ++i) {  // reset_kernel's explicit form (reset() :227-243)
+        if (mask && !mask[i]) continue;
+        st->x[i] = (uint8_t)w.px(origin[i]);
+        st->y[i] = (uint8_t)w.py(origin[i]);
+        st->fuel[i] = kFuelInit;
+        st->cargo[i] = 0;
+        st->origin[i] = (uint8_t)origin[i];
+        st->dest[i] = (uint8_t)dest[i];
+        if (st->ep_return) st->ep_return[i] = 0.0f;
+        if (st->ep_len) st->ep_len[i] = 0;
+        st->done[i] = 0;
+        st->err[i] = 0;
+        st->reward[i] = 0.0f;
+    }
+    return SE_OK;
+}
+
+int se_host_destroy(se_host* h) {
+    delete h;
     return SE_OK;
 }
 

@@ -72,8 +72,10 @@ _ERRORS = {
     N.ERR_NO_PORTS: (Exception, "No ports available"),  # :360
 }
 
-# Builds the stepper of a new environment. The default is the GPU; tests may
-# install another with _set_stepper_factory (CPU host-logic tests only).
+# Builds the stepper of a new environment: the host stepper (_host.HostStepper: the step
+# kernels' per-env code compiled for the host, one C call per step) unless
+# SHIPENV_STEPPER=gpu selects the kernel (_device.DeviceStepper: one launch and one
+# stream synchronise per step). Tests may install another with _set_stepper_factory.
 _STEPPER_FACTORY = None
 
 
@@ -82,12 +84,26 @@ def _set_stepper_factory(factory):
     _STEPPER_FACTORY = factory
 
 
+def stepper_kind():
+    """'host' (default) or 'gpu', from SHIPENV_STEPPER."""
+    import os
+
+    kind = os.environ.get("SHIPENV_STEPPER", "host").strip().lower()
+    if kind not in ("host", "gpu"):
+        raise ValueError(f"SHIPENV_STEPPER must be 'host' or 'gpu', not {kind!r}")
+    return kind
+
+
 def _new_stepper(water, px, py, pf, pc):
     if _STEPPER_FACTORY is not None:
         return _STEPPER_FACTORY(water, px, py, pf, pc)
-    from ._device import DeviceStepper
+    if stepper_kind() == "gpu":
+        from ._device import DeviceStepper
 
-    return DeviceStepper(water, px, py, pf, pc)
+        return DeviceStepper(water, px, py, pf, pc)
+    from ._host import HostStepper
+
+    return HostStepper(water, px, py, pf, pc)
 
 
 def _port_key(positions):
@@ -125,7 +141,7 @@ class Environment:
         self._stepper = None
         self._world_key = None
         self._g_ref = self._ground = None
-        self._pp = self._pf = self._pc = None
+        self._pp = self._pp_raw = self._pf = self._pc = None
         self._initialize_map(map_path)
 
     # ------------------------------------------------------------------ setup
@@ -228,7 +244,7 @@ class Environment:
         exact for every read the kernel makes."""
         g = self.np_game
         if (self._stepper is not None and g is self._g_ref and type(g) is np.ndarray
-                and _port_key(self.port_positions) == self._pp
+                and self._ports_unchanged()
                 and self.port_fuel == self._pf and self.port_cargo == self._pc
                 and (cell is None or (g.item(cell) == Entity.GROUND) == self._ground.item(cell))):
             return self._stepper
@@ -246,8 +262,22 @@ class Environment:
             self._world_key = key
         self._g_ref, self._ground = g, ground
         self._pp = ports
+        # list positions compare as lists (one C-level comparison); any other indexable
+        # is compared through its int key (_ports_unchanged)
+        self._pp_raw = [list(p) if type(p) is list else tuple(q) for p, q in zip(self.port_positions, ports)]
         self._pf, self._pc = list(self.port_fuel), list(self.port_cargo)
         return self._stepper
+
+    def _ports_unchanged(self):
+        """port_positions still equal the positions the device world was built from: the
+        list comparison first (the common case: add_port with lists), then, when that is
+        False or has no truth value (numpy positions), the int keys."""
+        try:
+            if self.port_positions == self._pp_raw:
+                return True
+        except ValueError:  # ndarray == ndarray inside the list comparison
+            pass
+        return _port_key(self.port_positions) == self._pp
 
     def _ship_xy(self):
         if len(self.ship_position) == 0:

@@ -5,8 +5,9 @@ what it produced as one JSON line.
 TEST INFRASTRUCTURE, build container only: it imports the reference's agents and
 utils from /root/reference (which never travels to the GPU box), so
 tests/test_agent_compat.py skips without it. With the drop-in, state transitions run
-through the C oracle (tests/oracle_stepper.py) when no GPU is visible; the oracle is
-pinned to the HIP kernel bit for bit by the GPU suite.
+through its default stepper, the product's host build of the step kernels' per-env code
+(se_host_step_replay; no GPU is needed). tests/test_compat_gpu.py pins that build to the
+HIP kernel bit for bit.
 
     python tests/agent_compat.py --env ref|ours --agent dqn|sarsa|mcts [--seed S]
 
@@ -33,13 +34,8 @@ def setup(which):
         sys.path.insert(0, os.path.join(ROOT, "shippingenv_amd", "dropin"))
         sys.path.insert(0, ROOT)
         sys.path.insert(0, HERE)
-        import torch
-
-        if not torch.cuda.is_available():
-            from oracle_stepper import OracleStepper
-            from shippingenv_amd.shipping import environment
-
-            environment._set_stepper_factory(OracleStepper)
+        # the drop-in's default stepper: the product's host build of the step code
+        # (SHIPENV_STEPPER=gpu in the environment runs the kernel instead)
     import shipping
 
     where = os.path.dirname(os.path.abspath(shipping.__file__))

@@ -6,7 +6,8 @@ Q-table, MCTS returns, and the global `random` stream left behind (BASELINE nort
 
 Build container only: the reference never travels to the GPU box. Each run is its own
 process (tests/agent_compat.py) because both packages are named `shipping`; the
-drop-in's transitions run through the C oracle when no GPU is visible."""
+drop-in's transitions run through its default host stepper (the product's own step code
+built for the host), so no GPU is needed."""
 import json
 import os
 import subprocess

@@ -41,11 +41,14 @@ def test_dropin_package_resolves(monkeypatch):
 
 
 def test_no_gpu_means_no_silent_fallback(monkeypatch):
+    """SHIPENV_STEPPER=gpu selects the kernel: with no GPU it raises, it never steps
+    somewhere else."""
     from shippingenv_amd import _native
     from shippingenv_amd.maps import BUILTIN_MAP
     from shippingenv_amd.shipping import Environment, environment
 
     environment._set_stepper_factory(None)
+    monkeypatch.setenv("SHIPENV_STEPPER", "gpu")
     import torch
 
     if torch.cuda.is_available():

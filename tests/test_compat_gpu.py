@@ -1,6 +1,7 @@
 """The drop-in shipping.Environment on the MI355X (HIP step kernel through the
-C-ABI) against the reference's own seeded traces: identical results, Python
-types, exceptions and global `random` stream."""
+C-ABI, SHIPENV_STEPPER=gpu) against the reference's own seeded traces: identical
+results, Python types, exceptions and global `random` stream; and its default host
+stepper (the same per-env code compiled for the host) against the kernel, bit for bit."""
 import time
 
 import pytest
@@ -12,12 +13,13 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
-def _device_backend():
+def _device_backend(monkeypatch):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from shippingenv_amd.shipping import environment
 
-    environment._set_stepper_factory(None)  # the product path: DeviceStepper
+    environment._set_stepper_factory(None)
+    monkeypatch.setenv("SHIPENV_STEPPER", "gpu")  # the kernel: DeviceStepper
 
 
 @pytest.mark.parametrize("seed", range(6))
@@ -70,5 +72,96 @@ def test_library_loaded_before_torch():
         "env.step([1, (0, 1)]) if env.np_game[41, 41] != 0 else env.step([1, (0, -1)])\n"
         "print('ok')\n")
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=120,
-                       env=dict(os.environ, PYTHONPATH=ROOT))
+                       env=dict(os.environ, PYTHONPATH=ROOT, SHIPENV_STEPPER="gpu"))
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+# ------------------------------------------------------------------ host stepper vs kernel
+def _kernel_replay(z, sel, water, with_ports):
+    import numpy as np
+
+    from shippingenv_amd.vec import TAPE_DTYPE, VecEnv
+
+    sl = slice(None) if with_ports else slice(0, 0)
+    ports = [[int(a), int(b)] for a, b in zip(z["port_x"][sl], z["port_y"][sl])]
+    env = VecEnv(len(sel), water=water, ports=ports, port_fuel=z["port_fuel"][sl], port_cargo=z["port_cargo"][sl])
+    for f in ("x", "y", "fuel", "cargo", "origin", "dest"):
+        v = z["pre_" + f][sel]
+        if f in ("origin", "dest"):
+            v = np.where(v < 0, 255, v)
+        t = getattr(env, f)
+        t.copy_(torch.from_numpy(np.ascontiguousarray(v).astype(t.cpu().numpy().dtype)))
+    tape = np.zeros(len(sel), TAPE_DTYPE)
+    for f in ("u_fuel", "u_gate", "u_type", "beta", "arrive_dest"):
+        tape[f] = z[f][sel]
+    env.step_replay(z["act_type"][sel], z["act_a"][sel], z["act_b"][sel], tape)
+    torch.cuda.synchronize()
+    out = {f: getattr(env, f).cpu().numpy() for f in ("x", "y", "fuel", "cargo", "origin", "dest", "reward",
+                                                        "done", "err")}
+    env.close()
+    return out
+
+
+def _golden():
+    from conftest import golden_files
+
+    return golden_files()
+
+
+@pytest.mark.parametrize("path", _golden(), ids=lambda p: p.rsplit("/", 1)[-1])
+def test_host_stepper_equals_kernel_on_golden_records(path, water):
+    """se_host_step_replay (host build of replay_env) and se_step_replay (the kernel) on
+    every golden record: every field bit for bit."""
+    import numpy as np
+
+    from conftest import load_golden
+    from test_host_step import host_replay
+
+    z = load_golden(path)
+    n = 0
+    for kind, with_ports in ((0, True), (2, False)):
+        sel = np.nonzero(z["kind"] == kind)[0]
+        if not len(sel):
+            continue
+        k = _kernel_replay(z, sel, water, with_ports)
+        h = host_replay(z, sel, water, with_ports)
+        for f, v in k.items():
+            hv = h[f]
+            if f == "fuel":
+                np.testing.assert_array_equal(hv.view(np.int64), v.view(np.int64), err_msg=f)
+            elif f == "reward":
+                np.testing.assert_array_equal(hv.view(np.int32), v.view(np.int32), err_msg=f)
+            else:
+                np.testing.assert_array_equal(hv.astype(np.int64), v.astype(np.int64), err_msg=f)
+        n += len(sel)
+    assert n > 1000
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_host_and_gpu_steppers_give_the_same_trace(monkeypatch, seed):
+    """The drop-in on either stepper reproduces the reference's seeded trace (the replay
+    checks every step against it), so the two steppers agree step for step."""
+    assert replay(load_script(seed)) > 600  # SHIPENV_STEPPER=gpu (fixture)
+    monkeypatch.setenv("SHIPENV_STEPPER", "host")
+    assert replay(load_script(seed)) > 600
+
+
+def test_default_stepper_is_host_and_gpu_is_selectable(monkeypatch):
+    from shippingenv_amd.maps import BUILTIN_MAP
+    from shippingenv_amd.shipping import Environment
+    from shippingenv_amd.shipping._device import DeviceStepper
+    from shippingenv_amd.shipping._host import HostStepper
+
+    for kind, cls in (("gpu", DeviceStepper), ("host", HostStepper)):
+        monkeypatch.setenv("SHIPENV_STEPPER", kind)
+        env = Environment(BUILTIN_MAP)
+        env.add_port([41, 40])
+        env.add_port([60, 22])
+        env.reset()
+        assert isinstance(env._stepper, cls)
+    monkeypatch.delenv("SHIPENV_STEPPER")
+    env = Environment(BUILTIN_MAP)
+    env.add_port([41, 40])
+    env.add_port([60, 22])
+    env.reset()
+    assert isinstance(env._stepper, HostStepper)
