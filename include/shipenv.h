@@ -153,6 +153,13 @@ int se_step_typed(se_env* env, const int32_t* type, const int32_t* a, const int3
 int se_step_replay(se_env* env, const int32_t* type, const int32_t* a, const int32_t* b,
                    se_tape* tape, void* stream);
 
+/* step() for agent-index actions (the se_step encoding) with the reference's draws from
+ * tape[i] instead of Philox: the production step kernel's own code path (the agent path
+ * se_step runs) in its replay-tape instantiation, for parity against the reference's
+ * records. Writes tape[i].used; a step that needs a variate tape[i] lacks answers
+ * SE_ERR_NEED_DRAW with no effect. The step counter does not advance. */
+int se_step_agent_replay(se_env* env, const int32_t* actions, se_tape* tape, void* stream);
+
 /* Host-resident environments (no device, no HIP call): the N = 1 drop-in
  * shipping.Environment steps here by default (shippingenv_amd/shipping/_host.py), with the
  * step kernels' own per-env code compiled for the host (replay_env in shipenv.hip), so a

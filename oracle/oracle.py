@@ -46,6 +46,7 @@ def _lib():
     lib.orc_valid_mask.argtypes = [P, i64] + [P] * 4
     lib.orc_philox4x32_10.argtypes = [P, P, P]
     lib.orc_gen_actions.argtypes = [i64, i32, u64, i64, u32, P]
+    lib.orc_decode_agent.argtypes = [i32, i64, P, P, P, P, P]
     lib.orc_sample_actions.argtypes = [P, i64] + [P] * 6 + [u64, i64, u32, P, P, P]
     lib.orc_feistel_perm.argtypes = [u32, u32, P]
     lib.orc_feistel_perm.restype = u32
@@ -187,6 +188,14 @@ def philox(ctr, key):
     out = np.zeros(4, np.uint32)
     lib().orc_philox4x32_10(_p(c), _p(k), _p(out))
     return out
+
+
+def decode_agent(idx, P):
+    """orc_decode_agent: (type, a, b, err) int32 arrays for agent indices idx."""
+    idx = np.ascontiguousarray(idx, np.int32)
+    out = [np.zeros(len(idx), np.int32) for _ in range(4)]
+    lib().orc_decode_agent(int(P), len(idx), idx.ctypes.data, *[o.ctypes.data for o in out])
+    return tuple(out)
 
 
 def gen_actions(n, P, seed, env_id_base=0, t=0):

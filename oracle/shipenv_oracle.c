@@ -341,6 +341,17 @@ static int decode_agent(int32_t P, int32_t act, int32_t* type, int32_t* a, int32
     return E_OK;
 }
 
+/* decode_agent for n indices (tests pin it to the reference's own outputs,
+ * tests/golden/decode_golden.json); err[i] = E_BAD_INDEX where the reference raises */
+int orc_decode_agent(int32_t P, int64_t n, const int32_t* act, int32_t* type, int32_t* a, int32_t* b,
+                     int32_t* err) {
+    for (int64_t i = 0; i < n; ++i) {
+        type[i] = a[i] = b[i] = 0;
+        err[i] = decode_agent(P, act[i], &type[i], &a[i], &b[i]);
+    }
+    return 0;
+}
+
 static void load(ship* s, int64_t i, const int32_t* x, const int32_t* y, const double* fuel,
                  const int32_t* cargo, const int32_t* origin, const int32_t* dest) {
     s->x = x[i]; s->y = y[i]; s->fuel = fuel[i];

@@ -48,6 +48,11 @@ int orc_step_batch(const orc_world* w, int64_t n, int act_mode, const int32_t* a
                    int32_t* cargo, int32_t* origin, int32_t* dest, double* reward, int32_t* done,
                    int32_t* err);
 
+/* utils/preprocessing.py:111-137 for n agent indices: typed (type, a, b), err 9 where
+ * the reference raises IndexError (index < -4). */
+int orc_decode_agent(int32_t P, int64_t n, const int32_t* act, int32_t* type, int32_t* a, int32_t* b,
+                     int32_t* err);
+
 /* Auto-reset variant (config 4): after a step whose done==1 the env is reset with
  * Philox slot RESET of the same t; ep_return (f32 sum of f32 rewards) and ep_len
  * are accumulated, finished episodes are summed into stats[3] = {sum_return,

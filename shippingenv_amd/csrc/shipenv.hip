@@ -616,6 +616,25 @@ __device__ __forceinline__ void st_stream(V* p, V v) {
     }
 }
 
+// Store cache policy of the full-group stores (experiments): 0 = st_stream above; else
+// the aux bits of a raw buffer store from a block-uniform base (16 = sc1, write-through
+// that drops the line from L2; 17 = sc0 sc1; 2 = nt).
+#ifndef SHIPENV_ST_POLICY
+#define SHIPENV_ST_POLICY 0
+#endif
+template <typename V>
+__device__ __forceinline__ void st_at(void* base, uint32_t byte_off, V v) {
+#if SHIPENV_ST_POLICY
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+    if constexpr (sizeof(V) == 16)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, byte_off, 0, SHIPENV_ST_POLICY);
+    else
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, byte_off, 0, SHIPENV_ST_POLICY);
+#else
+    st_stream(reinterpret_cast<V*>(reinterpret_cast<char*>(base) + byte_off), v);
+#endif
+}
+
 template <bool kNt = false, typename T>
 __device__ __forceinline__ void ld4_full(const T* __restrict__ p, int64_t g0, T (&v)[4],
                                          uint32_t lane = threadIdx.x) {
@@ -643,11 +662,10 @@ __device__ __forceinline__ void st4_full(T* __restrict__ p, int64_t g0, const T 
         w.y = __builtin_bit_cast(uint32_t, v[1]);
         w.z = __builtin_bit_cast(uint32_t, v[2]);
         w.w = __builtin_bit_cast(uint32_t, v[3]);
-        st_stream(reinterpret_cast<uint4*>(slab_of(p, g0)) + threadIdx.x, w);
+        st_at(slab_of(p, g0), 16u * threadIdx.x, w);
     } else {
-        double2* q = reinterpret_cast<double2*>(slab_of(p, g0)) + 2 * threadIdx.x;
-        st_stream(q, make_double2(v[0], v[1]));
-        st_stream(q + 1, make_double2(v[2], v[3]));
+        st_at(slab_of(p, g0), 32u * threadIdx.x, make_double2(v[0], v[1]));
+        st_at(slab_of(p, g0), 32u * threadIdx.x + 16u, make_double2(v[2], v[3]));
     }
 }
 
@@ -668,7 +686,7 @@ __device__ __forceinline__ uint32_t ld4u8_full(const uint8_t* __restrict__ p, in
     return ld_stream<kNt>(reinterpret_cast<const uint32_t*>(slab_of(p, g0)) + lane);
 }
 __device__ __forceinline__ void st4u8_full(uint8_t* __restrict__ p, int64_t g0, uint32_t w) {
-    st_stream(reinterpret_cast<uint32_t*>(slab_of(p, g0)) + threadIdx.x, w);
+    st_at(slab_of(p, g0), 4u * threadIdx.x, w);
 }
 __device__ __forceinline__ uint32_t ld4u8_tail(const uint8_t* __restrict__ p, int64_t base, int64_t n) {
     uint32_t w = 0;
@@ -1105,8 +1123,11 @@ __device__ __forceinline__ uint32_t cell_of(uint32_t p, uint32_t wh) {
 #ifndef SHIPENV_SPEC_LOSS
 #define SHIPENV_SPEC_LOSS -1
 #endif
+#ifndef SHIPENV_SPEC_ARRIVE
+#define SHIPENV_SPEC_ARRIVE 0  // 1 = draw the ARRIVE block early too (experiment)
+#endif
 struct Draws {
-    U4 fuel, gate, loss0;
+    U4 fuel, gate, loss0, arrive;
 };
 template <bool kSpecLoss>
 __device__ __forceinline__ Draws early_draws(const StepArgs& A, int64_t base) {
@@ -1115,6 +1136,7 @@ __device__ __forceinline__ Draws early_draws(const StepArgs& A, int64_t base) {
     d.fuel = draw(qk, A.t, kSlotFuel);
     d.gate = draw(qk, A.t, kSlotGate);
     d.loss0 = kSpecLoss ? draw(qk, A.t, loss_slot(0)) : U4{{0u, 0u, 0u, 0u}};
+    d.arrive = SHIPENV_SPEC_ARRIVE ? draw(qk, A.t, kSlotArrive) : U4{{0u, 0u, 0u, 0u}};
     return d;
 }
 
@@ -1185,10 +1207,17 @@ __device__ __forceinline__ uint32_t record_group(const StepArgs& A, int64_t base
     return (cut4 & 1u) | ((cut4 >> 7) & 2u) | ((cut4 >> 14) & 4u) | ((cut4 >> 21) & 8u);
 }
 
-template <bool kAuto, bool kFull, bool kNt, bool kRec = false>
+// kReplay (se_step_agent_replay; parity only): the same code with the reference's draws
+// from the tape instead of Philox words: u_fuel and u_gate as f64 uniforms (the gate
+// tested against fl(c/50) as env_begin<.., kReplay> does, so a cargo-0 ship's gate can
+// fire, lose nothing, and still consume the loss-type draw), the loss type, beta and
+// the arrival's new destination; SE_USED_* bits back in the tape, and a step that needs
+// a variate the tape lacks leaves its env untouched with SE_ERR_NEED_DRAW.
+template <bool kAuto, bool kFull, bool kNt, bool kRec = false, bool kReplay = false>
 __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWorld& w,
                                                  Group<false, kAuto, kNt>& G, At<kFull> at,
                                                  BlockStats& bs, Finished& F, const Draws& D) {
+    static_assert(!kReplay || (!kAuto && !kRec), "agent replay: no auto-reset, no ring record");
     const int64_t n = A.n, base = at.base;
     const int P = w.P;
     const uint32_t lim = (uint32_t)(w.H - 1) | ((uint32_t)(w.W - 1) << 16);
@@ -1262,17 +1291,43 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
     const U4 fb = D.fuel, gb = D.gate;
     uint32_t fire = 0, arrive = 0, fin = 0, dead = 0;
     double f[4], r[4];
+    // kReplay: the group's tape records (the partial last group's missing envs read none)
+    [[maybe_unused]] double tu[4], tg[4], tt[4], tb[4];
+    [[maybe_unused]] int td[4];
+    [[maybe_unused]] uint32_t need = 0;  // kReplay: envs whose step needs a variate the tape lacks
+    if constexpr (kReplay) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool live = kFull || base + j < n;
+            const se_tape* tp = A.tape + (live ? base + j : 0);
+            tu[j] = tp->u_fuel;
+            tg[j] = tp->u_gate;
+            tt[j] = tp->u_type;
+            tb[j] = tp->beta;
+            td[j] = tp->arrive_dest;
+        }
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         // fuel cost (:103-104): 1 * (1 + uniform(-0.1, 0.1)), uniform = -0.1 + 0.2 u
-        const double scale = 1.0 + (-0.1 + (double)fb.v[j] * kFifthPerWord);
+        double scale;
+        if constexpr (kReplay) scale = 1.0 + (-0.1 + 0.2 * tu[j]);
+        else scale = 1.0 + (-0.1 + (double)fb.v[j] * kFifthPerWord);
         const bool oof = G.f[j] < scale;  // :288-290 (the ship still moves)
         const double take = tf_ok[j] ? (double)val[j] : -0.0;
         f[j] = G.f[j] + (moved[j] ? -scale : take);
         // the gate random() <= cargo / 50 (:318-323) as w <= floor(fl(c/50) 2^32); the
         // table's entry 50 is all ones (cargo >= 50 always fires); cargo 0 loses nothing
-        const uint32_t thr = w.gate_thr[min(max(cg[j], 0), 50)];
-        const bool fires = do_move[j] & (cg[j] > 0) & (gb.v[j] <= thr);
+        bool fires;
+        if constexpr (kReplay) {
+            const double ug = tg[j];
+            const int ci = ((cg[j] > 0) & (cg[j] < 50)) ? cg[j] : 0;
+            fires = do_move[j] & ((cg[j] >= 50) | (ug <= w.likelihood(ci)));
+            need |= (uint32_t)(do_move[j] & ((tu[j] != tu[j]) | (ug != ug))) << j;
+        } else {
+            const uint32_t thr = w.gate_thr[min(max(cg[j], 0), 50)];
+            fires = do_move[j] & (cg[j] > 0) & (gb.v[j] <= thr);
+        }
         r[j] = w.rtab[ridx[j] | ((int)(do_move[j] & oof) << 2)];
         fire |= (uint32_t)fires << j;
         arrive |= (uint32_t)(do_move[j] & (pos[j] == pd16[j])) << j;  // :325
@@ -1376,7 +1431,26 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
     // --- second half: cargo loss (_calculate_cargo_loss :169-200), contract v5: the
     // r-th env of the quad whose gate fired takes block LOSS_r (word 0 the loss type,
     // words 1-3 the Beta(2, 2) uniforms); only waves with a firing gate run it
-    if (fire) {
+    [[maybe_unused]] uint32_t used_loss = 0, used_beta = 0;
+    if constexpr (kReplay) {
+        if (fire) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool fj = (fire >> j) & 1u;
+                const double lt = tt[j], beta = tb[j];
+                const bool partial = (cg[j] != 0) & (lt >= 0.1) & (lt <= 0.9);
+                const int part = (int)(beta * (double)cg[j]);  // int(betavariate(2,2) * cargo) (:195-197)
+                const int some = lt > 0.9 ? cg[j] : part;
+                const int loss = ((lt < 0.1) | (cg[j] == 0)) ? 0 : some;
+                const double rl = r[j] + (double)loss * -3.0;
+                r[j] = fj ? rl : r[j];
+                cg[j] = fj ? cg[j] - loss : cg[j];
+                used_loss |= (uint32_t)fj << j;
+                used_beta |= (uint32_t)(fj & partial) << j;
+                need |= (uint32_t)(fj & ((lt != lt) | (partial & (beta != beta)))) << j;
+            }
+        }
+    } else if (fire) {
         uint32_t lt[4], v1[4], v2[4], v3[4];
         const uint32_t rk[4] = {0u, fire & 1u, (uint32_t)__popc(fire & 3u), (uint32_t)__popc(fire & 7u)};
         U4 rr = kSpecLoss ? D.loss0 : draw(qk, t, loss_slot(0));
@@ -1417,12 +1491,19 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
     }
     // arrival (:325-337): +2 cargo, cargo 0, origin = dest, a new destination != origin
     if (arrive) {
-        const U4 ab = draw(qk, t, kSlotArrive);
+        [[maybe_unused]] U4 ab{{0u, 0u, 0u, 0u}};
+        if constexpr (!kReplay) ab = SHIPENV_SPEC_ARRIVE ? D.arrive : draw(qk, t, kSlotArrive);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const bool aj = (arrive >> j) & 1u;
             const double ra = (r[j] + (double)(2 * cg[j])) + 10.0;
-            const int nd = pick_other(ab.v[j], P, dst[j]);
+            int nd;
+            if constexpr (kReplay) {
+                nd = td[j];
+                need |= (uint32_t)(aj & (nd < 0)) << j;
+            } else {
+                nd = pick_other(ab.v[j], P, dst[j]);
+            }
             r[j] = aj ? ra : r[j];
             cg[j] = aj ? 0 : cg[j];
             org[j] = aj ? dst[j] : org[j];
@@ -1466,6 +1547,30 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
         store4(S.ep_len, at, epl);
     }
     if constexpr (kRec) F.cut = record_group(late_args(), base, rw, rec_x, rec_y, oo, od, rec_cut, epl);
+    if constexpr (kReplay) {
+        se_tape* tp = A.tape + base;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (!(kFull || base + j < n)) continue;
+            const bool mv = do_move[j];
+            tp[j].used = (int32_t)((mv ? (uint32_t)kUsedFuelGate : 0u) | (moved[j] ? (uint32_t)kUsedMoved : 0u) |
+                                   (((used_loss >> j) & 1u) ? (uint32_t)kUsedLossType : 0u) |
+                                   (((used_beta >> j) & 1u) ? (uint32_t)kUsedBeta : 0u) |
+                                   (((arrive >> j) & 1u) ? (uint32_t)kUsedArrive : 0u));
+            if ((need >> j) & 1u) {  // the env as it was: later stores of this thread win
+                const int64_t i = base + j;
+                S.x[i] = (uint8_t)byte_of(G.x, j);
+                S.y[i] = (uint8_t)byte_of(G.y, j);
+                S.fuel[i] = G.f[j];
+                S.cargo[i] = G.c[j];
+                S.origin[i] = (uint8_t)byte_of(G.org, j);
+                S.dest[i] = (uint8_t)byte_of(G.dst, j);
+                S.reward[i] = 0.0f;
+                S.done[i] = 0;
+                S.err[i] = (int8_t)SE_ERR_NEED_DRAW;
+            }
+        }
+    }
 }
 
 // Sum over the wave's 64 lanes in a fixed tree, so the result does not depend on
@@ -1572,12 +1677,14 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
         G.template load<true>(A, At<true>{last < 0 ? full - 1 : first, 0, A.n}, lane);
     }
     __builtin_amdgcn_sched_barrier(0);
-    constexpr bool kAgent = !kTyped && !kReplay && !SHIPENV_ABLATE;
-    Draws D;
-    if constexpr (kAgent) {
+    // agent-index actions: the production step, or its replay-tape form (parity)
+    constexpr bool kAgent = !kTyped && !SHIPENV_ABLATE;
+    constexpr bool kDraws = kAgent && !kReplay;
+    Draws D{};
+    if constexpr (kDraws) {
         D = early_draws<spec_loss<kAuto>()>(A, (first + threadIdx.x) * 4);
         // keep the draws ahead of the staging wait: they overlap the loads in flight
-        asm volatile("" : "+v"(D.fuel.v[0]), "+v"(D.gate.v[0]), "+v"(D.loss0.v[0]));
+        asm volatile("" : "+v"(D.fuel.v[0]), "+v"(D.gate.v[0]), "+v"(D.loss0.v[0]), "+v"(D.arrive.v[0]));
     }
 #if SHIPENV_ABLATE >= 2
     const LdsWorld w = world_view(A.dims, A.world);
@@ -1598,8 +1705,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
         if (SHIPENV_PREFETCH && more) Gn.template load<true>(A, At<true>{g0 + kStepBlock, 0, A.n});
         if (g < full) {
             if constexpr (kAgent) {
-                if (k > 0) D = early_draws<spec_loss<kAuto>()>(A, g * 4);
-                step_group_agent<kAuto, true, kNt, kRec>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F, D);
+                if constexpr (kDraws) {
+                    if (k > 0) D = early_draws<spec_loss<kAuto>()>(A, g * 4);
+                }
+                step_group_agent<kAuto, true, kNt, kRec, kReplay>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F, D);
                 if constexpr (kRec) cuts |= F.cut << (4 * k);
             } else
                 step_group<kTyped, kReplay, kAuto, true, kNt>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F);
@@ -1670,6 +1779,8 @@ __global__ __launch_bounds__(64) void step_tail_kernel(StepArgs A) {
     Finished F;
     if constexpr (!kTyped && !kReplay && !SHIPENV_ABLATE)
         step_group_agent<kAuto, false, false>(A, w, G, at, bs, F, early_draws<spec_loss<kAuto>()>(A, at.base));
+    else if constexpr (!kTyped && kReplay && !SHIPENV_ABLATE)
+        step_group_agent<kAuto, false, false, false, true>(A, w, G, at, bs, F, Draws{});
     else
         step_group<kTyped, kReplay, kAuto, false>(A, w, G, at, bs, F);
     if constexpr (kAuto) {
@@ -2434,7 +2545,8 @@ int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const 
         else step_kernel<false, false, true, false, true><<<grid, kStepBlock, lds, s>>>(A);
         HIP_TRY(hipGetLastError());
     } else if (env->n >= kEnvsPerThread) {  // at least one full group (step_kernel's first load assumes it)
-        if (!typed && !autoreset && ntl) step_kernel<false, false, false, true><<<grid, kStepBlock, lds, s>>>(A);
+        if (!typed && replay) step_kernel<false, true, false><<<grid, kStepBlock, lds, s>>>(A);  // agent replay
+        else if (!typed && !autoreset && ntl) step_kernel<false, false, false, true><<<grid, kStepBlock, lds, s>>>(A);
         else if (!typed && autoreset && ntl) step_kernel<false, false, true, true><<<grid, kStepBlock, lds, s>>>(A);
         else if (!typed && !autoreset) step_kernel<false, false, false><<<grid, kStepBlock, lds, s>>>(A);
         else if (!typed && autoreset) step_kernel<false, false, true><<<grid, kStepBlock, lds, s>>>(A);
@@ -2444,7 +2556,8 @@ int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const 
         HIP_TRY(hipGetLastError());
     }
     if (env->n & 3) {
-        if (!typed && !autoreset) step_tail_kernel<false, false, false><<<1, 64, 0, s>>>(A);
+        if (!typed && replay) step_tail_kernel<false, true, false><<<1, 64, 0, s>>>(A);
+        else if (!typed && !autoreset) step_tail_kernel<false, false, false><<<1, 64, 0, s>>>(A);
         else if (!typed && autoreset) step_tail_kernel<false, false, true><<<1, 64, 0, s>>>(A);
         else if (typed && replay) step_tail_kernel<true, true, false><<<1, 64, 0, s>>>(A);
         else if (typed && !autoreset) step_tail_kernel<true, false, false><<<1, 64, 0, s>>>(A);
@@ -2597,6 +2710,10 @@ int se_step_typed(se_env* env, const int32_t* type, const int32_t* a, const int3
 int se_step_replay(se_env* env, const int32_t* type, const int32_t* a, const int32_t* b,
                    se_tape* tape, void* stream) {
     return launch_step(env, true, true, type, a, b, tape, stream);
+}
+
+int se_step_agent_replay(se_env* env, const int32_t* actions, se_tape* tape, void* stream) {
+    return launch_step(env, false, true, actions, nullptr, nullptr, tape, stream);
 }
 
 int se_observe(se_env* env, float* obs, int64_t ld, void* stream) {

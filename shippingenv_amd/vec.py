@@ -213,6 +213,21 @@ class VecEnv:
         self._keep = (t, aa, bb, tp)
         return self.reward, self.done, self.err
 
+    def step_agent_replay(self, actions, tape):
+        """se_step_agent_replay: agent-index actions (the se_step encoding) with the
+        reference's draws from tape (numpy TAPE_DTYPE, n): the production agent-path
+        kernel in its replay-tape instantiation (parity). Returns (reward, done, err,
+        tape with `used` filled in)."""
+        a = self._dev(actions, torch.int32)
+        tape = np.ascontiguousarray(tape, TAPE_DTYPE)
+        if len(tape) != self.n:
+            raise ValueError("tape length != n")
+        tp = torch.from_numpy(tape.view(np.uint8).reshape(-1).copy()).to(self.device)
+        N.check(N.lib().se_step_agent_replay(self._h, _ptr(a), _ptr(tp), self._stream()))
+        self._keep = (a, tp)
+        used = tp.cpu().numpy().view(TAPE_DTYPE)
+        return self.reward, self.done, self.err, used
+
     def observe(self, out=None):
         """preprocess_state rows (utils/preprocessing.py:25-62) as f32 [n, 6+4P]."""
         if out is None:

@@ -106,6 +106,116 @@ def test_replay_matches_reference(path, water):
         env.close()
 
 
+def _reference_decode(P):
+    """index -> (type, a, b) | None from the reference's own map_action_to_env_action
+    (tests/golden/decode_golden.json, made by make_decode_golden.py)."""
+    import json
+
+    with open(os.path.join(GOLDEN, "decode_golden.json")) as f:
+        rows = json.load(f)["P"][str(P)]["rows"]
+    return {r[0]: (None if r[1] == "IndexError" else tuple(r[1:])) for r in rows}
+
+
+@pytest.mark.parametrize("path", golden_files(), ids=os.path.basename)
+def test_agent_path_replays_reference_records(path, water):
+    """The bench-timed agent-path kernel (step_group_agent, in its replay-tape
+    instantiation: se_step_agent_replay) on every golden step record whose typed action
+    the reference's decode produces: the record's action becomes the agent index the
+    reference maps to it (decode_golden.json), the variates come from the tape, and the
+    post-state, reward, done and error class must equal the reference's, bit for bit."""
+    z = load_golden(path)
+    P = len(z["port_x"])
+    inv = {}
+    for i, v in sorted(_reference_decode(P).items(), key=lambda kv: (kv[0] < 0, kv[0])):
+        if v is not None:
+            inv.setdefault(v, i)
+    idx = np.array([inv.get((int(t), int(a), int(b) if int(t) == 1 else 0), -1)
+                    for t, a, b in zip(z["act_type"], z["act_a"], z["act_b"])], np.int32)
+    sel = np.nonzero((z["kind"] == 0) & (idx >= 0))[0]
+    assert len(sel) > 1000
+    env = env_for(z, len(sel), water)
+    set_state(env, z, sel)
+    reward, done, err, tape = env.step_agent_replay(idx[sel], tape_of(z, sel))
+    got = get_state(env)
+    want = {f: z["post_" + f][sel] for f in FIELDS}
+    assert_state(got, want, os.path.basename(path) + " (agent path)")
+    np.testing.assert_array_equal(reward.cpu().numpy(), z["reward"][sel].astype(np.float32))
+    np.testing.assert_array_equal(done.cpu().numpy().astype(np.int32), z["done"][sel])
+    np.testing.assert_array_equal(err.cpu().numpy().astype(np.int32), z["err"][sel])
+    env.close()
+    # the draws the kernel reports consumed are the typed replay's (the drop-in's protocol;
+    # the host build of that replay is pinned to the kernel in test_compat_gpu.py)
+    from shippingenv_amd.shipping._host import host_step_replay
+
+    st = {f: (np.where(z["pre_" + f][sel] < 0, 255, z["pre_" + f][sel]) if f in ("origin", "dest")
+              else z["pre_" + f][sel]) for f in FIELDS}
+    h = host_step_replay(water, z["port_x"], z["port_y"], z["port_fuel"], z["port_cargo"], st,
+                         z["act_type"][sel], z["act_a"][sel], z["act_b"][sel], tape_of(z, sel))
+    np.testing.assert_array_equal(tape["used"], h["tape"]["used"])
+
+
+@pytest.mark.parametrize("P", [5, 64])
+def test_agent_path_decodes_every_index_as_the_reference(P, water):
+    """Every agent index the reference decoded (decode_golden.json, -6 .. A + 2) stepped
+    through the agent-path kernel equals the reference's typed action stepped through the
+    typed replay kernel, from the same states and draws; indices below -4 raise in the
+    reference (SE_ERR_BAD_INDEX, state untouched)."""
+    table = _reference_decode(P)
+    idx = np.array(sorted(table), np.int32)
+    reps = 8
+    acts = np.tile(idx, reps)
+    n = len(acts) // 4 * 4 + 4
+    acts = np.concatenate([acts, np.zeros(n - len(acts), np.int32)])
+    rng = np.random.default_rng(P)
+    if P == 5:
+        ports = [[41, 40], [60, 22], [78, 29], [49, 72], [62, 72]]
+    else:
+        from shippingenv_amd.vec import random_water_ports
+
+        ports = random_water_ports(water, 64, seed=3)
+    mk = lambda: VecEnv(n, water=water, ports=ports, seed=5)  # noqa: E731
+    a, b = mk(), mk()
+    for e in (a, b):
+        e.reset()
+    # states: half the envs at their origin port (TAKE / SELECT valid), half moved away
+    moves = torch.from_numpy(rng.integers(0, 4, n).astype(np.int32)).cuda()
+    keep = torch.from_numpy((np.arange(n) % 2 == 0).astype(np.uint8)).cuda()
+    cargo = torch.from_numpy(rng.integers(0, 60, n).astype(np.int32)).cuda()
+    for e in (a, b):
+        e.step(torch.where(keep.bool(), torch.full_like(moves, 4 + 0), moves))
+        e.cargo.copy_(cargo)
+    typ = np.zeros(n, np.int32)
+    va = np.zeros(n, np.int32)
+    vb = np.zeros(n, np.int32)
+    for k, i in enumerate(acts):
+        v = table.get(int(i))
+        if v is None:
+            typ[k] = 99  # an unknown category: raises with no draw, like the index error
+        else:
+            typ[k], va[k], vb[k] = v
+    from shippingenv_amd.vec import TAPE_DTYPE
+
+    tape = np.zeros(n, TAPE_DTYPE)
+    tape["u_fuel"], tape["u_gate"] = rng.random(n), rng.random(n)
+    tape["u_type"], tape["beta"] = rng.random(n), rng.random(n)
+    tape["arrive_dest"] = rng.integers(0, P, n)
+    ra, da, ea, _ = a.step_agent_replay(acts, tape)
+    rb, db, eb = b.step_replay(typ, va, vb, tape)
+    torch.cuda.synchronize()
+    ea, eb = ea.cpu().numpy(), eb.cpu().numpy()
+    bad = np.array([table.get(int(i)) is None for i in acts])
+    assert (ea[bad] == 9).all() and (eb[bad] == 7).all()
+    np.testing.assert_array_equal(ea[~bad], eb[~bad])
+    sa, sb = get_state(a), get_state(b)
+    for f in FIELDS:
+        np.testing.assert_array_equal(np.asarray(sa[f]).view(np.uint8), np.asarray(sb[f]).view(np.uint8), err_msg=f)
+    np.testing.assert_array_equal(ra.cpu().numpy(), rb.cpu().numpy())
+    np.testing.assert_array_equal(da.cpu().numpy(), db.cpu().numpy())
+    assert (eb[~bad] == 0).sum() > 100  # moves, selects and in-stock takes step
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("path", golden_files("tape"), ids=os.path.basename)
 def test_replay_resets_match_reference(path, water):
     z = load_golden(path)

@@ -4,6 +4,7 @@ and the agent-index decode (utils/preprocessing.py:111-137) checked as a propert
 CPU only: state transitions run through the C oracle (tests/oracle_stepper.py), which
 the GPU suite pins to the HIP kernel bit for bit.
 """
+import os
 import random
 
 import numpy as np
@@ -107,23 +108,71 @@ def test_out_of_fuel_moves_and_goes_negative(oracle_backend):
     assert env.fuel < 0
 
 
+def _decode_table(P):
+    """The reference's own map_action_to_env_action outputs (utils/preprocessing.py:111-137),
+    recorded by tests/golden/make_decode_golden.py: index -> (type, a, b) or IndexError."""
+    import json
+
+    from conftest import GOLDEN
+
+    with open(os.path.join(GOLDEN, "decode_golden.json")) as f:
+        rows = json.load(f)["P"][str(P)]["rows"]
+    return {r[0]: (None if r[1] == "IndexError" else tuple(r[1:])) for r in rows}
+
+
 def decode_reference(idx, P):
-    """map_action_to_env_action (utils/preprocessing.py:111-137), restated: Python list
-    indexing of the moves wraps -4..-1 and raises IndexError below."""
-    moves = [(0, -1), (-1, 0), (0, 1), (1, 0)]  # NORTH, EAST, SOUTH, WEST (shipping/type.py)
-    if idx < 4:
-        dx, dy = moves[idx]  # raises IndexError below -4, as the reference does
-        return 1, dx, dy
-    if idx < 4 + P:
-        return 2, idx - 4, 0
-    if idx < 4 + P + MAX_CARGO:
-        return 4, idx - (4 + P), 0
-    return 3, idx - (4 + P + MAX_CARGO), 0
+    """map_action_to_env_action as the reference computed it (decode_golden.json): Python
+    list indexing of the moves wraps -4..-1 and raises IndexError below."""
+    v = _decode_table(P)[idx]
+    if v is None:
+        raise IndexError("list index out of range")
+    return v
+
+
+@pytest.mark.parametrize("P", [5, 64])
+def test_decode_table_is_the_kernels_decode(P):
+    """The kernel's agent-index decode (decode_agent / step_group_agent, restated in the
+    oracle's orc_decode) against every index the reference decoded, including -4..-1 and
+    indices past the action space."""
+    from oracle import oracle as O
+
+    O.build()
+    table = _decode_table(P)
+    idx = np.array(sorted(table), np.int32)
+    ty, a, b, err = O.decode_agent(idx, P)
+    for k, i in enumerate(idx):
+        want = table[int(i)]
+        if want is None:
+            assert err[k] == 9, i  # SE_ERR_BAD_INDEX: the reference raises before env.step
+        else:
+            assert err[k] == 0 and (ty[k], a[k], b[k]) == want, (i, (ty[k], a[k], b[k]), want)
+
+
+def test_golden_agent_idx_column_is_the_reference_inverse():
+    """tests/golden's agent_idx column (the first index the reference's decode maps to the
+    record's typed action, -1 if none) against the reference's own table."""
+    from conftest import golden_files, load_golden
+
+    n = 0
+    for path in golden_files():
+        z = load_golden(path)
+        P = len(z["port_x"])
+        inv = {}
+        for i, v in sorted(_decode_table(P).items(), key=lambda kv: (kv[0] < 0, kv[0])):
+            if v is not None:
+                inv.setdefault(v, i)
+        for k in np.nonzero(z["kind"] == 0)[0]:
+            t, a, b = int(z["act_type"][k]), int(z["act_a"][k]), int(z["act_b"][k])
+            key = (t, a, b) if t == 1 else (t, a, 0)
+            want = inv.get(key, -1)
+            assert int(z["agent_idx"][k]) == want, (path, k, key)
+            n += want >= 0
+    assert n > 10000
 
 
 @settings(max_examples=60, deadline=None)
 @given(seed=st.integers(0, 2**31 - 1),
-       idx=st.lists(st.integers(-8, 4 + 5 + 50 + 200 + 8), min_size=16, max_size=16))
+       idx=st.lists(st.integers(-6, 4 + 5 + 50 + 200 + 2), min_size=16, max_size=16))
 def test_agent_index_decode_matches_the_reference_mapping(seed, idx):
     """A batch stepped with agent indices equals the same batch stepped with the typed
     actions map_action_to_env_action gives (the kernel's decode_agent and the oracle's

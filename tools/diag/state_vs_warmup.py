@@ -11,8 +11,9 @@ crosses the two, each case in a FRESH process (run it once per case):
     python tools/diag/state_vs_warmup.py --case reset_warm           # 1000 steps of another env first
     python tools/diag/state_vs_warmup.py --case steady_warm --load /tmp/s1000.pt
 
-Each prints one JSON line: per-launch HIP-event times of the 20 timed steps (events
-around every launch), their mean, and the state mix (envs at a port, cargo > 0).
+Each prints one JSON line: the wall time per step, the first launch from before its
+enqueue (its idle-queue start included), the back-to-back launches 2..20 (HIP events),
+and the state mix (envs at a port, cargo > 0).
 """
 import argparse
 import json
@@ -84,18 +85,23 @@ def main():
         env.step(acts[k])
     torch.cuda.synchronize()
     s = torch.cuda.current_stream()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(21)]
+    # as bench.py times it: events only around the launches (an event between every two
+    # launches breaks the back-to-back dispatch and adds ~2.5 us per launch)
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    rows = [acts[5 + k] for k in range(20)]
     t0 = time.perf_counter()
-    ev[0].record(s)
+    e0.record(s)
     for k in range(20):
-        env.step(acts[5 + k])
-        ev[k + 1].record(s)
+        env.step(rows[k])
+        if k == 0:
+            e1.record(s)
+    e2.record(s)
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / 20 * 1e6
-    per = [ev[k].elapsed_time(ev[k + 1]) * 1e3 for k in range(20)]
     print(json.dumps({"case": a.case, "n": a.n, "wall_us_per_step": round(wall, 3),
-                      "mean_us": round(sum(per) / 20, 3), "mean_us_after_first": round(sum(per[1:]) / 19, 3),
-                      "per_launch_us": [round(x, 2) for x in per], "mix_before": m0}))
+                      "first_launch_incl_start_us": round(e0.elapsed_time(e1) * 1e3, 3),
+                      "back_to_back_us": round(e1.elapsed_time(e2) * 1e3 / 19, 3),
+                      "mix_before": m0, "env": {k: os.environ.get(k) for k in ("ROC_ACTIVE_WAIT_TIMEOUT",)}}))
 
 
 if __name__ == "__main__":

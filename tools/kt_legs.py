@@ -5,7 +5,8 @@
 bench.py runs its legs in a fixed order, so the step launches of each leg are the
 next dispatches of that leg's kernel instantiation in the trace:
   config 3   step_kernel<false, false, false, true, false>  (kNt loads, N = 2^20): the first W + K
-  config 4   step_kernel<false, false, true, false, false>  (auto-reset): the first W + K
+  config 4   step_kernel<false, false, true, false, false>  (auto-reset): launches P + W .. P + W + K
+             after its P pre-roll steps (--preroll4, bench.py's default 1000)
   large_n    step_kernel<false, false, false, false, false> (N = 2^24): the last 105
 For each leg this prints the average kernel duration (end - start of the dispatch, as
 rocprofv3 records it) over the K timed launches, over the timed launches after the
@@ -54,12 +55,13 @@ def main():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--n", type=int, default=1 << 20)
+    p.add_argument("--preroll4", type=int, default=1000)
     a = p.parse_args()
     rows = load(a.trace)
     K, W = a.steps, a.warmup
     out = {"trace": a.trace,
            "config3": leg(rows, C3, 0, W + K, K),
-           "config4": leg(rows, C4, 0, W + K, K),
+           "config4": leg(rows, C4, a.preroll4, W + K, K),
            "large_n": leg(rows, BIG, 0, 105, 100, from_end=True)}
     for key, b in (("config3", 42), ("config4", 58)):
         if out[key]:
