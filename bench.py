@@ -337,32 +337,75 @@ def run_dqn(n, args, dist):
     e1.record(stream)
     torch.cuda.synchronize()
     torch_ms = e0.elapsed_time(e1) / 5
-    flop_env = 2 * (env.obs_size * 128 + 128 * 128 + 128 * A)  # the reference network's MACs x 2
-    achieved = flop_env * n / (pol_ms * 1e-3) / 1e12
-    # what the kernel issues per 32 envs at most: fc1 (the port block folded into the bias,
-    # one k-step per row tile), fc2, and fc3 over the compact rows (DESIGN §10)
+    # the fp32-faithful mode (se_policy_f32: the network in f32 on v_mfma_f32_32x32x2_f32)
+    pol.act(eps, 2000, precision="f32")
+    torch.cuda.synchronize()
+    k32 = 10
+    e0.record(stream)
+    for t in range(k32):
+        pol.act(eps, 2001 + t, precision="f32")
+    e1.record(stream)
+    torch.cuda.synchronize()
+    pol32_ms = e0.elapsed_time(e1) / k32
+    # greedy decisions of both modes against fp32 torch on these 2^20 states
+    # (agents/dqn.py:198-204: the first maximum of the fp32 network's Q over the valid actions)
+    a16 = pol.act(0.0, 3000).clone()
+    a32 = pol.act(0.0, 3000, precision="f32").clone()
+    mask = env.valid_mask()
+    dis16 = dis32 = 0
+    with torch.no_grad():
+        obs_all = env.observe()
+        for i in range(0, n, 1 << 17):
+            q = model(obs_all[i:i + (1 << 17)])
+            bits = ((mask[i:i + (1 << 17)].unsqueeze(-1) >> shifts) & 1).flatten(1)[:, :A].bool()
+            ref = q.masked_fill(~bits, float("-inf")).argmax(1).to(torch.int32)
+            dis16 += int((a16[i:i + (1 << 17)] != ref).sum())
+            dis32 += int((a32[i:i + (1 << 17)] != ref).sum())
+    del obs_all, mask
+    # FLOPs per env the kernels' algorithm evaluates: fc1 over the 6 dynamic inputs (the
+    # constant port block is folded into the bias), fc2, and fc3 over the compact rows (the
+    # actions some env can ever take, in 32-row tiles). The reference network's
+    # count (all A rows, all 6 + 4P inputs) is reported beside it as a count, not a rate.
     cmax = min(max(int(v) for v in env.port_cargo), 49)
     fmax = min(max(int(v) for v in env.port_fuel), 199)
+    rows3 = 32 * ((4 + env.P + cmax + fmax + 31) // 32)
+    flop_env = 2 * (6 * 128 + 128 * 128 + rows3 * 128)
+    flop_ref = 2 * (env.obs_size * 128 + 128 * 128 + 128 * A)  # the reference network's MACs x 2
+    achieved = flop_env * n / (pol_ms * 1e-3) / 1e12
+    achieved32 = flop_env * n / (pol32_ms * 1e-3) / 1e12
+    # what the kernel issues per 32 envs at most: fc1 (the port block folded into the bias,
+    # one k-step per row tile), fc2, and fc3 over the compact rows (DESIGN §10)
     mfma_tile = 4 + 32 + 8 * ((4 + env.P + cmax + fmax + 31) // 32)
     pol.close()
     env.close()
     return {
         "workload": "config 5: fused DQN policy (se_policy: obs + DQNNetwork 26->128->128->259 bf16 "
-                    "MFMA + masked argmax + eps-greedy 0.1) then se_step, N envs/GPU, random-init weights",
+                    "MFMA + masked argmax + eps-greedy 0.1) then se_step, N envs/GPU, random-init weights; "
+                    "policy_ms_f32 / roofline_f32: the fp32-faithful mode (se_policy_f32)",
         "value": round(n * dist.world * args.dqn_steps / wall, 1),
         "unit": "env-steps/s (policy + step)",
         "ms_per_step": round(wall / args.dqn_steps * 1e3, 4),
         "e2e_kernel_ms": round(e2e_ms, 4),
         "policy_ms": round(pol_ms, 4),
+        "policy_ms_f32": round(pol32_ms, 4),
+        "greedy_disagreement_vs_fp32_torch": {"bf16": round(dis16 / n, 5), "f32": round(dis32 / n, 6),
+                                              "states": n,
+                                              "note": "greedy actions on the config-5 states vs the first "
+                                                      "masked argmax of the fp32 torch DQNNetwork"},
+        "roofline_f32": {"bound": "mfma (f32)", "achieved": round(achieved32, 2), "peak": F32_MFMA_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved32 / F32_MFMA_PEAK_TFLOPS, 4),
+                         "flop_per_env": flop_env, "reference_network_flop_per_env": flop_ref,
+                         "note": "se_policy_f32 on the same FLOP basis (includes its per-call repack of "
+                                 "the f32 image)"},
         "torch_unfused_policy_ms": round(torch_ms, 4),
         "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": BF16_DENSE_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4),
                      "flop_per_env": flop_env, "traffic": None,
+                     "reference_network_flop_per_env": flop_ref,
                      "executed_mfma_per_32_envs": mfma_tile,
-                     "executed_tflops": round(mfma_tile * 32768 / 32 * n / (pol_ms * 1e-3) / 1e12, 1),
-                     "note": "achieved is on the reference network's FLOPs (all of fc3's rows, fc1's 26 "
-                             "inputs); the kernel issues at most executed_mfma_per_32_envs "
-                             "v_mfma_f32_32x32x16_bf16 per 32 envs"},
+                     "note": "achieved is on the FLOPs the fused step evaluates (fc1's 6 dynamic inputs, "
+                             "fc2, fc3's compact rows); at most executed_mfma_per_32_envs "
+                             "v_mfma_f32_32x32x16_bf16 per 32 envs (fc1 pads K to 16)"},
     }
 
 

@@ -251,6 +251,12 @@ int se_policy(se_qnet* q, int32_t* actions, double epsilon, uint32_t t, float* q
 /* Repack from the device weights of the last se_qnet_set_weights (same tensors, new values:
  * after an optimizer step). bump (optional, device int32): incremented once on the stream
  * (a training loop's update counter, advanced where the new weights take effect). */
+/* choose_action as se_policy, with DQNNetwork evaluated in fp32 as agents/dqn.py:198-200
+ * runs it (fp32 weights and activations on v_mfma_f32_32x32x2_f32: exact f32 products,
+ * f32 accumulation) instead of bf16: the fp32-faithful mode. Packs its image from the
+ * weights of the last se_qnet_set_weights (their current values) on every call. */
+int se_policy_f32(se_qnet* q, int32_t* actions, double epsilon, uint32_t t, float* q_out, int64_t ldq,
+                  void* stream);
 int se_qnet_repack(se_qnet* q, int32_t* bump, void* stream);
 int se_qnet_destroy(se_qnet* q);  /* destroy a qnet before the env it was created on */
 

@@ -32,7 +32,7 @@ ROLL_DONE, ROLL_MAX_STEPS, ROLL_RAISED, ROLL_ATTEMPTS, ROLL_BAD_SRC = 0, 1, 2, 3
 EXPORTS = (
     "se_create", "se_set_ports", "se_bind", "se_reset", "se_reset_to", "se_step",
     "se_step_typed", "se_step_replay", "se_step_agent_replay", "se_observe", "se_valid_mask", "se_gen_actions",
-    "se_sample_actions", "se_rollout", "se_qnet_create", "se_qnet_set_weights", "se_policy",
+    "se_sample_actions", "se_rollout", "se_qnet_create", "se_qnet_set_weights", "se_policy", "se_policy_f32",
     "se_qnet_repack", "se_policy_record",
     "se_qnet_destroy", "se_replay_create", "se_replay_begin", "se_replay_end", "se_replay_end_reset", "se_step_record",
     "se_replay_size",
@@ -89,6 +89,7 @@ def _declare(lib):
         "se_qnet_create": [C.POINTER(P), P],
         "se_qnet_set_weights": [P, P, P, P, P, P, P, P],
         "se_policy": [P, P, C.c_double, u32, P, i64, P],
+        "se_policy_f32": [P, P, C.c_double, u32, P, i64, P],
         "se_qnet_repack": [P, P, P],
         "se_policy_record": [P, P, P, C.c_double, u32, P],
         "se_qnet_destroy": [P],

@@ -264,6 +264,123 @@ __device__ __forceinline__ uint32_t range_bits(int lo, int hi) {
     return lo > hi ? 0u : (top & ~low);
 }
 
+// is_valid_action (dqn.py:125-175) of one env, as row ranges of a fc3 layout: moves
+// always; SELECT p at the ship's cell and != origin; TAKE_CARGO / TAKE_FUEL at a port
+// with 0 < amount <= stock. These helpers are the f32 policy kernel's form of the bf16
+// kernel's inline epilogue (policy_kernel below keeps it inline: in helper form the
+// compiler unrolled its fc3 loop and spilled SGPRs at its 128-VGPR budget); the GPU tests
+// require both kernels to choose the same first maximum from the same Q rows.
+struct EnvValid {
+    int cur, cst, fst;       // port on the ship's cell (-1), its stocks capped to the amounts
+    int c_lo, c_hi, f_lo, f_hi;
+    uint64_t sel;            // SELECT: bit p for each port on the ship's cell other than the origin
+};
+__device__ __forceinline__ EnvValid env_valid(const LdsWorld& w, const QnetDims& q, const uint64_t* SAME, int x,
+                                              int y, int origin) {
+    EnvValid v;
+    v.cur = w.port_at(x, y);
+    v.cst = v.cur >= 0 ? min(w.pcargo(max(v.cur, 0)), 49) : 0;
+    v.fst = v.cur >= 0 ? min(w.pfuel(max(v.cur, 0)), 199) : 0;
+    v.c_lo = q.cargo_row1();
+    v.c_hi = v.c_lo + v.cst - 1;
+    v.f_lo = q.fuel_row1();
+    v.f_hi = v.f_lo + v.fst - 1;
+    v.sel = v.cur >= 0 ? SAME[max(v.cur, 0)] & ~(origin >= 0 ? 1ull << origin : 0ull) : 0ull;
+    return v;
+}
+
+// can any row of tile mt be valid for this env (a tile no env of the wave can choose from
+// is skipped, MFMAs included)
+__device__ __forceinline__ bool tile_maybe(const EnvValid& v, int mt, int P) {
+    const int base = mt * 32, top = base + 31;
+    return (mt == 0) | ((v.cur >= 0) & (base < 4 + P)) | ((v.cst > 0) & (v.c_lo <= top) & (v.c_hi >= base)) |
+           ((v.fst > 0) & (v.f_lo <= top) & (v.f_hi >= base));
+}
+
+// valid rows of tile mt as bits of the tile
+__device__ __forceinline__ uint32_t tile_mask(const EnvValid& v, int mt, int P) {
+    const int base = mt * 32;
+    uint32_t m = range_bits(-base, 3 - base) | range_bits(v.c_lo - base, v.c_hi - base) |
+                 range_bits(v.f_lo - base, v.f_hi - base);
+    if (base < 4 + P) {  // SELECT rows 4 + p live in this tile (uniform): sel shifted by 4 - base
+        const int sh = base - 4;
+        m |= (uint32_t)(sh < 0 ? v.sel << -sh : (sh < 64 ? v.sel >> sh : 0ull));
+    }
+    return m;
+}
+
+// the masked first maximum over one fc3 tile's accumulator (ascending rows), registers
+// outside the wave-uniform mask rm skipped
+__device__ __forceinline__ void tile_argmax(const f32x16& c, uint32_t m, uint32_t rm, int base, int h, float& best,
+                                            int& bidx) {
+    m >>= 4 * h;  // register reg holds row base + 4h + (reg & 3) + 8 (reg >> 2)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        if (!((rm >> reg) & 1u)) continue;
+        const int i = (reg & 3) + 8 * (reg >> 2);
+        const bool better = ((m >> i) & 1u) && c[reg] > best;  // ascending rows: first max
+        best = better ? c[reg] : best;
+        bidx = better ? base + 4 * h + i : bidx;
+    }
+}
+
+__device__ __forceinline__ void tile_q_out(float* q_out, int64_t ldq, int rows, const f32x16& c, int64_t e, int base,
+                                           int h) {
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {  // the full layout: row = action
+        const int row = base + 4 * h + (reg & 3) + 8 * (reg >> 2);
+        if (row < rows) q_out[e * ldq + row] = c[reg];
+    }
+}
+
+// the two lane halves of an env merged (larger value, then lower index), then
+// epsilon-greedy (choose_action :186-203) and the action / replay record stores
+#define FINISH_ENV(v, e, live, h, best, bidx, x8, y8, o8, d8, ff)                                             \
+    finish_env(q, v, e, live, h, best, bidx, x8, y8, o8, d8, ff, A.actions, A.eps, A.seed, A.env_base, A.t,       \
+               A.rec_pos, A.rec_fuel, A.rec_act, A.rec_head, A.rec_cap)
+__device__ __forceinline__ void finish_env(const QnetDims& q, const EnvValid& v, int64_t e, bool live, int h, float best,
+                                           int bidx, uint32_t x8, uint32_t y8, uint32_t o8, uint32_t d8, float ff,
+                                           int32_t* actions, double eps, uint64_t seed, int64_t env_base, uint32_t t,
+                                           uint32_t* rec_pos, float* rec_fuel, int32_t* rec_act, int64_t rec_head,
+                                           int64_t rec_cap) {
+    const float ob2 = __shfl_xor(best, 32);
+    const int oi = __shfl_xor(bidx, 32);
+    if (ob2 > best || (ob2 == best && oi < bidx)) {
+        best = ob2;
+        bidx = oi;
+    }
+    if (h == 0 && live) {
+        const int P = q.P;
+        int act = bidx == 0x7fffffff ? 0 : q.action_of_row(bidx);  // no valid action: 0 (:188-189)
+        if (eps > 0.0) {
+            const U4 d = draw(env_key(seed, env_base + e), t, kSlotPolicy);
+            if (u32(d.v[0]) <= eps) {  // np.random.rand() <= epsilon (:191)
+                // random.choice(valid_actions) (:192): the k-th valid action, ascending
+                const int nsel = __popcll(v.sel);
+                int k = uniform_int(d.v[1], (uint32_t)(4 + nsel + v.cst + v.fst));
+                if (k < 4) {
+                    act = k;
+                } else if ((k -= 4) < nsel) {  // the k-th port of sel, ascending
+                    uint64_t b = v.sel;
+                    for (; k > 0; --k) b &= b - 1;
+                    act = 4 + __builtin_ctzll(b);
+                } else {
+                    k -= nsel;
+                    act = k < v.cst ? 5 + P + k : 55 + P + (k - v.cst);  // amounts k + 1 (action space)
+                }
+            }
+        }
+        actions[e] = act;
+        if (rec_pos) {  // replay_begin_kernel's record, from the state already in registers
+            int64_t slot = rec_head + e;
+            slot -= slot >= rec_cap ? rec_cap : 0;
+            rec_pos[slot] = x8 | y8 << 8 | o8 << 16 | d8 << 24;
+            rec_fuel[slot] = ff;
+            rec_act[slot] = act;
+        }
+    }
+}
+
 __global__ __launch_bounds__(kPolicyBlock)
 #if SHIPENV_POLICY_WAVES_PER_EU
 __attribute__((amdgpu_waves_per_eu(SHIPENV_POLICY_WAVES_PER_EU)))
@@ -463,6 +580,210 @@ void policy_kernel(PolicyArgs A) {
     }
 }
 
+// ------------------------------------------------------------------ the f32 policy step
+// The fp32-faithful form of the same step (se_policy_f32): DQNNetwork evaluated in f32 as
+// agents/dqn.py:198-200 runs it (fp32 weights, fp32 activations), on
+// v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulation; gfx950 has no xf32). Its
+// result D has the bf16 instruction's 32 x 32 layout (env on the lane, rows
+// (reg & 3) + 8 (reg >> 2) + 4h in 16 registers), so a layer's accumulator register s is
+// directly the next layer's B operand of k-step s, with the weights' columns permuted to
+// match (fragment element (tile, kt, s, lane) = W[tile*32 + (lane & 31)][kt*32 + acc_row(s)]).
+// One 32-env tile per wave: fc1 (6 live inputs, 3 k-steps of 2), fc2 (64 k-steps per row
+// tile), fc3 over the compact rows, then the bf16 kernel's masked first maximum and
+// epsilon-greedy (the helpers above). 512-thread workgroups (2 waves per SIMD: h1, h2 and
+// an accumulator in f32 need ~160 registers), one per CU with the image in LDS; fc3's
+// fragments are read from global memory (L2) when the layout does not fit beside it (the
+// full layout of q_out).
+struct QnetF32Dims {
+    QnetDims q;  // fc3's row layout (full or compact)
+    __host__ __device__ int w1() const { return 0; }                  // 4 x 3 x 64 f32 (3 KB)
+    __host__ __device__ int w2() const { return 4096; }               // [mt][kt][s/4][lane][s%4]: 64 KB
+    __host__ __device__ int b1() const { return w2() + 65536; }       // 128 f32, port block folded
+    __host__ __device__ int b2() const { return b1() + 4 * kQHidden; }
+    __host__ __device__ int b3() const { return b2() + 4 * kQHidden; }  // mt3 * 32 f32
+    __host__ __device__ int same() const { return b3() + q.mt3 * 128; }
+    __host__ __device__ int regm() const { return same() + 8 * q.P; }
+    __host__ __device__ int w3() const { return (regm() + 4 * q.mt3 + 15) & ~15; }  // mt3 x 16 KB, last
+    __host__ __device__ int bytes() const { return w3() + q.mt3 * 16384; }
+};
+
+struct PackF32Args {
+    const float *w1, *b1, *w2, *b2, *w3, *b3;
+    const uint32_t* world;
+    WorldDims dims;
+    QnetF32Dims d;
+    uint8_t* img;
+};
+
+__global__ __launch_bounds__(256) void qnet_pack_f32_kernel(PackF32Args A) {
+    const QnetF32Dims d = A.d;
+    const QnetDims q = d.q;
+    uint8_t* const img = A.img;
+    const int in1 = q.in1();
+    const int n_w1 = 4 * 3 * 64, n_w2 = 4 * 4 * 16 * 64, n_w3 = q.mt3 * 4 * 16 * 64;
+    const int total = n_w1 + n_w2 + n_w3 + 2 * kQHidden + q.mt3 * 32 + q.P + q.mt3;
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        if (t < n_w1) {  // fc1: (mt, s, lane) = W1[mt*32 + r][2s + h] over the 6 dynamic columns
+            const int lane = t & 63, st = t >> 6, s = st % 3, mt = st / 3;
+            const int col = 2 * s + (lane >> 5);  // x, y, fuel, "cargo" = fuel (:206), origin, dest
+            reinterpret_cast<float*>(img + d.w1())[t] = A.w1[(mt * 32 + (lane & 31)) * in1 + col];
+            continue;
+        }
+        if (t < n_w1 + n_w2 + n_w3) {  // fc2 / fc3: float index ((mt*4 + kt)*4 + s4)*256 + lane*4 + i
+            const bool second = t < n_w1 + n_w2;
+            const int u = t - (second ? n_w1 : n_w1 + n_w2);
+            const int i = u & 3, lane = (u >> 2) & 63, s4 = (u >> 8) & 3, kt = (u >> 10) & 3, mt = u >> 12;
+            const int s = 4 * s4 + i, h = lane >> 5;
+            const int col = kt * 32 + (s & 3) + 8 * (s >> 2) + 4 * h;  // the previous layer's acc row
+            const int row = mt * 32 + (lane & 31);
+            float v;
+            if (second) {
+                v = A.w2[row * kQHidden + col];
+            } else {
+                v = row < q.rows ? A.w3[q.action_of_row(row) * kQHidden + col] : 0.0f;
+            }
+            reinterpret_cast<float*>(img + (second ? d.w2() : d.w3()))[u] = v;
+            continue;
+        }
+        int u = t - (n_w1 + n_w2 + n_w3);
+        const LdsWorld wv = world_view(A.dims, A.world);  // the device image, read in place
+        const int P = q.P;
+        if (u < kQHidden) {  // b1 + fc1 over the constant port block, in f64 then f32 (as qnet_pack_kernel)
+            double acc = (double)A.b1[u];
+            for (int p = 0; p < P; ++p) {
+                const float* w = A.w1 + u * in1 + 6 + 4 * p;
+                acc += (double)w[0] * (double)wv.px(p) + (double)w[1] * (double)wv.py(p) +
+                       (double)w[2] * (double)wv.pfuel(p) + (double)w[3] * (double)wv.pcargo(p);
+            }
+            reinterpret_cast<float*>(img + d.b1())[u] = (float)acc;
+        } else if ((u -= kQHidden) < kQHidden) {
+            reinterpret_cast<float*>(img + d.b2())[u] = A.b2[u];
+        } else if ((u -= kQHidden) < q.mt3 * 32) {
+            reinterpret_cast<float*>(img + d.b3())[u] = u < q.rows ? A.b3[q.action_of_row(u)] : 0.0f;
+        } else if ((u -= q.mt3 * 32) < P) {  // bit p: port p stands on port u's cell (u included)
+            uint64_t same = 0;
+            for (int p = 0; p < P; ++p)
+                if (wv.pos[p] == wv.pos[u]) same |= 1ull << p;
+            reinterpret_cast<uint64_t*>(img + d.same())[u] = same;
+        } else {  // fc3 tile mt's epilogue registers, as qnet_pack_kernel
+            const int mt = u - P, base = mt * 32;
+            int cmax = 0, fmax = 0;
+            for (int p = 0; p < P; ++p) {
+                cmax = max(cmax, min(wv.pcargo(p), 49));
+                fmax = max(fmax, min(wv.pfuel(p), 199));
+            }
+            const int c_lo = 5 + P, c_hi = 4 + P + cmax, f_lo = 55 + P, f_hi = 54 + P + fmax;
+            uint32_t rm = 0;
+            for (int reg = 0; reg < 16; ++reg)
+                for (int h = 0; h < 2; ++h) {
+                    const int row = base + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                    const int a = q.action_of_row(row);
+                    const bool ok = row < q.rows && (a < 4 + P || (a >= c_lo && a <= c_hi) || (a >= f_lo && a <= f_hi));
+                    rm |= (uint32_t)ok << reg;
+                }
+            reinterpret_cast<uint32_t*>(img + d.regm())[mt] = rm;
+        }
+    }
+}
+
+constexpr int kPolicyF32Block = 512;
+constexpr int kPolicyF32Waves = kPolicyF32Block / 64;
+
+struct PolicyF32Args {
+    PolicyArgs p;  // qimg: the f32 image
+    QnetF32Dims d;
+};
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void relu16(f32x16& c) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) c[r] = fmaxf(c[r], 0.0f);
+}
+
+// acc + W x H for one 32-row tile over K = 128: W the tile's [kt][s4][lane] float4 fragments
+__device__ __forceinline__ f32x16 gemm128(const float4* W, const f32x16 (&H)[4], f32x16 c, int lane) {
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+            const float4 a = W[(kt * 4 + s4) * 64 + lane];
+            c = mfma32(a.x, H[kt][4 * s4 + 0], c);
+            c = mfma32(a.y, H[kt][4 * s4 + 1], c);
+            c = mfma32(a.z, H[kt][4 * s4 + 2], c);
+            c = mfma32(a.w, H[kt][4 * s4 + 3], c);
+        }
+    return c;
+}
+
+template <bool kW3Global>
+__global__ __launch_bounds__(kPolicyF32Block) void policy_f32_kernel(PolicyF32Args F) {
+    extern __shared__ uint4 smem[];
+    const PolicyArgs& A = F.p;
+    const QnetF32Dims D = F.d;
+    const QnetDims q = D.q;
+    const int staged = (kW3Global ? D.w3() : D.bytes()) / 16;
+    for (int i = threadIdx.x; i < staged; i += kPolicyF32Block) smem[i] = A.qimg[i];
+    const LdsWorld w = stage_world(A.world, A.dims, reinterpret_cast<uint32_t*>(smem + staged));
+    const uint8_t* qb = reinterpret_cast<const uint8_t*>(smem);
+    const float* W1 = reinterpret_cast<const float*>(qb + D.w1());
+    const float4* W2 = reinterpret_cast<const float4*>(qb + D.w2());
+    const float4* W3 = reinterpret_cast<const float4*>(
+        (kW3Global ? reinterpret_cast<const uint8_t*>(A.qimg) : qb) + D.w3());
+    const float* B1 = reinterpret_cast<const float*>(qb + D.b1());
+    const float* B2 = reinterpret_cast<const float*>(qb + D.b2());
+    const float* B3 = reinterpret_cast<const float*>(qb + D.b3());
+    const uint64_t* SAME = reinterpret_cast<const uint64_t*>(qb + D.same());
+    const uint32_t* REGM = reinterpret_cast<const uint32_t*>(qb + D.regm());
+
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+    const int P = q.P;
+    const int64_t tiles = (A.n + 31) >> 5;
+    const int64_t stride = (int64_t)gridDim.x * kPolicyF32Waves;
+    for (int64_t tile = (int64_t)blockIdx.x * kPolicyF32Waves + (threadIdx.x >> 6); tile < tiles; tile += stride) {
+        const int64_t e = tile * 32 + r;
+        const bool live = e < A.n;
+        const int64_t ei = live ? e : A.n - 1;
+        const double fuel = A.st.fuel[ei];
+        const uint32_t x8 = A.st.x[ei], y8 = A.st.y[ei], o8 = A.st.origin[ei], d8 = A.st.dest[ei];
+        const int origin = o8 == SE_NONE ? -1 : (int)o8, dest = d8 == SE_NONE ? -1 : (int)d8;
+        // the preprocess_state row as torch's FloatTensor holds it: fuel rounded to f32
+        const float ff = (float)fuel;
+        const float in0 = h ? (float)y8 : (float)x8, in2 = h ? (float)dest : (float)origin;
+        f32x16 h1[4], h2[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {  // fc1 over x, y | fuel, fuel | origin, dest, + relu
+            f32x16 c = bias_frag(B1 + mt * 32 + 4 * h);
+            c = mfma32(W1[(mt * 3 + 0) * 64 + lane], in0, c);
+            c = mfma32(W1[(mt * 3 + 1) * 64 + lane], ff, c);
+            c = mfma32(W1[(mt * 3 + 2) * 64 + lane], in2, c);
+            relu16(c);
+            h1[mt] = c;
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {  // fc2 + relu
+            h2[mt] = gemm128(W2 + mt * 16 * 64, h1, bias_frag(B2 + mt * 32 + 4 * h), lane);
+            relu16(h2[mt]);
+        }
+        const EnvValid v = env_valid(w, q, SAME, (int)x8, (int)y8, origin);
+        float best = -INFINITY;
+        int bidx = 0x7fffffff;
+#pragma nounroll
+        for (int mt = 0; mt < q.mt3; ++mt) {  // fc3 + the masked first-maximum argmax
+            const int base = mt * 32;
+            if (!A.q_out && !__any(tile_maybe(v, mt, P))) continue;
+            const uint32_t m = tile_mask(v, mt, P);
+            const uint32_t rm = __builtin_amdgcn_readfirstlane(REGM[mt]);
+            const f32x16 c = gemm128(W3 + mt * 16 * 64, h2, bias_frag(B3 + mt * 32 + 4 * h), lane);
+            tile_argmax(c, m, rm, base, h, best, bidx);
+            if (A.q_out && live) tile_q_out(A.q_out, A.ldq, q.rows, c, e, base, h);
+        }
+        FINISH_ENV(v, e, live, h, best, bidx, x8, y8, o8, d8, ff);
+    }
+}
+
 }  // namespace
 
 struct se_qnet {
@@ -475,6 +796,8 @@ struct se_qnet {
     int img_bytes = 0;
     uint64_t world_version = 0;
     bool packed = false;
+    uint8_t* d_img32 = nullptr;  // se_policy_f32's image, repacked from w[] at every call
+    int img32_bytes = 0;
 };
 
 extern "C" {
@@ -594,6 +917,70 @@ int se_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, float* 
     return launch_policy(qn, actions, epsilon, t, q_out, ldq, nullptr, stream);
 }
 
+int se_policy_f32(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, float* q_out, int64_t ldq,
+                  void* stream) {
+    if (!qn) return fail(SE_EINVAL, "null qnet");
+    se_env* env = qn->env;
+    int rc = check_ready(env);
+    if (rc) return rc;
+    if (!qn->packed) return fail(SE_ESTATE, "se_qnet_set_weights has not been called");
+    if (qn->world_version != env->world_version)
+        return fail(SE_ESTATE, "ports changed since se_qnet_set_weights (the port block is folded into fc1)");
+    if (!actions) return fail(SE_EINVAL, "null actions");
+    if (q_out && ldq < qn->q.A) return fail(SE_EINVAL, "ldq < number of actions");
+    if (!(epsilon >= 0.0)) return fail(SE_EINVAL, "epsilon must be >= 0");
+    if (env->n == 0) return SE_OK;
+    DeviceGuard g(env->device);
+    QnetF32Dims d;
+    d.q = q_out ? qn->q : qn->qc;  // the compact rows unless every row's Q is wanted
+    if (d.bytes() > qn->img32_bytes) {
+        if (qn->d_img32) HIP_TRY(hipFree(qn->d_img32));
+        qn->d_img32 = nullptr;
+        HIP_TRY(hipMalloc(&qn->d_img32, (size_t)d.bytes()));
+        qn->img32_bytes = d.bytes();
+    }
+    const hipStream_t s = (hipStream_t)stream;
+    // the image from the current weights (in place updates by an optimizer or T2 included)
+    PackF32Args pk{qn->w[0], qn->w[1], qn->w[2], qn->w[3], qn->w[4], qn->w[5], env->d_world, env->dims, d,
+                   qn->d_img32};
+    qnet_pack_f32_kernel<<<128, 256, 0, s>>>(pk);
+    HIP_TRY(hipGetLastError());
+    const size_t world = lds_bytes(env);
+    const bool w3_global = (size_t)d.bytes() + world > 160 * 1024;
+    const size_t lds = (size_t)(w3_global ? d.w3() : d.bytes()) + world;
+    if (lds > 160 * 1024) return fail(SE_EINVAL, "f32 network + world image exceed the 160 KB LDS");
+    static std::atomic<uint64_t> lds_set0{0}, lds_set1{0};
+    rc = allow_dynamic_lds(lds_set0, reinterpret_cast<const void*>(policy_f32_kernel<false>), 160 * 1024, env->device);
+    if (!rc) rc = allow_dynamic_lds(lds_set1, reinterpret_cast<const void*>(policy_f32_kernel<true>), 160 * 1024, env->device);
+    if (rc) return rc;
+    int dev_cus = 256;
+    if (hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, env->device) != hipSuccess)
+        dev_cus = 256;
+    const int64_t tiles = (env->n + 31) / 32;
+    const int64_t want = (tiles + kPolicyF32Waves - 1) / kPolicyF32Waves;
+    const int grid = (int)(want < dev_cus ? want : dev_cus);
+    PolicyF32Args F{};
+    F.d = d;
+    PolicyArgs& A = F.p;
+    A.world = env->d_world;
+    A.dims = env->dims;
+    A.qimg = reinterpret_cast<const uint4*>(qn->d_img32);
+    A.q = d.q;
+    A.n = env->n;
+    A.env_base = env->env_base;
+    A.seed = env->seed;
+    A.t = t;
+    A.eps = epsilon;
+    A.st = env->st;
+    A.actions = actions;
+    A.q_out = q_out;
+    A.ldq = ldq;
+    if (w3_global) policy_f32_kernel<true><<<grid, kPolicyF32Block, lds, s>>>(F);
+    else policy_f32_kernel<false><<<grid, kPolicyF32Block, lds, s>>>(F);
+    HIP_TRY(hipGetLastError());
+    return SE_OK;
+}
+
 int se_qnet_repack(se_qnet* qn, int32_t* bump, void* stream) {
     if (!qn) return fail(SE_EINVAL, "null qnet");
     if (!qn->packed) return fail(SE_ESTATE, "se_qnet_set_weights has not been called");
@@ -611,10 +998,11 @@ int se_qnet_repack(se_qnet* qn, int32_t* bump, void* stream) {
 
 int se_qnet_destroy(se_qnet* qn) {
     if (!qn) return SE_OK;
-    if (qn->d_img) {  // does not touch the env, which may be gone already
+    if (qn->d_img || qn->d_img32) {  // does not touch the env, which may be gone already
         DeviceGuard g(qn->device);
         (void)hipDeviceSynchronize();
-        (void)hipFree(qn->d_img);
+        if (qn->d_img) (void)hipFree(qn->d_img);
+        if (qn->d_img32) (void)hipFree(qn->d_img32);
     }
     delete qn;
     return SE_OK;

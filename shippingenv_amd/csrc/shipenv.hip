@@ -1652,8 +1652,11 @@ __device__ __forceinline__ void wave_compact(const StepArgs& A, const Finished& 
 // step_tail_kernel, so this loop carries no guarded scalar path. The world image's
 // loads, then the first group's, are all in flight before the LDS writes; each
 // iteration loads the next group after storing the current one.
+#ifndef SHIPENV_STEP_WPE
+#define SHIPENV_STEP_WPE 4  // minimum waves per SIMD the register allocation must allow
+#endif
 template <bool kTyped, bool kReplay, bool kAuto, bool kNt = false, bool kRec = false>
-__global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4))) void step_kernel(StepArgs A) {
+__global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(SHIPENV_STEP_WPE))) void step_kernel(StepArgs A) {
     static_assert(!kRec || (kAuto && !kTyped && !kReplay), "se_step_record: agent actions, auto-reset");
     extern __shared__ uint32_t lds[];
     const int64_t full = A.n >> 2;

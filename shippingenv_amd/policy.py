@@ -6,6 +6,8 @@ in torch. ``QPolicy`` packs its weights for the fused kernel (bf16 MFMA, f32
 accumulation), which computes for every env of a VecEnv the observation row,
 Q = DQNNetwork(obs), the first maximum over the valid actions and epsilon-greedy
 exploration (choose_action, :177-203) in one launch, without writing Q to HBM.
+``act(precision="f32")`` runs the same step with the network in fp32 (f32 MFMA), the
+precision the reference's agent evaluates it in.
 """
 from __future__ import annotations
 
@@ -76,12 +78,19 @@ class QPolicy:
         replay._act = self.actions
         return self.actions
 
-    def act(self, epsilon: float = 0.0, t: int = 0, q_out: torch.Tensor | None = None):
+    def act(self, epsilon: float = 0.0, t: int = 0, q_out: torch.Tensor | None = None,
+            precision: str = "bf16"):
         """int32 actions [n] in the agent-index encoding (VecEnv.step input).
-        q_out: optional f32 [n, >= A] to receive the Q rows (testing / inspection)."""
+        q_out: optional f32 [n, >= A] to receive the Q rows (testing / inspection).
+        precision: "bf16" (se_policy: bf16 weights and activations on bf16 MFMA, f32
+        accumulation) or "f32" (se_policy_f32: the network in fp32 as agents/dqn.py runs
+        it, on f32 MFMA; about 6x the time)."""
+        if precision not in ("bf16", "f32"):
+            raise ValueError("precision must be 'bf16' or 'f32'")
+        fn = N.lib().se_policy if precision == "bf16" else N.lib().se_policy_f32
         ldq = 0 if q_out is None else q_out.stride(0)
-        N.check(N.lib().se_policy(self._h, _ptr(self.actions), float(epsilon), int(t) & 0xFFFFFFFF,
-                                  None if q_out is None else _ptr(q_out), ldq, self.env._stream()))
+        N.check(fn(self._h, _ptr(self.actions), float(epsilon), int(t) & 0xFFFFFFFF,
+                   None if q_out is None else _ptr(q_out), ldq, self.env._stream()))
         return self.actions
 
     def close(self):
