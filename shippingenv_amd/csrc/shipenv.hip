@@ -47,6 +47,12 @@
 #ifndef SHIPENV_PREFETCH
 #define SHIPENV_PREFETCH 0  // 1 = load the next group before computing this one (step kernel)
 #endif
+#ifndef SHIPENV_EARLY_DRAWS
+#define SHIPENV_EARLY_DRAWS 1  // 0 = FUEL / GATE drawn where used, not ahead of the staging wait (experiment)
+#endif
+#ifndef SHIPENV_STAGE_ORDER
+#define SHIPENV_STAGE_ORDER 0  // 1 = write the world image to LDS before issuing the group's loads (experiment)
+#endif
 #ifndef SHIPENV_ABLATE
 #define SHIPENV_ABLATE 0  // 0 = the product; 1 = timing-only memory-traffic build, 2 = also no staging (tools/build_ablation.sh, tools/ablate_libs.sh)
 #endif
@@ -212,13 +218,17 @@ __device__ __forceinline__ Staged stage_issue(const uint32_t* __restrict__ g) {
     return st;
 }
 
-__device__ __forceinline__ LdsWorld stage_finish(const uint32_t* __restrict__ g, WorldDims d,
-                                                 uint32_t* lds, const Staged& st) {
+__device__ __forceinline__ void stage_write(const uint32_t* __restrict__ g, WorldDims d, uint32_t* lds,
+                                            const Staged& st) {
     uint4* l4 = reinterpret_cast<uint4*>(lds);
 #pragma unroll
     for (int k = 0; k < kStageRows; ++k) l4[threadIdx.x + kStepBlock * k] = st.r[k];
     for (int i = (int)threadIdx.x + kStepBlock * kStageRows; i < (d.total() + 3) / 4; i += kStepBlock)
         l4[i] = reinterpret_cast<const uint4*>(g)[i];  // larger maps / port tables: the remainder
+}
+__device__ __forceinline__ LdsWorld stage_finish(const uint32_t* __restrict__ g, WorldDims d,
+                                                 uint32_t* lds, const Staged& st) {
+    stage_write(g, d, lds, st);
     __syncthreads();
     return world_view(d, lds);
 }
@@ -1288,7 +1298,8 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
     }
     TRACE_STAMP(5);
     (void)gate_needed;  // drawn early (early_draws) whether or not an env needs it
-    const U4 fb = D.fuel, gb = D.gate;
+    const U4 fb = SHIPENV_EARLY_DRAWS ? D.fuel : draw(qk, t, kSlotFuel);
+    const U4 gb = SHIPENV_EARLY_DRAWS ? D.gate : draw(qk, t, kSlotGate);
     uint32_t fire = 0, arrive = 0, fin = 0, dead = 0;
     double f[4], r[4];
     // kReplay: the group's tape records (the partial last group's missing envs read none)
@@ -1669,6 +1680,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(SHIP
     const Staged st = stage_issue(A.world);
     // the image's loads first: the staging writes then wait for them alone
     __builtin_amdgcn_sched_barrier(0);
+#if SHIPENV_STAGE_ORDER == 1  // experiment: the image in LDS before the group's loads are issued
+    stage_write(A.world, A.dims, lds, st);
+    __builtin_amdgcn_sched_barrier(0);
+#endif
 #endif
     // first group: an unconditional load (lanes past the end re-read the last full
     // group; the host launches this kernel only when there is one), so the staging
@@ -1682,7 +1697,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(SHIP
     __builtin_amdgcn_sched_barrier(0);
     // agent-index actions: the production step, or its replay-tape form (parity)
     constexpr bool kAgent = !kTyped && !SHIPENV_ABLATE;
-    constexpr bool kDraws = kAgent && !kReplay;
+    constexpr bool kDraws = kAgent && !kReplay && SHIPENV_EARLY_DRAWS;
     Draws D{};
     if constexpr (kDraws) {
         D = early_draws<spec_loss<kAuto>()>(A, (first + threadIdx.x) * 4);
@@ -1691,6 +1706,9 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(SHIP
     }
 #if SHIPENV_ABLATE >= 2
     const LdsWorld w = world_view(A.dims, A.world);
+#elif SHIPENV_STAGE_ORDER == 1
+    __syncthreads();
+    const LdsWorld w = world_view(A.dims, lds);
 #else
     const LdsWorld w = stage_finish(A.world, A.dims, lds, st);
 #endif
