@@ -108,13 +108,14 @@ def make_actions(env, steps):
 
 def timed_loop(env, acts, first, steps, dist, reduce_every=0, counter=None):
     """K back-to-back launches bracketed by barrier + synchronize on both sides; wall
-    time is the max over ranks. HIP events on the launch stream give the GPU time per
-    launch (roofline.kernel_ms): from the end of launch 1 to the end of launch K, over
-    K - 1 launches, so the launch duration does not include the ~20 us the first launch
-    waits to start on an idle queue ("The short run"). The time from
-    before launch 1 over all K launches is returned as well."""
+    time is the max over ranks. Two HIP events on the launch stream give the GPU time per
+    launch (roofline.kernel_ms): one after launch 1, one after launch K, over K - 1 launches,
+    so the launch duration does not include the ~20 us launch 1 waits to start on an idle
+    queue ("The short run"). No event precedes launch 1: an event
+    record costs host time ahead of it and a bubble between kernels on the GPU
+    (tools/diag/timed_loop_forms.py: 0.15 us per step over the driver's 20 steps)."""
     stream = torch.cuda.current_stream(env.device)
-    e0, ef, e1 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    ef, e1 = (torch.cuda.Event(enable_timing=True) for _ in range(2))
     stats = torch.zeros(3, dtype=torch.float64, device=env.device)
     # the step's action rows as views made before the clock starts: indexing the
     # [steps, n] table inside the loop is harness work (1.4 us of host time per step,
@@ -123,7 +124,6 @@ def timed_loop(env, acts, first, steps, dist, reduce_every=0, counter=None):
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    e0.record(stream)
     for k in range(steps):
         env.step(rows[k])
         if k == 0:
@@ -138,8 +138,8 @@ def timed_loop(env, acts, first, steps, dist, reduce_every=0, counter=None):
     torch.cuda.synchronize()
     dist.barrier()
     wall = dist.max(time.perf_counter() - t0)
-    incl = e0.elapsed_time(e1) / steps
-    return wall, (ef.elapsed_time(e1) / (steps - 1) if steps > 1 else incl), incl
+    k_ms = ef.elapsed_time(e1) / (steps - 1) if steps > 1 else wall * 1e3 / steps
+    return wall, k_ms
 
 
 def run_config(n, ports, auto, args, dist, label, preroll=0):
@@ -169,8 +169,7 @@ def run_config(n, ports, auto, args, dist, label, preroll=0):
         env.clear_stats()
     every = max(1, min(100, args.steps // 2)) if auto else 0
     count = [0]
-    wall, k_ms, k_incl = timed_loop(env, acts, args.warmup, args.steps, dist, reduce_every=every,
-                                    counter=count)
+    wall, k_ms = timed_loop(env, acts, args.warmup, args.steps, dist, reduce_every=every, counter=count)
     stats = None
     if auto:
         s = env.episode_stats().clone()
@@ -180,7 +179,7 @@ def run_config(n, ports, auto, args, dist, label, preroll=0):
     del acts
     torch.cuda.empty_cache()
     info = {"preroll_steps": preroll, "allreduce_every": every, "allreduces_in_timed_region": count[0]}
-    return wall, k_ms, stats, k_incl, info
+    return wall, k_ms, stats, info
 
 
 def run_config1(args):
@@ -481,19 +480,16 @@ def run_dqn_train(n, args, dist):
     return out
 
 
-KERNEL_MS_BASIS = "HIP events on the launch stream, end of launch 1 to end of launch K, over K - 1 launches"
+KERNEL_MS_BASIS = ("HIP events on the launch stream, end of launch 1 to end of launch K, over K - 1 launches "
+                   "(rocprofv3 kernel-trace averages of the same launches: profiles/r03/kt_legs.json)")
 
 
-def roofline(bytes_per_step, n, k_ms, canonical, k_incl=None):
+def roofline(bytes_per_step, n, k_ms, canonical):
     """The roofline object of one leg. achieved = this build's algorithmic bytes per
     env-step (42 / 58 B) x n / the per-launch kernel time; the
     survey's canonical field widths (66 / 82 B) are given as a byte count only: the
     kernel does not move them, so no rate is derived from them."""
     achieved = bytes_per_step * n / (k_ms * 1e-3) / 1e9
-    extra = {}
-    if k_incl is not None:  # HIP events from before launch 1: includes its idle-queue start
-        extra = {"kernel_ms_incl_start": round(k_incl, 5),
-                 "frac_incl_start": round(bytes_per_step * n / (k_incl * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
     return {
         "bound": "hbm",
         "achieved": round(achieved, 1),
@@ -505,7 +501,7 @@ def roofline(bytes_per_step, n, k_ms, canonical, k_incl=None):
         "canonical_bytes_per_env_step": canonical,
         "kernel_ms": round(k_ms, 5),
         "kernel_ms_basis": KERNEL_MS_BASIS,
-    } | extra
+    }
 
 
 def pmc_traffic(key="step_kernel_bytes_per_launch"):
@@ -584,7 +580,7 @@ def main():
     from shippingenv_amd.vec import random_water_ports
 
     n = args.n
-    el3, k3, _, k3i, _ = run_config(n, None, False, args, dist, "config3")
+    el3, k3, _, _ = run_config(n, None, False, args, dist, "config3")
     value = n * dist.world * args.steps / el3
     out = {
         "metric": "env-steps/sec at N=2^20 parallel envs per GPU (config 3: full step, 5 default ports)",
@@ -607,7 +603,7 @@ def main():
             "ports": 5,
             "parallelism": f"env-shard dp{dist.world} (no data-path collective)",
         },
-        "roofline": roofline(BYTES_STEP, n, k3, CANONICAL_STEP, k3i),
+        "roofline": roofline(BYTES_STEP, n, k3, CANONICAL_STEP),
     }
     traffic, src = pmc_traffic()
     if traffic:
@@ -616,8 +612,7 @@ def main():
 
     if not args.no_config4:
         ports64 = random_water_ports(builtin_water(), 64, seed=3)
-        el4, k4, stats, k4i, info4 = run_config(n, ports64, True, args, dist, "config4",
-                                                preroll=args.preroll4)
+        el4, k4, stats, info4 = run_config(n, ports64, True, args, dist, "config4", preroll=args.preroll4)
         t4, src4 = pmc_traffic("step_kernel_auto_bytes_per_launch")
         out["config4"] = {
             "workload": "BASELINE configs[3]: N=2^20 envs/GPU, 64 random ports, auto-reset, "
@@ -627,7 +622,7 @@ def main():
                         f"roofline.kernel_ms: {KERNEL_MS_BASIS}",
             "value": round(n * dist.world * args.steps / el4, 1),
             "ms_per_step": round(el4 / args.steps * 1e3, 5),
-            "roofline": roofline(BYTES_STEP_AUTO, n, k4, CANONICAL_STEP_AUTO, k4i),
+            "roofline": roofline(BYTES_STEP_AUTO, n, k4, CANONICAL_STEP_AUTO),
             "episodes": stats[1],
             "mean_return": stats[0] / stats[1] if stats and stats[1] else None,
             "mean_len": stats[2] / stats[1] if stats and stats[1] else None,
@@ -655,12 +650,12 @@ def main():
     if args.large_n and dist.world == 1:
         small = argparse.Namespace(**vars(args))
         small.steps, small.warmup = 100, 5
-        el, k, _, ki, _ = run_config(args.large_n, None, False, small, dist, "large-n")
+        el, k, _, _ = run_config(args.large_n, None, False, small, dist, "large-n")
         out["large_n"] = {
             "envs": args.large_n,
             "note": "working set beyond the 256 MiB Infinity Cache: traffic reaches HBM",
             "value": round(args.large_n * small.steps / el, 1),
-            "roofline": roofline(BYTES_STEP, args.large_n, k, CANONICAL_STEP, ki),
+            "roofline": roofline(BYTES_STEP, args.large_n, k, CANONICAL_STEP),
         }
 
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:

@@ -106,7 +106,10 @@ constexpr int kCellGround = 255;
 // kStepBlock x 4-dword rows of the world image the step kernel stages unguarded
 // (one 16-byte load per thread and row), at least 12 KB: the 100x100 image with up
 // to 130 ports
-constexpr int kStageRows = (3072 + 4 * kStepBlock - 1) / (4 * kStepBlock);
+#ifndef SHIPENV_STAGE_MIN_WORDS
+#define SHIPENV_STAGE_MIN_WORDS 3072  // the unguarded window (experiments: 1024 = one row)
+#endif
+constexpr int kStageRows = (SHIPENV_STAGE_MIN_WORDS + 4 * kStepBlock - 1) / (4 * kStepBlock);
 constexpr int kStageWords = kStageRows * 4 * kStepBlock;
 
 struct WorldDims {

@@ -14,17 +14,14 @@ def _bench():
 
 def test_roofline_object_has_the_contract_keys():
     b = _bench()
-    r = b.roofline(b.BYTES_STEP, 1 << 20, 0.0085, b.CANONICAL_STEP, 0.0090)
+    r = b.roofline(b.BYTES_STEP, 1 << 20, 0.0085, b.CANONICAL_STEP)
     for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
         assert k in r, k
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     # achieved = algorithmic bytes per launch / launch time; frac = achieved / peak
     assert abs(r["achieved"] - b.BYTES_STEP * (1 << 20) / 8.5e-6 / 1e9) < 0.1
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-4
-    # the start-inclusive figure is reported beside the per-launch one, never instead of it
-    assert r["kernel_ms"] == 0.0085 and r["kernel_ms_incl_start"] == 0.009
-    assert r["frac_incl_start"] < r["frac"]
-    assert "kernel_ms_incl_start" not in b.roofline(b.BYTES_STEP, 1 << 20, 0.0085, b.CANONICAL_STEP)
+    assert r["kernel_ms"] == 0.0085
 
 
 def test_no_roofline_rate_above_its_peak():
