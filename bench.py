@@ -53,6 +53,10 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-config4", action="store_true")
+    p.add_argument("--preroll3", type=int, default=1000,
+                   help="config 3 workload setup: untimed steps from reset to the steady state mix the "
+                        "survey's 1000-step definition measures; 0 = time from reset (the from-reset "
+                        "figure is reported beside it either way)")
     p.add_argument("--preroll4", type=int, default=1000,
                    help="config 4 workload setup: untimed steps from reset to the steady episode mix "
                         "(episodes of ~240 steps end in every step), before the warm-up")
@@ -106,32 +110,47 @@ def make_actions(env, steps):
     return acts
 
 
-def timed_loop(env, acts, first, steps, dist, reduce_every=0, counter=None):
+def timed_loop(env, acts, first, steps, dist, reduce_every=0, counter=None, step_seq=False):
     """K back-to-back launches bracketed by barrier + synchronize on both sides; wall
     time is the max over ranks. Two HIP events on the launch stream give the GPU time per
     launch (roofline.kernel_ms): one after launch 1, one after launch K, over K - 1 launches,
     so the launch duration does not include the ~20 us launch 1 waits to start on an idle
     queue ("The short run"). No event precedes launch 1: an event
     record costs host time ahead of it and a bubble between kernels on the GPU
-    (tools/diag/timed_loop_forms.py: 0.15 us per step over the driver's 20 steps)."""
+    (tools/diag/timed_loop_forms.py: 0.15 us per step over the driver's 20 steps).
+
+    One VecEnv.step call per step, the drop-in's per-step API; step_seq=True issues the
+    same launches with VecEnv.step_seq (se_step_seq: the launch loop in native code, split
+    only where an event or a stats all-reduce goes between two steps). Unprofiled the two
+    give the same GPU time per launch (tools/diag/issue_forms.py: the Python loop keeps the
+    queue ahead of an 8 us kernel); under a kernel tracer, whose per-launch host cost
+    leaves gaps between Python-issued kernels, step_seq keeps them back to back."""
     stream = torch.cuda.current_stream(env.device)
     ef, e1 = (torch.cuda.Event(enable_timing=True) for _ in range(2))
-    stats = torch.zeros(3, dtype=torch.float64, device=env.device)
     # the step's action rows as views made before the clock starts: indexing the
     # [steps, n] table inside the loop is harness work (1.4 us of host time per step,
     # tools/diag/host_step_cost.py), not the step's
-    rows = [acts[first + k] for k in range(steps)]
+    if not step_seq:
+        chunks = [acts[first + k] for k in range(steps)]
+    else:  # [first step], then runs that end where an all-reduce follows
+        cuts = sorted({0, 1, steps} | ({k for k in range(reduce_every, steps, reduce_every)}
+                                       if reduce_every else set()))
+        chunks = [acts[first + a:first + b] for a, b in zip(cuts, cuts[1:])]
+    step = env.step_seq if step_seq else env.step
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(steps):
-        env.step(rows[k])
-        if k == 0:
+    done = 0
+    for c in chunks:
+        step(c)
+        done += c.shape[0] if step_seq else 1
+        if done == 1:
             ef.record(stream)
-        if reduce_every and (k + 1) % reduce_every == 0:
-            # episode-return aggregation over the GPUs (RCCL all-reduce of 3 doubles)
-            stats.copy_(env.episode_stats())
-            dist.D.reduce_episode_stats(stats)
+        if reduce_every and done % reduce_every == 0:
+            # episode-return aggregation over the GPUs (RCCL all-reduce of 3 doubles), in
+            # place in the env's stats buffer: a torch copy_ of the 24 bytes first went
+            # through a blit whose host side stalled the queue ~40 us (kernel trace r03)
+            dist.D.reduce_episode_stats(env.episode_stats())
             if counter is not None:
                 counter[0] += 1
     e1.record(stream)
@@ -142,7 +161,7 @@ def timed_loop(env, acts, first, steps, dist, reduce_every=0, counter=None):
     return wall, k_ms
 
 
-def run_config(n, ports, auto, args, dist, label, preroll=0):
+def run_config(n, ports, auto, args, dist, label, preroll=0, step_seq=False):
     """One leg: reset, `preroll` untimed steps of workload setup (actions generated one row
     at a time), W warm-up steps, then the K timed steps from rows resident in HBM.
     Auto-reset legs all-reduce the episode statistics (RCCL) every min(100, K // 2) steps
@@ -169,7 +188,8 @@ def run_config(n, ports, auto, args, dist, label, preroll=0):
         env.clear_stats()
     every = max(1, min(100, args.steps // 2)) if auto else 0
     count = [0]
-    wall, k_ms = timed_loop(env, acts, args.warmup, args.steps, dist, reduce_every=every, counter=count)
+    wall, k_ms = timed_loop(env, acts, args.warmup, args.steps, dist, reduce_every=every, counter=count,
+                            step_seq=step_seq)
     stats = None
     if auto:
         s = env.episode_stats().clone()
@@ -514,6 +534,25 @@ def pmc_traffic(key="step_kernel_bytes_per_launch"):
     return d.get(key), os.path.relpath(path, ROOT)
 
 
+TRACE_SUMMARY = os.path.join("profiles", "r03", "kt_legs_driver.json")
+
+
+def rocprof_leg(key):
+    """The committed kernel-trace average of one leg under the driver's bench command
+    (tools/trace_driver.sh -> tools/kt_legs.py), printed beside the live events figure.
+    The tracer's per-dispatch cost lengthens each 2^20-env launch by ~0.8 us (the same
+    launches unprofiled, tools/diag/issue_forms.py); at 2^24 the two
+    agree."""
+    path = os.path.join(ROOT, TRACE_SUMMARY)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        leg = json.load(f).get(key)
+    if not leg:
+        return None
+    return {"avg_us": leg["avg_us_timed"], "frac": leg["frac_from_trace"], "source": TRACE_SUMMARY}
+
+
 def cpu_threads():
     """Host threads for the threaded CPU leg: the job's CPU share (OMP_NUM_THREADS is
     16 on the GPU box, whose nproc counts the whole machine), else the affinity set."""
@@ -580,8 +619,14 @@ def main():
     from shippingenv_amd.vec import random_water_ports
 
     n = args.n
-    el3, k3, _, _ = run_config(n, None, False, args, dist, "config3")
+    # config 3 from reset first (ships at their origin ports, cargo rising: the first steps'
+    # state mix; DESIGN.md section 5, "The short run"), then the headline leg in steady
+    # state, then the headline leg issued through VecEnv.step_seq
+    el3r, k3r, _, _ = run_config(n, None, False, args, dist, "config3-from-reset", preroll=0)
+    el3, k3, _, info3 = run_config(n, None, False, args, dist, "config3", preroll=args.preroll3)
     value = n * dist.world * args.steps / el3
+    el3s, k3s, _, _ = run_config(n, None, False, args, dist, "config3-step-seq", preroll=args.preroll3,
+                                 step_seq=True)
     out = {
         "metric": "env-steps/sec at N=2^20 parallel envs per GPU (config 3: full step, 5 default ports)",
         "value": round(value, 1),
@@ -596,15 +641,31 @@ def main():
         "dtype": "f64+int (fuel/reward f64, positions/cargo int)",
         "data": "synthetic (Philox agent actions resident in HBM; reference map and ports)",
         "config": {
-            "workload": "BASELINE configs[2]: N=2^20 envs/GPU, full step, default 5 ports, from reset; "
+            "workload": "BASELINE configs[2]: N=2^20 envs/GPU, full step, default 5 ports; steady state "
+                        f"mix as in the survey's 1000-step run: {args.preroll3} untimed pre-roll steps from "
+                        "reset before the warm-up (from_reset: the same leg timed right after reset); "
+                        "one VecEnv.step call per step (step_seq: the same leg issued by "
+                        "VecEnv.step_seq, the native launch loop); "
                         f"roofline.kernel_ms: {KERNEL_MS_BASIS}",
+            "preroll_steps": args.preroll3,
             "envs_per_gpu": n,
             "global_envs": n * dist.world,
             "ports": 5,
             "parallelism": f"env-shard dp{dist.world} (no data-path collective)",
         },
         "roofline": roofline(BYTES_STEP, n, k3, CANONICAL_STEP),
+        "from_reset": {"value": round(n * dist.world * args.steps / el3r, 1),
+                       "ms_per_step": round(el3r / args.steps * 1e3, 5),
+                       "kernel_ms": round(k3r, 5),
+                       "frac": roofline(BYTES_STEP, n, k3r, CANONICAL_STEP)["frac"]},
+        "step_seq": {"value": round(n * dist.world * args.steps / el3s, 1),
+                     "ms_per_step": round(el3s / args.steps * 1e3, 5),
+                     "kernel_ms": round(k3s, 5),
+                     "frac": roofline(BYTES_STEP, n, k3s, CANONICAL_STEP)["frac"]},
     }
+    for key, obj in (("config3", out["roofline"]), ("config3_from_reset", out["from_reset"]),
+                     ("config3_step_seq", out["step_seq"])):
+        obj["rocprof_trace"] = rocprof_leg(key)
     traffic, src = pmc_traffic()
     if traffic:
         out["roofline"]["traffic"] = traffic
@@ -627,6 +688,7 @@ def main():
             "mean_return": stats[0] / stats[1] if stats and stats[1] else None,
             "mean_len": stats[2] / stats[1] if stats and stats[1] else None,
         } | info4
+        out["config4"]["roofline"]["rocprof_trace"] = rocprof_leg("config4")
         if t4:
             out["config4"]["roofline"]["traffic"] = t4
             out["config4"]["roofline"]["traffic_source"] = src4
@@ -655,7 +717,8 @@ def main():
             "envs": args.large_n,
             "note": "working set beyond the 256 MiB Infinity Cache: traffic reaches HBM",
             "value": round(args.large_n * small.steps / el, 1),
-            "roofline": roofline(BYTES_STEP, args.large_n, k, CANONICAL_STEP),
+            "roofline": roofline(BYTES_STEP, args.large_n, k, CANONICAL_STEP)
+            | {"rocprof_trace": rocprof_leg("large_n")},
         }
 
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:

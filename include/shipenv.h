@@ -143,6 +143,14 @@ int se_reset_to(se_env* env, const uint8_t* mask, const int32_t* origin, const i
  * (step counter, slot); the step counter advances by one per call. */
 int se_step(se_env* env, const int32_t* actions, void* stream);
 
+/* `steps` consecutive se_step calls issued from native code: step k takes its actions
+ * from actions + k * ld (ld >= n int32 entries, 16-byte aligned rows). The same
+ * launches as a host loop over se_step, without the caller's per-step overhead, so a
+ * fixed action schedule keeps the GPU queue full (a rollout of a pre-computed policy,
+ * the bench's timed region). reward/done/err hold the last step's outputs. An
+ * extension: the reference steps one call at a time (environment.py:359-376). */
+int se_step_seq(se_env* env, const int32_t* actions, int64_t ld, int32_t steps, void* stream);
+
 /* step() with the reference's typed action [ActionType, value] (environment.py:359-376):
  * type 1..4 (shipping/type.py:1-5); MOVE value = (a, b) any integers; others value = a. */
 int se_step_typed(se_env* env, const int32_t* type, const int32_t* a, const int32_t* b,

@@ -2726,6 +2726,18 @@ int se_step(se_env* env, const int32_t* actions, void* stream) {
     return launch_step(env, false, false, actions, nullptr, nullptr, nullptr, stream);
 }
 
+int se_step_seq(se_env* env, const int32_t* actions, int64_t ld, int32_t steps, void* stream) {
+    int rc = check_ready(env);
+    if (rc) return rc;
+    if (steps < 0) return fail(SE_EINVAL, "negative step count");
+    if (steps > 1 && (ld < env->n || (ld & 3))) return fail(SE_EINVAL, "row stride must be >= n and a multiple of 4");
+    for (int32_t k = 0; k < steps; ++k) {
+        rc = launch_step(env, false, false, actions + (int64_t)k * ld, nullptr, nullptr, nullptr, stream);
+        if (rc) return rc;
+    }
+    return SE_OK;
+}
+
 int se_step_typed(se_env* env, const int32_t* type, const int32_t* a, const int32_t* b,
                   void* stream) {
     return launch_step(env, true, false, type, a, b, nullptr, stream);

@@ -126,6 +126,7 @@ class VecEnv:
             self.done, self.err, self.ep_return, self.ep_len, self.done_recs, self.done_count)] + [None])
         N.check(lib.se_bind(self._h, C.byref(self._state)))
         self._se_step = lib.se_step
+        self._se_step_seq = lib.se_step_seq
         self._dev_index = self.device.index
         self._stats = torch.zeros(3, dtype=torch.float64, **kw)
 
@@ -190,6 +191,21 @@ class VecEnv:
                 and a.data_ptr() % 16 == 0):
             a = self._dev(actions, torch.int32)
         rc = self._se_step(self._h, a.data_ptr(), _raw_stream(self._dev_index))
+        if rc:
+            N.check(rc)
+        self._keep = a
+        return self.reward, self.done, self.err
+
+    def step_seq(self, actions):
+        """len(actions) consecutive step() calls issued from native code (se_step_seq):
+        actions is an int32 device tensor [K, n] (rows contiguous, 16-byte aligned), row k
+        the actions of step k. Returns the last step's (reward, done, err)."""
+        a = actions
+        if not (type(a) is torch.Tensor and a.dtype is torch.int32 and a.is_cuda and a.dim() == 2
+                and a.get_device() == self._dev_index and a.shape[1] == self.n and a.stride(1) == 1
+                and a.data_ptr() % 16 == 0 and (a.shape[0] < 2 or a.stride(0) % 4 == 0)):
+            raise ValueError("step_seq needs an int32 [K, n] device tensor with 16-byte aligned rows")
+        rc = self._se_step_seq(self._h, a.data_ptr(), a.stride(0), a.shape[0], _raw_stream(self._dev_index))
         if rc:
             N.check(rc)
         self._keep = a

@@ -597,3 +597,40 @@ def test_graph_captured_steps_equal_eager(auto):
         assert torch.equal(getattr(a, f), getattr(b, f)), f
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("auto,n", [(False, 50003), (True, 50003), (False, 1 << 16)])
+def test_step_seq_equals_step_calls(auto, n):
+    """se_step_seq (bench.py's timed issue path: K launches from native code, rows at a
+    padded stride) leaves every field bit-identical to K VecEnv.step calls."""
+    from shippingenv_amd.vec import random_water_ports
+
+    from conftest import golden_water
+
+    K = 24
+    ports = random_water_ports(golden_water(), 64, seed=3) if auto else None
+    a = VecEnv(n, seed=22, ports=ports, auto_reset=auto)
+    b = VecEnv(n, seed=22, ports=ports, auto_reset=auto)
+    ld = (n + 3) & ~3
+    buf = torch.zeros((K, ld), dtype=torch.int32, device=a.device)
+    for t in range(K):
+        a.gen_actions(t, out=buf[t, :n])
+    acts = buf[:, :n]
+    a.reset()
+    b.reset()
+    for t in range(K):
+        a.step(acts[t].contiguous())
+    b.step_seq(acts[:7])
+    b.step_seq(acts[7:])
+    torch.cuda.synchronize()
+    fa, fb = get_state(a), get_state(b)
+    for f in FIELDS:
+        np.testing.assert_array_equal(fa[f], fb[f], err_msg=f)
+    for f in ("reward", "done", "err", "ep_return", "ep_len"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    if auto:
+        assert torch.equal(a.episode_stats(), b.episode_stats())
+    with pytest.raises(ValueError):
+        b.step_seq(acts[0])  # one row, not [K, n]
+    a.close()
+    b.close()

@@ -4,13 +4,16 @@
 
 bench.py runs its legs in a fixed order, so the step launches of each leg are the
 next dispatches of that leg's kernel instantiation in the trace:
-  config 3   step_kernel<false, false, false, true, false>  (kNt loads, N = 2^20): the first W + K
+  config 3   step_kernel<false, false, false, true, false>  (kNt loads, N = 2^20): the from-reset
+             leg's W + K launches, then the headline leg's P3 pre-roll steps (--preroll3,
+             bench.py's default 1000) and its W + K, then the step_seq leg's P3 + W + K
   config 4   step_kernel<false, false, true, false, false>  (auto-reset): launches P + W .. P + W + K
              after its P pre-roll steps (--preroll4, bench.py's default 1000)
   large_n    step_kernel<false, false, false, false, false> (N = 2^24): the last 105
 For each leg this prints the average kernel duration (end - start of the dispatch, as
 rocprofv3 records it) over the K timed launches, over the timed launches after the
-first, and the per-launch list; with --bench, the bench line's own kernel_ms and frac
+first, the per-launch list, the idle gaps between consecutive timed launches and
+(end of launch K - end of launch 1) / (K - 1), the span bench.py's events measure; with --bench, the bench line's own kernel_ms and frac
 beside the figure recomputed from the trace (42 / 58 B per env-step over 8 TB/s).
 """
 from __future__ import annotations
@@ -37,15 +40,22 @@ def load(path):
 
 
 def leg(rows, tag, first, count, timed, from_end=False):
-    d = [(e - s) / 1e3 for s, e, n in rows if tag in n]
-    seq = d[-count:] if from_end else d[first:first + count]
+    se = [(s, e) for s, e, n in rows if tag in n]
+    seq = se[-count:] if from_end else se[first:first + count]
     t = seq[-timed:]
     if not t:
         return None
-    return {"launches_in_trace": len(d), "timed": len(t),
-            "avg_us_timed": round(sum(t) / len(t), 3),
-            "avg_us_timed_after_first": round(sum(t[1:]) / max(1, len(t) - 1), 3),
-            "first_timed_us": round(t[0], 3), "per_launch_us": [round(x, 3) for x in t]}
+    d = [(e - s) / 1e3 for s, e in t]
+    gaps = [(t[i + 1][0] - t[i][1]) / 1e3 for i in range(len(t) - 1)]
+    out = {"launches_in_trace": len(se), "timed": len(t),
+           "avg_us_timed": round(sum(d) / len(d), 3),
+           "avg_us_timed_after_first": round(sum(d[1:]) / max(1, len(d) - 1), 3),
+           "first_timed_us": round(d[0], 3), "per_launch_us": [round(x, 3) for x in d]}
+    if gaps:  # idle time between consecutive timed launches, and the events basis's span
+        out["avg_gap_us"] = round(sum(gaps) / len(gaps), 3)
+        out["max_gap_us"] = round(max(gaps), 3)
+        out["end1_to_endK_us_per_launch"] = round((t[-1][1] - t[0][1]) / 1e3 / len(gaps), 3)
+    return out
 
 
 def main():
@@ -55,15 +65,18 @@ def main():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--n", type=int, default=1 << 20)
+    p.add_argument("--preroll3", type=int, default=1000)
     p.add_argument("--preroll4", type=int, default=1000)
     a = p.parse_args()
     rows = load(a.trace)
     K, W = a.steps, a.warmup
     out = {"trace": a.trace,
-           "config3": leg(rows, C3, 0, W + K, K),
+           "config3_from_reset": leg(rows, C3, 0, W + K, K),
+           "config3": leg(rows, C3, W + K + a.preroll3, W + K, K),
+           "config3_step_seq": leg(rows, C3, 2 * (W + K) + 2 * a.preroll3, W + K, K),
            "config4": leg(rows, C4, a.preroll4, W + K, K),
            "large_n": leg(rows, BIG, 0, 105, 100, from_end=True)}
-    for key, b in (("config3", 42), ("config4", 58)):
+    for key, b in (("config3", 42), ("config3_from_reset", 42), ("config3_step_seq", 42), ("config4", 58)):
         if out[key]:
             us = out[key]["avg_us_timed"]
             out[key]["frac_from_trace"] = round(b * a.n / (us * 1e-6) / 1e9 / PEAK, 4)
