@@ -345,6 +345,15 @@ int se_qtrain_step_policy(se_qtrain* q, se_qnet* qn, int64_t batch, const float*
                           const float* next_obs, const int64_t* act, const float* rew,
                           const float* done, const float* weight, float gamma, float lr, float beta1,
                           float beta2, float eps, int32_t* step_dev, float* loss_out, void* stream);
+/* se_replay_sample then se_qtrain_step_policy (qn nullable: se_qtrain_step) in two launches
+ * instead of three: the first kernel draws its own minibatch rows from r's ring, the very
+ * transitions se_replay_sample(r, batch, t_dev = ctr) picks, without writing the batch
+ * buffers. ctr: device int32[2], both entries = the updates taken so far; the sampler key is
+ * ctr[0], the first kernel sets ctr[1] = ctr[0] + 1 (the bias-correction count) and the
+ * second copies it back into ctr[0]. Same bits as the sampler plus the step with
+ * step_dev = ctr (then advanced); r must record the same env as q and not be mid-record. */
+int se_qtrain_step_replay(se_qtrain* q, se_qnet* qn, se_replay* r, int64_t batch, float gamma, float lr,
+                          float beta1, float beta2, float eps, int32_t* ctr, float* loss_out, void* stream);
 /* Data-parallel update (one learner per GPU, the same parameters on every rank): se_qtrain_step
  * split at the exchange. se_qtrain_grad writes this rank's gradient sums (before the division
  * by sum w) and {sum w (q - y)^2, sum w} into grad, a device f32 vector of

@@ -37,7 +37,7 @@ EXPORTS = (
     "se_qnet_destroy", "se_replay_create", "se_replay_begin", "se_replay_end", "se_replay_end_reset", "se_step_record",
     "se_replay_size",
     "se_replay_sample", "se_replay_destroy", "se_qtrain_create", "se_qtrain_bind", "se_qtrain_pack",
-    "se_qtrain_step", "se_qtrain_step_policy", "se_qtrain_grad_size", "se_qtrain_grad", "se_qtrain_apply",
+    "se_qtrain_step", "se_qtrain_step_policy", "se_qtrain_step_replay", "se_qtrain_grad_size", "se_qtrain_grad", "se_qtrain_apply",
     "se_qtrain_destroy",
     "se_episode_stats", "se_clear_stats", "se_done_layout", "se_done_list", "se_done_compact",
     "se_get_counters", "se_set_counters",
@@ -107,6 +107,7 @@ def _declare(lib):
         "se_qtrain_pack": [P, C.c_int32, P],
         "se_qtrain_step": [P, i64, P, P, P, P, P, P] + [C.c_float] * 5 + [P, P, P],
         "se_qtrain_step_policy": [P, P, i64, P, P, P, P, P, P] + [C.c_float] * 5 + [P, P, P],
+        "se_qtrain_step_replay": [P, P, P, i64] + [C.c_float] * 5 + [P, P, P],
         "se_qtrain_grad_size": [P],
         "se_qtrain_grad": [P, i64, P, P, P, P, P, P, C.c_float, P, P],
         "se_qtrain_apply": [P, P, P] + [C.c_float] * 4 + [P, P, P],

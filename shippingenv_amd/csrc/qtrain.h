@@ -211,6 +211,12 @@ struct QtStepArgs {
     const float *rew, *done, *weight;
     float gamma;
     int32_t* bump;  // se_qtrain_step_policy: the update counter, advanced once here (T2 reads it after)
+    // se_qtrain_step_replay: the minibatch drawn here from the ring (the sampler's picks, key
+    // t = ctr[0]) instead of read from obs ... weight; block 0 sets ctr[1] = t + 1 (T2's count)
+    int32_t from_ring;  // 0: the minibatch buffers above
+    Ring ring;
+    uint64_t seed;
+    int32_t* ctr;
 };
 
 #ifndef SHIPENV_QTRACE
@@ -259,6 +265,8 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     float* LW = G + 32;             // [32] w_j d_j^2
     float* WT = LW + 32;            // [32] w_j
     int* ACT = reinterpret_cast<int*>(WT + 32);
+    float* RW = WT + 64;            // [32] r_j
+    float* DN = RW + 32;            // [32] done_j
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wt = wave & 3;
     const bool tgt = wave >= 4;
     const int64_t r0 = (int64_t)blockIdx.x * kQT;
@@ -276,21 +284,49 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     fa.load(A.W.pw2[net] + wt * 64 * 64, lane);
     f32x16 acc1 = bias_init(A.W.c1[net], wt, lane, 128);
 
-    for (int e = tid; e < 2 * 8 * 32; e += kQTBlock) {
-        const int which = e >> 8, c = (e >> 5) & 7, j = e & 31;
-        const int64_t row = r0 + j;
-        float v = 0.0f;
-        if (c < 6 && row < A.B) v = (which ? A.next_obs : A.obs)[row * in + c];
-        (which ? XN : X)[c * kLS + j] = v;
-    }
-    if (tid < 32) {
-        // an action outside [0, A) (the reference's gather would raise) takes no part in the
-        // update (weight 0), and its W3 row gather reads row 0 instead of past the matrix
-        const int64_t row = r0 + tid;
-        const int64_t a = row < A.B ? A.act[row] : -1;
-        const bool live = a >= 0 && a < A.d.A;
-        ACT[tid] = live ? (int)a : 0;
-        WT[tid] = live ? A.weight[row] : 0.0f;
+    if (A.from_ring) {  // the sampler's pick of row r0 + tid, straight into the tiles
+        if (tid < 32) {
+            const Ring& ring = A.ring;
+            const int64_t size = *ring.d_size;
+            const uint32_t t = (uint32_t)A.ctr[0];
+            const U4 key = draw(env_key(A.seed, kReplayKeyId), t, kSlotReplay);
+            const int64_t row = r0 + tid;
+            Pick pk{-1, 0u, 0u, 0.0f, 0.0f, 0.0f, 0, 0};
+            if (row < A.B) pk = pick_transition(ring, size, key, feistel_half((uint32_t)size), row, A.B);
+            const bool ok = pk.slot >= 0;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                X[c * kLS + tid] = c < 6 && ok ? ship_col(pk.sp, pk.sf, c) : 0.0f;
+                XN[c * kLS + tid] = c < 6 && ok ? ship_col(pk.np, pk.nf, c) : 0.0f;
+            }
+            // as the sampler's act / weight rows read below: act = ok ? a : 0, weight = ok
+            const int64_t a = row < A.B ? (ok ? (int64_t)pk.ac : 0) : -1;
+            const bool live = a >= 0 && a < A.d.A;
+            ACT[tid] = live ? (int)a : 0;
+            WT[tid] = live && ok ? 1.0f : 0.0f;
+            RW[tid] = ok ? pk.rw : 0.0f;
+            DN[tid] = ok && (pk.fl & kRecDone) ? 1.0f : 0.0f;
+            if (blockIdx.x == 0 && tid == 0) A.ctr[1] = (int32_t)(t + 1u);  // T2's Adam count
+        }
+    } else {
+        for (int e = tid; e < 2 * 8 * 32; e += kQTBlock) {
+            const int which = e >> 8, c = (e >> 5) & 7, j = e & 31;
+            const int64_t row = r0 + j;
+            float v = 0.0f;
+            if (c < 6 && row < A.B) v = (which ? A.next_obs : A.obs)[row * in + c];
+            (which ? XN : X)[c * kLS + j] = v;
+        }
+        if (tid < 32) {
+            // an action outside [0, A) (the reference's gather would raise) takes no part in the
+            // update (weight 0), and its W3 row gather reads row 0 instead of past the matrix
+            const int64_t row = r0 + tid;
+            const int64_t a = row < A.B ? A.act[row] : -1;
+            const bool live = a >= 0 && a < A.d.A;
+            ACT[tid] = live ? (int)a : 0;
+            WT[tid] = live ? A.weight[row] : 0.0f;
+            RW[tid] = row < A.B ? A.rew[row] : 0.0f;
+            DN[tid] = row < A.B ? A.done[row] : 0.0f;
+        }
     }
     __syncthreads(); QSTAMP(1);
 
@@ -372,7 +408,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         const int64_t row = r0 + tid;
         float mx = QM[tid];
         for (int w = 1; w < 8; ++w) mx = fmaxf(mx, QM[w * 32 + tid]);
-        Y[tid] = row < A.B ? A.rew[row] + (A.gamma * mx) * (1.0f - A.done[row]) : 0.0f;
+        Y[tid] = row < A.B ? RW[tid] + (A.gamma * mx) * (1.0f - DN[tid]) : 0.0f;
     }
     __syncthreads(); QSTAMP(5);
 
@@ -520,6 +556,7 @@ struct QtAdamArgs {
     // from grad (summed over the ranks in between) instead of the partials
     int32_t mode;
     float* grad;  // [grad_floats(d)], layout of the Grad offsets below
+    int32_t* ctr_sync;  // se_qtrain_step_replay: block 0 sets *ctr_sync = *step_dev (ctr[0] = ctr[1])
 };
 
 // The data-parallel gradient: the sums T2 forms before dividing by sum(w), in a flat f32
@@ -661,6 +698,8 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
     const int tid = threadIdx.x, in = A.d.in;
     QSTAMP(10);  // T2's stamps: slots 10-13 of the same rows (4 waves)
     const AdamStep adam(A);
+    // every block has read the count; ctr[0] is read by the next update's T1 only
+    if (A.ctr_sync && blockIdx.x == 0 && tid == 0) *A.ctr_sync = *A.step_dev;
     // sum(w): this thread's share loads now, and the workgroup reduces it after its own
     // sum (inv is first needed by the Adam step), so the two round trips overlap
     const int mode = A.mode;  // block-uniform
@@ -1017,37 +1056,41 @@ int qtrain_check_qnet(se_qtrain* q, se_qnet* qn) {
 
 QtAdamArgs adam_args(se_qtrain* q, se_qnet* qn, int64_t batch, const int64_t* act, float lr, float beta1,
                      float beta2, float eps, const int32_t* step_dev, float* loss_out, int32_t bumped,
-                     int32_t mode, float* grad) {
+                     int32_t mode, float* grad, int32_t* ctr_sync = nullptr) {
     const int64_t tiles = (batch + kQT - 1) / kQT;
     return QtAdamArgs{q->W, q->on, q->m, q->v, q->d, batch, tiles, act, lr, beta1, beta2, eps, step_dev, loss_out,
                       {qn ? qn->d_img : nullptr, qn ? qn->d_img + qn->c_off : nullptr},
-                      {qn ? qn->q : QnetDims{}, qn ? qn->qc : QnetDims{}}, bumped, mode, grad};
+                      {qn ? qn->q : QnetDims{}, qn ? qn->qc : QnetDims{}}, bumped, mode, grad, ctr_sync};
 }
 
 // T1, then T2 in mode 0 (grad null: sums + Adam) or mode 1 (the sums into grad)
+// ring: T1 draws the minibatch itself (se_qtrain_step_replay; step_dev = ctr, two counters)
 int qtrain_step(se_qtrain* q, se_qnet* qn, int64_t batch, const float* obs, const float* next_obs,
                 const int64_t* act, const float* rew, const float* done, const float* weight, float gamma,
                 float lr, float beta1, float beta2, float eps, int32_t* step_dev, float* loss_out,
-                void* stream, float* grad = nullptr) {
+                void* stream, float* grad = nullptr, const se_replay* ring = nullptr) {
     if (int rc0 = qtrain_check_bound(q)) return rc0;
     if (batch < 1 || batch > q->max_batch) return fail(SE_EINVAL, "batch must be in [1, max_batch]");
-    if (!obs || !next_obs || !act || !rew || !done || !weight || (!grad && (!step_dev || !loss_out)))
-        return fail(SE_EINVAL, "null batch / counter / loss pointer");
+    if (!ring && (!obs || !next_obs || !act || !rew || !done || !weight))
+        return fail(SE_EINVAL, "null batch pointer");
+    if (!grad && (!step_dev || !loss_out)) return fail(SE_EINVAL, "null counter / loss pointer");
     int rc = qtrain_check_qnet(q, qn);
     if (rc) return rc;
     DeviceGuard g(q->device);
     const hipStream_t s = (hipStream_t)stream;
     const int64_t tiles = (batch + kQT - 1) / kQT;
-    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 5 * 32) * 4;
+    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 7 * 32) * 4;
     static std::atomic<uint64_t> lds_set{0};
     rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(qtrain_tile_kernel), (int)lds, q->device);
     if (rc) return rc;
     QtStepArgs A{q->W, q->on, q->tg, q->d, batch, obs, next_obs, act, rew, done, weight, gamma,
-                 qn ? step_dev : nullptr};
+                 qn && !ring ? step_dev : nullptr, ring ? 1 : 0, ring ? ring->ring : Ring{},
+                 ring ? ring->env->seed : 0, ring ? step_dev : nullptr};
     qtrain_tile_kernel<<<(unsigned)tiles, kQTBlock, lds, s>>>(A);
     HIP_TRY(hipGetLastError());
-    const QtAdamArgs B = adam_args(q, qn, batch, act, lr, beta1, beta2, eps, step_dev, loss_out, qn ? 1 : 0,
-                                   grad ? 1 : 0, grad);
+    // T2 counts Adam steps from ctr[1] (set by T1) when T1 drew the batch, and syncs ctr[0]
+    const QtAdamArgs B = adam_args(q, qn, batch, act, lr, beta1, beta2, eps, ring ? step_dev + 1 : step_dev,
+                                   loss_out, qn || ring ? 1 : 0, grad ? 1 : 0, grad, ring ? step_dev : nullptr);
     qtrain_adam_kernel<<<384 + 65 * q->d.mt3, kQRBlock, 0, s>>>(B);
     HIP_TRY(hipGetLastError());
     return SE_OK;
@@ -1070,6 +1113,15 @@ int se_qtrain_step_policy(se_qtrain* q, se_qnet* qn, int64_t batch, const float*
     if (!qn) return fail(SE_EINVAL, "null qnet");
     return qtrain_step(q, qn, batch, obs, next_obs, act, rew, done, weight, gamma, lr, beta1, beta2, eps,
                        step_dev, loss_out, stream);
+}
+
+int se_qtrain_step_replay(se_qtrain* q, se_qnet* qn, se_replay* r, int64_t batch, float gamma, float lr,
+                          float beta1, float beta2, float eps, int32_t* ctr, float* loss_out, void* stream) {
+    if (!r) return fail(SE_EINVAL, "null replay");
+    if (!q || r->env != q->env) return fail(SE_EINVAL, "the replay and the qtrain belong to different envs");
+    if (r->open) return fail(SE_ESTATE, "se_replay_begin without se_replay_end");
+    return qtrain_step(q, qn, batch, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, gamma, lr, beta1, beta2,
+                       eps, ctr, loss_out, stream, nullptr, r);
 }
 
 int64_t se_qtrain_grad_size(const se_qtrain* q) { return q ? Grad::size(q->d) : 0; }

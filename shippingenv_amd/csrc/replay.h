@@ -237,6 +237,41 @@ __device__ __forceinline__ float ship_col(uint32_t pos, float fuel, int c) {
 }
 
 
+// Minibatch slot j's transition (update()'s random.sample, agents/dqn.py:213-214): the
+// keyed permutation's entry j, else j + B, j + 2B, ... while the one found is flagged
+// (a raised step), up to kReplayTries; slot -1 when none is found. Shared by the sampler
+// and the update kernel that draws its own rows (se_qtrain_step_replay), so both pick
+// the same transitions bit for bit.
+struct Pick {
+    int64_t slot;
+    uint32_t sp, np;
+    float sf, nf, rw;
+    int32_t ac;
+    uint8_t fl;
+};
+
+__device__ __forceinline__ Pick pick_transition(const Ring& ring, int64_t size, const U4& key, uint32_t h,
+                                                int64_t j, int64_t B) {
+    Pick p{-1, 0u, 0u, 0.0f, 0.0f, 0.0f, 0, 0};
+    for (int k = 0; k < kReplayTries; ++k) {
+        const int64_t pos = j + (int64_t)k * B;
+        if (pos >= size) break;
+        const uint32_t l = feistel_perm((uint32_t)pos, (uint32_t)size, h, key.v);
+        p.fl = ring.flags[l];
+        p.sp = ring.s_pos[l];
+        p.sf = ring.s_fuel[l];
+        p.np = ring.n_pos[l];
+        p.nf = ring.n_fuel[l];
+        p.ac = ring.act[l];
+        p.rw = ring.rew[l];
+        if (!(p.fl & kRecInvalid)) {
+            p.slot = l;
+            break;
+        }
+    }
+    return p;
+}
+
 // kSampleRows transitions per workgroup. The first wave picks the slots, loading each
 // candidate's flags and its transition together (a flagged one is then dropped), and
 // writes its row's six ship columns; all threads then write the constant port block from
@@ -263,36 +298,18 @@ __global__ __launch_bounds__(kBlock) void replay_sample_kernel(SampleBatchArgs A
         const uint32_t h = feistel_half((uint32_t)size);
         const int64_t j = r0 + threadIdx.x;
         int64_t slot = -1;
-        uint32_t sp = 0, np = 0;
-        float sf = 0.0f, nf = 0.0f, rw = 0.0f;
-        int32_t ac = 0;
-        uint8_t fl = 0;
         if (j < A.B) {
-            for (int k = 0; k < kReplayTries; ++k) {
-                const int64_t pos = j + (int64_t)k * A.B;
-                if (pos >= size) break;
-                const uint32_t l = feistel_perm((uint32_t)pos, (uint32_t)size, h, key.v);
-                fl = A.ring.flags[l];
-                sp = A.ring.s_pos[l];
-                sf = A.ring.s_fuel[l];
-                np = A.ring.n_pos[l];
-                nf = A.ring.n_fuel[l];
-                ac = A.ring.act[l];
-                rw = A.ring.rew[l];
-                if (!(fl & kRecInvalid)) {
-                    slot = l;
-                    break;
-                }
-            }
+            const Pick pk = pick_transition(A.ring, size, key, h, j, A.B);
+            slot = pk.slot;
             const bool ok = slot >= 0;
-            A.act[j] = ok ? (int64_t)ac : 0;
-            A.rew[j] = ok ? rw : 0.0f;
-            A.done[j] = ok && (fl & kRecDone) ? 1.0f : 0.0f;
+            A.act[j] = ok ? (int64_t)pk.ac : 0;
+            A.rew[j] = ok ? pk.rw : 0.0f;
+            A.done[j] = ok && (pk.fl & kRecDone) ? 1.0f : 0.0f;
             A.weight[j] = ok ? 1.0f : 0.0f;
 #pragma unroll
             for (int c = 0; c < 6; ++c) {
-                A.obs[j * width + c] = ok ? ship_col(sp, sf, c) : 0.0f;
-                A.next_obs[j * width + c] = ok ? ship_col(np, nf, c) : 0.0f;
+                A.obs[j * width + c] = ok ? ship_col(pk.sp, pk.sf, c) : 0.0f;
+                A.next_obs[j * width + c] = ok ? ship_col(pk.np, pk.nf, c) : 0.0f;
             }
         }
         slot_of[threadIdx.x] = slot;

@@ -8,14 +8,17 @@ One ``VecDQNAgent.step()`` is one iteration of the reference's training loop
   ``se_replay_end``, which append to the device replay ring (include/shipenv.h).
 * the loop's episode breaks: a step that raised (:304-309) or ``max_steps``
   (:281). ``se_replay_end`` marks these envs and ``se_reset`` restarts them.
-* update() (:206-245): ``se_replay_sample`` draws the minibatch. ``se_qtrain_step``
-  (FusedUpdate, csrc/qtrain.h) computes the MSE to r + gamma * max target Q * (1 - done),
-  the backward pass and Adam in two f32 MFMA kernels. Then comes the epsilon decay.
-  ``fused=False`` runs the same update with torch autograd and torch.optim.Adam.
+* update() (:206-245): ``se_qtrain_step_replay`` (FusedUpdate, csrc/qtrain.h) draws the
+  minibatch from the ring (the transitions ``se_replay_sample`` would pick), computes the
+  MSE to r + gamma * max target Q * (1 - done), the backward pass and Adam in two f32 MFMA
+  kernels, and rewrites the policy's bf16 weights. Then comes the epsilon decay.
+  ``fused=False`` runs the same update with torch autograd and torch.optim.Adam on the
+  minibatch ``se_replay_sample`` writes.
 
-After ``graph_warmup`` eager updates, the update is captured in one HIP graph. The
-graph holds the sampler, the update kernels, the repacking of the policy's bf16
-weights and the update counter's increment, so each later update is one graph launch.
+The fused update is two launches, issued eagerly: a HIP graph replay of them measured
+5-6 us slower per update (the graph launch's own gap; tools/diag/update_forms.py). The
+torch path (about 50 small kernels) is captured in one HIP graph after ``graph_warmup``
+eager updates; ``graph=True`` / ``False`` forces either form on either path.
 
 Differences from the single-env reference, by construction:
 * The batch holds distinct transitions, like random.sample; see se_replay_sample.
@@ -185,6 +188,18 @@ class FusedUpdate:
                                               float(gamma), self.lr, self.betas[0], self.betas[1], self.eps,
                                               _ptr(step_dev), _ptr(loss_out), self.env._stream()))
 
+    def step_replay(self, memory, batch: int, gamma: float, ctr: torch.Tensor, loss_out: torch.Tensor,
+                    policy=None):
+        """memory.sample(t_dev=ctr) then step_policy(..., step_dev=ctr) (step() without a
+        policy), in two launches (se_qtrain_step_replay): the first draws its minibatch rows
+        from the ring itself. ctr: device int32 [2], both entries the updates taken so far."""
+        if ctr.dtype != torch.int32 or ctr.numel() < 2 or not ctr.is_contiguous():
+            raise ValueError("ctr must be a contiguous int32 device tensor of 2 entries")
+        N.check(N.lib().se_qtrain_step_replay(self._h, None if policy is None else policy._h, memory._h,
+                                              int(batch), float(gamma), self.lr, self.betas[0],
+                                              self.betas[1], self.eps, _ptr(ctr), _ptr(loss_out),
+                                              self.env._stream()))
+
     # ---- data parallel (one learner per GPU): the update split at the gradient exchange
     def grad_size(self) -> int:
         """Floats in the gradient vector of grad() / apply() (layout: grad_layout)."""
@@ -256,7 +271,7 @@ class VecDQNAgent:
                  epsilon_decay: float = DQN_EPSILON_DECAY, memory_size: int | None = None,
                  batch_size: int = DQN_BATCH_SIZE, target_update_every: int = 1000,
                  hidden_size: int = HIDDEN, max_steps: int = MAX_STEPS_PER_EPISODE,
-                 updates_per_step: int = 1, graph: bool = True, graph_warmup: int = 3,
+                 updates_per_step: int = 1, graph: bool | None = None, graph_warmup: int = 3,
                  fused: bool = True, model: DQNNetwork | None = None,
                  data_parallel: bool = False, process_group=None):
         if not env.auto_reset:
@@ -289,8 +304,11 @@ class VecDQNAgent:
         self.cut = torch.zeros(env.n, dtype=torch.uint8, device=dev)
         self.t = 0         # vector steps taken (policy exploration counter)
         self.updates = 0   # update() calls that trained
-        self._ctr = torch.zeros(1, dtype=torch.int32, device=dev)  # sampler key, = updates
-        self.use_graph, self.graph_warmup = bool(graph), int(graph_warmup)
+        # updates taken so far, twice: [0] the sampler key, [1] the fused update's Adam count
+        # (se_qtrain_step_replay advances [1], then copies it into [0])
+        self._ctr = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.use_graph = (not self.fused) if graph is None else bool(graph)
+        self.graph_warmup = int(graph_warmup)
         self._graph = None
         self._loss = torch.zeros((), dtype=torch.float32, device=dev)
         # data parallel (opt-in): every rank steps its own envs into its own ring; the update
@@ -360,11 +378,13 @@ class VecDQNAgent:
         allreduce_gradient(self._grad, self.group)
 
     def _update_body(self):
-        self.memory.sample(self.batch, t_dev=self._ctr)
         if self.fused:  # _ctr = Adam steps taken so far
-            # the update, the policy's new images and the counter's advance: two launches
-            self.trainer.step_policy(self.batch, self.gamma, self._ctr, self._loss, self.policy)
+            # the minibatch draw, the update, the policy's new images and the counter's
+            # advance: two launches (the batch buffers are not written)
+            self.trainer.step_replay(self.memory, self.batch_size, self.gamma, self._ctr, self._loss,
+                                     self.policy)
             return
+        self.memory.sample(self.batch, t_dev=self._ctr)
         loss = dqn_loss(self.model, self.target_model, self.batch, self.gamma)
         self.optimizer.zero_grad(set_to_none=False)
         loss.backward()
@@ -372,6 +392,7 @@ class VecDQNAgent:
         self._loss.copy_(loss.detach())
         # the next choose_action sees the new weights; the update counter advances in the same launch
         self.policy.repack(bump=self._ctr)
+        self._ctr[1:].copy_(self._ctr[:1])
 
     def _capture_one(self, body):
         g = torch.cuda.CUDAGraph()

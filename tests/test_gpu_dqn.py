@@ -245,10 +245,11 @@ def test_fused_update_matches_reference_update(n, ports64, batch):
         m0 = [t.clone() for t in tr.exp_avg]
         v0 = [t.clone() for t in tr.exp_avg_sq]
         loss = agent.step()
+        agent.memory.sample(agent.batch, t=k)  # the minibatch the fused update drew (key k)
         assert loss is not None and agent.batch.weight.min().item() == 1.0
         ref = _Ref64(before, target, agent.batch, agent.gamma, agent.learning_rate, k, m0, v0)
         ref.check(loss, list(agent.model.parameters()), tr.exp_avg, tr.exp_avg_sq, what=f"fused step {k}")
-    assert int(agent._ctr.item()) == 5
+    assert int(agent._ctr[0].item()) == 5
 
 
 def test_torch_update_matches_reference_update():
@@ -323,7 +324,7 @@ def test_training_loop_bookkeeping():
     assert np.isfinite(loss.item())
     assert agent.updates == 12 and agent.memory.size == 30000
     assert agent.epsilon == pytest.approx(0.995 ** 12)
-    assert int(agent._ctr.item()) == 12
+    assert int(agent._ctr[0].item()) == 12
     # the policy acts with the trained weights: greedy actions = argmax of the new Q
     q = torch.empty((env.n, env.action_space_size), dtype=torch.float32, device=env.device)
     agent.policy.act(0.0, 99, q_out=q)
@@ -378,9 +379,9 @@ def test_fused_launches_equal_the_unfused_loop():
         assert torch.equal(agents[0].cut, agents[1].cut), k
         for f in ("x", "y", "fuel", "cargo", "origin", "dest", "ep_len", "ep_return", "done", "err"):
             assert torch.equal(getattr(envs[0], f), getattr(envs[1], f)), (k, f)
-        assert int(agents[0]._ctr.item()) == int(agents[1]._ctr.item()), k
+        assert int(agents[0]._ctr[0].item()) == int(agents[1]._ctr[0].item()), k
     assert agents[0].memory.size == agents[1].memory.size
-    assert int(agents[0]._ctr.item()) > 0 and int(agents[0].cut.sum()) >= 0
+    assert int(agents[0]._ctr[0].item()) > 0 and int(agents[0].cut.sum()) >= 0
     for p, q in zip(agents[0].model.parameters(), agents[1].model.parameters()):
         assert torch.equal(p, q)
     qs, acts = [], []
@@ -464,17 +465,63 @@ def test_update_with_policy_refuses_a_foreign_qnet():
         agent.step()
     other = QPolicy(env, DQNNetwork(env.obs_size, env.action_space_size))
     _OPEN.append(other)
+    agent.memory.sample(agent.batch, t=7)
     before = [p.detach().clone() for p in agent.model.parameters()]
-    ctr = int(agent._ctr.item())
+    ctr = int(agent._ctr[0].item())
     with pytest.raises(N.ShipEnvError, match="not packed from the online parameters"):
         agent.trainer.step_policy(agent.batch, agent.gamma, agent._ctr, agent._loss, other)
     torch.cuda.synchronize()
-    assert int(agent._ctr.item()) == ctr  # refused before any launch
+    assert int(agent._ctr[0].item()) == ctr  # refused before any launch
     for p, q in zip(agent.model.parameters(), before):
         assert torch.equal(p, q)
     agent.trainer.step_policy(agent.batch, agent.gamma, agent._ctr, agent._loss, agent.policy)
     torch.cuda.synchronize()
-    assert int(agent._ctr.item()) == ctr + 1
+    assert int(agent._ctr[0].item()) == ctr + 1
+
+
+@pytest.mark.parametrize("n,batch,with_policy", [(4096, 512, True), (4099, 300, False)])
+def test_update_drawing_its_own_batch_equals_sampler_then_step(n, batch, with_policy):
+    """se_qtrain_step_replay (the first kernel draws its minibatch rows from the ring) against
+    se_replay_sample + se_qtrain_step_policy / se_qtrain_step on a twin agent: loss, weights,
+    Adam moments, the counter and the policy's Q rows agree bit for bit, update after update,
+    on a ring holding raised (flagged) transitions and with a partial last 32-sample tile."""
+    from shippingenv_amd.dqn import VecDQNAgent
+
+    agents = []
+    for _ in range(2):
+        env = make_env(n, seed=17)
+        torch.manual_seed(4)
+        agent = VecDQNAgent(env, graph=False, batch_size=batch, epsilon=0.6, target_update_every=0)
+        _OPEN.append(agent)
+        for _ in range(3):
+            agent.step()
+        agents.append(agent)
+    a, b = agents
+    assert bool((a.memory.size >= batch))
+    for k in range(4):
+        ctr0 = int(a._ctr[0].item())
+        a.trainer.step_replay(a.memory, batch, a.gamma, a._ctr, a._loss, a.policy if with_policy else None)
+        b.memory.sample(b.batch, t_dev=b._ctr)
+        if with_policy:
+            b.trainer.step_policy(b.batch, b.gamma, b._ctr, b._loss, b.policy)
+        else:
+            b.trainer.step(b.batch, b.gamma, b._ctr, b._loss)
+            b._ctr.add_(1)
+        torch.cuda.synchronize()
+        assert a._ctr.tolist() == [ctr0 + 1, ctr0 + 1], k
+        assert int(b._ctr[0].item()) == ctr0 + 1, k
+        assert a._loss.item() == b._loss.item(), k
+        for p, q in zip(a.model.parameters(), b.model.parameters()):
+            assert torch.equal(p, q), k
+        for p, q in zip(a.trainer.exp_avg + a.trainer.exp_avg_sq, b.trainer.exp_avg + b.trainer.exp_avg_sq):
+            assert torch.equal(p, q), k
+    if with_policy:
+        qs = []
+        for ag in agents:
+            q = torch.full((ag.env.n, ag.env.action_space_size), float("nan"), device=ag.env.device)
+            ag.policy.act(0.0, 0, q_out=q)
+            qs.append(q)
+        assert torch.equal(qs[0], qs[1])
 
 
 def test_out_of_range_action_is_weight_zero():
@@ -494,6 +541,8 @@ def test_out_of_range_action_is_weight_zero():
         agents.append(agent)
     for a, b in zip(agents[0].model.parameters(), agents[1].model.parameters()):
         assert torch.equal(a, b)
+    for ag in agents:
+        ag.memory.sample(ag.batch, t=99)
     bad, ref = (ag.batch for ag in agents)
     bad.act[[0, 17]] = torch.tensor([agents[0].env.action_space_size, -3], device=bad.act.device)
     ref.weight[[0, 17]] = 0.0
@@ -546,7 +595,7 @@ def test_grad_then_apply_is_the_fused_step_bit_for_bit():
         if la is not None:
             assert la.item() == lb.item(), k
         assert torch.equal(agents[0].policy.actions, agents[1].policy.actions), k
-        assert int(agents[0]._ctr.item()) == int(agents[1]._ctr.item()), k
+        assert int(agents[0]._ctr[0].item()) == int(agents[1]._ctr[0].item()), k
     assert agents[1]._graphs is not None and agents[1].exchanges == 10
     for p, q in zip(agents[0].model.parameters(), agents[1].model.parameters()):
         assert torch.equal(p, q)
@@ -629,7 +678,7 @@ def test_rank_gradients_sum_to_the_union_update():
             assert bool(((got - ref).abs() <= tol).all()), (name, float((got - ref).abs().max()))
         parts.append(b)
         grads.append(g)
-    k = int(agent._ctr.item())
+    k = int(agent._ctr[0].item())
     before = copy.deepcopy(agent.model)
     target = copy.deepcopy(agent.target_model)
     m0 = [t.clone() for t in tr.exp_avg]

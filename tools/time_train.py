@@ -41,7 +41,7 @@ def main():
     env = VecEnv(a.n, seed=2026, auto_reset=True, device="cuda:0")
     env.reset()
     torch.manual_seed(2026)
-    agent = VecDQNAgent(env, batch_size=a.batch, memory_size=4 * a.n, graph=not a.eager)
+    agent = VecDQNAgent(env, batch_size=a.batch, memory_size=4 * a.n, graph=False if a.eager else None)
     for _ in range(6):
         agent.step()
     torch.cuda.synchronize()
