@@ -501,7 +501,8 @@ def run_dqn_train(n, args, dist):
 
 
 KERNEL_MS_BASIS = ("HIP events on the launch stream, end of launch 1 to end of launch K, over K - 1 launches "
-                   "(rocprofv3 kernel-trace averages of the same launches: profiles/r03/kt_legs.json)")
+                   "(rocprofv3 kernel-trace averages of the driver's command: profiles/r03/kt_legs_driver.json, "
+                   "also under roofline.rocprof_trace)")
 
 
 def roofline(bytes_per_step, n, k_ms, canonical):

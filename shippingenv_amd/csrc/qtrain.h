@@ -80,6 +80,14 @@ struct QtWork {
     uint32_t* present; // [tiles]: bit rt = the tile holds an action of fc3 row tile rt
 };
 
+#ifndef SHIPENV_QT_NT
+#define SHIPENV_QT_NT 0  // 1 = T1's gradient partials leave with nontemporal stores (experiment)
+#endif
+__device__ __forceinline__ void st_part(float* p, float v) {
+    if constexpr (SHIPENV_QT_NT != 0) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 __device__ __forceinline__ int acc_r(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
 
 __device__ __forceinline__ f32x16 mfma_f32(float a, float b, f32x16 c) {
@@ -456,7 +464,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             for (int s = 0; s < 16; ++s)
                 acc = mfma_f32(DZ2[(wt * 32 + c) * kLS + 2 * s + h], HA[(ct * 32 + c) * kLS + 2 * s + h], acc);
 #pragma unroll
-            for (int r = 0; r < 16; ++r) out[(wt * 32 + acc_r(r, lane)) * 128 + ct * 32 + c] = acc[r];
+            for (int r = 0; r < 16; ++r) st_part(out + (wt * 32 + acc_r(r, lane)) * 128 + ct * 32 + c, acc[r]);
         }
     }
     // partial dW3[a][f] = sum_j (a_j == a) g_j h2[f][j] over the action tiles present:
@@ -493,7 +501,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
                 for (int s = 0; s < 16; ++s) acc = mfma_f32(av[s], bv[s], acc);
                 float* out = A.W.part_w3 + (((int64_t)blockIdx.x * A.d.mt3 + rt) * 32) * 128;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) out[acc_r(r, lane) * 128 + ct * 32 + c] = acc[r];
+                for (int r = 0; r < 16; ++r) st_part(out + acc_r(r, lane) * 128 + ct * 32 + c, acc[r]);
                 if (ct == 0) {  // db3[a]: the even samples' sum plus the odd samples' sum
                     float s3 = 0.0f;
 #pragma unroll
@@ -686,6 +694,86 @@ __device__ __forceinline__ float tile_sum64(const float* src, int64_t stride, in
     return r;
 }
 
+// tile_sum64 over the tiles whose present[] word holds `bit` only (the W3 blocks: a 32-sample
+// tile holds about 3 of the 9-10 action tiles). Chunk by chunk of 1024 tiles, thread t tests
+// tiles 4t .. 4t + 3 and the block writes the present ones, in tile order, to an LDS list
+// (wave prefix by ballot popcounts, then the four wave offsets); thread (grp, q) then adds
+// float4 q of list entries grp, grp + 16, ... with kU independent loads per round, and the
+// groups combine as in tile_sum64. Only present partials are loaded: the branch-free form
+// requested every tile's line (an absent tile's from tile 0), 3x the bytes.
+template <int kU>
+__device__ __forceinline__ float tile_sum64_present(const float* src, int64_t stride, int64_t e0, int64_t tiles,
+                                                    const uint32_t* present, uint32_t bit, float4* red, int* list,
+                                                    int* wtot) {
+    const int t = threadIdx.x, q = t & 15, grp = t >> 4, lane = t & 63, w = t >> 6;
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int64_t c0 = 0; c0 < tiles; c0 += 4 * kQRBlock) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t k = c0 + 4 * t + j;
+            m |= (k < tiles && (present[k] & bit)) ? 1u << j : 0u;
+        }
+        // exclusive prefix of popc(m) over the block: per bit-plane ballots within the wave
+        const uint64_t below = (1ull << lane) - 1ull;
+        int pre = 0, tot = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t b = __ballot((m >> j) & 1u);
+            pre += __popcll(b & below);
+            tot += __popcll(b);
+        }
+        if (lane == 0) wtot[w] = tot;
+        __syncthreads();
+        int off = 0, total = 0;
+#pragma unroll
+        for (int v = 0; v < kQRBlock / 64; ++v) {
+            off += v < w ? wtot[v] : 0;
+            total += wtot[v];
+        }
+        int pos = off + pre;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if ((m >> j) & 1u) list[pos++] = (int)(4 * t + j);
+        __syncthreads();
+        for (int i0 = grp; i0 < total; i0 += 16 * kU) {
+            float4 v[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int i = i0 + 16 * u;
+                const int64_t k = c0 + (i < total ? list[i] : 0);
+                v[u] = *reinterpret_cast<const float4*>(src + k * stride + e0 + 4 * q);
+                if (i >= total) v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                acc.x += v[u].x;
+                acc.y += v[u].y;
+                acc.z += v[u].z;
+                acc.w += v[u].w;
+            }
+        }
+        __syncthreads();  // list and wtot are rewritten by the next chunk
+    }
+#pragma unroll
+    for (int m = 16; m <= 32; m <<= 1) {
+        acc.x += __shfl_xor(acc.x, m);
+        acc.y += __shfl_xor(acc.y, m);
+        acc.z += __shfl_xor(acc.z, m);
+        acc.w += __shfl_xor(acc.w, m);
+    }
+    if ((t & 63) < 16) red[(t >> 6) * 16 + q] = acc;
+    __syncthreads();
+    float r = 0.0f;
+    if (t < 64) {
+        const int j = t >> 2, c = t & 3;
+        const float* f = reinterpret_cast<const float*>(red);
+        r = (f[4 * j + c] + f[4 * (16 + j) + c]) + (f[4 * (32 + j) + c] + f[4 * (48 + j) + c]);
+    }
+    __syncthreads();  // red may be reused
+    return r;
+}
+
 __device__ __forceinline__ float comp(const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
 
 // Workgroups: [0, 128) W1 row f (+ b1, the fold, the loss at f = 0); [128, 384) W2 64-element
@@ -695,6 +783,9 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
     __shared__ float red[kQRBlock];
     __shared__ float4 red4[kQRBlock];
     __shared__ float sums[8];
+    __shared__ float rowbuf[6 + 4 * SE_MAX_PORTS];  // W1 blocks: the updated row, for the folds
+    __shared__ int list[4 * kQRBlock];              // W3 blocks: the present tiles of a chunk
+    __shared__ int wtot[kQRBlock / 64];
     const int tid = threadIdx.x, in = A.d.in;
     QSTAMP(10);  // T2's stamps: slots 10-13 of the same rows (4 waves)
     const AdamStep adam(A);
@@ -714,6 +805,27 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
     const int b = blockIdx.x;
     if (b < 128) {  // W1 row f: 6 dynamic columns + db1 reduced over the tiles, the port columns
         const int f = b;
+        float* w1row = A.on.w1 + (int64_t)f * in;
+        // the Adam operands of this thread's columns (tid, tid + 256: in <= 262) and of b1, loaded
+        // now so their round trip overlaps the sums
+        float pw[2] = {0.f, 0.f}, pm[2] = {0.f, 0.f}, pv[2] = {0.f, 0.f}, bw = 0.f, bm = 0.f, bv = 0.f;
+        if (mode != 1) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int c = tid + u * kQRBlock;
+                if (c < in) {
+                    const int64_t i = (int64_t)f * in + c;
+                    pw[u] = w1row[c];
+                    pm[u] = A.m.w1[i];
+                    pv[u] = A.v.w1[i];
+                }
+            }
+            if (tid == 0) {
+                bw = A.on.b1[f];
+                bm = A.m.b1[f];
+                bv = A.v.b1[f];
+            }
+        }
         float x[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         if (mode == 2) {
 #pragma unroll
@@ -753,12 +865,18 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             for (int c = 0; c < 7; ++c) sums[c] = x[c];
         __syncthreads();
         const float s1 = sums[6];
-        float* w1row = A.on.w1 + (int64_t)f * in;
-        for (int c = tid; c < in; c += kQRBlock) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int c = tid + u * kQRBlock;
+            if (c >= in) continue;
             const float g = (c < 6 ? sums[c] : s1 * A.W.portvec[c - 6]) * inv;
             const int64_t i = (int64_t)f * in + c;
-            const float p = adam(w1row[c], g, A.m.w1[i], A.v.w1[i]);
+            float mm = pm[u], vv = pv[u];
+            const float p = adam(pw[u], g, mm, vv);
+            A.m.w1[i] = mm;
+            A.v.w1[i] = vv;
             w1row[c] = p;
+            rowbuf[c] = p;
             if (c < 6) {
                 A.W.pw1[0][((f >> 5) * 3 + (c >> 1)) * 64 + (f & 31) + 32 * (c & 1)] = p;
                 if (A.img[0])  // the policy's fc1 fragment: element j holds column fc1_col(j)
@@ -769,16 +887,20 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                             if (fc1_col(j) == c) put_bf16(A.img[l] + A.q[l].w1() + ((f >> 5) * 64 + (f & 31)) * 16 + 2 * j, p);
             }
         }
-        if (tid == 0) sums[7] = adam(A.on.b1[f], s1 * inv, A.m.b1[f], A.v.b1[f]);
-        __syncthreads();  // the new row and b1 are complete before the fold reads them
+        if (tid == 0) {
+            sums[7] = adam(bw, s1 * inv, bm, bv);
+            A.m.b1[f] = bm;
+            A.v.b1[f] = bv;
+        }
+        __syncthreads();  // the new row (rowbuf) and b1 are complete before the folds read them
         const float b1 = sums[7];
         if (tid == 0) A.on.b1[f] = b1;
-        const float xf = fold_row(w1row, in, A.W.portvec, red);  // the pack kernel's bits
+        const float xf = fold_row(rowbuf, in, A.W.portvec, red);  // the pack kernel's bits
         if (tid == 0) A.W.c1[0][f] = b1 + xf;
         if (A.img[0] && tid == 0) {  // the policy's b1: qnet_pack_kernel's f64 fold, same order
             double acc = (double)b1;
             for (int p = 0; p < A.d.P; ++p) {
-                const float* wp = w1row + 6 + 4 * p;
+                const float* wp = rowbuf + 6 + 4 * p;
                 const float* pv = A.W.portvec + 4 * p;
                 acc += (double)wp[0] * (double)pv[0] + (double)wp[1] * (double)pv[1] +
                        (double)wp[2] * (double)pv[2] + (double)wp[3] * (double)pv[3];
@@ -799,6 +921,22 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         }
     } else if (b < 384) {  // W2 elements e0 .. e0 + 63 (row-major [f2][f1])
         const int64_t e0 = (int64_t)(b - 128) * 64;
+        const int f2 = (int)(e0 >> 7);
+        // the Adam operands, loaded ahead of the sums (as in the W1 blocks)
+        float pw = 0.f, pm = 0.f, pv = 0.f, bw = 0.f, bm = 0.f, bv = 0.f;
+        if (mode != 1) {
+            if (tid < 64) {
+                const int64_t e = e0 + tid;
+                pw = A.on.w2[e];
+                pm = A.m.w2[e];
+                pv = A.v.w2[e];
+            }
+            if ((e0 & 127) == 0 && tid == 0) {
+                bw = A.on.b2[f2];
+                bm = A.m.b2[f2];
+                bv = A.v.b2[f2];
+            }
+        }
         float g;
         if (mode == 2) {
             g = tid < 64 ? G[Grad::w2 + e0 + tid] : 0.0f;
@@ -807,7 +945,6 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             if (mode == 1) {
                 if (tid < 64) G[Grad::w2 + e0 + tid] = g;
                 if ((e0 & 127) == 0) {
-                    const int f2 = (int)(e0 >> 7);
                     float x = 0.0f;
                     for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[t * 128 + f2];
                     const float s2 = block_sum256(x, red);
@@ -819,8 +956,10 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         const float inv = weight_inv();
         QSTAMP(12);
         if (tid < 64) {
-            const int e = (int)e0 + tid, f2 = e >> 7, f1 = e & 127;
-            const float p = adam(A.on.w2[e], g * inv, A.m.w2[e], A.v.w2[e]);
+            const int e = (int)e0 + tid, f1 = e & 127;
+            const float p = adam(pw, g * inv, pm, pv);
+            A.m.w2[e] = pm;
+            A.v.w2[e] = pv;
             A.on.w2[e] = p;
             A.W.pw2[0][frag_index(f2, f1)] = p;
             A.W.pw2t[frag_index(f1, f2)] = p;
@@ -829,7 +968,6 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                 for (int l = 0; l < 2; ++l) put_bf16(A.img[l] + A.q[l].w2() + pol_offset(f2, f1), p);
         }
         if ((e0 & 127) == 0) {
-            const int f2 = (int)(e0 >> 7);
             float s2;
             if (mode == 2) {
                 s2 = G[Grad::b2 + f2];
@@ -839,7 +977,9 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                 s2 = block_sum256(x, red);
             }
             if (tid == 0) {
-                const float p = adam(A.on.b2[f2], s2 * inv, A.m.b2[f2], A.v.b2[f2]);
+                const float p = adam(bw, s2 * inv, bm, bv);
+                A.m.b2[f2] = bm;
+                A.v.b2[f2] = bv;
                 A.on.b2[f2] = p;
                 if (A.img[0])
 #pragma unroll
@@ -850,12 +990,21 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         const int k = b - 384, rt = k >> 6;
         const int64_t e0 = (int64_t)(k & 63) * 64;
         const uint32_t bit = 1u << rt;
+        const int a3 = rt * 32 + (int)((e0 + tid) >> 7), f3 = (int)((e0 + tid) & 127);
+        const int64_t i3 = (int64_t)a3 * 128 + f3;
+        const bool own = tid < 64 && a3 < A.d.A;  // this thread's element, if it has one
+        float pw = 0.f, pm = 0.f, pv = 0.f;  // its Adam operands, loaded ahead of the sums
+        if (mode != 1 && own) {
+            pw = A.on.w3[i3];
+            pm = A.m.w3[i3];
+            pv = A.v.w3[i3];
+        }
         float g;
         if (mode == 2) {
             g = tid < 64 ? G[Grad::w3 + (int64_t)rt * 32 * 128 + e0 + tid] : 0.0f;
         } else {
-            g = tile_sum64<16>(A.W.part_w3 + (int64_t)rt * 32 * 128, (int64_t)A.d.mt3 * 32 * 128, e0, A.tiles,
-                               A.W.present, bit, red4);
+            g = tile_sum64_present<8>(A.W.part_w3 + (int64_t)rt * 32 * 128, (int64_t)A.d.mt3 * 32 * 128, e0,
+                                      A.tiles, A.W.present, bit, red4, list, wtot);
             if (mode == 1) {
                 if (tid < 64) G[Grad::w3 + (int64_t)rt * 32 * 128 + e0 + tid] = g;
                 return;
@@ -863,19 +1012,17 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         }
         const float inv = weight_inv();
         QSTAMP(12);
-        if (tid < 64) {
-            const int e = (int)e0 + tid, a = rt * 32 + (e >> 7), f = e & 127;
-            if (a < A.d.A) {
-                const int64_t i = (int64_t)a * 128 + f;
-                const float p = adam(A.on.w3[i], g * inv, A.m.w3[i], A.v.w3[i]);
-                A.on.w3[i] = p;
-                if (A.img[0])
+        if (own) {
+            const float p = adam(pw, g * inv, pm, pv);
+            A.m.w3[i3] = pm;
+            A.v.w3[i3] = pv;
+            A.on.w3[i3] = p;
+            if (A.img[0])
 #pragma unroll
-                    for (int l = 0; l < 2; ++l) {
-                        const int row = row_of_action(A.q[l], a);
-                        if (row >= 0) put_bf16(A.img[l] + A.q[l].w3() + pol_offset(row, f), p);
-                    }
-            }
+                for (int l = 0; l < 2; ++l) {
+                    const int row = row_of_action(A.q[l], a3);
+                    if (row >= 0) put_bf16(A.img[l] + A.q[l].w3() + pol_offset(row, f3), p);
+                }
         }
     } else {  // b3 of rows 32 rt .. 32 rt + 31: 32 rows x 8 tile groups
         // its own workgroup: behind a W3 block's sum it was the kernel's critical path.
@@ -883,6 +1030,14 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         // an absent action tile, so no presence test: a conditional load per tile kept these
         // blocks busy 3x as long as the rest of the kernel)
         const int rt = b - 384 - 64 * A.d.mt3;
+        const int a3 = rt * 32 + (tid & 31);
+        const bool own = tid < 32 && a3 < A.d.A;
+        float pw = 0.f, pm = 0.f, pv = 0.f;  // the Adam operands, loaded ahead of the sums
+        if (mode != 1 && own) {
+            pw = A.on.b3[a3];
+            pm = A.m.b3[a3];
+            pv = A.v.b3[a3];
+        }
         float s3;
         if (mode == 2) {
             s3 = G[Grad::b3(A.d) + rt * 32 + (tid & 31)];
@@ -916,14 +1071,15 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         }
         {
             const float inv = weight_inv();
-            const int a = rt * 32 + (tid & 31);
-            if (tid < 32 && a < A.d.A) {
-                const float p = adam(A.on.b3[a], s3 * inv, A.m.b3[a], A.v.b3[a]);
-                A.on.b3[a] = p;
+            if (own) {
+                const float p = adam(pw, s3 * inv, pm, pv);
+                A.m.b3[a3] = pm;
+                A.v.b3[a3] = pv;
+                A.on.b3[a3] = p;
                 if (A.img[0])
 #pragma unroll
                     for (int l = 0; l < 2; ++l) {
-                        const int row = row_of_action(A.q[l], a);
+                        const int row = row_of_action(A.q[l], a3);
                         if (row >= 0) reinterpret_cast<float*>(A.img[l] + A.q[l].b3())[row] = p;
                     }
             }

@@ -22,7 +22,13 @@ def main():
     p.add_argument("--n", type=int, default=1 << 20)
     p.add_argument("--batch", type=int, default=8192)
     p.add_argument("--iters", type=int, default=50)
+    p.add_argument("--lib", default=None)
+    p.add_argument("--forms", default="graph,eager")
     a = p.parse_args()
+    if a.lib:
+        from shippingenv_amd import _native
+
+        _native.LIB_PATH = os.path.abspath(a.lib)
     from shippingenv_amd.dqn import VecDQNAgent
     from shippingenv_amd.vec import VecEnv
 
@@ -36,7 +42,7 @@ def main():
     s = torch.cuda.current_stream()
     graph = agent._graph
     for rep in range(3):
-        for form in ("graph", "eager"):
+        for form in a.forms.split(","):
             agent._graph = graph if form == "graph" else None
             agent.use_graph = form == "graph"
             agent.update()  # one untimed
@@ -50,7 +56,7 @@ def main():
             t1 = time.perf_counter()
             torch.cuda.synchronize()
             t2 = time.perf_counter()
-            print(json.dumps({"rep": rep, "form": form, "iters": a.iters,
+            print(json.dumps({"lib": os.path.basename(a.lib or "default"), "rep": rep, "form": form, "iters": a.iters,
                               "gpu_ms_per_update": round(e0.elapsed_time(e1) / a.iters, 4),
                               "host_issue_ms_per_update": round((t1 - t0) * 1e3 / a.iters, 4),
                               "wall_ms_per_update": round((t2 - t0) * 1e3 / a.iters, 4)}), flush=True)
