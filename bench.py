@@ -80,7 +80,13 @@ class Dist:
         from shippingenv_amd import dist as D
 
         self.D = D
-        self.rank, self.world, self.local, self.dev = D.init_from_env()
+        # rehearsal of the N-rank launch on fewer GPUs (never for a measurement):
+        # SHIPENV_SHARE_GPUS=1 puts local rank r on GPU r % device_count, and
+        # SHIPENV_DIST_BACKEND=gloo replaces RCCL, which refuses two ranks on one GPU
+        gpu = None
+        if os.environ.get("SHIPENV_SHARE_GPUS") == "1" and torch.cuda.is_available():
+            gpu = int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count()
+        self.rank, self.world, self.local, self.dev = D.init_from_env(os.environ.get("SHIPENV_DIST_BACKEND"), gpu)
         if self.world != want:
             raise SystemExit(f"--gpus {want} but WORLD_SIZE={self.world}")
         import torch.distributed as tdist

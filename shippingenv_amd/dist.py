@@ -29,20 +29,22 @@ def shard_bounds(n_global, world, rank):
     return rank * per, per
 
 
-def init_from_env(backend=None):
-    """Initialise torch.distributed from RANK/WORLD_SIZE/LOCAL_RANK (torchrun) or
-    run single-process. Returns (rank, world, local_rank, device)."""
+def init_from_env(backend=None, gpu=None):
+    """Initialise torch.distributed from RANK / WORLD_SIZE / LOCAL_RANK (as torchrun sets
+    them; MASTER_ADDR defaults to 127.0.0.1) or run single-process. One process per GPU:
+    local rank r drives GPU r, unless `gpu` names the device (a caller rehearsing several
+    ranks on fewer GPUs passes it, with backend "gloo": RCCL refuses two ranks on one GPU).
+    Backend: "nccl" (RCCL) on GPUs, "gloo" on CPU, unless given. Returns (rank, world,
+    local_rank, device)."""
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # Rehearsal of the N-rank path on fewer GPUs (not for measurement):
-    # SHIPENV_SHARE_GPUS=1 maps local rank r to GPU r % device_count, and
-    # SHIPENV_DIST_BACKEND=gloo replaces RCCL, which refuses two ranks on one GPU.
-    backend = backend or os.environ.get("SHIPENV_DIST_BACKEND") or None
     if torch.cuda.is_available():
-        dev = local % torch.cuda.device_count() if os.environ.get("SHIPENV_SHARE_GPUS") == "1" else local
+        dev = local if gpu is None else int(gpu)
+        if not 0 <= dev < torch.cuda.device_count():
+            raise RuntimeError(f"local rank {local} has no GPU (device {dev} of {torch.cuda.device_count()})")
         torch.cuda.set_device(dev)
         device = torch.device("cuda", dev)
     else:
@@ -92,10 +94,10 @@ def summarize(stats):
 class ShardedVecEnv:
     """This rank's shard of a multi-GPU environment set (a VecEnv with global ids)."""
 
-    def __init__(self, n_per_rank, **kw):
+    def __init__(self, n_per_rank, gpu=None, backend=None, **kw):
         from .vec import VecEnv
 
-        self.rank, self.world, self.local, self.device = init_from_env()
+        self.rank, self.world, self.local, self.device = init_from_env(backend, gpu)
         first, count = shard_bounds(n_per_rank * self.world, self.world, self.rank)
         self.first = first
         self.env = VecEnv(count, env_id_base=first, device=self.device, **kw)

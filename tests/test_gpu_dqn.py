@@ -704,14 +704,14 @@ def _dp_worker(rank, world, port, out):
 
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), SHIPENV_SHARE_GPUS="1")
+                      LOCAL_RANK=str(rank))
     import torch.distributed as dist
 
     from shippingenv_amd import dist as D
     from shippingenv_amd.dqn import DQNNetwork, VecDQNAgent
 
-    r, w, _, dev = D.init_from_env(backend="gloo")
-    env = D.ShardedVecEnv(2048, seed=9, auto_reset=True)  # the INTEGRATION.md recipe
+    r, w, _, dev = D.init_from_env(backend="gloo", gpu=0)  # the ranks share the one GPU
+    env = D.ShardedVecEnv(2048, gpu=0, seed=9, auto_reset=True)  # the INTEGRATION.md recipe
     assert env.first == r * 2048
     env.reset()
     torch.manual_seed(100 + r)  # different initial weights: the broadcast must align them
@@ -766,14 +766,14 @@ def _dp_mismatch_worker(rank, world, port, out, what="n"):
 
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), SHIPENV_SHARE_GPUS="1")
+                      LOCAL_RANK=str(rank))
     import torch.distributed as dist
 
     from shippingenv_amd import dist as D
     from shippingenv_amd.dqn import VecDQNAgent
     from shippingenv_amd.vec import VecEnv
 
-    r, w, _, dev = D.init_from_env(backend="gloo")
+    r, w, _, dev = D.init_from_env(backend="gloo", gpu=0)  # the ranks share the one GPU
     if what == "n":  # different env counts
         env = VecEnv(2048 * (1 + r), seed=9, env_id_base=r * 4096, device=dev, auto_reset=True)
     else:  # the same count and port positions, different port stocks

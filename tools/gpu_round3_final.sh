@@ -1,0 +1,11 @@
+#!/bin/bash
+# round-3 evidence: the GPU suite, smoke(), the driver's bench command twice, and its kernel trace
+set -u
+TAG=${1:-r03y}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+timeout -k 10 900 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread tests -m gpu > $OUT/tests_gpu.log 2>&1 || exit $?
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
+timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_drv.json 2> $OUT/bench_drv.err || exit $?
+timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_drv2.json 2> $OUT/bench_drv2.err || exit $?
+bash tools/trace_driver.sh $TAG || exit $?
