@@ -508,7 +508,7 @@ def run_dqn_train(n, args, dist):
 
 KERNEL_MS_BASIS = ("HIP events on the launch stream, end of launch 1 to end of launch K, over K - 1 launches "
                    "(rocprofv3 kernel-trace averages of the driver's command: profiles/r03/kt_legs_driver.json, "
-                   "also under roofline.rocprof_trace)")
+                   "printed per leg as rocprof_trace from profiles/rocprof_legs.json)")
 
 
 def roofline(bytes_per_step, n, k_ms, canonical):
@@ -541,7 +541,7 @@ def pmc_traffic(key="step_kernel_bytes_per_launch"):
     return d.get(key), os.path.relpath(path, ROOT)
 
 
-TRACE_SUMMARY = os.path.join("profiles", "r03", "kt_legs_driver.json")
+TRACE_SUMMARY = os.path.join("profiles", "rocprof_legs.json")  # profiles/r03/kt_legs_driver.json, condensed
 
 
 def rocprof_leg(key):
@@ -737,6 +737,10 @@ def main():
                            "frac": roofline(BYTES_STEP, args.large_n, kr, CANONICAL_STEP)["frac"],
                            "rocprof_trace": rocprof_leg("large_n_from_reset")},
         }
+        tb, srcb = pmc_traffic("step_kernel_big_bytes_per_launch")
+        if tb:
+            out["large_n"]["roofline"]["traffic"] = tb
+            out["large_n"]["roofline"]["traffic_source"] = srcb
 
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
         log("[cpu] timing the C restatement")

@@ -34,3 +34,16 @@ def test_no_roofline_rate_above_its_peak():
         assert r["canonical_bytes_per_env_step"] == 66
         assert [key for key in r if key.endswith("achieved")] == ["achieved"]
     assert b.KERNEL_MS_BASIS in b.roofline(b.BYTES_STEP, 1, 1.0, 66)["kernel_ms_basis"]
+
+
+def test_committed_trace_summary_covers_every_leg():
+    """bench.py prints each leg's committed kernel-trace average (roofline.rocprof_trace) from
+    profiles/rocprof_legs.json, a file outside the gpurun-ignored profiles/r0* directories, so
+    the GPU box's run sees it; every timed leg must be in it, with a frac below 1."""
+    b = _bench()
+    for key in ("config3", "config3_from_reset", "config3_step_seq", "config4", "large_n",
+                "large_n_from_reset"):
+        r = b.rocprof_leg(key)
+        assert r is not None, key
+        assert 0 < r["frac"] < 1 and r["avg_us"] > 0, key
+    assert not b.TRACE_SUMMARY.startswith(os.path.join("profiles", "r0"))

@@ -77,6 +77,9 @@ def main():
                        "step_kernel_auto_bytes_per_launch":
                            round(traffic["c4"]["bytes_per_launch"]) if "c4" in traffic else None,
                        "workload_auto": "config 4, N=2^20 (done-list records and the stats slab included)",
+                       "step_kernel_big_bytes_per_launch":
+                           round(traffic["big"]["bytes_per_launch"]) if "big" in traffic else None,
+                       "workload_big": "config 3, N=2^24 (the large_n leg)",
                        "correction": "FETCH_SIZE x2 (gfx950 half-count), WRITE_SIZE x1, KiB->B"},
                       f, indent=1)
     print(json.dumps({"traffic": traffic, "kernels": {k: {n: v["avg_us"] for n, v in d.items()
