@@ -1003,7 +1003,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         if (mode == 2) {
             g = tid < 64 ? G[Grad::w3 + (int64_t)rt * 32 * 128 + e0 + tid] : 0.0f;
         } else {
-            g = tile_sum64_present<8>(A.W.part_w3 + (int64_t)rt * 32 * 128, (int64_t)A.d.mt3 * 32 * 128, e0,
+            g = tile_sum64_present<16>(A.W.part_w3 + (int64_t)rt * 32 * 128, (int64_t)A.d.mt3 * 32 * 128, e0,
                                       A.tiles, A.W.present, bit, red4, list, wtot);
             if (mode == 1) {
                 if (tid < 64) G[Grad::w3 + (int64_t)rt * 32 * 128 + e0 + tid] = g;
