@@ -350,10 +350,13 @@ int se_qtrain_step_policy(se_qtrain* q, se_qnet* qn, int64_t batch, const float*
  * transitions se_replay_sample(r, batch, t_dev = ctr) picks, without writing the batch
  * buffers. ctr: device int32[2], both entries = the updates taken so far; the sampler key is
  * ctr[0], the first kernel sets ctr[1] = ctr[0] + 1 (the bias-correction count) and the
- * second copies it back into ctr[0]. Same bits as the sampler plus the step with
+ * second copies it back into ctr[0]. t >= 0: the caller's copy of ctr[0] (and the ring's size
+ * as recorded on the host), so the first kernel does not wait on those device words; t < 0
+ * reads them on the device (a graph capture, whose replays advance ctr). Same bits as the sampler plus the step with
  * step_dev = ctr (then advanced); r must record the same env as q and not be mid-record. */
 int se_qtrain_step_replay(se_qtrain* q, se_qnet* qn, se_replay* r, int64_t batch, float gamma, float lr,
-                          float beta1, float beta2, float eps, int32_t* ctr, float* loss_out, void* stream);
+                          float beta1, float beta2, float eps, int32_t* ctr, int64_t t, float* loss_out,
+                          void* stream);
 /* Data-parallel update (one learner per GPU, the same parameters on every rank): se_qtrain_step
  * split at the exchange. se_qtrain_grad writes this rank's gradient sums (before the division
  * by sum w) and {sum w (q - y)^2, sum w} into grad, a device f32 vector of

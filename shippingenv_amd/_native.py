@@ -107,7 +107,7 @@ def _declare(lib):
         "se_qtrain_pack": [P, C.c_int32, P],
         "se_qtrain_step": [P, i64, P, P, P, P, P, P] + [C.c_float] * 5 + [P, P, P],
         "se_qtrain_step_policy": [P, P, i64, P, P, P, P, P, P] + [C.c_float] * 5 + [P, P, P],
-        "se_qtrain_step_replay": [P, P, P, i64] + [C.c_float] * 5 + [P, P, P],
+        "se_qtrain_step_replay": [P, P, P, i64] + [C.c_float] * 5 + [P, i64, P, P],
         "se_qtrain_grad_size": [P],
         "se_qtrain_grad": [P, i64, P, P, P, P, P, P, C.c_float, P, P],
         "se_qtrain_apply": [P, P, P] + [C.c_float] * 4 + [P, P, P],

@@ -225,6 +225,9 @@ struct QtStepArgs {
     Ring ring;
     uint64_t seed;
     int32_t* ctr;
+    // the sampler key and the ring's size as the host knows them at enqueue (eager calls), so
+    // the picks do not wait on a device load first; -1: read ctr[0] / the ring's size word
+    int64_t t_host, size_host;
 };
 
 #ifndef SHIPENV_QTRACE
@@ -295,8 +298,8 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     if (A.from_ring) {  // the sampler's pick of row r0 + tid, straight into the tiles
         if (tid < 32) {
             const Ring& ring = A.ring;
-            const int64_t size = *ring.d_size;
-            const uint32_t t = (uint32_t)A.ctr[0];
+            const int64_t size = A.size_host >= 0 ? A.size_host : *ring.d_size;
+            const uint32_t t = A.t_host >= 0 ? (uint32_t)A.t_host : (uint32_t)A.ctr[0];
             const U4 key = draw(env_key(A.seed, kReplayKeyId), t, kSlotReplay);
             const int64_t row = r0 + tid;
             Pick pk{-1, 0u, 0u, 0.0f, 0.0f, 0.0f, 0, 0};
@@ -1224,7 +1227,7 @@ QtAdamArgs adam_args(se_qtrain* q, se_qnet* qn, int64_t batch, const int64_t* ac
 int qtrain_step(se_qtrain* q, se_qnet* qn, int64_t batch, const float* obs, const float* next_obs,
                 const int64_t* act, const float* rew, const float* done, const float* weight, float gamma,
                 float lr, float beta1, float beta2, float eps, int32_t* step_dev, float* loss_out,
-                void* stream, float* grad = nullptr, const se_replay* ring = nullptr) {
+                void* stream, float* grad = nullptr, const se_replay* ring = nullptr, int64_t t_host = -1) {
     if (int rc0 = qtrain_check_bound(q)) return rc0;
     if (batch < 1 || batch > q->max_batch) return fail(SE_EINVAL, "batch must be in [1, max_batch]");
     if (!ring && (!obs || !next_obs || !act || !rew || !done || !weight))
@@ -1241,7 +1244,8 @@ int qtrain_step(se_qtrain* q, se_qnet* qn, int64_t batch, const float* obs, cons
     if (rc) return rc;
     QtStepArgs A{q->W, q->on, q->tg, q->d, batch, obs, next_obs, act, rew, done, weight, gamma,
                  qn && !ring ? step_dev : nullptr, ring ? 1 : 0, ring ? ring->ring : Ring{},
-                 ring ? ring->env->seed : 0, ring ? step_dev : nullptr};
+                 ring ? ring->env->seed : 0, ring ? step_dev : nullptr, ring ? t_host : -1,
+                 ring && t_host >= 0 ? ring->size : -1};
     qtrain_tile_kernel<<<(unsigned)tiles, kQTBlock, lds, s>>>(A);
     HIP_TRY(hipGetLastError());
     // T2 counts Adam steps from ctr[1] (set by T1) when T1 drew the batch, and syncs ctr[0]
@@ -1272,12 +1276,14 @@ int se_qtrain_step_policy(se_qtrain* q, se_qnet* qn, int64_t batch, const float*
 }
 
 int se_qtrain_step_replay(se_qtrain* q, se_qnet* qn, se_replay* r, int64_t batch, float gamma, float lr,
-                          float beta1, float beta2, float eps, int32_t* ctr, float* loss_out, void* stream) {
+                          float beta1, float beta2, float eps, int32_t* ctr, int64_t t, float* loss_out,
+                          void* stream) {
     if (!r) return fail(SE_EINVAL, "null replay");
     if (!q || r->env != q->env) return fail(SE_EINVAL, "the replay and the qtrain belong to different envs");
     if (r->open) return fail(SE_ESTATE, "se_replay_begin without se_replay_end");
+    if (t > 0xFFFFFFFFll) return fail(SE_EINVAL, "the sampler key t must be < 2^32 (or negative: read ctr[0])");
     return qtrain_step(q, qn, batch, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, gamma, lr, beta1, beta2,
-                       eps, ctr, loss_out, stream, nullptr, r);
+                       eps, ctr, loss_out, stream, nullptr, r, t < 0 ? -1 : t);
 }
 
 int64_t se_qtrain_grad_size(const se_qtrain* q) { return q ? Grad::size(q->d) : 0; }

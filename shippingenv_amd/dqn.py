@@ -189,16 +189,18 @@ class FusedUpdate:
                                               _ptr(step_dev), _ptr(loss_out), self.env._stream()))
 
     def step_replay(self, memory, batch: int, gamma: float, ctr: torch.Tensor, loss_out: torch.Tensor,
-                    policy=None):
+                    policy=None, t: int | None = None):
         """memory.sample(t_dev=ctr) then step_policy(..., step_dev=ctr) (step() without a
         policy), in two launches (se_qtrain_step_replay): the first draws its minibatch rows
-        from the ring itself. ctr: device int32 [2], both entries the updates taken so far."""
+        from the ring itself. ctr: device int32 [2], both entries the updates taken so far.
+        t: the caller's copy of ctr[0] (eager calls: the first kernel then does not wait on
+        the device counter); None reads it on the device (graph capture)."""
         if ctr.dtype != torch.int32 or ctr.numel() < 2 or not ctr.is_contiguous():
             raise ValueError("ctr must be a contiguous int32 device tensor of 2 entries")
         N.check(N.lib().se_qtrain_step_replay(self._h, None if policy is None else policy._h, memory._h,
                                               int(batch), float(gamma), self.lr, self.betas[0],
-                                              self.betas[1], self.eps, _ptr(ctr), _ptr(loss_out),
-                                              self.env._stream()))
+                                              self.betas[1], self.eps, _ptr(ctr), -1 if t is None else int(t),
+                                              _ptr(loss_out), self.env._stream()))
 
     # ---- data parallel (one learner per GPU): the update split at the gradient exchange
     def grad_size(self) -> int:
@@ -381,8 +383,10 @@ class VecDQNAgent:
         if self.fused:  # _ctr = Adam steps taken so far
             # the minibatch draw, the update, the policy's new images and the counter's
             # advance: two launches (the batch buffers are not written)
+            # eager: the host's update count is ctr[0], so T1 need not load it first
+            t = None if torch.cuda.is_current_stream_capturing() else self.updates
             self.trainer.step_replay(self.memory, self.batch_size, self.gamma, self._ctr, self._loss,
-                                     self.policy)
+                                     self.policy, t=t)
             return
         self.memory.sample(self.batch, t_dev=self._ctr)
         loss = dqn_loss(self.model, self.target_model, self.batch, self.gamma)

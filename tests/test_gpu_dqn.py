@@ -479,12 +479,14 @@ def test_update_with_policy_refuses_a_foreign_qnet():
     assert int(agent._ctr[0].item()) == ctr + 1
 
 
-@pytest.mark.parametrize("n,batch,with_policy", [(4096, 512, True), (4099, 300, False)])
-def test_update_drawing_its_own_batch_equals_sampler_then_step(n, batch, with_policy):
+@pytest.mark.parametrize("n,batch,with_policy,host_t", [(4096, 512, True, True), (4099, 300, False, False)])
+def test_update_drawing_its_own_batch_equals_sampler_then_step(n, batch, with_policy, host_t):
     """se_qtrain_step_replay (the first kernel draws its minibatch rows from the ring) against
     se_replay_sample + se_qtrain_step_policy / se_qtrain_step on a twin agent: loss, weights,
     Adam moments, the counter and the policy's Q rows agree bit for bit, update after update,
-    on a ring holding raised (flagged) transitions and with a partial last 32-sample tile."""
+    on a ring holding raised (flagged) transitions and with a partial last 32-sample tile.
+    host_t: the sampler key and the ring size passed from the host instead of read on the
+    device."""
     from shippingenv_amd.dqn import VecDQNAgent
 
     agents = []
@@ -500,7 +502,8 @@ def test_update_drawing_its_own_batch_equals_sampler_then_step(n, batch, with_po
     assert bool((a.memory.size >= batch))
     for k in range(4):
         ctr0 = int(a._ctr[0].item())
-        a.trainer.step_replay(a.memory, batch, a.gamma, a._ctr, a._loss, a.policy if with_policy else None)
+        a.trainer.step_replay(a.memory, batch, a.gamma, a._ctr, a._loss, a.policy if with_policy else None,
+                              t=ctr0 if host_t else None)
         b.memory.sample(b.batch, t_dev=b._ctr)
         if with_policy:
             b.trainer.step_policy(b.batch, b.gamma, b._ctr, b._loss, b.policy)

@@ -24,6 +24,8 @@ def main():
     p.add_argument("--iters", type=int, default=50)
     p.add_argument("--lib", default=None)
     p.add_argument("--forms", default="graph,eager")
+    p.add_argument("--device-key", action="store_true",
+                   help="eager updates read the sampler key and ring size on the device (t=None)")
     a = p.parse_args()
     if a.lib:
         from shippingenv_amd import _native
@@ -36,6 +38,9 @@ def main():
     env.reset()
     torch.manual_seed(2026)
     agent = VecDQNAgent(env, batch_size=a.batch, memory_size=4 * a.n, graph=True)
+    if a.device_key:
+        step_replay = agent.trainer.step_replay
+        agent.trainer.step_replay = lambda *args, t=None, **kw: step_replay(*args, t=None, **kw)
     for _ in range(6):
         agent.step()
     torch.cuda.synchronize()
@@ -56,7 +61,8 @@ def main():
             t1 = time.perf_counter()
             torch.cuda.synchronize()
             t2 = time.perf_counter()
-            print(json.dumps({"lib": os.path.basename(a.lib or "default"), "rep": rep, "form": form, "iters": a.iters,
+            print(json.dumps({"lib": os.path.basename(a.lib or "default"), "device_key": a.device_key,
+                              "rep": rep, "form": form, "iters": a.iters,
                               "gpu_ms_per_update": round(e0.elapsed_time(e1) / a.iters, 4),
                               "host_issue_ms_per_update": round((t1 - t0) * 1e3 / a.iters, 4),
                               "wall_ms_per_update": round((t2 - t0) * 1e3 / a.iters, 4)}), flush=True)
