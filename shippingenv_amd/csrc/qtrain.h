@@ -19,9 +19,11 @@
 // * dH1 = W2^T dZ2 on MFMA, then dZ1 = dH1 (h1 > 0).
 // * Per-tile partial gradients: dW2 = dZ2 H1^T (MFMA, K = 32 samples), dW1 of the six
 //   dynamic columns, db1, db2, the loss sum and the weight sum.
-// * Per-tile partial dW3 = G H2^T on MFMA, with G[a][j] = (a_j == a) g_j built in the
-//   operand from the tile's action list. Only the 32-row action tiles that hold one of
-//   the tile's actions are computed and stored; a presence bitmask marks them.
+// * Per-tile partial dW3 over the tile's distinct actions: row r of a 32 x 128 partial is
+//   sum_j [first(j) = r] g_j h2_j, first(j) the first sample of the tile with a_j's action
+//   (one G H2^T on MFMA, K = 32), and a slot map names row r's action. A tile's 32 samples
+//   hold at most 32 actions, so this is 4 MFMA chains whatever the actions are; the
+//   action-tile layout it replaces ran 4 chains per 32-action tile present (up to 36).
 // * The port block of every observation row is the same, so fc1 runs on the six
 //   dynamic columns with W1[:, 6:] . port + b1 folded into its bias. dW1[:, 6:] is then
 //   db1 (x) port.
@@ -30,7 +32,9 @@
 // per W1 row):
 // * Sums the tile partials with the threads spread over the tiles: 16 tile groups x 16
 //   float4 columns, then a fixed tree. Every load is independent, so the reduction
-//   streams instead of walking one dependent load per tile.
+//   streams instead of walking one dependent load per tile. A W3 workgroup owns one action
+//   row: it finds the tiles whose slot map holds the action (one slot at most per tile) and
+//   sums those rows in tile order.
 // * Divides by sum(w): the MSE mean, since w = 1 on a full batch.
 // * Takes one Adam step on the parameters in place (torch nn.Linear layout).
 // * Rewrites the online net's MFMA fragment images, and refolds fc1's bias for the
@@ -75,9 +79,11 @@ struct QtWork {
     float* part_b1;  // [tiles][128]
     float* part_b2;  // [tiles][128]
     float* part_lw;  // [tiles][2]: sum w d^2, sum w
-    float* part_w3;  // [tiles][mt3][32][128]: only the action tiles present in the tile
-    float* part_b3;  // [tiles][mt3][32]
-    uint32_t* present; // [tiles]: bit rt = the tile holds an action of fc3 row tile rt
+    // dW3 / db3 per distinct action of a tile: slot r sums the samples whose action first
+    // occurs at sample r of the tile; part_map[t][r] is that action, or -1 (no such slot)
+    float* part_w3;  // [tiles][32][128]: only the rows of live slots are stored
+    float* part_b3;  // [tiles][32]
+    int32_t* part_map; // [tiles][32]
 };
 
 #ifndef SHIPENV_QT_NT
@@ -105,12 +111,38 @@ struct Frags {
     }
 };
 
-// acc += A (fragments in registers) x B (an LDS [k][kLS] tile)
-template <int kSteps>
+#ifndef SHIPENV_QT_LOOKAHEAD
+#define SHIPENV_QT_LOOKAHEAD 8  // B operands read this many k-steps ahead of their MFMA (0: as needed)
+#endif
+// acc += A (fragments in registers) x B (an LDS [k][kLS] tile), k-steps [S0, S1). The B
+// operands are read kLookahead k-steps ahead of the MFMA that uses them, pinned in that
+// order by scheduling groups (one LDS read, one MFMA): left to itself the compiler read
+// each pair just before its two MFMAs, so every pair waited out an LDS round trip.
+template <int kSteps, int S0 = 0, int S1 = kSteps>
 __device__ __forceinline__ f32x16 gemm_lds(const Frags<kSteps>& a, const float* src, f32x16 acc, int lane) {
     const int h = lane >> 5, c = lane & 31;
+    constexpr int N = S1 - S0;
+    constexpr int L = SHIPENV_QT_LOOKAHEAD < N ? SHIPENV_QT_LOOKAHEAD : N;
+    if constexpr (L == 0) {
 #pragma unroll
-    for (int s = 0; s < kSteps; ++s) acc = mfma_f32(a.v[s], src[(2 * s + h) * kLS + c], acc);
+        for (int s = S0; s < S1; ++s) acc = mfma_f32(a.v[s], src[(2 * s + h) * kLS + c], acc);
+    } else {
+        float b[N];
+#pragma unroll
+        for (int i = 0; i < L; ++i) b[i] = src[(2 * (S0 + i) + h) * kLS + c];
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            if (i + L < N) b[i + L] = src[(2 * (S0 + i + L) + h) * kLS + c];
+            acc = mfma_f32(a.v[S0 + i], b[i], acc);
+        }
+#pragma unroll
+        for (int i = 0; i < L; ++i) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // the prologue reads
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            if (i + L < N) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // read k-step i + L
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                 // MFMA k-step i
+        }
+    }
     return acc;
 }
 
@@ -278,6 +310,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     int* ACT = reinterpret_cast<int*>(WT + 32);
     float* RW = WT + 64;            // [32] r_j
     float* DN = RW + 32;            // [32] done_j
+    int* FST = reinterpret_cast<int*>(DN + 32);  // [32] first(j): the dW3 slot of sample j
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wt = wave & 3;
     const bool tgt = wave >= 4;
     const int64_t r0 = (int64_t)blockIdx.x * kQT;
@@ -354,10 +387,20 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     // fc1, fc2 of both networks: online on states, target on next_states
     store_relu(tgt ? TA : HA, wt, gemm_lds(f1, tgt ? XN : X, acc1, lane), lane);
     __syncthreads(); QSTAMP(2); QCLOCK(14);
-    if (wave < A.d.mt3) fb.load(A.W.pw3t + wave * 64 * 64, lane);
+    // fc3's fragments (64 loads per lane, ~1 us of the CU's memory pipeline for 8 waves)
+    // are issued after fc2's first MFMAs: ahead of them, the chain's wait for its bias
+    // (the counter is in order) also waited for every fragment load
+    f32x16 acc = bias_init(tgt ? A.tg.b2 : A.on.b2, wt, lane, 128);
+    f32x16 acc3 = {};
     {
-        f32x16 acc = bias_init(tgt ? A.tg.b2 : A.on.b2, wt, lane, 128);
-        acc = gemm_lds(fa, tgt ? TA : HA, acc, lane);
+        acc = gemm_lds<64, 0, 2>(fa, tgt ? TA : HA, acc, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        if (wave < A.d.mt3) {
+            acc3 = bias_init(A.tg.b3, wave, lane, A.d.A);
+            fb.load(A.W.pw3t + wave * 64 * 64, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        acc = gemm_lds<64, 2, 64>(fa, tgt ? TA : HA, acc, lane);
         store_relu(tgt ? TB : HB, wt, acc, lane);
     }
     __syncthreads(); QSTAMP(3);
@@ -380,11 +423,10 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         }
         float m = -INFINITY;
         if (wave < A.d.mt3) {
-            f32x16 acc = bias_init(A.tg.b3, wave, lane, A.d.A);
-            acc = gemm_lds(fb, TB, acc, lane);
+            acc3 = gemm_lds(fb, TB, acc3, lane);
 #pragma unroll
             for (int r = 0; r < 16; ++r)
-                if (wave * 32 + acc_r(r, lane) < A.d.A) m = fmaxf(m, acc[r]);
+                if (wave * 32 + acc_r(r, lane) < A.d.A) m = fmaxf(m, acc3[r]);
         }
         if (!tgt) fb.load(A.W.pw2t + wt * 64 * 64, lane);  // dH1's operands
         m = fmaxf(m, __shfl_xor(m, 32));  // lane & 31 = sample
@@ -396,13 +438,21 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
                 acc[r] = row < A.d.A ? A.tg.b3[row] : 0.0f;
             }
             const float* hb = TB + (lane >> 4) * kLS + sh * 16 + (lane & 15);
+            constexpr int L = 8;  // B operands read L steps ahead (pinned as in gemm_lds)
+            float bq[32];
 #pragma unroll
-            for (int t0 = 0; t0 < 32; t0 += 8) {
-                float bv[8];
+            for (int i = 0; i < L; ++i) bq[i] = hb[4 * i * kLS];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) bv[i] = hb[4 * (t0 + i) * kLS];
+            for (int i = 0; i < 32; ++i) {
+                if (i + L < 32) bq[i + L] = hb[4 * (i + L) * kLS];
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[i], bq[i], acc, 0, 0, 0);
+            }
 #pragma unroll
-                for (int i = 0; i < 8; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[t0 + i], bv[i], acc, 0, 0, 0);
+            for (int i = 0; i < L; ++i) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+                if (i + L < 32) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             }
             float qm = -INFINITY;  // over this lane's 4 rows, then the 16 rows of the quadrant
 #pragma unroll
@@ -432,6 +482,20 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         s += __shfl_xor(s, 2);
         s += __shfl_xor(s, 4);
         s += __shfl_xor(s, 8);
+        // the first sample of the tile with sample qj's action (its dW3 slot): this thread
+        // tests samples 2 qpart and 2 qpart + 1, then a min over the 16 threads. Spread over
+        // the workgroup it is free; on wave 0's 32 lanes alone it cost 0.45 us (readlanes)
+        // and 2 us (a loop of dependent LDS reads).
+        {
+            const int aq = ACT[qj], k0 = 2 * qpart;
+            int fk = ACT[k0 + 1] == aq ? k0 + 1 : 32;
+            fk = ACT[k0] == aq ? k0 : fk;
+            fk = min(fk, __shfl_xor(fk, 1));
+            fk = min(fk, __shfl_xor(fk, 2));
+            fk = min(fk, __shfl_xor(fk, 4));
+            fk = min(fk, __shfl_xor(fk, 8));
+            if (qpart == 0) FST[qj] = fk;
+        }
         if (qpart == 0) {
             const float d = (s + A.on.b3[ACT[qj]]) - Y[qj];
             G[qj] = 2.0f * WT[qj] * d;
@@ -460,64 +524,71 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             DZ1[f * kLS + c] = HA[f * kLS + c] > 0.0f ? acc[r] : 0.0f;
         }
     } else {  // partial dW2[f2][f1] = sum_j dZ2[f2][j] h1[f1][j]: row tile wt, 4 column tiles
+        // the A operands (row tile wt of dZ2) once; each column tile's B operands read while
+        // the previous tile's chain runs
         float* out = A.W.part_w2 + (int64_t)blockIdx.x * 128 * 128;
+        float a2[16], b2[2][16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) a2[s] = DZ2[(wt * 32 + c) * kLS + 2 * s + h];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) b2[0][s] = HA[c * kLS + 2 * s + h];
+#pragma unroll
         for (int ct = 0; ct < 4; ++ct) {
             f32x16 acc = {};
 #pragma unroll
-            for (int s = 0; s < 16; ++s)
-                acc = mfma_f32(DZ2[(wt * 32 + c) * kLS + 2 * s + h], HA[(ct * 32 + c) * kLS + 2 * s + h], acc);
+            for (int s = 0; s < 16; ++s) {
+                if (ct < 3) b2[(ct + 1) & 1][s] = HA[((ct + 1) * 32 + c) * kLS + 2 * s + h];
+                acc = mfma_f32(a2[s], b2[ct & 1][s], acc);
+            }
 #pragma unroll
             for (int r = 0; r < 16; ++r) st_part(out + (wt * 32 + acc_r(r, lane)) * 128 + ct * 32 + c, acc[r]);
         }
-    }
-    // partial dW3[a][f] = sum_j (a_j == a) g_j h2[f][j] over the action tiles present:
-    // (row tile, column tile) pairs round-robin over the 8 waves; db3 by the wave of a row
-    // tile's first pair. Each lane holds the action and g of its 16 k-step samples
-    // j = 2s + h in registers, so an A operand is a compare and a select, and a pair's 16
-    // B operands are read from LDS in one batch ahead of its MFMA chain (reading ACT and G
-    // per MFMA put two dependent LDS round trips in front of every MFMA).
-    {
-        int aj[16];
-        float gj[16];
-        uint32_t pres = 0;
+        // pinned order: the operands of tile 0, then per tile its chain with the next tile's
+        // reads interleaved, then its stores (the compiler otherwise read each pair just
+        // before its two MFMAs)
+        __builtin_amdgcn_sched_group_barrier(0x100, 32, 0);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                if (ct < 3) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x040, 16, 0);
+        }
+        // partial dW3 over the tile's distinct actions, column tile wt: row r (slot r) =
+        // sum_j [first(j) = r] g_j h2[f][j]. A lane holds its 16 k-step samples' slots and g
+        // (j = 2s + h), so an A operand is a compare and a select; the 16 B operands are read
+        // from LDS in one batch ahead of the chain. Only the live slots' rows are stored.
+        const bool live_slot = FST[c] == c && r0 + c < A.B;
+        const uint32_t slots = (uint32_t)__ballot(live_slot);  // lanes 0-31 = slots 0-31
+        float bv[16], av[16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) bv[s] = HB[(wt * 32 + c) * kLS + 2 * s + h];
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
             const int j = 2 * s + h;
-            aj[s] = ACT[j];
-            gj[s] = G[j];
-            pres |= r0 + j < A.B ? 1u << (aj[s] >> 5) : 0u;
+            av[s] = FST[j] == c ? G[j] : 0.0f;
         }
-        const uint32_t present = __builtin_amdgcn_readfirstlane(pres | (uint32_t)__shfl_xor((int)pres, 32));
-        int k = 0;
-        for (int rt = 0; rt < A.d.mt3; ++rt) {
-            if (!((present >> rt) & 1u)) continue;  // block-uniform
-            const int a = rt * 32 + c;
-            for (int ct = 0; ct < 4; ++ct, ++k) {
-                if ((k & 7) != wave) continue;  // wave-uniform
-                float bv[16], av[16];
+        f32x16 acc = {};
 #pragma unroll
-                for (int s = 0; s < 16; ++s) bv[s] = HB[(ct * 32 + c) * kLS + 2 * s + h];
+        for (int s = 0; s < 16; ++s) acc = mfma_f32(av[s], bv[s], acc);
+        float* o3 = A.W.part_w3 + (int64_t)blockIdx.x * 32 * 128;
 #pragma unroll
-                for (int s = 0; s < 16; ++s) av[s] = aj[s] == a ? gj[s] : 0.0f;
-                f32x16 acc = {};
+        for (int r = 0; r < 16; ++r) {
+            const int row = acc_r(r, lane);
+            if ((slots >> row) & 1u) st_part(o3 + row * 128 + wt * 32 + c, acc[r]);
+        }
+        if (wt == 0) {  // db3 of slot c: the even samples' sum plus the odd samples' sum
+            float s3 = 0.0f;
 #pragma unroll
-                for (int s = 0; s < 16; ++s) acc = mfma_f32(av[s], bv[s], acc);
-                float* out = A.W.part_w3 + (((int64_t)blockIdx.x * A.d.mt3 + rt) * 32) * 128;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) st_part(out + acc_r(r, lane) * 128 + ct * 32 + c, acc[r]);
-                if (ct == 0) {  // db3[a]: the even samples' sum plus the odd samples' sum
-                    float s3 = 0.0f;
-#pragma unroll
-                    for (int s = 0; s < 16; ++s) s3 += av[s];
-                    const float o3 = __shfl_xor(s3, 32);
-                    if (h == 0) A.W.part_b3[((int64_t)blockIdx.x * A.d.mt3 + rt) * 32 + c] = s3 + o3;
-                }
+            for (int s = 0; s < 16; ++s) s3 += av[s];
+            const float x3 = __shfl_xor(s3, 32);
+            if (h == 0) {
+                A.W.part_b3[(int64_t)blockIdx.x * 32 + c] = s3 + x3;
+                A.W.part_map[(int64_t)blockIdx.x * 32 + c] = live_slot ? ACT[c] : -1;
             }
         }
-        if (tid == 0) A.W.present[blockIdx.x] = present;
-        // db3 of the absent action tiles is 0: stored, so T2 sums part_b3 with no presence test
-        if (tid < 32 * A.d.mt3 && !((present >> (tid >> 5)) & 1u))
-            A.W.part_b3[(int64_t)blockIdx.x * A.d.mt3 * 32 + tid] = 0.0f;
     }
     __syncthreads(); QSTAMP(8);  // dZ1 complete
     // partial dW1 (dynamic columns), db1, db2, loss and weight sums
@@ -646,30 +717,20 @@ __device__ __forceinline__ float block_sum256(float x, float* red) {
 }
 
 // sum over the tiles of 64 consecutive floats (src + t * stride + e0): thread (grp, q) adds
-// float4 q of tiles grp, grp + 16, ... (skipping tiles without `bit` in present[] when
-// present is given); the 16 groups then combine in a fixed order (xor 16 and 32 inside a
-// wave, then the four waves). Thread t < 64 returns element t of the 64.
-template <int kU>  // tiles per group and round (a round: presence words, then the loads)
-__device__ __forceinline__ float tile_sum64(const float* src, int64_t stride, int64_t e0, int64_t tiles,
-                                            const uint32_t* present, uint32_t bit, float4* red) {
+// float4 q of tiles grp, grp + 16, ...; the 16 groups then combine in a fixed order (xor 16
+// and 32 inside a wave, then the four waves). Thread t < 64 returns element t of the 64.
+template <int kU>  // tiles per group and round (a round: kU independent loads)
+__device__ __forceinline__ float tile_sum64(const float* src, int64_t stride, int64_t e0, int64_t tiles, float4* red) {
     const int t = threadIdx.x, q = t & 15, grp = t >> 4;
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     for (int64_t k0 = grp; k0 < tiles; k0 += 16 * kU) {  // kU tiles per round, loads independent
-        uint32_t pm[kU];
         float4 v[kU];
 #pragma unroll
         for (int i = 0; i < kU; ++i) {
             const int64_t k = k0 + 16 * i;
-            pm[i] = k < tiles ? (present ? present[k] & bit : 1u) : 0u;
+            v[i] = k < tiles ? *reinterpret_cast<const float4*>(src + k * stride + e0 + 4 * q)
+                             : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         }
-        // every load issues: an absent tile reads tile 0's line (cached) and is dropped, so
-        // the loads need no branch around each one
-#pragma unroll
-        for (int i = 0; i < kU; ++i)
-            v[i] = *reinterpret_cast<const float4*>(src + (pm[i] ? (k0 + 16 * i) * stride : 0) + e0 + 4 * q);
-#pragma unroll
-        for (int i = 0; i < kU; ++i)
-            if (!pm[i]) v[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
         for (int i = 0; i < kU; ++i) {
             acc.x += v[i].x;
@@ -697,36 +758,38 @@ __device__ __forceinline__ float tile_sum64(const float* src, int64_t stride, in
     return r;
 }
 
-// tile_sum64 over the tiles whose present[] word holds `bit` only (the W3 blocks: a 32-sample
-// tile holds about 3 of the 9-10 action tiles). Chunk by chunk of 1024 tiles, thread t tests
-// tiles 4t .. 4t + 3 and the block writes the present ones, in tile order, to an LDS list
-// (wave prefix by ballot popcounts, then the four wave offsets); thread (grp, q) then adds
-// float4 q of list entries grp, grp + 16, ... with kU independent loads per round, and the
-// groups combine as in tile_sum64. Only present partials are loaded: the branch-free form
-// requested every tile's line (an absent tile's from tile 0), 3x the bytes.
+// dW3 row a and db3[a] summed over the tiles in tile order. A tile holds action a in at
+// most one slot (its slot map, T1). Chunk by chunk of 256 tiles, thread t scans tile
+// c0 + t's 32 map entries (8 int4 loads) for a; the tiles that hold it are listed in tile
+// order (wave ballot prefix, then the four wave offsets); thread (grp, q) then adds
+// float4 q of the rows of list entries grp, grp + 8, ... with kU independent loads per
+// round, and the 8 groups combine in a fixed tree. However the actions are spread, a row
+// sums at most one partial per tile. Thread t < 128 returns dW3[a][t], thread 128 db3[a].
 template <int kU>
-__device__ __forceinline__ float tile_sum64_present(const float* src, int64_t stride, int64_t e0, int64_t tiles,
-                                                    const uint32_t* present, uint32_t bit, float4* red, int* list,
-                                                    int* wtot) {
-    const int t = threadIdx.x, q = t & 15, grp = t >> 4, lane = t & 63, w = t >> 6;
+__device__ __forceinline__ float slot_row_sum(const float* w3, const float* b3, const int32_t* map, int64_t tiles,
+                                              int a, float4* red, int* list, int* wtot) {
+    const int t = threadIdx.x, q = t & 31, grp = t >> 5, lane = t & 63, w = t >> 6;
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    for (int64_t c0 = 0; c0 < tiles; c0 += 4 * kQRBlock) {
-        uint32_t m = 0;
+    float accb = 0.0f;
+    for (int64_t c0 = 0; c0 < tiles; c0 += kQRBlock) {
+        const int64_t tt = c0 + t;
+        int slot = -1;
+        if (tt < tiles) {
+            const int4* mp = reinterpret_cast<const int4*>(map + tt * 32);
+            int4 v[8];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int64_t k = c0 + 4 * t + j;
-            m |= (k < tiles && (present[k] & bit)) ? 1u << j : 0u;
-        }
-        // exclusive prefix of popc(m) over the block: per bit-plane ballots within the wave
-        const uint64_t below = (1ull << lane) - 1ull;
-        int pre = 0, tot = 0;
+            for (int i = 0; i < 8; ++i) v[i] = mp[i];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint64_t b = __ballot((m >> j) & 1u);
-            pre += __popcll(b & below);
-            tot += __popcll(b);
+            for (int i = 0; i < 8; ++i) {
+                slot = v[i].x == a ? 4 * i : slot;
+                slot = v[i].y == a ? 4 * i + 1 : slot;
+                slot = v[i].z == a ? 4 * i + 2 : slot;
+                slot = v[i].w == a ? 4 * i + 3 : slot;
+            }
         }
-        if (lane == 0) wtot[w] = tot;
+        const uint64_t bal = __ballot(slot >= 0);
+        const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) wtot[w] = __popcll(bal);
         __syncthreads();
         int off = 0, total = 0;
 #pragma unroll
@@ -734,19 +797,22 @@ __device__ __forceinline__ float tile_sum64_present(const float* src, int64_t st
             off += v < w ? wtot[v] : 0;
             total += wtot[v];
         }
-        int pos = off + pre;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if ((m >> j) & 1u) list[pos++] = (int)(4 * t + j);
+        if (slot >= 0) list[off + pre] = t * 32 + slot;  // the row within the chunk
         __syncthreads();
-        for (int i0 = grp; i0 < total; i0 += 16 * kU) {
+        for (int i0 = grp; i0 < total; i0 += 8 * kU) {
             float4 v[kU];
+            float vb[kU];
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
-                const int i = i0 + 16 * u;
-                const int64_t k = c0 + (i < total ? list[i] : 0);
-                v[u] = *reinterpret_cast<const float4*>(src + k * stride + e0 + 4 * q);
-                if (i >= total) v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                const int i = i0 + 8 * u;
+                const bool ok = i < total;
+                const int64_t row = c0 * 32 + (ok ? list[i] : 0);
+                v[u] = *reinterpret_cast<const float4*>(w3 + row * 128 + 4 * q);
+                vb[u] = b3[row];
+                if (!ok) {
+                    v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                    vb[u] = 0.0f;
+                }
             }
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
@@ -754,40 +820,41 @@ __device__ __forceinline__ float tile_sum64_present(const float* src, int64_t st
                 acc.y += v[u].y;
                 acc.z += v[u].z;
                 acc.w += v[u].w;
+                accb += vb[u];
             }
         }
         __syncthreads();  // list and wtot are rewritten by the next chunk
     }
-#pragma unroll
-    for (int m = 16; m <= 32; m <<= 1) {
-        acc.x += __shfl_xor(acc.x, m);
-        acc.y += __shfl_xor(acc.y, m);
-        acc.z += __shfl_xor(acc.z, m);
-        acc.w += __shfl_xor(acc.w, m);
-    }
-    if ((t & 63) < 16) red[(t >> 6) * 16 + q] = acc;
+    red[grp * 32 + q] = acc;
+    float* rb = reinterpret_cast<float*>(list);  // free after the last chunk's barrier
+    if (q == 0) rb[grp] = accb;
     __syncthreads();
     float r = 0.0f;
-    if (t < 64) {
-        const int j = t >> 2, c = t & 3;
+    if (t < 128) {
+        const int qq = t >> 2, c = t & 3;
         const float* f = reinterpret_cast<const float*>(red);
-        r = (f[4 * j + c] + f[4 * (16 + j) + c]) + (f[4 * (32 + j) + c] + f[4 * (48 + j) + c]);
+        float e[8];
+#pragma unroll
+        for (int g = 0; g < 8; ++g) e[g] = f[4 * (g * 32 + qq) + c];
+        r = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
+    } else if (t == 128) {
+        r = ((rb[0] + rb[1]) + (rb[2] + rb[3])) + ((rb[4] + rb[5]) + (rb[6] + rb[7]));
     }
-    __syncthreads();  // red may be reused
+    __syncthreads();  // red and list may be reused
     return r;
 }
 
 __device__ __forceinline__ float comp(const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
 
 // Workgroups: [0, 128) W1 row f (+ b1, the fold, the loss at f = 0); [128, 384) W2 64-element
-// blocks (+ b2 on a row's first block); then mt3 x 64 W3 blocks of the [rt][32][128] layout;
-// then mt3 b3 blocks (tile rt's 32 biases).
+// blocks (+ b2 on a row's first block); then mt3 x 32 W3 rows (+ b3 of the row).
 __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
     __shared__ float red[kQRBlock];
     __shared__ float4 red4[kQRBlock];
     __shared__ float sums[8];
     __shared__ float rowbuf[6 + 4 * SE_MAX_PORTS];  // W1 blocks: the updated row, for the folds
-    __shared__ int list[4 * kQRBlock];              // W3 blocks: the present tiles of a chunk
+    __shared__ float portbuf[4 * SE_MAX_PORTS];     // W1 blocks: the port block, for the folds
+    __shared__ int list[kQRBlock];                  // W3 rows: the tiles of a chunk that hold the row
     __shared__ int wtot[kQRBlock / 64];
     const int tid = threadIdx.x, in = A.d.in;
     QSTAMP(10);  // T2's stamps: slots 10-13 of the same rows (4 waves)
@@ -798,9 +865,12 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
     // sum (inv is first needed by the Adam step), so the two round trips overlap
     const int mode = A.mode;  // block-uniform
     float* G = A.grad;
-    float wsum = 0.0f;
+    float wsum = 0.0f, lsum = 0.0f;  // lsum: the loss sum, W1 block 0 (mode 0) only
     if (mode == 0 || (mode == 1 && blockIdx.x == 0))
-        for (int64_t t = tid; t < A.tiles; t += kQRBlock) wsum += A.W.part_lw[2 * t + 1];
+        for (int64_t t = tid; t < A.tiles; t += kQRBlock) {
+            wsum += A.W.part_lw[2 * t + 1];
+            if (mode == 0 && blockIdx.x == 0) lsum += A.W.part_lw[2 * t];
+        }
     auto weight_inv = [&]() {
         return 1.0f / fmaxf(mode == 2 ? G[Grad::lw(A.d) + 1] : block_sum256(wsum, red), 1.0f);
     };
@@ -812,6 +882,9 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         // the Adam operands of this thread's columns (tid, tid + 256: in <= 262) and of b1, loaded
         // now so their round trip overlaps the sums
         float pw[2] = {0.f, 0.f}, pm[2] = {0.f, 0.f}, pv[2] = {0.f, 0.f}, bw = 0.f, bm = 0.f, bv = 0.f;
+        // the port block (in - 6 <= 256 values): one per thread, into LDS before the sums'
+        // barrier, so the Adam step and the folds read it there (they waited on a global load)
+        const float port_c = mode != 1 && tid < in - 6 ? A.W.portvec[tid] : 0.0f;
         if (mode != 1) {
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
@@ -834,6 +907,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
 #pragma unroll
             for (int c = 0; c < 6; ++c) x[c] = G[Grad::w1d + f * 6 + c];
             x[6] = G[Grad::b1 + f];
+            if (tid < in - 6) portbuf[tid] = port_c;  // visible after the barrier below
         } else {
             for (int64_t t = tid; t < A.tiles; t += kQRBlock) {
                 const float* p = A.W.part_w1d + (t * 128 + f) * 6;
@@ -841,6 +915,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                 for (int c = 0; c < 6; ++c) x[c] += p[c];
                 x[6] += A.W.part_b1[t * 128 + f];
             }
+            if (mode == 0 && tid < in - 6) portbuf[tid] = port_c;  // visible after block_sum's barrier
             block_sum<7>(x, red);
             if (mode == 1) {
                 if (tid == 0) {
@@ -872,7 +947,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         for (int u = 0; u < 2; ++u) {
             const int c = tid + u * kQRBlock;
             if (c >= in) continue;
-            const float g = (c < 6 ? sums[c] : s1 * A.W.portvec[c - 6]) * inv;
+            const float g = (c < 6 ? sums[c] : s1 * portbuf[c - 6]) * inv;
             const int64_t i = (int64_t)f * in + c;
             float mm = pm[u], vv = pv[u];
             const float p = adam(pw[u], g, mm, vv);
@@ -898,13 +973,13 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         __syncthreads();  // the new row (rowbuf) and b1 are complete before the folds read them
         const float b1 = sums[7];
         if (tid == 0) A.on.b1[f] = b1;
-        const float xf = fold_row(rowbuf, in, A.W.portvec, red);  // the pack kernel's bits
+        const float xf = fold_row(rowbuf, in, portbuf, red);  // the pack kernel's bits
         if (tid == 0) A.W.c1[0][f] = b1 + xf;
         if (A.img[0] && tid == 0) {  // the policy's b1: qnet_pack_kernel's f64 fold, same order
             double acc = (double)b1;
             for (int p = 0; p < A.d.P; ++p) {
                 const float* wp = rowbuf + 6 + 4 * p;
-                const float* pv = A.W.portvec + 4 * p;
+                const float* pv = portbuf + 4 * p;
                 acc += (double)wp[0] * (double)pv[0] + (double)wp[1] * (double)pv[1] +
                        (double)wp[2] * (double)pv[2] + (double)wp[3] * (double)pv[3];
             }
@@ -913,13 +988,8 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         }
         if (f == 0) {  // the loss: sum w d^2 / sum w
             float loss;
-            if (mode == 2) {
-                loss = G[Grad::lw(A.d)];
-            } else {
-                float l = 0.0f;
-                for (int64_t t = tid; t < A.tiles; t += kQRBlock) l += A.W.part_lw[2 * t];
-                loss = block_sum256(l, red);
-            }
+            // (mode 0: this thread's share was loaded at the start, with the weight sum)
+            loss = mode == 2 ? G[Grad::lw(A.d)] : block_sum256(lsum, red);
             if (tid == 0) *A.loss_out = loss * inv;
         }
     } else if (b < 384) {  // W2 elements e0 .. e0 + 63 (row-major [f2][f1])
@@ -944,7 +1014,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         if (mode == 2) {
             g = tid < 64 ? G[Grad::w2 + e0 + tid] : 0.0f;
         } else {
-            g = tile_sum64<16>(A.W.part_w2, 128 * 128, e0, A.tiles, nullptr, 0, red4);
+            g = tile_sum64<16>(A.W.part_w2, 128 * 128, e0, A.tiles, red4);
             if (mode == 1) {
                 if (tid < 64) G[Grad::w2 + e0 + tid] = g;
                 if ((e0 & 127) == 0) {
@@ -989,103 +1059,56 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                     for (int l = 0; l < 2; ++l) reinterpret_cast<float*>(A.img[l] + A.q[l].b2())[f2] = p;
             }
         }
-    } else if (b < 384 + 64 * A.d.mt3) {  // W3 block: tile rt, elements e0 .. e0 + 63 of its [32][128]
-        const int k = b - 384, rt = k >> 6;
-        const int64_t e0 = (int64_t)(k & 63) * 64;
-        const uint32_t bit = 1u << rt;
-        const int a3 = rt * 32 + (int)((e0 + tid) >> 7), f3 = (int)((e0 + tid) & 127);
+    } else {  // W3 row a3 and b3[a3] (rows up to mt3 x 32: the padding rows' sums are 0)
+        const int a3 = b - 384;
+        const bool row_live = a3 < A.d.A;
+        const int f3 = tid;  // threads < 128: element f3 of the row; thread 128: b3
         const int64_t i3 = (int64_t)a3 * 128 + f3;
-        const bool own = tid < 64 && a3 < A.d.A;  // this thread's element, if it has one
-        float pw = 0.f, pm = 0.f, pv = 0.f;  // its Adam operands, loaded ahead of the sums
-        if (mode != 1 && own) {
-            pw = A.on.w3[i3];
-            pm = A.m.w3[i3];
-            pv = A.v.w3[i3];
+        float pw = 0.f, pm = 0.f, pv = 0.f;  // the Adam operands, loaded ahead of the sums
+        if (mode != 1 && row_live) {
+            if (tid < 128) {
+                pw = A.on.w3[i3];
+                pm = A.m.w3[i3];
+                pv = A.v.w3[i3];
+            } else if (tid == 128) {
+                pw = A.on.b3[a3];
+                pm = A.m.b3[a3];
+                pv = A.v.b3[a3];
+            }
         }
-        float g;
+        float g = 0.0f;  // dW3[a3][tid] (tid < 128) or db3[a3] (tid = 128)
         if (mode == 2) {
-            g = tid < 64 ? G[Grad::w3 + (int64_t)rt * 32 * 128 + e0 + tid] : 0.0f;
+            if (tid < 128) g = G[Grad::w3 + i3];
+            else if (tid == 128) g = G[Grad::b3(A.d) + a3];
         } else {
-            g = tile_sum64_present<16>(A.W.part_w3 + (int64_t)rt * 32 * 128, (int64_t)A.d.mt3 * 32 * 128, e0,
-                                      A.tiles, A.W.present, bit, red4, list, wtot);
+            g = slot_row_sum<16>(A.W.part_w3, A.W.part_b3, A.W.part_map, A.tiles, a3, red4, list, wtot);
             if (mode == 1) {
-                if (tid < 64) G[Grad::w3 + (int64_t)rt * 32 * 128 + e0 + tid] = g;
+                if (tid < 128) G[Grad::w3 + i3] = g;
+                else if (tid == 128) G[Grad::b3(A.d) + a3] = g;
                 return;
             }
         }
         const float inv = weight_inv();
         QSTAMP(12);
-        if (own) {
+        if (row_live && tid <= 128) {
             const float p = adam(pw, g * inv, pm, pv);
-            A.m.w3[i3] = pm;
-            A.v.w3[i3] = pv;
-            A.on.w3[i3] = p;
+            if (tid < 128) {
+                A.m.w3[i3] = pm;
+                A.v.w3[i3] = pv;
+                A.on.w3[i3] = p;
+            } else {
+                A.m.b3[a3] = pm;
+                A.v.b3[a3] = pv;
+                A.on.b3[a3] = p;
+            }
             if (A.img[0])
 #pragma unroll
                 for (int l = 0; l < 2; ++l) {
                     const int row = row_of_action(A.q[l], a3);
-                    if (row >= 0) put_bf16(A.img[l] + A.q[l].w3() + pol_offset(row, f3), p);
+                    if (row < 0) continue;
+                    if (tid < 128) put_bf16(A.img[l] + A.q[l].w3() + pol_offset(row, f3), p);
+                    else reinterpret_cast<float*>(A.img[l] + A.q[l].b3())[row] = p;
                 }
-        }
-    } else {  // b3 of rows 32 rt .. 32 rt + 31: 32 rows x 8 tile groups
-        // its own workgroup: behind a W3 block's sum it was the kernel's critical path.
-        // Tiles grp, grp + 8, ... in order, kU independent loads per round (T1 stores 0 for
-        // an absent action tile, so no presence test: a conditional load per tile kept these
-        // blocks busy 3x as long as the rest of the kernel)
-        const int rt = b - 384 - 64 * A.d.mt3;
-        const int a3 = rt * 32 + (tid & 31);
-        const bool own = tid < 32 && a3 < A.d.A;
-        float pw = 0.f, pm = 0.f, pv = 0.f;  // the Adam operands, loaded ahead of the sums
-        if (mode != 1 && own) {
-            pw = A.on.b3[a3];
-            pm = A.m.b3[a3];
-            pv = A.v.b3[a3];
-        }
-        float s3;
-        if (mode == 2) {
-            s3 = G[Grad::b3(A.d) + rt * 32 + (tid & 31)];
-        } else {
-            const int r = tid & 31, grp = tid >> 5;
-            float x = 0.0f;
-            constexpr int kU = 32;  // 256 tiles (B = 8192) in one round
-            for (int64_t t0 = grp; t0 < A.tiles; t0 += 8 * kU) {
-                float v[kU];
-#pragma unroll
-                for (int i = 0; i < kU; ++i)
-                    v[i] = t0 + 8 * i < A.tiles ? A.W.part_b3[((t0 + 8 * i) * A.d.mt3 + rt) * 32 + r] : 0.0f;
-#pragma unroll
-                for (int i = 0; i < kU; ++i) x += v[i];
-            }
-            QSTAMP(12);
-            __syncthreads();
-            red[tid] = x;
-            __syncthreads();
-#pragma unroll
-            for (int s = 4; s > 0; s >>= 1) {
-                if (grp < s) red[tid] += red[tid + 32 * s];
-                __syncthreads();
-            }
-            s3 = red[tid & 31];
-            __syncthreads();  // weight_inv reuses red
-            if (mode == 1) {
-                if (tid < 32) G[Grad::b3(A.d) + rt * 32 + tid] = s3;
-                return;
-            }
-        }
-        {
-            const float inv = weight_inv();
-            if (own) {
-                const float p = adam(pw, s3 * inv, pm, pv);
-                A.m.b3[a3] = pm;
-                A.v.b3[a3] = pv;
-                A.on.b3[a3] = p;
-                if (A.img[0])
-#pragma unroll
-                    for (int l = 0; l < 2; ++l) {
-                        const int row = row_of_action(A.q[l], a3);
-                        if (row >= 0) reinterpret_cast<float*>(A.img[l] + A.q[l].b3())[row] = p;
-                    }
-            }
         }
     }
     QSTAMP(13);
@@ -1142,8 +1165,8 @@ int se_qtrain_create(se_qtrain** out, se_env* env, int64_t max_batch) {
     const size_t mt3 = (size_t)q->d.mt3;
     const size_t sizes[] = {4 * 3 * 64, 4 * 3 * 64, 4 * 64 * 64, 4 * 64 * 64, 4 * 64 * 64,
                             mt3 * 64 * 64, 128, 128, (size_t)(4 * P),
-                            T * 128 * 128, T * 128 * 6, T * 128, T * 128, T * 2, T * mt3 * 32 * 128,
-                            T * mt3 * 32, T};
+                            T * 128 * 128, T * 128 * 6, T * 128, T * 128, T * 2, T * 32 * 128,
+                            T * 32, T * 32};
     size_t total = 0, off[17];
     for (int i = 0; i < 17; ++i) {
         off[i] = total;
@@ -1157,7 +1180,7 @@ int se_qtrain_create(se_qtrain** out, se_env* env, int64_t max_batch) {
     auto at = [&](int i) { return b + off[i] / 4; };
     q->W = QtWork{{at(0), at(1)}, {at(2), at(3)}, at(4), at(5), {at(6), at(7)}, at(8),
                   at(9), at(10), at(11), at(12), at(13), at(14), at(15),
-                  reinterpret_cast<uint32_t*>(at(16))};
+                  reinterpret_cast<int32_t*>(at(16))};
     *out = q;
     return SE_OK;
 }
@@ -1238,7 +1261,7 @@ int qtrain_step(se_qtrain* q, se_qnet* qn, int64_t batch, const float* obs, cons
     DeviceGuard g(q->device);
     const hipStream_t s = (hipStream_t)stream;
     const int64_t tiles = (batch + kQT - 1) / kQT;
-    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 7 * 32) * 4;
+    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 8 * 32) * 4;
     static std::atomic<uint64_t> lds_set{0};
     rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(qtrain_tile_kernel), (int)lds, q->device);
     if (rc) return rc;
@@ -1251,7 +1274,7 @@ int qtrain_step(se_qtrain* q, se_qnet* qn, int64_t batch, const float* obs, cons
     // T2 counts Adam steps from ctr[1] (set by T1) when T1 drew the batch, and syncs ctr[0]
     const QtAdamArgs B = adam_args(q, qn, batch, act, lr, beta1, beta2, eps, ring ? step_dev + 1 : step_dev,
                                    loss_out, qn || ring ? 1 : 0, grad ? 1 : 0, grad, ring ? step_dev : nullptr);
-    qtrain_adam_kernel<<<384 + 65 * q->d.mt3, kQRBlock, 0, s>>>(B);
+    qtrain_adam_kernel<<<384 + 32 * q->d.mt3, kQRBlock, 0, s>>>(B);
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }
@@ -1304,7 +1327,7 @@ int se_qtrain_apply(se_qtrain* q, se_qnet* qn, const float* grad, float lr, floa
     DeviceGuard g(q->device);
     const QtAdamArgs B = adam_args(q, qn, 0, nullptr, lr, beta1, beta2, eps, step_dev, loss_out, 0, 2,
                                    const_cast<float*>(grad));
-    qtrain_adam_kernel<<<384 + 65 * q->d.mt3, kQRBlock, 0, (hipStream_t)stream>>>(B);
+    qtrain_adam_kernel<<<384 + 32 * q->d.mt3, kQRBlock, 0, (hipStream_t)stream>>>(B);
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }

@@ -54,8 +54,9 @@ def main():
     d = np.diff(wgmax, axis=1)
     out["phase_median_us"] = {phases[k + 1]: round(float(np.median(d[:, k])), 3) for k in range(9)}
     out["start_spread_us"] = float(np.percentile(rel[:, :, 0].min(axis=1), 99))
-    # T2 (slots 10-13, 4 waves): W1 rows [0, 128), W2 blocks [128, 384), W3 blocks, then b3 blocks
-    nb = 384 + 64 * ((4 + int(env.P) + 250 + 31) // 32)
+    # T2 (slots 10-13, 4 waves): W1 rows [0, 128), W2 blocks [128, 384), then one block per
+    # W3 row (mt3 x 32 rows, b3 with its row)
+    nb = 384 + 32 * ((4 + int(env.P) + 250 + 31) // 32)
     t2 = buf.reshape(wg, 8, stamps)[:nb, :4, 10:14].astype(np.int64)
     t20 = t2[:, :, 0].min()
     r2 = (t2 - t20) / 100.0
@@ -67,16 +68,6 @@ def main():
         out["t2_" + name] = {"start_p50": float(np.median(w2[lo:hi, 0])), "start_max": float(w2[lo:hi, 0].max()),
                              "wsum": float(np.median(d2[:, 0])), "sum": float(np.median(d2[:, 1])),
                              "adam": float(np.median(d2[:, 2])), "end_max": float(w2[lo:hi, 3].max())}
-    mt3 = (nb - 384) // 64
-    b3 = buf.reshape(wg, 8, stamps)[nb:nb + mt3, :4, 10:14].astype(np.int64)
-    rb = (b3 - t20) / 100.0
-    wb = rb.max(axis=1)
-    out["t2_b3"] = {"start": [round(float(v), 2) for v in rb[:, :, 0].min(axis=1)],
-                    "after_wsum": [round(float(v), 2) for v in wb[:, 1]],
-                    "after_loop": [round(float(v), 2) for v in wb[:, 2]],
-                    "end": [round(float(v), 2) for v in wb[:, 3]]}
-    out["t2_w3_sum_by_tile_p50"] = [round(float(np.median(np.diff(w2[384 + k * 64:384 + (k + 1) * 64], axis=1)[:, 1])), 2)
-                                    for k in range(mt3)]
     cyc = buf.reshape(wg, 8, stamps)[:tiles, :, 14:16].astype(np.int64)
     rt = buf.reshape(wg, 8, stamps)[:tiles, :, [2, 4]].astype(np.int64)
     ghz = (cyc[:, :, 1] - cyc[:, :, 0]) / ((rt[:, :, 1] - rt[:, :, 0]) * 10.0)  # cycles per ns
