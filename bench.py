@@ -185,8 +185,11 @@ def run_config(n, ports, auto, args, dist, label, preroll=0, step_seq=False):
         row = torch.empty(n, dtype=torch.int32, device=env.device)
         for t in range(preroll):  # action rows of their own (t offset past the timed rows)
             env.step(env.gen_actions(1_000_000 + t, out=row))
-    for k in range(args.warmup):
-        env.step(acts[k])
+    for k in range(args.warmup):  # the timed leg's own issue path (and kernel) warmed up
+        if step_seq:
+            env.step_seq(acts[k:k + 1])
+        else:
+            env.step(acts[k])
     if auto:  # the stats path runs inside the timed region: load its kernels now
         dist.D.reduce_episode_stats(env.episode_stats().clone())
     torch.cuda.synchronize()
@@ -507,7 +510,7 @@ def run_dqn_train(n, args, dist):
 
 
 KERNEL_MS_BASIS = ("HIP events on the launch stream, end of launch 1 to end of launch K, over K - 1 launches "
-                   "(rocprofv3 kernel-trace averages of the driver's command: profiles/r03/kt_legs_driver.json, "
+                   "(rocprofv3 kernel-trace averages of the driver's command: profiles/r03c/kt_legs.json, "
                    "printed per leg as rocprof_trace from profiles/rocprof_legs.json)")
 
 
@@ -547,9 +550,11 @@ TRACE_SUMMARY = os.path.join("profiles", "rocprof_legs.json")  # profiles/r03/kt
 def rocprof_leg(key):
     """The committed kernel-trace average of one leg under the driver's bench command
     (tools/trace_driver.sh -> tools/kt_legs.py), printed beside the live events figure.
-    The tracer's per-dispatch cost lengthens each 2^20-env launch by ~0.8 us (the same
-    launches unprofiled, tools/diag/issue_forms.py); at 2^24 the two
-    agree."""
+    The headline's launches (se_step_seq) are a trace row of their own,
+    step_kernel<false, false, false, true, false, true>: W + K calls, back to back under the
+    tracer too. Legs issued one Python call per launch leave the traced GPU idle between
+    launches, which lengthens each 2^20-env launch; at 2^24 every
+    form agrees."""
     path = os.path.join(ROOT, TRACE_SUMMARY)
     if not os.path.exists(path):
         return None
@@ -628,12 +633,13 @@ def main():
     n = args.n
     # config 3 from reset first (ships at their origin ports, cargo rising: the first steps'
     # state mix; DESIGN.md section 5, "The short run"), then the headline leg in steady
-    # state, then the headline leg issued through VecEnv.step_seq
+    # state, its K steps issued by VecEnv.step_seq (the native launch loop, whose kernel has
+    # a trace name of its own), then the same steady leg with one VecEnv.step call per step
     el3r, k3r, _, _ = run_config(n, None, False, args, dist, "config3-from-reset", preroll=0)
-    el3, k3, _, info3 = run_config(n, None, False, args, dist, "config3", preroll=args.preroll3)
+    el3, k3, _, info3 = run_config(n, None, False, args, dist, "config3", preroll=args.preroll3,
+                                   step_seq=True)
     value = n * dist.world * args.steps / el3
-    el3s, k3s, _, _ = run_config(n, None, False, args, dist, "config3-step-seq", preroll=args.preroll3,
-                                 step_seq=True)
+    el3p, k3p, _, _ = run_config(n, None, False, args, dist, "config3-step-py", preroll=args.preroll3)
     out = {
         "metric": "env-steps/sec at N=2^20 parallel envs per GPU (config 3: full step, 5 default ports)",
         "value": round(value, 1),
@@ -651,8 +657,9 @@ def main():
             "workload": "BASELINE configs[2]: N=2^20 envs/GPU, full step, default 5 ports; steady state "
                         f"mix as in the survey's 1000-step run: {args.preroll3} untimed pre-roll steps from "
                         "reset before the warm-up (from_reset: the same leg timed right after reset); "
-                        "one VecEnv.step call per step (step_seq: the same leg issued by "
-                        "VecEnv.step_seq, the native launch loop); "
+                        "the K timed steps issued by VecEnv.step_seq (se_step_seq, the native launch loop: "
+                        "its kernel, step_kernel<..., true>, is the trace row of exactly these launches; "
+                        "step_py: the same leg with one VecEnv.step call per step); "
                         f"roofline.kernel_ms: {KERNEL_MS_BASIS}",
             "preroll_steps": args.preroll3,
             "envs_per_gpu": n,
@@ -665,13 +672,13 @@ def main():
                        "ms_per_step": round(el3r / args.steps * 1e3, 5),
                        "kernel_ms": round(k3r, 5),
                        "frac": roofline(BYTES_STEP, n, k3r, CANONICAL_STEP)["frac"]},
-        "step_seq": {"value": round(n * dist.world * args.steps / el3s, 1),
-                     "ms_per_step": round(el3s / args.steps * 1e3, 5),
-                     "kernel_ms": round(k3s, 5),
-                     "frac": roofline(BYTES_STEP, n, k3s, CANONICAL_STEP)["frac"]},
+        "step_py": {"value": round(n * dist.world * args.steps / el3p, 1),
+                    "ms_per_step": round(el3p / args.steps * 1e3, 5),
+                    "kernel_ms": round(k3p, 5),
+                    "frac": roofline(BYTES_STEP, n, k3p, CANONICAL_STEP)["frac"]},
     }
     for key, obj in (("config3", out["roofline"]), ("config3_from_reset", out["from_reset"]),
-                     ("config3_step_seq", out["step_seq"])):
+                     ("config3_step_py", out["step_py"])):
         obj["rocprof_trace"] = rocprof_leg(key)
     traffic, src = pmc_traffic()
     if traffic:

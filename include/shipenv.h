@@ -147,8 +147,10 @@ int se_step(se_env* env, const int32_t* actions, void* stream);
  * from actions + k * ld (ld >= n int32 entries, 16-byte aligned rows). The same
  * launches as a host loop over se_step, without the caller's per-step overhead, so a
  * fixed action schedule keeps the GPU queue full (a rollout of a pre-computed policy,
- * the bench's timed region). reward/done/err hold the last step's outputs. An
- * extension: the reference steps one call at a time (environment.py:359-376). */
+ * the bench's timed region). reward/done/err hold the last step's outputs. The kernel
+ * is the same code as se_step's, under a name of its own in a kernel trace (without
+ * auto-reset). An extension: the reference steps one call at a time
+ * (environment.py:359-376). */
 int se_step_seq(se_env* env, const int32_t* actions, int64_t ld, int32_t steps, void* stream);
 
 /* step() with the reference's typed action [ActionType, value] (environment.py:359-376):

@@ -1669,7 +1669,10 @@ __device__ __forceinline__ void wave_compact(const StepArgs& A, const Finished& 
 #ifndef SHIPENV_STEP_WPE
 #define SHIPENV_STEP_WPE 4  // minimum waves per SIMD the register allocation must allow
 #endif
-template <bool kTyped, bool kReplay, bool kAuto, bool kNt = false, bool kRec = false>
+// kSeq: the same code, instantiated apart for se_step_seq's launches (the agent path without
+// auto-reset), so a kernel trace lists them under a name of their own: bench.py's headline leg
+// issues its timed steps that way, and its trace row then holds exactly those launches.
+template <bool kTyped, bool kReplay, bool kAuto, bool kNt = false, bool kRec = false, bool kSeq = false>
 __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(SHIPENV_STEP_WPE))) void step_kernel(StepArgs A) {
     static_assert(!kRec || (kAuto && !kTyped && !kReplay), "se_step_record: agent actions, auto-reset");
     extern __shared__ uint32_t lds[];
@@ -2527,7 +2530,8 @@ int check_ready(se_env* env) {
 }
 
 int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const int32_t* a,
-                const int32_t* b, se_tape* tape, void* stream, const StepRecord* rec = nullptr) {
+                const int32_t* b, se_tape* tape, void* stream, const StepRecord* rec = nullptr,
+                bool seq = false) {
     int rc = check_ready(env);
     if (rc) return rc;
     if (!act || (typed && (!a || !b)) || (replay && !tape))
@@ -2570,6 +2574,10 @@ int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const 
         HIP_TRY(hipGetLastError());
     } else if (env->n >= kEnvsPerThread) {  // at least one full group (step_kernel's first load assumes it)
         if (!typed && replay) step_kernel<false, true, false><<<grid, kStepBlock, lds, s>>>(A);  // agent replay
+        else if (seq && !typed && !autoreset && ntl)
+            step_kernel<false, false, false, true, false, true><<<grid, kStepBlock, lds, s>>>(A);
+        else if (seq && !typed && !autoreset)
+            step_kernel<false, false, false, false, false, true><<<grid, kStepBlock, lds, s>>>(A);
         else if (!typed && !autoreset && ntl) step_kernel<false, false, false, true><<<grid, kStepBlock, lds, s>>>(A);
         else if (!typed && autoreset && ntl) step_kernel<false, false, true, true><<<grid, kStepBlock, lds, s>>>(A);
         else if (!typed && !autoreset) step_kernel<false, false, false><<<grid, kStepBlock, lds, s>>>(A);
@@ -2732,7 +2740,7 @@ int se_step_seq(se_env* env, const int32_t* actions, int64_t ld, int32_t steps, 
     if (steps < 0) return fail(SE_EINVAL, "negative step count");
     if (steps > 1 && (ld < env->n || (ld & 3))) return fail(SE_EINVAL, "row stride must be >= n and a multiple of 4");
     for (int32_t k = 0; k < steps; ++k) {
-        rc = launch_step(env, false, false, actions + (int64_t)k * ld, nullptr, nullptr, nullptr, stream);
+        rc = launch_step(env, false, false, actions + (int64_t)k * ld, nullptr, nullptr, nullptr, stream, nullptr, true);
         if (rc) return rc;
     }
     return SE_OK;

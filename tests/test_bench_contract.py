@@ -41,7 +41,7 @@ def test_committed_trace_summary_covers_every_leg():
     profiles/rocprof_legs.json, a file outside the gpurun-ignored profiles/r0* directories, so
     the GPU box's run sees it; every timed leg must be in it, with a frac below 1."""
     b = _bench()
-    for key in ("config3", "config3_from_reset", "config3_step_seq", "config4", "large_n",
+    for key in ("config3", "config3_from_reset", "config3_step_py", "config4", "large_n",
                 "large_n_from_reset"):
         r = b.rocprof_leg(key)
         assert r is not None, key

@@ -4,12 +4,15 @@
 
 bench.py runs its legs in a fixed order, so the step launches of each leg are the
 next dispatches of that leg's kernel instantiation in the trace:
-  config 3   step_kernel<false, false, false, true, false>  (kNt loads, N = 2^20): the from-reset
-             leg's W + K launches, then the headline leg's P3 pre-roll steps (--preroll3,
-             bench.py's default 1000) and its W + K, then the step_seq leg's P3 + W + K
-  config 4   step_kernel<false, false, true, false, false>  (auto-reset): launches P + W .. P + W + K
+  config 3   step_kernel<false, false, false, true, false, false> (kNt loads, N = 2^20, se_step):
+             the from-reset leg's W + K launches, then the headline leg's P3 pre-roll steps
+             (--preroll3, bench.py's default 1000), then the step_py
+             leg's P3 + W + K
+             step_kernel<false, false, false, true, false, true> (the same code, se_step_seq):
+             the headline leg's W warm-up and K timed launches, and nothing else
+  config 4   step_kernel<false, false, true, false, false, false> (auto-reset): launches P + W .. P + W + K
              after its P pre-roll steps (--preroll4, bench.py's default 1000)
-  large_n    step_kernel<false, false, false, false, false> (N = 2^24): the from-reset leg's
+  large_n    step_kernel<false, false, false, false, false, false> (N = 2^24): the from-reset leg's
              105 launches, then the steady leg's P3 pre-roll steps and its 105 (the last)
 For each leg this prints the average kernel duration (end - start of the dispatch, as
 rocprofv3 records it) over the K timed launches, over the timed launches after the
@@ -23,9 +26,10 @@ import argparse
 import csv
 import json
 
-C3 = "step_kernel<false, false, false, true, false>"
-C4 = "step_kernel<false, false, true, false, false>"
-BIG = "step_kernel<false, false, false, false, false>"
+C3 = "step_kernel<false, false, false, true, false, false>"
+C3S = "step_kernel<false, false, false, true, false, true>"
+C4 = "step_kernel<false, false, true, false, false, false>"
+BIG = "step_kernel<false, false, false, false, false, false>"
 PEAK = 8000.0
 
 
@@ -75,12 +79,12 @@ def main():
     K, W = a.steps, a.warmup
     out = {"trace": a.trace,
            "config3_from_reset": leg(rows, C3, 0, W + K, K),
-           "config3": leg(rows, C3, W + K + a.preroll3, W + K, K),
-           "config3_step_seq": leg(rows, C3, 2 * (W + K) + 2 * a.preroll3, W + K, K),
+           "config3": leg(rows, C3S, 0, W + K, K),
+           "config3_step_py": leg(rows, C3, W + K + 2 * a.preroll3, W + K, K),
            "config4": leg(rows, C4, a.preroll4, W + K, K),
            "large_n_from_reset": leg(rows, BIG, 0, 2 * 105 + a.preroll3, 100, from_end=True, head=105),
            "large_n": leg(rows, BIG, 0, 105, 100, from_end=True)}
-    for key, b in (("config3", 42), ("config3_from_reset", 42), ("config3_step_seq", 42), ("config4", 58)):
+    for key, b in (("config3", 42), ("config3_from_reset", 42), ("config3_step_py", 42), ("config4", 58)):
         if out[key]:
             us = out[key]["avg_us_timed"]
             out[key]["frac_from_trace"] = round(b * a.n / (us * 1e-6) / 1e9 / PEAK, 4)
