@@ -451,6 +451,9 @@ void policy_kernel(PolicyArgs A) {
 #ifndef SHIPENV_FC2_SPLIT
 #define SHIPENV_FC2_SPLIT 4  // one pass per row tile: no spills at 128 VGPRs (2 passes spill 7, 1 spills 14)
 #endif
+#ifndef SHIPENV_POLICY_LOOKAHEAD
+#define SHIPENV_POLICY_LOOKAHEAD 1  // fc2 fragments read this many k-steps ahead (0: as needed; 3 no better, 2 spills)
+#endif
         // fc2 + relu in SHIPENV_FC2_SPLIT passes over the 4 row tiles: the tiles of a pass
         // advance together (consecutive MFMAs independent, a k-step's fragments read in one
         // batch); with two passes the accumulators take 32 VGPRs instead of 64 and the
@@ -461,6 +464,28 @@ void policy_kernel(PolicyArgs A) {
             f32x16 c2[kFc2Tiles];
 #pragma unroll
             for (int i = 0; i < kFc2Tiles; ++i) c2[i] = bias_frag(B2 + (pass * kFc2Tiles + i) * 32 + 4 * h);
+#if SHIPENV_POLICY_LOOKAHEAD > 0
+            static_assert(kFc2Tiles == 1, "the fragment lookahead is written for one tile per pass");
+            // the tile's 8 fragments read SHIPENV_POLICY_LOOKAHEAD k-steps ahead of their MFMA,
+            // pinned in that order (one LDS read, one MFMA): left to itself the compiler read
+            // each fragment right before its MFMA and waited out the LDS round trip every time
+            constexpr int L = SHIPENV_POLICY_LOOKAHEAD;
+            bf16x8 wf[8];
+#pragma unroll
+            for (int k = 0; k < L; ++k) wf[k] = W2f[(pass * 8 + k) * 64 + lane];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (k + L < 8) wf[k + L] = W2f[(pass * 8 + k + L) * 64 + lane];
+                c2[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k], h1[k >> 1][k & 1], c2[0], 0, 0, 0);
+            }
+#pragma unroll
+            for (int k = 0; k < L; ++k) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (k + L < 8) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            }
+#else
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
@@ -473,6 +498,7 @@ void policy_kernel(PolicyArgs A) {
                     for (int i = 0; i < kFc2Tiles; ++i)
                         c2[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i], h1[kt][s], c2[i], 0, 0, 0);
                 }
+#endif
 #pragma unroll
             for (int i = 0; i < kFc2Tiles; ++i) relu_pack(c2[i], h2[pass * kFc2Tiles + i]);
         }
