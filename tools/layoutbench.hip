@@ -118,7 +118,8 @@ int main() {
         s.world = alloc<uint32_t>(4096);
         const double bytes = 42.0 * n;
         const int reps = n > (1 << 20) ? 100 : 400;
-        for (int blocks : {1024, 2048}) {
+        // 2048 workgroups (grid-stride) and one group per thread (the step kernel's grid)
+        for (int blocks : {2048, (int)(groups / 256)}) {
             float t1 = time_it([&] { k1<false, false><<<blocks, 256, 0>>>(s, groups); }, reps);
             float t2 = time_it([&] { k1<true, false><<<blocks, 256, 4096>>>(s, groups); }, reps);
             float t3 = time_it([&] { k3<false><<<blocks, 256>>>(s, groups); }, reps);
