@@ -274,18 +274,8 @@ __device__ uint64_t g_qtrace[kQTraceWg * 8 * kQTraceStamps];
         if ((threadIdx.x & 63) == 0 && blockIdx.x < kQTraceWg)                                 \
             g_qtrace[(blockIdx.x * 8 + (threadIdx.x >> 6)) * kQTraceStamps + (k)] = t_;        \
     } while (0)
-// the shader clock (s_memtime) beside the 100 MHz stamps, in slots 14 and 15
-#define QCLOCK(k)                                                                              \
-    do {                                                                                       \
-        const uint64_t c_ = __builtin_readcyclecounter();                                      \
-        if ((threadIdx.x & 63) == 0 && blockIdx.x < kQTraceWg)                                 \
-            g_qtrace[(blockIdx.x * 8 + (threadIdx.x >> 6)) * kQTraceStamps + (k)] = c_;        \
-    } while (0)
 #else
 #define QSTAMP(k) \
-    do {          \
-    } while (0)
-#define QCLOCK(k) \
     do {          \
     } while (0)
 #endif
@@ -386,7 +376,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
 
     // fc1, fc2 of both networks: online on states, target on next_states
     store_relu(tgt ? TA : HA, wt, gemm_lds(f1, tgt ? XN : X, acc1, lane), lane);
-    __syncthreads(); QSTAMP(2); QCLOCK(14);
+    __syncthreads(); QSTAMP(2);
     // fc3's fragments (64 loads per lane, ~1 us of the CU's memory pipeline for 8 waves)
     // are issued after fc2's first MFMAs: ahead of them, the chain's wait for its bias
     // (the counter is in order) also waited for every fragment load
@@ -403,6 +393,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         acc = gemm_lds<64, 2, 64>(fa, tgt ? TA : HA, acc, lane);
         store_relu(tgt ? TB : HB, wt, acc, lane);
     }
+    QSTAMP(14);  // this wave's fc2 done (its relu stores wait for the chain's last MFMA)
     __syncthreads(); QSTAMP(3);
     // target fc3 over all A rows and the max over actions: tile `wave` on each wave, and the
     // mt3 - 8 (at most 2) tiles beyond the eighth in 16 x 16 quadrants, so every SIMD gets the
@@ -464,7 +455,8 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         }
         if (lane < 32) QM[wave * 32 + lane] = m;
     }
-    __syncthreads(); QSTAMP(4); QCLOCK(15);
+    QSTAMP(15);  // this wave's fc3 done
+    __syncthreads(); QSTAMP(4);
     if (tid < 32) {
         const int64_t row = r0 + tid;
         float mx = QM[tid];

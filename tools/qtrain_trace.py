@@ -68,10 +68,12 @@ def main():
         out["t2_" + name] = {"start_p50": float(np.median(w2[lo:hi, 0])), "start_max": float(w2[lo:hi, 0].max()),
                              "wsum": float(np.median(d2[:, 0])), "sum": float(np.median(d2[:, 1])),
                              "adam": float(np.median(d2[:, 2])), "end_max": float(w2[lo:hi, 3].max())}
-    cyc = buf.reshape(wg, 8, stamps)[:tiles, :, 14:16].astype(np.int64)
-    rt = buf.reshape(wg, 8, stamps)[:tiles, :, [2, 4]].astype(np.int64)
-    ghz = (cyc[:, :, 1] - cyc[:, :, 0]) / ((rt[:, :, 1] - rt[:, :, 0]) * 10.0)  # cycles per ns
-    out["t1_shader_clock_ghz_fc2_fc3"] = [round(float(np.percentile(ghz, q)), 3) for q in (10, 50, 90)]
+    # slots 14 / 15: each wave's fc2 / fc3 chain done (before the phase's barrier), from the
+    # phase start (the slowest wave's stamp after the previous barrier), per wave of a workgroup
+    raw = buf.reshape(wg, 8, stamps)[:tiles].astype(np.int64)
+    for name, s_end, s0 in (("fc2", 14, 2), ("fc3", 15, 3)):
+        d_w = (raw[:, :, s_end] - raw[:, :, s0].max(axis=1, keepdims=True)) / 100.0
+        out[name + "_wave_done_median_us"] = [round(float(np.median(d_w[:, k])), 2) for k in range(8)]
     print(json.dumps(out))
     agent.close()
     env.close()
