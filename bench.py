@@ -510,7 +510,7 @@ def run_dqn_train(n, args, dist):
 
 
 KERNEL_MS_BASIS = ("HIP events on the launch stream, end of launch 1 to end of launch K, over K - 1 launches "
-                   "(rocprofv3 kernel-trace averages of the driver's command: profiles/r03c/kt_legs.json, "
+                   "(rocprofv3 kernel-trace averages of the driver's command: profiles/r03d/kt_legs.json, "
                    "printed per leg as rocprof_trace from profiles/rocprof_legs.json)")
 
 
