@@ -1,9 +1,10 @@
 """Phase timeline of the DQN update's T1 kernel (diagnostic; needs a build with
 -DSHIPENV_QTRACE=1): s_memrealtime (100 MHz) stamps per wave at kernel start and after
 each of its barriers (1 inputs staged, 2 fc1, 3 fc2, 4 target fc3 + max, 5 targets y,
-6 q and g, 7 dZ2, 8 dH1 / dW2 / dW3), then 9 at the end. Runs a few training steps
-and prints, for the last T1 launch, per-phase medians over workgroups (us) and the
-launch span.
+6 q and g, 7 dZ2, 8 dH1 / dW2 / dW3), then 9 at the end, and 14 / 15 when a wave's own fc2 /
+fc3 chain is done (before the phase's barrier). Runs a few training steps and prints, for the
+last T1 launch, per-phase medians over workgroups (us), the launch span and each wave's fc2 /
+fc3 completion; T2's stamps (slots 10-13) per block kind.
 
     bash -c 'hipcc ... -DSHIPENV_QTRACE=1 -o /tmp/qt.so ...'; python tools/qtrain_trace.py --lib /tmp/qt.so
 """
