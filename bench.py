@@ -3,6 +3,11 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n ENVS_PER_GPU]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py launches its own N
+ranks (spawn_ranks: N fresh child processes, one per GPU, RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_* set; the parent makes no GPU call), forwards rank 0's line and
+exits non-zero if any rank fails. Under torchrun the ranks are torchrun's.
+
 A "step" is one se_step launch over all envs of the GPU (one pass of the hot
 path over one batch). Workload for `value`: BASELINE config 3 — N = 2^20 envs
 per GPU, full step (moves, cargo pickup/delivery, rewards), the reference's 5
@@ -39,6 +44,9 @@ BYTES_STEP_AUTO = BYTES_STEP + 4 + 4 + 4 + 4  # + ep_return f32 and ep_len i32, 
 CANONICAL_STEP, CANONICAL_STEP_AUTO = 66, 82
 
 
+LITERAL_STEPS, LITERAL_WARMUP = 1000, 10  # "Warm-up 10 steps, time 1000 steps"
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -63,7 +71,8 @@ def parse():
     p.add_argument("--large-n", type=int, default=1 << 24,
                    help="extra HBM-resident run (working set beyond the 256 MiB MALL); 0 = skip")
     p.add_argument("--dqn-steps", type=int, default=50,
-                   help="config 5: timed DQN policy + step iterations at N envs/GPU; 0 = skip")
+                   help="config 5: timed DQN policy + step iterations at N envs/GPU (fp32 policy, then "
+                        "bf16); 0 = skip")
     p.add_argument("--train-steps", type=int, default=30,
                    help="timed vectorised DQN training iterations (policy, step, replay, update); 0 = skip")
     p.add_argument("--train-batch", type=int, default=8192, help="DQN minibatch per update")
@@ -73,25 +82,36 @@ def parse():
     return p.parse_args()
 
 
+REHEARSAL_ENV = "SHIPENV_REHEARSE"  # "1": every rank on GPU 0 over gloo (launch rehearsal, never a measurement)
+
+
 class Dist:
-    """torch.distributed glue (shippingenv_amd.dist): barrier, max over ranks, stats all-reduce."""
+    """torch.distributed glue (shippingenv_amd.dist): barrier, max over ranks, stats all-reduce.
+    Backend "nccl" (RCCL) with local rank r on GPU r. SHIPENV_REHEARSE=1 rehearses the N-rank
+    launch on a box with fewer GPUs: every rank on GPU r % device_count over gloo (RCCL refuses
+    two ranks on one GPU); the line then says "rehearsal" in its dist object."""
 
     def __init__(self, want):
         from shippingenv_amd import dist as D
 
         self.D = D
-        # rehearsal of the N-rank launch on fewer GPUs (never for a measurement):
-        # SHIPENV_SHARE_GPUS=1 puts local rank r on GPU r % device_count, and
-        # SHIPENV_DIST_BACKEND=gloo replaces RCCL, which refuses two ranks on one GPU
-        gpu = None
-        if os.environ.get("SHIPENV_SHARE_GPUS") == "1" and torch.cuda.is_available():
+        self.rehearsal = os.environ.get(REHEARSAL_ENV) == "1"
+        gpu, backend = None, None
+        if self.rehearsal and torch.cuda.is_available():
             gpu = int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count()
-        self.rank, self.world, self.local, self.dev = D.init_from_env(os.environ.get("SHIPENV_DIST_BACKEND"), gpu)
+            backend = "gloo"
+        self.rank, self.world, self.local, self.dev = D.init_from_env(backend, gpu)
         if self.world != want:
             raise SystemExit(f"--gpus {want} but WORLD_SIZE={self.world}")
         import torch.distributed as tdist
 
         self.pg = tdist if self.world > 1 else None
+        self.info = {"world_size": tdist.get_world_size() if self.pg else 1,
+                     "backend": tdist.get_backend() if self.pg else None,
+                     "device": str(self.dev),
+                     "launcher": os.environ.get("SHIPENV_LAUNCHER", "torchrun" if self.world > 1 else None)}
+        if self.rehearsal:
+            self.info["rehearsal"] = "all ranks on one GPU over gloo: a launch rehearsal, not scaling data"
 
     def barrier(self):
         if self.pg:
@@ -107,6 +127,69 @@ class Dist:
     def close(self):
         if self.pg:
             self.pg.destroy_process_group()
+
+
+def spawn_ranks(n, argv, script=None, env=None, grace_s=30.0):
+    """Run `script argv` as N fresh processes, rank r with RANK = LOCAL_RANK = r (GPU r),
+    WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and a free MASTER_PORT, as torchrun would. The
+    parent makes no GPU or HIP call (it only imports torch, which initialises nothing).
+    Rank 0's stdout (the one JSON line) is forwarded to stdout; every rank's stderr is
+    inherited. If a rank exits non-zero the others get `grace_s` seconds, then SIGTERM
+    (SIGKILL 10 s later): a rank left waiting in a collective for a dead peer would hang.
+    Returns 0 if every rank succeeded, else the first non-zero exit status (1 for a signal)."""
+    import socket
+    import subprocess
+    import tempfile
+
+    script = os.path.abspath(script or __file__)
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    base = dict(os.environ if env is None else env)
+    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n), SHIPENV_LAUNCHER="bench.spawn_ranks")
+    out0 = tempfile.TemporaryFile(mode="w+b")
+    procs = []
+    try:
+        for r in range(n):
+            e = dict(base, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0")
+            procs.append(subprocess.Popen([sys.executable, script, *argv], env=e,
+                                          stdout=out0 if r == 0 else subprocess.DEVNULL))
+        first_bad, t_bad = None, None
+        while True:
+            codes = [p.poll() for p in procs]
+            for r, c in enumerate(codes):
+                if c not in (None, 0) and first_bad is None:
+                    first_bad, t_bad = (r, c), time.monotonic()
+                    log(f"[launcher] rank {r} exited with status {c}")
+            if all(c is not None for c in codes):
+                break
+            if first_bad is not None and time.monotonic() - t_bad > grace_s:
+                for p in procs:
+                    if p.poll() is None:
+                        p.terminate()
+                for p in procs:
+                    try:
+                        p.wait(10)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                break
+            time.sleep(0.05)
+    finally:
+        for p in procs:  # an exception or signal in the parent: no orphaned ranks
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    codes = [p.returncode for p in procs]
+    bad = [c for c in codes if c != 0]
+    if bad:
+        log(f"[launcher] rank exit statuses {codes}")
+        c = first_bad[1] if first_bad else bad[0]
+        return c if c > 0 else 1
+    out0.seek(0)
+    sys.stdout.write(out0.read().decode())
+    sys.stdout.flush()
+    return 0
 
 
 def make_actions(env, steps):
@@ -310,43 +393,86 @@ F32_MFMA_PEAK_TFLOPS = 157.3  # v_mfma_f32_32x32x2_f32, MI355X_MICROARCH.md
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, no sparsity)
 
 
-def run_dqn(n, args, dist):
-    """Config 5: the DQN rollout consumer. Per iteration: the fused policy
-    step (observation, DQNNetwork 26->128->128->259 on bf16 MFMA, masked first-max
-    argmax, epsilon-greedy; se_policy) then the env step, on N envs per GPU with
-    random-init weights (no checkpoint: no network). Also timed: the policy launch
-    alone, and the unfused torch path (observe -> nn.Module fp32 -> masked argmax)."""
+def policy_step_loop(env, pol, prec, eps, t0_key, steps, dist, every):
+    """`steps` iterations of policy + step (the config-5 consumer loop), bracketed by barrier +
+    synchronize, with the episode-statistics all-reduce every `every` steps inside the region.
+    Returns (wall max over ranks, events ms per iteration, all-reduces)."""
+    stream = torch.cuda.current_stream(env.device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    count = 0
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for k in range(steps):
+        env.step(pol.act(eps, t0_key + k, precision=prec))
+        if every and (k + 1) % every == 0:
+            dist.D.reduce_episode_stats(env.episode_stats())
+            count += 1
+    e1.record(stream)
+    torch.cuda.synchronize()
+    dist.barrier()
+    wall = dist.max(time.perf_counter() - t0)
+    return wall, e0.elapsed_time(e1) / steps, count
+
+
+def run_config5(n, args, dist):
+    """BASELINE configs[4] / SURVEY 8(d) config 5: N envs per GPU (global ids rank*N + i),
+    auto-reset on done (default 5 ports), the DQN rollout consumer (agents/dqn.py:177-204:
+    DQNNetwork 26->128->128->259 forward + the first maximum over the valid actions +
+    epsilon-greedy, fused in se_policy_f32 / se_policy) then se_step, and the RCCL SUM
+    all-reduce of {sum of returns, episodes, sum of lengths} every min(100, K // 2) steps
+    inside the timed region. `value` evaluates the network in fp32, the reference's own
+    precision (se_policy_f32, f32 MFMA); the bf16 policy's figure is beside it. Also: the
+    env kernel alone (se_step over the same auto-reset shard) and the unfused torch policy."""
     from shippingenv_amd.policy import DQNNetwork, QPolicy
     from shippingenv_amd.vec import VecEnv
 
-    env = VecEnv(n, seed=args.seed, env_id_base=dist.rank * n, device=dist.dev)
+    K = args.dqn_steps
+    env = VecEnv(n, seed=args.seed, env_id_base=dist.rank * n, device=dist.dev, auto_reset=True)
     env.reset()
     torch.manual_seed(args.seed)
     model = DQNNetwork(env.obs_size, env.action_space_size).to(env.device)
     pol = QPolicy(env, model)
     eps = 0.1
-    for t in range(5):
-        env.step(pol.act(eps, t))
+    every = max(1, min(100, K // 2))
     stream = torch.cuda.current_stream(env.device)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    dist.barrier()
+    legs = {}
+    for i, prec in enumerate(("f32", "bf16")):
+        for t in range(5):  # warm-up: both kernels and the stats path loaded
+            env.step(pol.act(eps, 100_000 * i + t, precision=prec))
+        dist.D.reduce_episode_stats(env.episode_stats().clone())
+        torch.cuda.synchronize()
+        env.clear_stats()
+        wall, e2e_ms, count = policy_step_loop(env, pol, prec, eps, 100_000 * i + 5, K, dist, every)
+        s = env.episode_stats().clone()
+        dist.D.reduce_episode_stats(s)
+        st = s.cpu().tolist()
+        # the policy launch alone on the state the loop left (fresh draws)
+        e0.record(stream)
+        for t in range(K):
+            pol.act(eps, 500_000 + 100_000 * i + t, precision=prec)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        legs[prec] = {"value": round(n * dist.world * K / wall, 1),
+                      "ms_per_step": round(wall / K * 1e3, 4),
+                      "e2e_kernel_ms": round(e2e_ms, 4),
+                      "policy_ms": round(e0.elapsed_time(e1) / K, 4),
+                      "allreduces_in_timed_region": count,
+                      "episodes": st[1],
+                      "mean_return": st[0] / st[1] if st[1] else None}
+    # the env kernel alone: se_step over the same shard, the policy's last actions each step
+    acts = pol.act(0.0, 999_999).clone()
+    for _ in range(3):
+        env.step(acts)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
     e0.record(stream)
-    for t in range(args.dqn_steps):
-        env.step(pol.act(eps, 5 + t))
+    for _ in range(K):
+        env.step(acts)
     e1.record(stream)
     torch.cuda.synchronize()
-    dist.barrier()
-    wall = dist.max(time.perf_counter() - t0)
-    e2e_ms = e0.elapsed_time(e1) / args.dqn_steps
-    # the policy launch alone (same state, fresh draws)
-    e0.record(stream)
-    for t in range(args.dqn_steps):
-        pol.act(eps, 1000 + t)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    pol_ms = e0.elapsed_time(e1) / args.dqn_steps
+    step_ms = e0.elapsed_time(e1) / K
     # unfused torch reference path, fp32 as agents/dqn.py runs it (a few iterations)
     A = env.action_space_size
     shifts = torch.arange(7, -1, -1, device=env.device, dtype=torch.uint8)
@@ -365,17 +491,7 @@ def run_dqn(n, args, dist):
     e1.record(stream)
     torch.cuda.synchronize()
     torch_ms = e0.elapsed_time(e1) / 5
-    # the fp32-faithful mode (se_policy_f32: the network in f32 on v_mfma_f32_32x32x2_f32)
-    pol.act(eps, 2000, precision="f32")
-    torch.cuda.synchronize()
-    k32 = 10
-    e0.record(stream)
-    for t in range(k32):
-        pol.act(eps, 2001 + t, precision="f32")
-    e1.record(stream)
-    torch.cuda.synchronize()
-    pol32_ms = e0.elapsed_time(e1) / k32
-    # greedy decisions of both modes against fp32 torch on these 2^20 states
+    # greedy decisions of both modes against fp32 torch on these states
     # (agents/dqn.py:198-204: the first maximum of the fp32 network's Q over the valid actions)
     a16 = pol.act(0.0, 3000).clone()
     a32 = pol.act(0.0, 3000, precision="f32").clone()
@@ -399,41 +515,53 @@ def run_dqn(n, args, dist):
     rows3 = 32 * ((4 + env.P + cmax + fmax + 31) // 32)
     flop_env = 2 * (6 * 128 + 128 * 128 + rows3 * 128)
     flop_ref = 2 * (env.obs_size * 128 + 128 * 128 + 128 * A)  # the reference network's MACs x 2
-    achieved = flop_env * n / (pol_ms * 1e-3) / 1e12
+    pol32_ms, pol_ms = legs["f32"]["policy_ms"], legs["bf16"]["policy_ms"]
     achieved32 = flop_env * n / (pol32_ms * 1e-3) / 1e12
+    achieved = flop_env * n / (pol_ms * 1e-3) / 1e12
     # what the kernel issues per 32 envs at most: fc1 (the port block folded into the bias,
     # one k-step per row tile), fc2, and fc3 over the compact rows
     mfma_tile = 4 + 32 + 8 * ((4 + env.P + cmax + fmax + 31) // 32)
     pol.close()
     env.close()
+    f32 = legs["f32"]
     return {
-        "workload": "config 5: fused DQN policy (se_policy: obs + DQNNetwork 26->128->128->259 bf16 "
-                    "MFMA + masked argmax + eps-greedy 0.1) then se_step, N envs/GPU, random-init weights; "
-                    "policy_ms_f32 / roofline_f32: the fp32-faithful mode (se_policy_f32)",
-        "value": round(n * dist.world * args.dqn_steps / wall, 1),
-        "unit": "env-steps/s (policy + step)",
-        "ms_per_step": round(wall / args.dqn_steps * 1e3, 4),
-        "e2e_kernel_ms": round(e2e_ms, 4),
-        "policy_ms": round(pol_ms, 4),
-        "policy_ms_f32": round(pol32_ms, 4),
+        "workload": "BASELINE configs[4]: N envs/GPU (global ids rank*N + i), auto-reset, default 5 ports; "
+                    "per step the fused DQN policy (obs + DQNNetwork 26->128->128->259 + masked first argmax "
+                    "+ eps-greedy 0.1; fp32 on f32 MFMA, se_policy_f32) then se_step; RCCL SUM all-reduce "
+                    "of {sum return, episodes, sum len} every min(100, K // 2) steps in the timed region; "
+                    "random-init weights. bf16: the same loop on the bf16 policy (se_policy)",
+        "value": f32["value"],
+        "unit": "env-steps/s (policy + step, end to end)",
+        "precision": "fp32 (the reference's network precision, agents/dqn.py:198-204)",
+        "n_gpus": dist.world,
+        "global_envs": n * dist.world,
+        "steps": K,
+        "ms_per_step": f32["ms_per_step"],
+        "e2e_kernel_ms": f32["e2e_kernel_ms"],
+        "policy_ms": f32["policy_ms"],
+        "allreduce_every": every,
+        "allreduces_in_timed_region": f32["allreduces_in_timed_region"],
+        "episodes": f32["episodes"],
+        "mean_return": f32["mean_return"],
+        "env_kernel": {"value": round(n * dist.world / (step_ms * 1e-3), 1), "kernel_ms": round(step_ms, 5),
+                       "unit": "env-steps/s (se_step alone, auto-reset shard, events)"},
+        "bf16": legs["bf16"],
         "greedy_disagreement_vs_fp32_torch": {"bf16": round(dis16 / n, 5), "f32": round(dis32 / n, 6),
                                               "states": n,
                                               "note": "greedy actions on the config-5 states vs the first "
                                                       "masked argmax of the fp32 torch DQNNetwork"},
-        "roofline_f32": {"bound": "mfma (f32)", "achieved": round(achieved32, 2), "peak": F32_MFMA_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved32 / F32_MFMA_PEAK_TFLOPS, 4),
-                         "flop_per_env": flop_env, "reference_network_flop_per_env": flop_ref,
-                         "note": "se_policy_f32 on the same FLOP basis (includes its per-call repack of "
-                                 "the f32 image)"},
         "torch_unfused_policy_ms": round(torch_ms, 4),
-        "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": BF16_DENSE_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4),
-                     "flop_per_env": flop_env, "traffic": None,
-                     "reference_network_flop_per_env": flop_ref,
-                     "executed_mfma_per_32_envs": mfma_tile,
-                     "note": "achieved is on the FLOPs the fused step evaluates (fc1's 6 dynamic inputs, "
-                             "fc2, fc3's compact rows); at most executed_mfma_per_32_envs "
-                             "v_mfma_f32_32x32x16_bf16 per 32 envs (fc1 pads K to 16)"},
+        "roofline": {"bound": "mfma (f32)", "achieved": round(achieved32, 2), "peak": F32_MFMA_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved32 / F32_MFMA_PEAK_TFLOPS, 4),
+                     "flop_per_env": flop_env, "traffic": None, "reference_network_flop_per_env": flop_ref,
+                     "note": "se_policy_f32 (includes its per-call repack of the f32 image); achieved on the "
+                             "FLOPs the fused step evaluates (fc1's 6 dynamic inputs, fc2, fc3's compact rows)"},
+        "roofline_bf16": {"bound": "mfma", "achieved": round(achieved, 1), "peak": BF16_DENSE_PEAK_TFLOPS,
+                          "unit": "TFLOP/s", "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4),
+                          "flop_per_env": flop_env, "traffic": None,
+                          "executed_mfma_per_32_envs": mfma_tile,
+                          "note": "at most executed_mfma_per_32_envs v_mfma_f32_32x32x16_bf16 per 32 envs "
+                                  "(fc1 pads K to 16)"},
     }
 
 
@@ -509,9 +637,7 @@ def run_dqn_train(n, args, dist):
     return out
 
 
-KERNEL_MS_BASIS = ("HIP events on the launch stream, end of launch 1 to end of launch K, over K - 1 launches "
-                   "(rocprofv3 kernel-trace averages of the driver's command: profiles/r03d/kt_legs.json, "
-                   "printed per leg as rocprof_trace from profiles/rocprof_legs.json)")
+KERNEL_MS_BASIS = "HIP events on the launch stream, end of launch 1 to end of launch K, over K - 1 launches (this run)"
 
 
 def roofline(bytes_per_step, n, k_ms, canonical):
@@ -544,25 +670,24 @@ def pmc_traffic(key="step_kernel_bytes_per_launch"):
     return d.get(key), os.path.relpath(path, ROOT)
 
 
-TRACE_SUMMARY = os.path.join("profiles", "rocprof_legs.json")  # profiles/r03/kt_legs_driver.json, condensed
+TRACE_SUMMARY = os.path.join("profiles", "rocprof_legs.json")  # condensed from a profiles/r0*/kt_legs*.json
 
 
-def rocprof_leg(key):
-    """The committed kernel-trace average of one leg under the driver's bench command
-    (tools/trace_driver.sh -> tools/kt_legs.py), printed beside the live events figure.
-    The headline's launches (se_step_seq) are a trace row of their own,
-    step_kernel<false, false, false, true, false, true>: W + K calls, back to back under the
-    tracer too. Legs issued one Python call per launch leave the traced GPU idle between
-    launches, which lengthens each 2^20-env launch; at 2^24 every
-    form agrees."""
+def committed_trace(key):
+    """A leg's kernel-trace average from the committed rocprofv3 summary (tools/trace_driver.sh
+    -> tools/kt_legs.py -> profiles/rocprof_legs.json), with the commit and date of the code
+    it was traced on. It is NOT a figure of this run: it goes under its own key
+    ("committed_trace") beside the live events figure, so a stale trace shows as such."""
     path = os.path.join(ROOT, TRACE_SUMMARY)
     if not os.path.exists(path):
         return None
     with open(path) as f:
-        leg = json.load(f).get(key)
+        d = json.load(f)
+    leg = d.get(key)
     if not leg:
         return None
-    return {"avg_us": leg["avg_us_timed"], "frac": leg["frac_from_trace"], "source": TRACE_SUMMARY}
+    return {"avg_us": leg["avg_us_timed"], "frac": leg["frac_from_trace"], "source": TRACE_SUMMARY,
+            "traced_code": d.get("traced_code"), "trace": d.get("trace")}
 
 
 def cpu_threads():
@@ -626,6 +751,9 @@ def cpu_baseline(n_workload, ports_seed, budget_s):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the driver's plain `python3 bench.py --gpus N`: launch the N ranks here
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     dist = Dist(args.gpus)
     from shippingenv_amd.maps import builtin_water
     from shippingenv_amd.vec import random_water_ports
@@ -640,8 +768,14 @@ def main():
                                    step_seq=True)
     value = n * dist.world * args.steps / el3
     el3p, k3p, _, _ = run_config(n, None, False, args, dist, "config3-step-py", preroll=args.preroll3)
+    # SURVEY 8(d) config 3 to the letter: se_reset, warm-up 10, time 1000 steps (whatever K is)
+    lit = argparse.Namespace(**vars(args))
+    lit.steps, lit.warmup = LITERAL_STEPS, LITERAL_WARMUP
+    el3l, k3l, _, _ = run_config(n, None, False, lit, dist, "config3-literal", preroll=0, step_seq=True)
     out = {
-        "metric": "env-steps/sec at N=2^20 parallel envs per GPU (config 3: full step, 5 default ports)",
+        "metric": "env-steps/sec at N=2^20 parallel envs per GPU (config 3: full step, 5 default ports; "
+                  "K steps in the steady state after a 1000-step pre-roll; config3_literal: the survey's "
+                  "1000 steps from reset)",
         "value": round(value, 1),
         "unit": "env-steps/s",
         "n_gpus": dist.world,
@@ -676,10 +810,18 @@ def main():
                     "ms_per_step": round(el3p / args.steps * 1e3, 5),
                     "kernel_ms": round(k3p, 5),
                     "frac": roofline(BYTES_STEP, n, k3p, CANONICAL_STEP)["frac"]},
+        "config3_literal": {"workload": f"SURVEY 8(d) config 3 as written: se_reset, warm-up {LITERAL_WARMUP}, "
+                                        f"{LITERAL_STEPS} timed steps (VecEnv.step_seq), N=2^20 envs/GPU",
+                            "steps": LITERAL_STEPS, "warmup": LITERAL_WARMUP,
+                            "value": round(n * dist.world * LITERAL_STEPS / el3l, 1),
+                            "ms_per_step": round(el3l / LITERAL_STEPS * 1e3, 5),
+                            "kernel_ms": round(k3l, 5),
+                            "frac": roofline(BYTES_STEP, n, k3l, CANONICAL_STEP)["frac"]},
+        "dist": dist.info,
     }
     for key, obj in (("config3", out["roofline"]), ("config3_from_reset", out["from_reset"]),
-                     ("config3_step_py", out["step_py"])):
-        obj["rocprof_trace"] = rocprof_leg(key)
+                     ("config3_step_py", out["step_py"]), ("config3_literal", out["config3_literal"])):
+        obj["committed_trace"] = committed_trace(key)
     traffic, src = pmc_traffic()
     if traffic:
         out["roofline"]["traffic"] = traffic
@@ -702,7 +844,7 @@ def main():
             "mean_return": stats[0] / stats[1] if stats and stats[1] else None,
             "mean_len": stats[2] / stats[1] if stats and stats[1] else None,
         } | info4
-        out["config4"]["roofline"]["rocprof_trace"] = rocprof_leg("config4")
+        out["config4"]["roofline"]["committed_trace"] = committed_trace("config4")
         if t4:
             out["config4"]["roofline"]["traffic"] = t4
             out["config4"]["roofline"]["traffic_source"] = src4
@@ -714,7 +856,7 @@ def main():
         out["rollouts"] = run_rollouts(n, args, dist)
 
     if args.dqn_steps:
-        out["config5_dqn"] = run_dqn(n, args, dist)
+        out["config5"] = run_config5(n, args, dist)
 
     if args.train_steps:  # N > 1: data parallel (gradient all-reduce per update)
         try:
@@ -738,11 +880,11 @@ def main():
             "preroll_steps": args.preroll3,
             "value": round(args.large_n * small.steps / el, 1),
             "roofline": roofline(BYTES_STEP, args.large_n, k, CANONICAL_STEP)
-            | {"rocprof_trace": rocprof_leg("large_n")},
+            | {"committed_trace": committed_trace("large_n")},
             "from_reset": {"value": round(args.large_n * small.steps / elr, 1),
                            "kernel_ms": round(kr, 5),
                            "frac": roofline(BYTES_STEP, args.large_n, kr, CANONICAL_STEP)["frac"],
-                           "rocprof_trace": rocprof_leg("large_n_from_reset")},
+                           "committed_trace": committed_trace("large_n_from_reset")},
         }
         tb, srcb = pmc_traffic("step_kernel_big_bytes_per_launch")
         if tb:

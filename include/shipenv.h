@@ -291,6 +291,8 @@ int se_replay_end(se_replay* r, uint8_t* cut, int32_t max_steps, void* stream);
  * se_replay_end_reset = se_replay_end + se_reset(cut): the cut episodes restart in the
  * same pass, with the draws se_reset would make (the env's reset epoch advances). */
 int se_policy_record(se_qnet* q, se_replay* r, int32_t* actions, double epsilon, uint32_t t, void* stream);
+/* se_policy_record with the network in fp32 (se_policy_f32's kernel): the same record. */
+int se_policy_record_f32(se_qnet* q, se_replay* r, int32_t* actions, double epsilon, uint32_t t, void* stream);
 int se_replay_end_reset(se_replay* r, uint8_t* cut, int32_t max_steps, void* stream);
 /* se_step_record = se_step + se_replay_end_reset in one launch: the step kernel writes the
  * ring's reward / done / s' record and restarts the cut envs from the state it holds

@@ -33,7 +33,7 @@ EXPORTS = (
     "se_create", "se_set_ports", "se_bind", "se_reset", "se_reset_to", "se_step", "se_step_seq",
     "se_step_typed", "se_step_replay", "se_step_agent_replay", "se_observe", "se_valid_mask", "se_gen_actions",
     "se_sample_actions", "se_rollout", "se_qnet_create", "se_qnet_set_weights", "se_policy", "se_policy_f32",
-    "se_qnet_repack", "se_policy_record",
+    "se_qnet_repack", "se_policy_record", "se_policy_record_f32",
     "se_qnet_destroy", "se_replay_create", "se_replay_begin", "se_replay_end", "se_replay_end_reset", "se_step_record",
     "se_replay_size",
     "se_replay_sample", "se_replay_destroy", "se_qtrain_create", "se_qtrain_bind", "se_qtrain_pack",
@@ -93,6 +93,7 @@ def _declare(lib):
         "se_policy_f32": [P, P, C.c_double, u32, P, i64, P],
         "se_qnet_repack": [P, P, P],
         "se_policy_record": [P, P, P, C.c_double, u32, P],
+        "se_policy_record_f32": [P, P, P, C.c_double, u32, P],
         "se_qnet_destroy": [P],
         "se_replay_create": [P, P, i64],
         "se_replay_begin": [P, P, P],

@@ -934,17 +934,8 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }
-}  // namespace
-
-extern "C" {
-
-int se_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, float* q_out, int64_t ldq,
-              void* stream) {
-    return launch_policy(qn, actions, epsilon, t, q_out, ldq, nullptr, stream);
-}
-
-int se_policy_f32(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, float* q_out, int64_t ldq,
-                  void* stream) {
+int launch_policy_f32(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, float* q_out, int64_t ldq,
+                      const PolicyRecord* rec, void* stream) {
     if (!qn) return fail(SE_EINVAL, "null qnet");
     se_env* env = qn->env;
     int rc = check_ready(env);
@@ -1001,10 +992,31 @@ int se_policy_f32(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
     A.actions = actions;
     A.q_out = q_out;
     A.ldq = ldq;
+    if (rec) {
+        A.rec_pos = rec->pos;
+        A.rec_fuel = rec->fuel;
+        A.rec_act = rec->act;
+        A.rec_head = rec->head;
+        A.rec_cap = rec->cap;
+    }
     if (w3_global) policy_f32_kernel<true><<<grid, kPolicyF32Block, lds, s>>>(F);
     else policy_f32_kernel<false><<<grid, kPolicyF32Block, lds, s>>>(F);
     HIP_TRY(hipGetLastError());
     return SE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int se_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, float* q_out, int64_t ldq,
+              void* stream) {
+    return launch_policy(qn, actions, epsilon, t, q_out, ldq, nullptr, stream);
+}
+
+int se_policy_f32(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, float* q_out, int64_t ldq,
+                  void* stream) {
+    return launch_policy_f32(qn, actions, epsilon, t, q_out, ldq, nullptr, stream);
 }
 
 int se_qnet_repack(se_qnet* qn, int32_t* bump, void* stream) {

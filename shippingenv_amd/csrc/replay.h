@@ -472,6 +472,17 @@ int se_policy_record(se_qnet* qn, se_replay* r, int32_t* actions, double epsilon
     return SE_OK;
 }
 
+int se_policy_record_f32(se_qnet* qn, se_replay* r, int32_t* actions, double epsilon, uint32_t t, void* stream) {
+    if (!qn || !r) return fail(SE_EINVAL, "null qnet / replay");
+    if (qn->env != r->env) return fail(SE_EINVAL, "the qnet and the replay belong to different envs");
+    if (r->open) return fail(SE_ESTATE, "se_replay_begin twice without se_replay_end");
+    const PolicyRecord rec{r->ring.s_pos, r->ring.s_fuel, r->ring.act, r->head, r->cap};
+    const int rc = launch_policy_f32(qn, actions, epsilon, t, nullptr, 0, &rec, stream);
+    if (rc) return rc;
+    r->open = true;
+    return SE_OK;
+}
+
 int se_replay_size(se_replay* r, int64_t* size, int64_t* capacity) {
     if (!r) return fail(SE_EINVAL, "null replay");
     if (size) *size = r->size;

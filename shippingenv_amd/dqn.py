@@ -30,6 +30,7 @@ Differences from the single-env reference, by construction:
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -45,6 +46,8 @@ DQN_EPSILON_MIN = 0.01
 DQN_EPSILON_DECAY = 0.995
 DQN_LEARNING_RATE = 0.001
 MAX_STEPS_PER_EPISODE = 1000
+
+_DEBUG = os.environ.get("SHIPENV_DEBUG") == "1"
 
 
 def _ptr(t):
@@ -194,9 +197,16 @@ class FusedUpdate:
         policy), in two launches (se_qtrain_step_replay): the first draws its minibatch rows
         from the ring itself. ctr: device int32 [2], both entries the updates taken so far.
         t: the caller's copy of ctr[0] (eager calls: the first kernel then does not wait on
-        the device counter); None reads it on the device (graph capture)."""
+        the device counter); None reads it on the device (graph capture). t must equal
+        ctr[0] exactly: the first kernel writes ctr[1] = t + 1, which becomes Adam's step
+        count and the next ctr[0], so a stale t would rewind the counter. SHIPENV_DEBUG=1
+        checks it (one host sync per call)."""
         if ctr.dtype != torch.int32 or ctr.numel() < 2 or not ctr.is_contiguous():
             raise ValueError("ctr must be a contiguous int32 device tensor of 2 entries")
+        if t is not None and _DEBUG and not torch.cuda.is_current_stream_capturing():
+            dev_t = int(ctr[0].item())
+            if dev_t != int(t):
+                raise ValueError(f"step_replay: t = {t} but ctr[0] = {dev_t} (t must be ctr[0])")
         N.check(N.lib().se_qtrain_step_replay(self._h, None if policy is None else policy._h, memory._h,
                                               int(batch), float(gamma), self.lr, self.betas[0],
                                               self.betas[1], self.eps, _ptr(ctr), -1 if t is None else int(t),
@@ -275,7 +285,7 @@ class VecDQNAgent:
                  hidden_size: int = HIDDEN, max_steps: int = MAX_STEPS_PER_EPISODE,
                  updates_per_step: int = 1, graph: bool | None = None, graph_warmup: int = 3,
                  fused: bool = True, model: DQNNetwork | None = None,
-                 data_parallel: bool = False, process_group=None):
+                 data_parallel: bool = False, process_group=None, precision: str = "bf16"):
         if not env.auto_reset:
             raise ValueError("VecDQNAgent needs an auto-reset VecEnv (finished episodes restart in se_step)")
         self.env = env
@@ -285,6 +295,11 @@ class VecDQNAgent:
         self.learning_rate, self.batch_size = float(learning_rate), int(batch_size)
         self.target_update_every, self.max_steps = int(target_update_every), int(max_steps)
         self.updates_per_step = int(updates_per_step)
+        if precision not in ("bf16", "f32"):
+            raise ValueError("precision must be 'bf16' or 'f32'")
+        # the acting network's precision: "f32" evaluates it in fp32 as agents/dqn.py:198-200
+        # does (se_policy_f32, about 7x the policy time); the update is f32 either way
+        self.precision = precision
         dev = env.device
         self.model = (model if model is not None else
                       DQNNetwork(self.state_size, self.action_size, hidden_size)).to(dev)
@@ -447,12 +462,12 @@ class VecDQNAgent:
     # ------------------------------------------------------------------ acting
     def choose_actions(self, deterministic: bool = False) -> torch.Tensor:
         """choose_action (agents/dqn.py:177-203) for every env."""
-        return self.policy.act(0.0 if deterministic else self.epsilon, self.t)
+        return self.policy.act(0.0 if deterministic else self.epsilon, self.t, precision=self.precision)
 
     def step(self):
         """One training-loop iteration for every env; returns the last update's loss (or None)."""
         # choose_action + remember(state, action): one launch (se_policy_record)
-        a = self.policy.act_record(self.memory, self.epsilon, self.t)
+        a = self.policy.act_record(self.memory, self.epsilon, self.t, precision=self.precision)
         # env.step, remember's reward / next_state, and the episodes that raised or reached
         # max_steps start over (env.reset(cut)): one launch (se_step_record)
         self.memory.step_end(a, self.cut, self.max_steps)

@@ -70,11 +70,15 @@ class QPolicy:
         step); bump (device int32 [1]) is advanced by one on the stream (se_qnet_repack)."""
         N.check(N.lib().se_qnet_repack(self._h, _ptr(bump) if bump is not None else None, self.env._stream()))
 
-    def act_record(self, replay, epsilon: float = 0.0, t: int = 0):
+    def act_record(self, replay, epsilon: float = 0.0, t: int = 0, precision: str = "bf16"):
         """act() plus the replay ring's remember(state, action) in the same launch
-        (se_policy_record; replay: shippingenv_amd.dqn.ReplayBuffer)."""
-        N.check(N.lib().se_policy_record(self._h, replay._h, _ptr(self.actions), float(epsilon),
-                                         int(t) & 0xFFFFFFFF, self.env._stream()))
+        (se_policy_record / se_policy_record_f32; replay: shippingenv_amd.dqn.ReplayBuffer).
+        precision as act()."""
+        if precision not in ("bf16", "f32"):
+            raise ValueError("precision must be 'bf16' or 'f32'")
+        fn = N.lib().se_policy_record if precision == "bf16" else N.lib().se_policy_record_f32
+        N.check(fn(self._h, replay._h, _ptr(self.actions), float(epsilon), int(t) & 0xFFFFFFFF,
+                   self.env._stream()))
         replay._act = self.actions
         return self.actions
 

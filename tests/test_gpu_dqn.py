@@ -333,8 +333,10 @@ def test_training_loop_bookkeeping():
     assert float((q - q32).abs().max()) <= 0.03 * float(q32.abs().max())
 
 
-def test_fused_launches_equal_the_unfused_loop():
-    """The training loop's fused launches (se_policy_record = policy + remember(s, a);
+@pytest.mark.parametrize("precision", ["bf16", "f32"])
+def test_fused_launches_equal_the_unfused_loop(precision):
+    """The training loop's fused launches (se_policy_record / se_policy_record_f32 = policy
+    + remember(s, a), in the agent's precision;
     se_replay_end_reset = remember(r, s') + reset of the cut episodes; se_qtrain_step_policy
     = the update + the policy's repack + the counter's advance) give, bit for bit, what the
     separate launches give: actions, env state, losses, the update counter, the weights,
@@ -366,7 +368,8 @@ def test_fused_launches_equal_the_unfused_loop():
     for cls in (VecDQNAgent, Unfused):
         env = make_env(4096 + 4, seed=21)
         torch.manual_seed(0)
-        agent = cls(env, graph=False, batch_size=512, epsilon=0.4, target_update_every=3, max_steps=7)
+        agent = cls(env, graph=False, batch_size=512, epsilon=0.4, target_update_every=3, max_steps=7,
+                    precision=precision)
         _OPEN.append(agent)
         agents.append(agent)
         envs.append(env)

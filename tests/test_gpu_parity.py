@@ -634,3 +634,89 @@ def test_step_seq_equals_step_calls(auto, n):
         b.step_seq(acts[0])  # one row, not [K, n]
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("P", [5, 64])
+def test_agent_replay_need_draw_restores_state(P, water):
+    """tapes that lack a variate the step needs. se_step_agent_replay answers
+    SE_ERR_NEED_DRAW (10) and puts back the env's old state (shipenv.hip: the group restore
+    after its stores, full groups and the n % 4 tail); the typed replay kernel and the host
+    build of the same code (se_host_step_replay, the drop-in's stepper) must agree bit for
+    bit on state, reward, done, err and the `used` bits, and a NEED_DRAW env must equal its
+    pre-state. n = 4k + 3; each tape field is NaN (or arrive_dest -1) for ~30 % of envs;
+    a quarter of the envs sit one move from their destination port (arrivals)."""
+    from shippingenv_amd.shipping._host import host_step_replay
+    from shippingenv_amd.vec import TAPE_DTYPE, random_water_ports
+
+    table = _reference_decode(P)
+    ports = [[41, 40], [60, 22], [78, 29], [49, 72], [62, 72]] if P == 5 else random_water_ports(water, 64, seed=3)
+    rng = np.random.default_rng(100 + P)
+    n = 4 * 1000 + 3
+    valid = sorted(i for i, v in table.items() if v is not None and i >= 0)
+    acts = np.where(rng.random(n) < 0.7, rng.integers(0, 4, n), rng.choice(valid, n)).astype(np.int32)
+    mk = lambda: VecEnv(n, water=water, ports=ports, seed=6)  # noqa: E731
+    a, b = mk(), mk()
+    for e in (a, b):
+        e.reset()
+        e.step(torch.ones(n, dtype=torch.int32, device=e.device))  # everyone moves east once
+    st0 = get_state(a)
+    # arrivals: a quarter of the envs one move from their destination port
+    px, py = np.array([p[0] for p in ports]), np.array([p[1] for p in ports])
+    dxy = {0: (0, -1), 1: (-1, 0), 2: (0, 1), 3: (1, 0)}  # N, E, S, W (shipping/type.py:8-16)
+    for i in np.nonzero(rng.random(n) < 0.25)[0]:
+        k = int(rng.integers(0, 4))
+        d = st0["dest"][i]
+        x, y = px[d] - dxy[k][0], py[d] - dxy[k][1]
+        if 0 <= x < 100 and 0 <= y < 100:
+            st0["x"][i], st0["y"][i] = x, y
+            acts[i] = k
+    st0["cargo"] = rng.integers(0, 60, n).astype(np.int32)
+    st0["fuel"] = np.where(rng.random(n) < 0.1, rng.random(n) * 1.5, 50 + rng.random(n) * 100)
+    for e in (a, b):
+        for f in FIELDS:
+            v = st0[f]
+            if f in ("origin", "dest"):
+                v = np.where(v < 0, 255, v)
+            t = getattr(e, f)
+            t.copy_(torch.from_numpy(np.ascontiguousarray(v).astype(t.cpu().numpy().dtype)))
+    tape = np.zeros(n, TAPE_DTYPE)
+    for f in ("u_fuel", "u_gate", "u_type", "beta"):
+        tape[f] = np.where(rng.random(n) < 0.3, np.nan, rng.random(n))
+    tape["u_gate"] = np.where(np.isnan(tape["u_gate"]), np.nan, tape["u_gate"] * 0.5)  # the gate fires often
+    tape["arrive_dest"] = np.where(rng.random(n) < 0.3, -1, rng.integers(0, P, n))
+    typ, va, vb = (np.zeros(n, np.int32) for _ in range(3))
+    for k, i in enumerate(acts):
+        typ[k], va[k], vb[k] = table[int(i)]
+    ra, da, ea, used_a = a.step_agent_replay(acts, tape)
+    rb, db, eb = b.step_replay(typ, va, vb, tape)
+    torch.cuda.synchronize()
+    used_b = b._keep[3].cpu().numpy().view(TAPE_DTYPE)
+    hs = {f: (np.where(st0[f] < 0, 255, st0[f]) if f in ("origin", "dest") else st0[f]) for f in FIELDS}
+    h = host_step_replay(water, a.port_x, a.port_y, a.port_fuel, a.port_cargo, hs, typ, va, vb, tape)
+    sa, sb = get_state(a), get_state(b)
+    hstate = {f: (np.where(h[f] == 255, -1, h[f].astype(np.int32)) if f in ("origin", "dest")
+                  else (h[f] if f == "fuel" else h[f].astype(np.int32))) for f in FIELDS}
+    for f in FIELDS:
+        for other, name in ((sb, "typed"), (hstate, "host")):
+            np.testing.assert_array_equal(np.asarray(sa[f]).view(np.uint8), np.asarray(other[f]).view(np.uint8),
+                                          err_msg=f"{f}: agent vs {name}")
+    ea, eb = ea.cpu().numpy().astype(np.int32), eb.cpu().numpy().astype(np.int32)
+    np.testing.assert_array_equal(ea, eb)
+    np.testing.assert_array_equal(ea, h["err"].astype(np.int32))
+    for x, name in ((rb.cpu().numpy(), "typed"), (h["reward"], "host")):
+        np.testing.assert_array_equal(ra.cpu().numpy().view(np.uint32), x.view(np.uint32), err_msg=name)
+    np.testing.assert_array_equal(da.cpu().numpy(), db.cpu().numpy())
+    np.testing.assert_array_equal(da.cpu().numpy(), h["done"])
+    np.testing.assert_array_equal(used_a["used"], used_b["used"])
+    np.testing.assert_array_equal(used_a["used"], h["tape"]["used"])
+    need = ea == 10
+    assert need.sum() > 100 and (ea == 0).sum() > 100, (need.sum(), (ea == 0).sum())
+    for f in FIELDS:  # NEED_DRAW: the pre-state, untouched
+        np.testing.assert_array_equal(np.asarray(sa[f])[need].view(np.uint8),
+                                      np.asarray(st0[f])[need].view(np.uint8), err_msg=f"restore {f}")
+    assert (ra.cpu().numpy()[need] == 0).all() and (da.cpu().numpy()[need] == 0).all()
+    # quads that mix NEED_DRAW and stepped envs (the restore is per env, not per group)
+    q = need[:n - 3].reshape(-1, 4)
+    assert ((q.sum(1) > 0) & (q.sum(1) < 4)).sum() > 50
+    a.close()
+    b.close()
