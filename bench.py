@@ -73,6 +73,8 @@ def parse():
     p.add_argument("--dqn-steps", type=int, default=50,
                    help="config 5: timed DQN policy + step iterations at N envs/GPU (fp32 policy, then "
                         "bf16); 0 = skip")
+    p.add_argument("--preroll5", type=int, default=300,
+                   help="config 5: untimed policy + step iterations from reset (bf16 policy) before the legs")
     p.add_argument("--train-steps", type=int, default=30,
                    help="timed vectorised DQN training iterations (policy, step, replay, update); 0 = skip")
     p.add_argument("--train-batch", type=int, default=8192, help="DQN minibatch per update")
@@ -438,6 +440,10 @@ def run_config5(n, args, dist):
     every = max(1, min(100, K // 2))
     stream = torch.cuda.current_stream(env.device)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # pre-roll with the bf16 policy (fast) to the steady episode mix: episodes of ~240 steps
+    # then end in every timed step, so the all-reduced returns are the consumer's real ones
+    for t in range(args.preroll5):
+        env.step(pol.act(eps, 200_000 + t))
     legs = {}
     for i, prec in enumerate(("f32", "bf16")):
         for t in range(5):  # warm-up: both kernels and the stats path loaded
@@ -529,7 +535,8 @@ def run_config5(n, args, dist):
                     "per step the fused DQN policy (obs + DQNNetwork 26->128->128->259 + masked first argmax "
                     "+ eps-greedy 0.1; fp32 on f32 MFMA, se_policy_f32) then se_step; RCCL SUM all-reduce "
                     "of {sum return, episodes, sum len} every min(100, K // 2) steps in the timed region; "
-                    "random-init weights. bf16: the same loop on the bf16 policy (se_policy)",
+                    "random-init weights; untimed pre-roll of preroll_steps bf16 policy steps from reset. "
+                    "bf16: the same loop on the bf16 policy (se_policy)",
         "value": f32["value"],
         "unit": "env-steps/s (policy + step, end to end)",
         "precision": "fp32 (the reference's network precision, agents/dqn.py:198-204)",
@@ -539,6 +546,7 @@ def run_config5(n, args, dist):
         "ms_per_step": f32["ms_per_step"],
         "e2e_kernel_ms": f32["e2e_kernel_ms"],
         "policy_ms": f32["policy_ms"],
+        "preroll_steps": args.preroll5,
         "allreduce_every": every,
         "allreduces_in_timed_region": f32["allreduces_in_timed_region"],
         "episodes": f32["episodes"],

@@ -53,10 +53,11 @@ class Sample:
             O.reset(self.world, st, seed=seed, env_id_base=s, epoch=0)
         self.loss_pairs = self.reset_pairs = 0
 
-    def step(self, t, auto, stats=None, acts_dev=None):
+    def step(self, t, t_act, auto, stats=None, acts_dev=None):
+        """One step: draws at the env's step counter t, the synthetic agent's row t_act."""
         O = self.O
         for st, s in zip(self.sts, self.starts):
-            a = O.gen_actions(SLICE, self.P, self.seed, s, t)
+            a = O.gen_actions(SLICE, self.P, self.seed, s, t_act)
             if acts_dev is not None:
                 np.testing.assert_array_equal(a, acts_dev[s:s + SLICE])
             cargo0, origin0 = st.cargo.copy(), st.origin.copy()
@@ -111,7 +112,7 @@ def test_headline_kseq_after_preroll_vs_oracle(oracle_mod):
     row = torch.empty(N, dtype=torch.int32, device=env.device)
     for k in range(PREROLL):
         env.step(env.gen_actions(1_000_000 + k, out=row))
-        smp.step(1_000_000 + k, False)
+        smp.step(k, 1_000_000 + k, False)
         if k in (0, 499):
             smp.check(env, f"pre-roll step {k}")
     smp.check(env, "after the pre-roll")
@@ -119,11 +120,11 @@ def test_headline_kseq_after_preroll_vs_oracle(oracle_mod):
     acts = torch.stack([env.gen_actions(t) for t in range(TIMED)])
     for t in range(5):
         env.step_seq(acts[t:t + 1])
-        smp.step(t, False, acts_dev=acts[t].cpu().numpy())
+        smp.step(PREROLL + t, t, False, acts_dev=acts[t].cpu().numpy())
         smp.check(env, f"step_seq step {t}")
     env.step_seq(acts[5:])
     for t in range(5, TIMED):
-        smp.step(t, False)
+        smp.step(PREROLL + t, t, False)
     smp.check(env, "step_seq steps 5..19")
     # in steady state about 3 % of ships carry cargo
     carrying = float((env.cargo > 0).float().mean())
@@ -149,7 +150,7 @@ def test_config4_autoreset_after_preroll_vs_oracle(oracle_mod):
     row = torch.empty(N, dtype=torch.int32, device=env.device)
     for k in range(PREROLL):
         env.step(env.gen_actions(1_000_000 + k, out=row))
-        smp.step(1_000_000 + k, True, stats=stats)
+        smp.step(k, 1_000_000 + k, True, stats=stats)
         if k in (0, 499):
             smp.check(env, f"pre-roll step {k}", auto=True)
     smp.check(env, "after the pre-roll", auto=True)
@@ -157,7 +158,7 @@ def test_config4_autoreset_after_preroll_vs_oracle(oracle_mod):
     for t in range(TIMED):
         acts = env.gen_actions(t)
         env.step(acts)
-        smp.step(t, True, stats=stats, acts_dev=acts.cpu().numpy() if t < 2 else None)
+        smp.step(PREROLL + t, t, True, stats=stats, acts_dev=acts.cpu().numpy() if t < 2 else None)
         smp.check(env, f"timed step {t}", auto=True)
         if t == TIMED - 1:  # the done list of the last step lists exactly the sampled dones
             ids = env.done_list()[0].cpu().numpy()
