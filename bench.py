@@ -894,6 +894,20 @@ def main():
                            "frac": roofline(BYTES_STEP, args.large_n, kr, CANONICAL_STEP)["frac"],
                            "committed_trace": committed_trace("large_n_from_reset")},
         }
+        if not args.no_config4:
+            # config 4 at the same size in its steady episode mix (the same pre-roll): the
+            # auto-reset step with the traffic beyond the Infinity Cache
+            ports64 = random_water_ports(builtin_water(), 64, seed=3)
+            el4b, k4b, st4b, _ = run_config(args.large_n, ports64, True, small, dist, "large-n-config4",
+                                            preroll=args.preroll4)
+            out["large_n"]["config4"] = {
+                "value": round(args.large_n * small.steps / el4b, 1),
+                "ms_per_step": round(el4b / small.steps * 1e3, 5),
+                "roofline": roofline(BYTES_STEP_AUTO, args.large_n, k4b, CANONICAL_STEP_AUTO)
+                | {"committed_trace": committed_trace("large_n_config4")},
+                "episodes": st4b[1],
+                "preroll_steps": args.preroll4,
+            }
         tb, srcb = pmc_traffic("step_kernel_big_bytes_per_launch")
         if tb:
             out["large_n"]["roofline"]["traffic"] = tb

@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "libshipenv_hip.so")
+# SHIPENV_LIB names another build of the same library (an A/B variant under _lib/abl)
+LIB_PATH = os.environ.get("SHIPENV_LIB") or os.path.join(HERE, "_lib", "libshipenv_hip.so")
 ABI_VERSION = 1
 
 SE_FLAG_AUTO_RESET = 1

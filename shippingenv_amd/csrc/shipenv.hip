@@ -722,6 +722,9 @@ struct At {
 };
 
 // The inputs of the 4 envs of one group.
+#ifndef SHIPENV_EP_EARLY
+#define SHIPENV_EP_EARLY 0  // 1 = auto-reset: the episode counters load with the group (experiment)
+#endif
 template <bool kTyped, bool kAuto, bool kNt = false>
 struct Group {
     uint32_t x, y, org, dst;  // packed u8 x4
@@ -749,6 +752,10 @@ struct Group {
                 ld4_full<kNt>(A.act_a, at.g0, p, lane);
                 ld4_full<kNt>(A.act_b, at.g0, q, lane);
             }
+            if (kAuto && SHIPENV_EP_EARLY) {
+                ld4_full<kNt>(S.ep_return, at.g0, e, lane);
+                ld4_full<kNt>(S.ep_len, at.g0, l, lane);
+            }
         } else {
             x = ld4u8_tail(S.x, at.base, at.n);
             y = ld4u8_tail(S.y, at.base, at.n);
@@ -770,6 +777,7 @@ struct Group {
     // episode counters of a full group: loaded late (step_group), they would
     // otherwise hold 8 registers across the whole step
     __device__ __forceinline__ void load_episode(const StepArgs& A, At<true> at) {
+        if (SHIPENV_EP_EARLY) return;
         ld4_full<kNt>(A.st.ep_return, at.g0, e);
         ld4_full<kNt>(A.st.ep_len, at.g0, l);
     }

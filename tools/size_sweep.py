@@ -24,7 +24,7 @@ BYTES = {3: 42, 4: 58}
 PEAK = 8000.0  # GB/s, MI355X HBM3E
 
 
-def one(n, config, steps):
+def one(n, config, steps, preroll=0):
     from shippingenv_amd.maps import builtin_water
     from shippingenv_amd.vec import VecEnv, random_water_ports
 
@@ -35,6 +35,10 @@ def one(n, config, steps):
     for t in range(rows):
         env.gen_actions(t, out=acts[t])
     env.reset()
+    row = torch.empty(n, dtype=torch.int32, device="cuda:0")
+    for t in range(preroll):  # the bench's steady state: untimed steps from reset, rows of their own
+        env.step(env.gen_actions(1_000_000 + t, out=row))
+    del row
     for t in range(10):
         env.step(acts[t % rows])
     torch.cuda.synchronize()
@@ -47,7 +51,7 @@ def one(n, config, steps):
     del acts
     torch.cuda.empty_cache()
     gbps = BYTES[config] * n / (us * 1e-6) / 1e9
-    return {"n": n, "config": config, "steps": steps, "us_per_step": round(us, 3),
+    return {"n": n, "config": config, "steps": steps, "preroll": preroll, "us_per_step": round(us, 3),
             "env_steps_per_s": round(n / (us * 1e-6), 1), "achieved_gbps": round(gbps, 1),
             "frac": round(gbps / PEAK, 4), "bytes_per_env_step": BYTES[config]}
 
@@ -57,6 +61,8 @@ def main():
     p.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "size_sweep.json"))
     p.add_argument("--log2n", default="14-25", help="config-3 sizes: a range lo-hi or a list a,b")
     p.add_argument("--log2n4", default="18,20,22,24", help="config-4 sizes ('' = none)")
+    p.add_argument("--preroll", type=int, default=1000,
+                   help="untimed steps from reset before timing (bench.py's steady state; 0 = from reset)")
     a = p.parse_args()
 
     def sizes(spec):
@@ -71,12 +77,12 @@ def main():
     res = []
     for n, c in runs:
         steps = 1000 if n <= (1 << 20) else max(50, (1000 << 20) // n)
-        r = one(n, c, steps)
+        r = one(n, c, steps, a.preroll)
         print(json.dumps(r), flush=True)
         res.append(r)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
-        json.dump({"device": torch.cuda.get_device_name(0),
+        json.dump({"device": torch.cuda.get_device_name(0), "preroll": a.preroll,
                    "nt_loads_env": os.environ.get("SHIPENV_NT_LOADS"), "runs": res}, f, indent=1)
 
 

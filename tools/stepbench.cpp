@@ -59,6 +59,7 @@ static void* dev(size_t bytes) {
 int main(int argc, char** argv) {
     int64_t n = 1 << 20;
     int config = 3, steps = 1000, rows = 0, warm = 20;  // rows > 0: cycle through that many action rows
+    int preroll = 0;  // untimed steps from reset before the warm-up (the bench's steady state), one row each
     bool gen_late = false;  // generate the timed rows after the warm-up steps (right before timing)
     bool per_launch = false;  // also print every timed launch's own event-pair duration
     std::vector<std::string> libs;
@@ -69,6 +70,7 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--rows")) rows = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--warm")) warm = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--gen-late")) gen_late = true;
+        else if (!strcmp(argv[i], "--preroll")) preroll = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--per-launch")) per_launch = true;
         else libs.push_back(argv[i]);
     }
@@ -156,6 +158,15 @@ int main(int argc, char** argv) {
         int32_t* acts = (int32_t*)dev((size_t)total * n * 4);
         for (int t = 0; t < (gen_late ? warm : total); ++t) SE(a.gen(env, acts + (size_t)t * n, (uint32_t)t, s));
         SE(a.reset(env, nullptr, s));
+        if (preroll > 0) {
+            int32_t* row = (int32_t*)dev((size_t)n * 4);
+            for (int t = 0; t < preroll; ++t) {
+                SE(a.gen(env, row, (uint32_t)(1000000 + t), s));
+                SE(a.step(env, row, s));
+            }
+            CK(hipStreamSynchronize(s));
+            CK(hipFree(row));
+        }
         for (int t = 0; t < warm; ++t) SE(a.step(env, acts + (size_t)t * n, s));
         if (gen_late)
             for (int t = warm; t < total; ++t) SE(a.gen(env, acts + (size_t)t * n, (uint32_t)t, s));
@@ -188,8 +199,8 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
         const char* base = strrchr(path.c_str(), '/');
         printf("{\"lib\": \"%s\", \"n\": %lld, \"config\": %d, \"steps\": %d, \"action_rows\": %d, "
-               "\"warm\": %d, \"gen_late\": %d, \"us_per_step\": %.3f}\n",
-               base ? base + 1 : path.c_str(), (long long)n, config, steps, r, warm, (int)gen_late,
+               "\"warm\": %d, \"preroll\": %d, \"gen_late\": %d, \"us_per_step\": %.3f}\n",
+               base ? base + 1 : path.c_str(), (long long)n, config, steps, r, warm, preroll, (int)gen_late,
                1000.0 * ms / steps);
         fflush(stdout);
         SE(a.destroy(env));
