@@ -52,10 +52,6 @@ constexpr int kQHidden = 128;     // DQNNetwork hidden_size (dqn.py:24, default 
 #ifndef SHIPENV_POLICY_WAVES_PER_EU
 #define SHIPENV_POLICY_WAVES_PER_EU 0  // 0: the compiler's choice from the block size
 #endif
-#ifndef SHIPENV_POLICY16
-#define SHIPENV_POLICY16 0  // 1: the 16 x 16 MFMA form of the bf16 policy (policy16_kernel and its image layout)
-#endif
-constexpr bool kPolicy16 = SHIPENV_POLICY16 != 0;
 constexpr int kPolicyBlock = SHIPENV_POLICY_BLOCK;
 constexpr int kPolicyWgPerCu = SHIPENV_POLICY_WG_PER_CU;
 constexpr int kPolicyWaves = kPolicyBlock / 64;
@@ -80,19 +76,15 @@ struct QnetDims {
     // row of TAKE_CARGO amount 1 and of TAKE_FUEL amount 1
     __host__ __device__ int cargo_row1() const { return compact ? 4 + P : 5 + P; }
     __host__ __device__ int fuel_row1() const { return compact ? 4 + P + cmax : 55 + P; }
-    // 32 x 32 layout: 4 fc1 tiles, 4 x 4 x 2 fc2 fragments, mt3 x 4 x 2 fc3 fragments.
-    // 16 x 16 layout (kPolicy16): 8 fc1 blocks, 8 x 4 fc2 fragments, 2 mt3 x 4 fc3 fragments
-    // (16-row blocks, 32-wide k-steps), the same bytes for fc2 and fc3.
-    __host__ __device__ int w1() const { return 0; }
-    __host__ __device__ int w2() const { return (kPolicy16 ? 8 : 4) * 1024; }
-    __host__ __device__ int w3() const { return w2() + 32 * 1024; }
+    __host__ __device__ int w1() const { return 0; }                    // 4 fc1 tiles
+    __host__ __device__ int w2() const { return 4 * 1024; }              // 4 x 4 x 2 fc2 fragments
+    __host__ __device__ int w3() const { return w2() + 32 * 1024; }      // mt3 x 4 x 2 fc3 fragments
     __host__ __device__ int b1() const { return w3() + mt3 * 8 * 1024; } // 128 f32, port block folded
     __host__ __device__ int b2() const { return b1() + 4 * kQHidden; }
     __host__ __device__ int b3() const { return b2() + 4 * kQHidden; }   // mt3 * 32 f32 (0 beyond A)
     __host__ __device__ int same() const { return b3() + mt3 * 128; }    // P uint64: ports on port p's cell
-    // fc3 epilogue masks: per 32-row tile (32 x 32) / per 16-row block (16 x 16), uint32
-    __host__ __device__ int regm() const { return same() + 8 * P; }
-    __host__ __device__ int bytes() const { return (regm() + 4 * mt3 * (kPolicy16 ? 2 : 1) + 15) & ~15; }
+    __host__ __device__ int regm() const { return same() + 8 * P; }      // mt3 uint32: fc3 epilogue regs
+    __host__ __device__ int bytes() const { return (regm() + 4 * mt3 + 15) & ~15; }
 };
 
 QnetDims qnet_dims(int P, bool compact = false, int cmax = 0, int fmax = 0) {
@@ -129,48 +121,19 @@ __device__ __forceinline__ int fc1_col(int j) {
 
 __device__ __forceinline__ int acc_row(int s, int j, int h) { return 16 * s + 8 * (j >> 2) + 4 * h + (j & 3); }
 
-// 16 x 16 layout (v_mfma_f32_16x16x32_bf16): lane l = c + 16 g holds A[row c][k = 8g + j] and
-// B[k = 8g + j][col c]; the result D has col c, rows 4g + r in its 4 registers. A layer's
-// 128 outputs for 16 envs are 8 blocks of 16 rows; k-step s of the next layer takes blocks 2s
-// and 2s + 1, element j of lane group g being input feature pi16(s, g, j) (the rows lane g
-// holds), and the weights' k order is permuted to match.
-__host__ __device__ __forceinline__ int pi16(int s, int g, int j) { return 32 * s + 16 * (j >> 2) + 4 * g + (j & 3); }
-
 __global__ __launch_bounds__(256) void qnet_pack_kernel(PackArgs A) {
     const QnetDims q = A.q[blockIdx.y];
     uint8_t* const img = A.img[blockIdx.y];
     if (A.bump && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *A.bump += 1;
     const int in1 = q.in1();
-    const int nm = kPolicy16 ? 2 * q.mt3 : q.mt3;  // epilogue mask words
-    const int n_w1 = (kPolicy16 ? 8 : 4) * 64, n_w2 = 32 * 64, n_w3 = q.mt3 * 8 * 64;
+    const int n_w1 = 4 * 64, n_w2 = 32 * 64, n_w3 = q.mt3 * 8 * 64;
     for (int t = blockIdx.x * blockDim.x + threadIdx.x;
-         t < n_w1 + n_w2 + n_w3 + 2 * kQHidden + q.mt3 * 32 + q.P + nm; t += gridDim.x * blockDim.x) {
+         t < n_w1 + n_w2 + n_w3 + 2 * kQHidden + q.mt3 * 32 + q.P + q.mt3; t += gridDim.x * blockDim.x) {
         if (t < n_w1 + n_w2 + n_w3) {
             int f = t >> 6;
             const int lane = t & 63, r = lane & 31, h = lane >> 5;
             bf16x8 v;
             uint8_t* dst;
-            if (kPolicy16) {  // 16-row blocks: fragment (block, k-step), lane c + 16 g
-                const int c = lane & 15, g = lane >> 4;
-                if (t < n_w1) {  // fc1 block f: k = 8g + j, only g = 0 live
-                    const int row = f * 16 + c;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) v[j] = g == 0 ? (__bf16)A.w1[row * in1 + fc1_col(j)] : (__bf16)0.0f;
-                    dst = img + q.w1() + f * 1024 + lane * 16;
-                } else {
-                    const bool second = t < n_w1 + n_w2;
-                    f -= second ? 8 : 8 + 32;  // fragment index block * 4 + s
-                    const int s = f & 3, row = (f >> 2) * 16 + c;
-                    const float* W = second ? A.w2 : A.w3;
-                    const bool in = second || row < q.rows;
-                    const int wrow = second ? row : q.action_of_row(row);
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) v[j] = in ? (__bf16)W[wrow * kQHidden + pi16(s, g, j)] : (__bf16)0.0f;
-                    dst = img + (second ? q.w2() : q.w3()) + f * 1024 + lane * 16;
-                }
-                *reinterpret_cast<bf16x8*>(dst) = v;
-                continue;
-            }
             if (t < n_w1) {  // fc1 tile f
                 const int row = f * 32 + r;
 #pragma unroll
@@ -218,24 +181,22 @@ __global__ __launch_bounds__(256) void qnet_pack_kernel(PackArgs A) {
             // base + (reg & 3) + 8 (reg >> 2) + 4h, h = 0, 1) can hold a valid action of
             // ANY env: a move or SELECT (row < 4 + P), or an amount within the largest
             // stock (is_valid_action, dqn.py:125-175). The epilogue skips the others.
-            const int mt = u - P, base = mt * (kPolicy16 ? 16 : 32);
+            const int mt = u - P, base = mt * 32;
             int cmax = 0, fmax = 0;
             for (int p = 0; p < P; ++p) {
                 cmax = max(cmax, min(wv.pcargo(p), 49));
                 fmax = max(fmax, min(wv.pfuel(p), 199));
             }
             const int c_lo = 5 + P, c_hi = 4 + P + cmax, f_lo = 55 + P, f_hi = 54 + P + fmax;
-            auto ok_row = [&](int row) {
-                const int a = q.action_of_row(row);
-                return row < q.rows && (a < 4 + P || (a >= c_lo && a <= c_hi) || (a >= f_lo && a <= f_hi));
-            };
             uint32_t rm = 0;
-            if (kPolicy16) {  // 16 x 16: bit i = row base + i
-                for (int i = 0; i < 16; ++i) rm |= (uint32_t)ok_row(base + i) << i;
-            } else {
-                for (int reg = 0; reg < 16; ++reg)
-                    for (int h = 0; h < 2; ++h) rm |= (uint32_t)ok_row(base + (reg & 3) + 8 * (reg >> 2) + 4 * h) << reg;
-            }
+            for (int reg = 0; reg < 16; ++reg)
+                for (int h = 0; h < 2; ++h) {
+                    const int row = base + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                    const int a = q.action_of_row(row);
+                    const bool ok = row < q.rows && (a < 4 + P || (a >= c_lo && a <= c_hi) ||
+                                                     (a >= f_lo && a <= f_hi));
+                    rm |= (uint32_t)ok << reg;
+                }
             reinterpret_cast<uint32_t*>(img + q.regm())[mt] = rm;
         }
     }
@@ -645,310 +606,6 @@ void policy_kernel(PolicyArgs A) {
     }
 }
 
-// ------------------------------------------------------------------ 16 x 16 tiles
-// policy16_kernel (kPolicy16): the same step on v_mfma_f32_16x16x32_bf16, 16 envs per wave
-// tile (env on the result's column, lane & 15; lane group g = lane >> 4 holds rows 4g..4g+3 of
-// each 16-row block). Per env it issues the same MFMA cycles and the same VALU as the
-// 32 x 32 form (an instruction covers 64 (env, row) pairs either way), with a quarter of
-// the accumulator registers per chain.
-typedef __attribute__((ext_vector_type(4))) float f32x4q;
-
-__device__ __forceinline__ f32x4q mfma16(const bf16x8& a, const bf16x8& b, f32x4q c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ f32x4q bias4(const float* b) {
-    const float4 v = *reinterpret_cast<const float4*>(b);
-    return f32x4q{v.x, v.y, v.z, v.w};
-}
-// blocks 2s and 2s + 1 of a layer's output -> k-step s of the next layer (pi16), relu after
-// the bf16 rounding as relu_pack
-__device__ __forceinline__ bf16x8 relu_pack16(const f32x4q& a, const f32x4q& b) {
-    u32x4 w;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        const f32x4q& src = p < 2 ? a : b;
-        const int i = 2 * (p & 1);
-        const bf16x2 v = __builtin_convertvector(f32x2{src[i], src[i + 1]}, bf16x2);
-        w[p] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(i16x2, v), i16x2{0, 0}));
-    }
-    return __builtin_bit_cast(bf16x8, w);
-}
-// valid rows base .. base + 15 of the layout for one env (bit i = row base + i)
-__device__ __forceinline__ uint32_t block_mask(const EnvValid& v, int base, int P) {
-    uint32_t m = range_bits(-base, 3 - base) | range_bits(v.c_lo - base, v.c_hi - base) |
-                 range_bits(v.f_lo - base, v.f_hi - base);
-    if (base < 4 + P) {
-        const int sh = base - 4;
-        m |= (uint32_t)(sh < 0 ? v.sel << -sh : (sh < 64 ? v.sel >> sh : 0ull));
-    }
-    return m & 0xffffu;
-}
-// can any row of block b be valid for this env
-__device__ __forceinline__ bool block_maybe(const EnvValid& v, int base, int P) {
-    const int top = base + 15;
-    return (base == 0) | ((v.cur >= 0) & (base < 4 + P)) | ((v.cst > 0) & (v.c_lo <= top) & (v.c_hi >= base)) |
-           ((v.fst > 0) & (v.f_lo <= top) & (v.f_hi >= base));
-}
-
-template <bool kQout>
-__global__ __launch_bounds__(kPolicyBlock) void policy16_kernel(PolicyArgs A) {
-    extern __shared__ uint4 smem[];
-    const QnetDims q = A.q;
-    const int qwords = q.bytes() / 16;
-    for (int i = threadIdx.x; i < qwords; i += kPolicyBlock) smem[i] = A.qimg[i];
-    const LdsWorld w = stage_world(A.world, A.dims, reinterpret_cast<uint32_t*>(smem + qwords));
-    const uint8_t* qb = reinterpret_cast<const uint8_t*>(smem);
-    const bf16x8* W1f = reinterpret_cast<const bf16x8*>(qb + q.w1());
-    const bf16x8* W2f = reinterpret_cast<const bf16x8*>(qb + q.w2());
-    const bf16x8* W3f = reinterpret_cast<const bf16x8*>(qb + q.w3());
-    const float* B1 = reinterpret_cast<const float*>(qb + q.b1());
-    const float* B2 = reinterpret_cast<const float*>(qb + q.b2());
-    const float* B3 = reinterpret_cast<const float*>(qb + q.b3());
-    const uint64_t* SAME = reinterpret_cast<const uint64_t*>(qb + q.same());
-
-    const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-    const int P = q.P, nb3 = 2 * q.mt3;
-    const int64_t tiles = (A.n + 15) >> 4;
-    const int64_t stride = (int64_t)gridDim.x * kPolicyWaves;
-    struct EnvIn {
-        double fuel;
-        uint32_t x, y, o8, d8;
-    };
-    auto load_env = [&](int64_t tile) {
-        const int64_t e = tile * 16 + c;
-        const int64_t ei = e < A.n ? e : A.n - 1;
-        return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei]};
-    };
-    int64_t tile = (int64_t)blockIdx.x * kPolicyWaves + (threadIdx.x >> 6);
-    EnvIn nxt = load_env(tile < tiles ? tile : 0);
-    for (; tile < tiles; tile += stride) {
-        const EnvIn cur_in = nxt;
-        if (tile + stride < tiles) nxt = load_env(tile + stride);
-        const int64_t e = tile * 16 + c;
-        const bool live = e < A.n;
-        const int x = (int)cur_in.x, y = (int)cur_in.y;
-        const int origin = cur_in.o8 == SE_NONE ? -1 : (int)cur_in.o8;
-        const int dest = cur_in.d8 == SE_NONE ? -1 : (int)cur_in.d8;
-        const float ff = (float)cur_in.fuel;
-        const __bf16 fh = (__bf16)ff, fl = (__bf16)(ff - (float)fh);
-        bf16x8 ob;
-        ob[0] = (__bf16)(float)x;
-        ob[1] = (__bf16)(float)y;
-        ob[2] = fh;
-        ob[3] = fl;
-        ob[4] = fh;
-        ob[5] = fl;
-        ob[6] = (__bf16)(float)origin;
-        ob[7] = (__bf16)(float)dest;
-        if (g) ob = bf16x8{};  // k = 8..31 of fc1's one k-step are padding
-
-        bf16x8 h1[4], h2[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {  // fc1 + relu: blocks 2s, 2s + 1 -> k-step s of fc2
-            const f32x4q a0 = mfma16(W1f[(2 * s) * 64 + lane], ob, bias4(B1 + 32 * s + 4 * g));
-            const f32x4q a1 = mfma16(W1f[(2 * s + 1) * 64 + lane], ob, bias4(B1 + 32 * s + 16 + 4 * g));
-            h1[s] = relu_pack16(a0, a1);
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {  // fc2 + relu: two independent 4-MFMA chains per k-step of fc3
-            f32x4q a0 = bias4(B2 + 32 * s2 + 4 * g), a1 = bias4(B2 + 32 * s2 + 16 + 4 * g);
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                a0 = mfma16(W2f[((2 * s2) * 4 + s) * 64 + lane], h1[s], a0);
-                a1 = mfma16(W2f[((2 * s2 + 1) * 4 + s) * 64 + lane], h1[s], a1);
-            }
-            h2[s2] = relu_pack16(a0, a1);
-        }
-        const EnvValid v = env_valid(w, q, SAME, x, y, origin);
-        float best = -INFINITY;
-        int bidx = 0x7fffffff;
-        for (int b = 0; b < nb3; ++b) {  // fc3 + the masked first-maximum argmax, one 16-row block at a time
-            const int base = 16 * b;
-            if (!kQout && !__any(block_maybe(v, base, P))) continue;
-            f32x4q acc = bias4(B3 + base + 4 * g);
-#pragma unroll
-            for (int s = 0; s < 4; ++s) acc = mfma16(W3f[(b * 4 + s) * 64 + lane], h2[s], acc);
-            const uint32_t m = block_mask(v, base, P) >> (4 * g);  // rows base + 4g + r
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const bool better = ((m >> r) & 1u) && acc[r] > best;  // ascending rows: first max
-                best = better ? acc[r] : best;
-                bidx = better ? base + 4 * g + r : bidx;
-            }
-            if (kQout && live) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {  // the full layout: row = action
-                    const int row = base + 4 * g + r;
-                    if (row < q.rows) A.q_out[e * A.ldq + row] = acc[r];
-                }
-            }
-        }
-        // the four lane groups hold the same env: larger value, then lower row (xor 16
-        // here, xor 32 in finish_env, whose writer is lane group 0)
-        const float ob2 = __shfl_xor(best, 16);
-        const int oi = __shfl_xor(bidx, 16);
-        if (ob2 > best || (ob2 == best && oi < bidx)) {
-            best = ob2;
-            bidx = oi;
-        }
-        FINISH_ENV(v, e, live, g, best, bidx, cur_in.x, cur_in.y, cur_in.o8, cur_in.d8, ff);
-        (void)dest;
-    }
-}
-
-// policy16_pipe_kernel: policy16_kernel's greedy path (no q_out) for layouts of at most four
-// 16-row fc3 blocks (P = 5 and every layout up to 64 compact rows), software-pipelined two
-// tiles deep within each wave: the fc1 / fc2 MFMA chains of tile i are issued in the same
-// basic block as the argmax epilogue of tile i - 1 (branch-free VALU on registers the chains
-// do not touch), so one wave's own MFMA shadow covers its epilogue instead of waiting on the
-// other waves of the SIMD. Exactly the same arithmetic as policy16_kernel, tile by tile.
-#ifndef SHIPENV_POLICY_PIPE
-#define SHIPENV_POLICY_PIPE 1  // 0: policy16_kernel for every layout (experiment)
-#endif
-constexpr int kPipeBlocks = 4;
-
-__global__ __launch_bounds__(kPolicyBlock) void policy16_pipe_kernel(PolicyArgs A) {
-    extern __shared__ uint4 smem[];
-    const QnetDims q = A.q;
-    const int qwords = q.bytes() / 16;
-    for (int i = threadIdx.x; i < qwords; i += kPolicyBlock) smem[i] = A.qimg[i];
-    const LdsWorld w = stage_world(A.world, A.dims, reinterpret_cast<uint32_t*>(smem + qwords));
-    const uint8_t* qb = reinterpret_cast<const uint8_t*>(smem);
-    const bf16x8* W1f = reinterpret_cast<const bf16x8*>(qb + q.w1());
-    const bf16x8* W2f = reinterpret_cast<const bf16x8*>(qb + q.w2());
-    const bf16x8* W3f = reinterpret_cast<const bf16x8*>(qb + q.w3());
-    const float* B1 = reinterpret_cast<const float*>(qb + q.b1());
-    const float* B2 = reinterpret_cast<const float*>(qb + q.b2());
-    const float* B3 = reinterpret_cast<const float*>(qb + q.b3());
-    const uint64_t* SAME = reinterpret_cast<const uint64_t*>(qb + q.same());
-
-    const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-    const int P = q.P, nb3 = 2 * q.mt3;  // <= kPipeBlocks (the host checks)
-    const int64_t tiles = (A.n + 15) >> 4;
-    const int64_t stride = (int64_t)gridDim.x * kPolicyWaves;
-    struct EnvIn {
-        double fuel;
-        uint32_t x, y, o8, d8;
-    };
-    auto load_env = [&](int64_t t) {
-        const int64_t e = t * 16 + c;
-        const int64_t ei = e < A.n ? e : A.n - 1;
-        return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei]};
-    };
-    // one tile in flight: its fc3 accumulators and what its epilogue and finish need
-    struct Pend {
-        f32x4q acc[kPipeBlocks];
-        EnvValid v;
-        int64_t e;
-        uint32_t x8, y8, o8, d8;
-        float ff;
-    };
-    // fc1, fc2 and the validity of one tile: h2 and the pending record (acc not yet set)
-    auto front = [&](const EnvIn& in, int64_t t, bf16x8 (&h2)[4], Pend& pd) {
-        pd.e = t * 16 + c;
-        pd.x8 = in.x;
-        pd.y8 = in.y;
-        pd.o8 = in.o8;
-        pd.d8 = in.d8;
-        const int origin = in.o8 == SE_NONE ? -1 : (int)in.o8;
-        const int dest = in.d8 == SE_NONE ? -1 : (int)in.d8;
-        const float ff = (float)in.fuel;
-        pd.ff = ff;
-        const __bf16 fh = (__bf16)ff, fl = (__bf16)(ff - (float)fh);
-        bf16x8 ob;
-        ob[0] = (__bf16)(float)in.x;
-        ob[1] = (__bf16)(float)in.y;
-        ob[2] = fh;
-        ob[3] = fl;
-        ob[4] = fh;
-        ob[5] = fl;
-        ob[6] = (__bf16)(float)origin;
-        ob[7] = (__bf16)(float)dest;
-        if (g) ob = bf16x8{};
-        bf16x8 h1[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const f32x4q a0 = mfma16(W1f[(2 * s) * 64 + lane], ob, bias4(B1 + 32 * s + 4 * g));
-            const f32x4q a1 = mfma16(W1f[(2 * s + 1) * 64 + lane], ob, bias4(B1 + 32 * s + 16 + 4 * g));
-            h1[s] = relu_pack16(a0, a1);
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {
-            f32x4q a0 = bias4(B2 + 32 * s2 + 4 * g), a1 = bias4(B2 + 32 * s2 + 16 + 4 * g);
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                a0 = mfma16(W2f[((2 * s2) * 4 + s) * 64 + lane], h1[s], a0);
-                a1 = mfma16(W2f[((2 * s2 + 1) * 4 + s) * 64 + lane], h1[s], a1);
-            }
-            h2[s2] = relu_pack16(a0, a1);
-        }
-        pd.v = env_valid(w, q, SAME, (int)in.x, (int)in.y, origin);
-    };
-    // fc3 over the blocks some env of the wave can choose from (the others keep their bias:
-    // no env of the wave has a valid row there, so the epilogue's masks drop them)
-    auto fc3 = [&](const bf16x8 (&h2)[4], Pend& pd) {
-#pragma unroll
-        for (int b = 0; b < kPipeBlocks; ++b) {
-            pd.acc[b] = bias4(B3 + 16 * b + 4 * g);
-            if (b < nb3 && __any(block_maybe(pd.v, 16 * b, P))) {
-#pragma unroll
-                for (int s = 0; s < 4; ++s) pd.acc[b] = mfma16(W3f[(b * 4 + s) * 64 + lane], h2[s], pd.acc[b]);
-            }
-        }
-    };
-    // the masked first maximum of one tile (branch-free), merged over lane groups g ^ 1
-    auto argmax = [&](const Pend& pd, float& best, int& bidx) {
-        best = -INFINITY;
-        bidx = 0x7fffffff;
-#pragma unroll
-        for (int b = 0; b < kPipeBlocks; ++b) {
-            const uint32_t m = (b < nb3 ? block_mask(pd.v, 16 * b, P) : 0u) >> (4 * g);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const bool better = ((m >> r) & 1u) && pd.acc[b][r] > best;
-                best = better ? pd.acc[b][r] : best;
-                bidx = better ? 16 * b + 4 * g + r : bidx;
-            }
-        }
-        const float ob2 = __shfl_xor(best, 16);
-        const int oi = __shfl_xor(bidx, 16);
-        if (ob2 > best || (ob2 == best && oi < bidx)) {
-            best = ob2;
-            bidx = oi;
-        }
-    };
-
-    int64_t tile = (int64_t)blockIdx.x * kPolicyWaves + (threadIdx.x >> 6);
-    if (tile >= tiles) return;
-    EnvIn nxt = load_env(tile);
-    Pend pd;
-    {
-        const EnvIn in = nxt;
-        if (tile + stride < tiles) nxt = load_env(tile + stride);
-        bf16x8 h2[4];
-        front(in, tile, h2, pd);
-        fc3(h2, pd);
-    }
-    for (tile += stride; tile < tiles; tile += stride) {
-        const EnvIn in = nxt;
-        if (tile + stride < tiles) nxt = load_env(tile + stride);
-        // tile i's MFMA chains and tile i - 1's epilogue in one basic block
-        float best;
-        int bidx;
-        argmax(pd, best, bidx);
-        Pend pn;
-        bf16x8 h2[4];
-        front(in, tile, h2, pn);
-        FINISH_ENV(pd.v, pd.e, pd.e < A.n, g, best, bidx, pd.x8, pd.y8, pd.o8, pd.d8, pd.ff);
-        fc3(h2, pn);
-        pd = pn;
-    }
-    float best;
-    int bidx;
-    argmax(pd, best, bidx);
-    FINISH_ENV(pd.v, pd.e, pd.e < A.n, g, best, bidx, pd.x8, pd.y8, pd.o8, pd.d8, pd.ff);
-}
-
 // ------------------------------------------------------------------ the f32 policy step
 // The fp32-faithful form of the same step (se_policy_f32): DQNNetwork evaluated in f32 as
 // agents/dqn.py:198-200 runs it (fp32 weights, fp32 activations), on
@@ -1241,20 +898,14 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
     // the compact layout unless every row's Q is wanted
     const QnetDims& q = q_out ? qn->q : qn->qc;
     const size_t lds = (size_t)q.bytes() + lds_bytes(env);
-    static std::atomic<uint64_t> lds_set{0}, lds16{0}, lds16q{0};
-    rc = kPolicy16 ? allow_dynamic_lds(lds16, reinterpret_cast<const void*>(policy16_kernel<false>), 160 * 1024, env->device)
-                   : allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(policy_kernel), 160 * 1024, env->device);
-    static std::atomic<uint64_t> lds16p{0};
-    if (!rc && kPolicy16)
-        rc = allow_dynamic_lds(lds16q, reinterpret_cast<const void*>(policy16_kernel<true>), 160 * 1024, env->device);
-    if (!rc && kPolicy16)
-        rc = allow_dynamic_lds(lds16p, reinterpret_cast<const void*>(policy16_pipe_kernel), 160 * 1024, env->device);
+    static std::atomic<uint64_t> lds_set{0};
+    rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(policy_kernel), 160 * 1024, env->device);
     if (rc) return rc;
     if (lds > 160 * 1024) return fail(SE_EINVAL, "network + world image exceed the 160 KB LDS");
     int dev_cus = 256;
     if (hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, env->device) != hipSuccess)
         dev_cus = 256;
-    const int64_t tiles = kPolicy16 ? (env->n + 15) / 16 : (env->n + 31) / 32;
+    const int64_t tiles = (env->n + 31) / 32;
     const int64_t want = (tiles + kPolicyWaves - 1) / kPolicyWaves;
     const int64_t resident = (int64_t)dev_cus * kPolicyWgPerCu;  // workgroups resident at once
     const int grid = (int)(want < resident ? want : resident);
@@ -1279,11 +930,7 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
         A.rec_head = rec->head;
         A.rec_cap = rec->cap;
     }
-    if (!kPolicy16) policy_kernel<<<grid, kPolicyBlock, lds, (hipStream_t)stream>>>(A);
-    else if (q_out) policy16_kernel<true><<<grid, kPolicyBlock, lds, (hipStream_t)stream>>>(A);
-    else if (SHIPENV_POLICY_PIPE && 2 * q.mt3 <= kPipeBlocks)
-        policy16_pipe_kernel<<<grid, kPolicyBlock, lds, (hipStream_t)stream>>>(A);
-    else policy16_kernel<false><<<grid, kPolicyBlock, lds, (hipStream_t)stream>>>(A);
+    policy_kernel<<<grid, kPolicyBlock, lds, (hipStream_t)stream>>>(A);
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }

@@ -648,20 +648,9 @@ struct Grad {
 // byte offset of W[row][k] within a packed policy image's fc2 / fc3 fragments: fragment
 // ((row / 32) * 4 + k / 32) * 2 + s, lane row % 32 + 32 h, element j, where
 // k % 32 = 16 s + 8 (j >> 2) + 4 h + (j & 3) (qnet_pack_kernel's acc_row map)
-// The 16 x 16 layout (kPolicy16): fragment (row / 16) * 4 + k / 32, lane row % 16 + 16 g,
-// element j, where k % 32 = 16 (j >> 2) + 4 g + (j & 3) (qpolicy.h pi16)
 __device__ __forceinline__ int pol_offset(int row, int k) {
-    if constexpr (kPolicy16) {
-        const int kk = k & 31, g = (kk >> 2) & 3, j = 4 * (kk >> 4) + (kk & 3);
-        return (((row >> 4) * 4 + (k >> 5)) * 64 + (row & 15) + 16 * g) * 16 + 2 * j;
-    }
     const int kk = k & 31, s = kk >> 4, h = (kk >> 2) & 1, j = 4 * ((kk >> 3) & 1) + (kk & 3);
     return ((((row >> 5) * 4 + (k >> 5)) * 2 + s) * 64 + (row & 31) + 32 * h) * 16 + 2 * j;
-}
-// byte offset of element j of fc1 row f's fragment (lane 0 .. 31 of tile f / 32, or lane
-// 0 .. 15 of block f / 16)
-__device__ __forceinline__ int pol_fc1_offset(int f, int j) {
-    return kPolicy16 ? ((f >> 4) * 64 + (f & 15)) * 16 + 2 * j : ((f >> 5) * 64 + (f & 31)) * 16 + 2 * j;
 }
 
 __device__ __forceinline__ void put_bf16(uint8_t* p, float v) { *reinterpret_cast<__bf16*>(p) = (__bf16)v; }
@@ -965,7 +954,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                     for (int l = 0; l < 2; ++l)
 #pragma unroll
                         for (int j = 0; j < 8; ++j)
-                            if (fc1_col(j) == c) put_bf16(A.img[l] + A.q[l].w1() + pol_fc1_offset(f, j), p);
+                            if (fc1_col(j) == c) put_bf16(A.img[l] + A.q[l].w1() + ((f >> 5) * 64 + (f & 31)) * 16 + 2 * j, p);
             }
         }
         if (tid == 0) {
