@@ -74,7 +74,7 @@ def parse():
                    help="config 5: timed DQN policy + step iterations at N envs/GPU (fp32 policy, then "
                         "bf16); 0 = skip")
     p.add_argument("--preroll5", type=int, default=300,
-                   help="config 5: untimed policy + step iterations from reset (bf16 policy) before the legs")
+                   help="config 5: untimed policy + step iterations from reset (eps 1.0) before the legs")
     p.add_argument("--train-steps", type=int, default=30,
                    help="timed vectorised DQN training iterations (policy, step, replay, update); 0 = skip")
     p.add_argument("--train-batch", type=int, default=8192, help="DQN minibatch per update")
@@ -211,32 +211,41 @@ def timed_loop(env, acts, first, steps, dist, reduce_every=0, counter=None, step
     (tools/diag/timed_loop_forms.py: 0.15 us per step over the driver's 20 steps).
 
     One VecEnv.step call per step, the drop-in's per-step API; step_seq=True issues the
-    same launches with VecEnv.step_seq (se_step_seq: the launch loop in native code, split
-    only where an event or a stats all-reduce goes between two steps). Unprofiled the two
-    give the same GPU time per launch (tools/diag/issue_forms.py: the Python loop keeps the
-    queue ahead of an 8 us kernel); under a kernel tracer, whose per-launch host cost
-    leaves gaps between Python-issued kernels, step_seq keeps them back to back."""
+    same launches with VecEnv.step_seq (se_step_seq_mark: the launch loop in native code,
+    which records the launch-1 event itself, split only where a stats all-reduce goes
+    between two steps). On a box whose Python issue rate is slower than an 8 us kernel
+    (BENCH r04a: step_py 10.5 us per launch by events) only step_seq keeps the queue full."""
     stream = torch.cuda.current_stream(env.device)
     ef, e1 = (torch.cuda.Event(enable_timing=True) for _ in range(2))
+    for e in (ef, e1):  # the HIP events exist before the clock starts (torch creates them lazily)
+        e.record(stream)
     # the step's action rows as views made before the clock starts: indexing the
     # [steps, n] table inside the loop is harness work (1.4 us of host time per step,
     # tools/diag/host_step_cost.py), not the step's
     if not step_seq:
         chunks = [acts[first + k] for k in range(steps)]
-    else:  # [first step], then runs that end where an all-reduce follows
-        cuts = sorted({0, 1, steps} | ({k for k in range(reduce_every, steps, reduce_every)}
-                                       if reduce_every else set()))
+    else:  # runs that end where an all-reduce follows; the first run records ef after its
+        # launch 1 from native code (se_step_seq_mark): splitting the run there for a Python
+        # record cost ~0.7 us per step over the driver's 20 (tools/diag/wall_forms.py, r04w)
+        cuts = sorted({0, steps} | ({k for k in range(reduce_every, steps, reduce_every)}
+                                    if reduce_every else set()))
         chunks = [acts[first + a:first + b] for a, b in zip(cuts, cuts[1:])]
-    step = env.step_seq if step_seq else env.step
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     done = 0
     for c in chunks:
-        step(c)
-        done += c.shape[0] if step_seq else 1
-        if done == 1:
-            ef.record(stream)
+        if step_seq:
+            if done == 0:
+                env.step_seq(c, mark=ef, mark_after=1)
+            else:
+                env.step_seq(c)
+            done += c.shape[0]
+        else:
+            env.step(c)
+            done += 1
+            if done == 1:
+                ef.record(stream)
         if reduce_every and done % reduce_every == 0:
             # episode-return aggregation over the GPUs (RCCL all-reduce of 3 doubles), in
             # place in the env's stats buffer: a torch copy_ of the 24 bytes first went
@@ -440,10 +449,14 @@ def run_config5(n, args, dist):
     every = max(1, min(100, K // 2))
     stream = torch.cuda.current_stream(env.device)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    # pre-roll with the bf16 policy (fast) to the steady episode mix: episodes of ~240 steps
-    # then end in every timed step, so the all-reduced returns are the consumer's real ones
+    # pre-roll at the agent's initial exploration rate (DQN_EPSILON = 1.0,
+    # utils/constants.py:33): random valid actions take the ships out of their origin ports.
+    # A random-init network's greedy choice at a port is almost never a move (4 of ~250
+    # valid actions), so from reset at eps 0.1 no ship leaves port and no episode ends in
+    # the timed steps (BENCH r04a: 0 episodes). After it, ships at sea move greedily, burn
+    # fuel and finish episodes, so the all-reduced returns are the consumer's real ones.
     for t in range(args.preroll5):
-        env.step(pol.act(eps, 200_000 + t))
+        env.step(pol.act(1.0, 200_000 + t))
     legs = {}
     for i, prec in enumerate(("f32", "bf16")):
         for t in range(5):  # warm-up: both kernels and the stats path loaded
@@ -535,7 +548,8 @@ def run_config5(n, args, dist):
                     "per step the fused DQN policy (obs + DQNNetwork 26->128->128->259 + masked first argmax "
                     "+ eps-greedy 0.1; fp32 on f32 MFMA, se_policy_f32) then se_step; RCCL SUM all-reduce "
                     "of {sum return, episodes, sum len} every min(100, K // 2) steps in the timed region; "
-                    "random-init weights; untimed pre-roll of preroll_steps bf16 policy steps from reset. "
+                    "random-init weights; untimed pre-roll of preroll_steps policy steps from reset at "
+                    "eps 1.0 (the agent's initial exploration rate). "
                     "bf16: the same loop on the bf16 policy (se_policy)",
         "value": f32["value"],
         "unit": "env-steps/s (policy + step, end to end)",

@@ -153,6 +153,13 @@ int se_step(se_env* env, const int32_t* actions, void* stream);
  * (environment.py:359-376). */
 int se_step_seq(se_env* env, const int32_t* actions, int64_t ld, int32_t steps, void* stream);
 
+/* se_step_seq that also records `event` (a hipEvent_t, may be NULL) on the stream right
+ * after launch number `mark_after` (1..steps): a timer mark inside the sequence without
+ * splitting it into two calls (the host round trip between them left the GPU idle for
+ * several microseconds; tools/diag/wall_forms.py). */
+int se_step_seq_mark(se_env* env, const int32_t* actions, int64_t ld, int32_t steps, void* stream,
+                     void* event, int32_t mark_after);
+
 /* step() with the reference's typed action [ActionType, value] (environment.py:359-376):
  * type 1..4 (shipping/type.py:1-5); MOVE value = (a, b) any integers; others value = a. */
 int se_step_typed(se_env* env, const int32_t* type, const int32_t* a, const int32_t* b,

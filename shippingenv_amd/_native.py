@@ -31,7 +31,7 @@ ROLL_DONE, ROLL_MAX_STEPS, ROLL_RAISED, ROLL_ATTEMPTS, ROLL_BAD_SRC = 0, 1, 2, 3
 
 # every symbol include/shipenv.h declares
 EXPORTS = (
-    "se_create", "se_set_ports", "se_bind", "se_reset", "se_reset_to", "se_step", "se_step_seq",
+    "se_create", "se_set_ports", "se_bind", "se_reset", "se_reset_to", "se_step", "se_step_seq", "se_step_seq_mark",
     "se_step_typed", "se_step_replay", "se_step_agent_replay", "se_observe", "se_valid_mask", "se_gen_actions",
     "se_sample_actions", "se_rollout", "se_qnet_create", "se_qnet_set_weights", "se_policy", "se_policy_f32",
     "se_qnet_repack", "se_policy_record", "se_policy_record_f32",
@@ -80,6 +80,7 @@ def _declare(lib):
         "se_reset_to": [P, P, P, P, P],
         "se_step": [P, P, P],
         "se_step_seq": [P, P, i64, i32, P],
+        "se_step_seq_mark": [P, P, i64, i32, P, P, i32],
         "se_step_typed": [P, P, P, P, P],
         "se_step_replay": [P, P, P, P, P, P],
         "se_step_agent_replay": [P, P, P, P],

@@ -2742,16 +2742,26 @@ int se_step(se_env* env, const int32_t* actions, void* stream) {
     return launch_step(env, false, false, actions, nullptr, nullptr, nullptr, stream);
 }
 
-int se_step_seq(se_env* env, const int32_t* actions, int64_t ld, int32_t steps, void* stream) {
+int se_step_seq_mark(se_env* env, const int32_t* actions, int64_t ld, int32_t steps, void* stream,
+                     void* event, int32_t mark_after) {
     int rc = check_ready(env);
     if (rc) return rc;
     if (steps < 0) return fail(SE_EINVAL, "negative step count");
     if (steps > 1 && (ld < env->n || (ld & 3))) return fail(SE_EINVAL, "row stride must be >= n and a multiple of 4");
+    if (event && (mark_after < 1 || mark_after > steps)) return fail(SE_EINVAL, "mark_after must be in [1, steps]");
     for (int32_t k = 0; k < steps; ++k) {
         rc = launch_step(env, false, false, actions + (int64_t)k * ld, nullptr, nullptr, nullptr, stream, nullptr, true);
         if (rc) return rc;
+        if (event && k + 1 == mark_after) {
+            DeviceGuard g(env->device);
+            HIP_TRY(hipEventRecord((hipEvent_t)event, (hipStream_t)stream));
+        }
     }
     return SE_OK;
+}
+
+int se_step_seq(se_env* env, const int32_t* actions, int64_t ld, int32_t steps, void* stream) {
+    return se_step_seq_mark(env, actions, ld, steps, stream, nullptr, 0);
 }
 
 int se_step_typed(se_env* env, const int32_t* type, const int32_t* a, const int32_t* b,

@@ -196,15 +196,26 @@ class VecEnv:
         self._keep = a
         return self.reward, self.done, self.err
 
-    def step_seq(self, actions):
+    def step_seq(self, actions, mark=None, mark_after=1):
         """len(actions) consecutive step() calls issued from native code (se_step_seq):
         actions is an int32 device tensor [K, n] (rows contiguous, 16-byte aligned), row k
-        the actions of step k. Returns the last step's (reward, done, err)."""
+        the actions of step k. mark: a torch.cuda.Event recorded on the current stream right
+        after launch `mark_after` (se_step_seq_mark), a timer mark inside the one native
+        call. Returns the last step's (reward, done, err)."""
         a = actions
         if not (type(a) is torch.Tensor and a.dtype is torch.int32 and a.is_cuda and a.dim() == 2
                 and a.get_device() == self._dev_index and a.shape[1] == self.n and a.stride(1) == 1
                 and a.data_ptr() % 16 == 0 and (a.shape[0] < 2 or a.stride(0) % 4 == 0)):
             raise ValueError("step_seq needs an int32 [K, n] device tensor with 16-byte aligned rows")
+        if mark is not None:
+            if mark.cuda_event == 0:  # torch creates the HIP event on its first record
+                mark.record()
+            rc = N.lib().se_step_seq_mark(self._h, a.data_ptr(), a.stride(0), a.shape[0],
+                                          _raw_stream(self._dev_index), mark.cuda_event, int(mark_after))
+            if rc:
+                N.check(rc)
+            self._keep = a
+            return self.reward, self.done, self.err
         rc = self._se_step_seq(self._h, a.data_ptr(), a.stride(0), a.shape[0], _raw_stream(self._dev_index))
         if rc:
             N.check(rc)

@@ -621,8 +621,14 @@ def test_step_seq_equals_step_calls(auto, n):
     for t in range(K):
         a.step(acts[t].contiguous())
     b.step_seq(acts[:7])
-    b.step_seq(acts[7:])
+    # the rest with a timer mark after its launch 3 (se_step_seq_mark, bench.py's timed loop)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    b.step_seq(acts[7:], mark=e0, mark_after=3)
+    e1.record()
     torch.cuda.synchronize()
+    assert e0.elapsed_time(e1) > 0.0
+    with pytest.raises(Exception):
+        b.step_seq(acts[:2], mark=e0, mark_after=3)  # mark_after beyond the run: SE_EINVAL
     fa, fb = get_state(a), get_state(b)
     for f in FIELDS:
         np.testing.assert_array_equal(fa[f], fb[f], err_msg=f)

@@ -199,9 +199,9 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
         const char* base = strrchr(path.c_str(), '/');
         printf("{\"lib\": \"%s\", \"n\": %lld, \"config\": %d, \"steps\": %d, \"action_rows\": %d, "
-               "\"warm\": %d, \"preroll\": %d, \"gen_late\": %d, \"us_per_step\": %.3f}\n",
+               "\"warm\": %d, \"preroll\": %d, \"gen_late\": %d, \"step_blocks\": \"%s\", \"us_per_step\": %.3f}\n",
                base ? base + 1 : path.c_str(), (long long)n, config, steps, r, warm, preroll, (int)gen_late,
-               1000.0 * ms / steps);
+               getenv("SHIPENV_STEP_BLOCKS") ? getenv("SHIPENV_STEP_BLOCKS") : "default", 1000.0 * ms / steps);
         fflush(stdout);
         SE(a.destroy(env));
         for (void* p : {(void*)st.x, (void*)st.y, (void*)st.origin, (void*)st.dest, (void*)st.done,
