@@ -111,6 +111,9 @@ struct Frags {
     }
 };
 
+#ifndef SHIPENV_QT_W3U
+#define SHIPENV_QT_W3U 16  // T2: dW3 rows gathered per thread and round (8 x kU rows per round)
+#endif
 #ifndef SHIPENV_QT_LOOKAHEAD
 #define SHIPENV_QT_LOOKAHEAD 8  // B operands read this many k-steps ahead of their MFMA (0: as needed)
 #endif
@@ -1073,7 +1076,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             if (tid < 128) g = G[Grad::w3 + i3];
             else if (tid == 128) g = G[Grad::b3(A.d) + a3];
         } else {
-            g = slot_row_sum<16>(A.W.part_w3, A.W.part_b3, A.W.part_map, A.tiles, a3, red4, list, wtot);
+            g = slot_row_sum<SHIPENV_QT_W3U>(A.W.part_w3, A.W.part_b3, A.W.part_map, A.tiles, a3, red4, list, wtot);
             if (mode == 1) {
                 if (tid < 128) G[Grad::w3 + i3] = g;
                 else if (tid == 128) G[Grad::b3(A.d) + a3] = g;

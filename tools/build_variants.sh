@@ -4,7 +4,7 @@
 # shippingenv_amd/_lib/abl/<name>.so:
 #   VARIANTS="a:-DSHIPENV_FC2_SPLIT=2 b:-DSHIPENV_FC2_SPLIT=4,-DSHIPENV_POLICY_BLOCK=640" bash tools/build_variants.sh
 set -eu
-D=shippingenv_amd/_lib/abl
+D=${ABL_DIR:-shippingenv_amd/_lib/abl}
 mkdir -p $D && rm -f $D/*.so
 B="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math --offload-arch=gfx950"
 S="shippingenv_amd/csrc/shipenv.hip shippingenv_amd/csrc/mapload.cpp"
