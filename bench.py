@@ -204,11 +204,11 @@ def make_actions(env, steps):
 def timed_loop(env, acts, first, steps, dist, reduce_every=0, counter=None, step_seq=False):
     """K back-to-back launches bracketed by barrier + synchronize on both sides; wall
     time is the max over ranks. Two HIP events on the launch stream give the GPU time per
-    launch (roofline.kernel_ms): one after launch 1, one after launch K, over K - 1 launches,
-    so the launch duration does not include the ~20 us launch 1 waits to start on an idle
-    queue ("The short run"). No event precedes launch 1: an event
-    record costs host time ahead of it and a bubble between kernels on the GPU
-    (tools/diag/timed_loop_forms.py: 0.15 us per step over the driver's 20 steps).
+    launch (roofline.kernel_ms): one right before launch 1, one after launch K, over K
+    launches. The first is taken by the GPU when it reaches it, so the ~20 us that launch 1's
+    command takes to reach an idle queue (DESIGN.md section 5, "The short run") is not in it;
+    the few microseconds between the event and launch 1's dispatch are (a conservative
+    basis: the kernel time it gives is at most the trace's launch average plus those).
 
     One VecEnv.step call per step, the drop-in's per-step API; step_seq=True issues the
     same launches with VecEnv.step_seq (se_step_seq_mark: the launch loop in native code,
@@ -224,9 +224,10 @@ def timed_loop(env, acts, first, steps, dist, reduce_every=0, counter=None, step
     # tools/diag/host_step_cost.py), not the step's
     if not step_seq:
         chunks = [acts[first + k] for k in range(steps)]
-    else:  # runs that end where an all-reduce follows; the first run records ef after its
-        # launch 1 from native code (se_step_seq_mark): splitting the run there for a Python
-        # record cost ~0.7 us per step over the driver's 20 (tools/diag/wall_forms.py, r04w)
+    else:  # runs that end where an all-reduce follows; the first run records ef right before
+        # its launch 1 from native code (se_step_seq_mark, mark_after = 0): splitting the run
+        # after launch 1 for a Python record cost ~0.7 us per step over the driver's 20, and a
+        # native record there 0.2-0.4 (tools/diag/wall_forms.py, profiles/r04/wall_forms*)
         cuts = sorted({0, steps} | ({k for k in range(reduce_every, steps, reduce_every)}
                                     if reduce_every else set()))
         chunks = [acts[first + a:first + b] for a, b in zip(cuts, cuts[1:])]
@@ -237,15 +238,15 @@ def timed_loop(env, acts, first, steps, dist, reduce_every=0, counter=None, step
     for c in chunks:
         if step_seq:
             if done == 0:
-                env.step_seq(c, mark=ef, mark_after=1)
+                env.step_seq(c, mark=ef, mark_after=0)
             else:
                 env.step_seq(c)
             done += c.shape[0]
         else:
+            if done == 0:
+                ef.record(stream)
             env.step(c)
             done += 1
-            if done == 1:
-                ef.record(stream)
         if reduce_every and done % reduce_every == 0:
             # episode-return aggregation over the GPUs (RCCL all-reduce of 3 doubles), in
             # place in the env's stats buffer: a torch copy_ of the 24 bytes first went
@@ -257,7 +258,7 @@ def timed_loop(env, acts, first, steps, dist, reduce_every=0, counter=None, step
     torch.cuda.synchronize()
     dist.barrier()
     wall = dist.max(time.perf_counter() - t0)
-    k_ms = ef.elapsed_time(e1) / (steps - 1) if steps > 1 else wall * 1e3 / steps
+    k_ms = ef.elapsed_time(e1) / steps
     return wall, k_ms
 
 
@@ -659,7 +660,8 @@ def run_dqn_train(n, args, dist):
     return out
 
 
-KERNEL_MS_BASIS = "HIP events on the launch stream, end of launch 1 to end of launch K, over K - 1 launches (this run)"
+KERNEL_MS_BASIS = ("HIP events on the launch stream, one right before launch 1 and one after launch K, over K "
+                   "launches (this run)")
 
 
 def roofline(bytes_per_step, n, k_ms, canonical):

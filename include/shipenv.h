@@ -154,9 +154,9 @@ int se_step(se_env* env, const int32_t* actions, void* stream);
 int se_step_seq(se_env* env, const int32_t* actions, int64_t ld, int32_t steps, void* stream);
 
 /* se_step_seq that also records `event` (a hipEvent_t, may be NULL) on the stream right
- * after launch number `mark_after` (1..steps): a timer mark inside the sequence without
- * splitting it into two calls (the host round trip between them left the GPU idle for
- * several microseconds; tools/diag/wall_forms.py). */
+ * after launch number `mark_after` (0..steps; 0 = before the first launch): a timer mark
+ * in the same native call as the launches, with no host round trip between them
+ * (tools/diag/wall_forms.py). */
 int se_step_seq_mark(se_env* env, const int32_t* actions, int64_t ld, int32_t steps, void* stream,
                      void* event, int32_t mark_after);
 

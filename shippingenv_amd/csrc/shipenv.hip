@@ -1637,6 +1637,14 @@ __device__ __forceinline__ int wave_sum_int(int v) {
            (__builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48));
 }
 
+// Statistics slab update. SHIPENV_SLAB_ATOMIC = 0 (default): lanes 0-2 of each wave load the
+// wave's entry at the kernel's start and store old + sum at its end (plain loads and stores;
+// the entry is this wave's alone during a launch). At N = 2^24 the three no-return f64
+// atomics per wave (memory-side 64-B requests) cost config 4 ~16 us of ~190
+// (SHIPENV_ABL4 = 4 ablation, profiles/r04/c4split.jsonl).
+#ifndef SHIPENV_SLAB_ATOMIC
+#define SHIPENV_SLAB_ATOMIC 0
+#endif
 // slab[i] += v without reading it back into the wave: the add runs in L2 and the
 // wave does not wait for it. Only this wave's lane 0 adds to its own entry during
 // a launch (step_tail_kernel adds in a later launch), so the order of additions is
@@ -1709,6 +1717,16 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(SHIP
         G.template load<true>(A, At<true>{last < 0 ? full - 1 : first, 0, A.n}, lane);
     }
     __builtin_amdgcn_sched_barrier(0);
+    // auto-reset: this wave's statistics so far ({sum ret, episodes, sum len} on lanes 0-2),
+    // loaded now so the end of the wave adds to them without waiting (SHIPENV_SLAB_ATOMIC = 0)
+    // (kRec keeps the atomics: two more registers there spilled)
+    constexpr bool kSlabRmw = kAuto && !kRec && (SHIPENV_ABL4 & 4) == 0 && !SHIPENV_SLAB_ATOMIC;
+    [[maybe_unused]] double slab_prev = 0.0;
+    if constexpr (kSlabRmw) {
+        const uint32_t l = threadIdx.x & 63;
+        const double* sl = late_args().slab + 4 * (blockIdx.x * (kStepBlock / 64) + (threadIdx.x >> 6));
+        slab_prev = sl[l < 3 ? l : 0];
+    }
     // agent-index actions: the production step, or its replay-tape form (parity)
     constexpr bool kAgent = !kTyped && !SHIPENV_ABLATE;
     constexpr bool kDraws = kAgent && !kReplay && SHIPENV_EARLY_DRAWS;
@@ -1785,11 +1803,20 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(SHIP
             len = wave_sum((double)bs.len);
             eps = wave_sum_int(bs.eps);
         }
-        if (eps != 0 && (threadIdx.x & 63) == 0) {
+        if constexpr (!kSlabRmw) {
+            if (eps != 0 && (threadIdx.x & 63) == 0) {
+                double* sl = late_args().slab + 4 * (blockIdx.x * (kStepBlock / 64) + (threadIdx.x >> 6));
+                slab_add(sl + 0, ret);
+                slab_add(sl + 1, (double)eps);
+                slab_add(sl + 2, len);
+            }
+        } else if (eps != 0 && (threadIdx.x & 63) < 3) {
+            // the same additions in the same order as a read-modify-write from registers:
+            // lanes 0-2 hold the entry's old values (loaded at the kernel's start), and no
+            // other wave touches this entry during the launch
+            const uint32_t l = threadIdx.x & 63;
             double* sl = late_args().slab + 4 * (blockIdx.x * (kStepBlock / 64) + (threadIdx.x >> 6));
-            slab_add(sl + 0, ret);
-            slab_add(sl + 1, (double)eps);
-            slab_add(sl + 2, len);
+            sl[l] = slab_prev + (l == 0 ? ret : l == 1 ? (double)eps : len);
         }
     }
 }
@@ -2748,14 +2775,15 @@ int se_step_seq_mark(se_env* env, const int32_t* actions, int64_t ld, int32_t st
     if (rc) return rc;
     if (steps < 0) return fail(SE_EINVAL, "negative step count");
     if (steps > 1 && (ld < env->n || (ld & 3))) return fail(SE_EINVAL, "row stride must be >= n and a multiple of 4");
-    if (event && (mark_after < 1 || mark_after > steps)) return fail(SE_EINVAL, "mark_after must be in [1, steps]");
-    for (int32_t k = 0; k < steps; ++k) {
-        rc = launch_step(env, false, false, actions + (int64_t)k * ld, nullptr, nullptr, nullptr, stream, nullptr, true);
-        if (rc) return rc;
-        if (event && k + 1 == mark_after) {
+    if (event && (mark_after < 0 || mark_after > steps)) return fail(SE_EINVAL, "mark_after must be in [0, steps]");
+    for (int32_t k = 0; k <= steps; ++k) {
+        if (event && k == mark_after) {
             DeviceGuard g(env->device);
             HIP_TRY(hipEventRecord((hipEvent_t)event, (hipStream_t)stream));
         }
+        if (k == steps) break;
+        rc = launch_step(env, false, false, actions + (int64_t)k * ld, nullptr, nullptr, nullptr, stream, nullptr, true);
+        if (rc) return rc;
     }
     return SE_OK;
 }

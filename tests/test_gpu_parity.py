@@ -620,9 +620,10 @@ def test_step_seq_equals_step_calls(auto, n):
     b.reset()
     for t in range(K):
         a.step(acts[t].contiguous())
-    b.step_seq(acts[:7])
-    # the rest with a timer mark after its launch 3 (se_step_seq_mark, bench.py's timed loop)
+    # timer marks inside the runs (se_step_seq_mark): before launch 1 (bench.py's timed loop)
+    # and after launch 3
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    b.step_seq(acts[:7], mark=e1, mark_after=0)
     b.step_seq(acts[7:], mark=e0, mark_after=3)
     e1.record()
     torch.cuda.synchronize()

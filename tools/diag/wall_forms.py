@@ -7,9 +7,11 @@ setting is read at runtime initialisation:
   dev_kernarg        HIP_FORCE_DEV_KERNARG=1 (kernel arguments in device memory)
   spin               hipSetDeviceFlags(hipDeviceScheduleSpin) before the first HIP call
   dev_kernarg+spin   both
-and, inside each child, two loop forms alternated: `events` (bench.py's loop: an event
-after launch 1 and after launch K) and `bare` (the K launches in one native call, no
-event), whose wall time shows what the mid-loop event costs.
+  active_wait        ROC_ACTIVE_WAIT_TIMEOUT=2000 (the host spins up to 2 ms on a signal before
+                     it sleeps on the interrupt)
+and, inside each child, three loop forms rotated: `events` (bench.py's native-issue loop, an
+event after launch 1 and after launch K), `bare` (the K launches in one native call, no event)
+and `py` (bench.py's loop with one VecEnv.step call per step).
 
     python tools/diag/wall_forms.py [--reps 15] [--settings default,spin]
 One JSON line per (setting, form): median / min wall us per step, events us per launch.
@@ -28,6 +30,7 @@ SETTINGS = {
     "dev_kernarg": {"HIP_FORCE_DEV_KERNARG": "1"},
     "spin": {"SHIPENV_DIAG_SPIN": "1"},
     "dev_kernarg+spin": {"HIP_FORCE_DEV_KERNARG": "1", "SHIPENV_DIAG_SPIN": "1"},
+    "active_wait": {"ROC_ACTIVE_WAIT_TIMEOUT": "2000"},
 }
 
 
@@ -61,12 +64,13 @@ def child(reps, K):
     for k in range(5):
         env.step_seq(acts[k:k + 1])
     torch.cuda.synchronize()
-    res = {"events": {"wall": [], "events": []}, "bare": {"wall": []}}
+    res = {"events": {"wall": [], "events": []}, "bare": {"wall": []}, "py": {"wall": [], "events": []}}
+    forms = ("events", "bare", "py")
     for rep in range(reps):
         first = (rep * 3) % 64
-        for form in ("events", "bare") if rep % 2 == 0 else ("bare", "events"):
-            if form == "events":
-                wall, k_ms = b.timed_loop(env, acts, first, K, dist, step_seq=True)
+        for form in forms[rep % 3:] + forms[:rep % 3]:
+            if form in ("events", "py"):
+                wall, k_ms = b.timed_loop(env, acts, first, K, dist, step_seq=form == "events")
                 res[form]["events"].append(round(k_ms * 1e3, 3))
             else:
                 torch.cuda.synchronize()

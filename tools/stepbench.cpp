@@ -1,7 +1,8 @@
 // stepbench.cpp — K back-to-back se_step calls driven from C++ (tuning tool): the
 // step rate without the Python host path, for one or more library builds.
 //   hipcc -O2 -std=c++17 -o tools/stepbench tools/stepbench.cpp -ldl
-//   tools/stepbench [--n N] [--config 3|4] [--steps K] [--rows R] lib.so [lib2.so ...]
+//   tools/stepbench [--n N] [--config 3|4|5|6] [--steps K] [--rows R] lib.so [lib2.so ...]
+// (config 5: 64 ports without auto-reset; 6: the 5 ports with auto-reset)
 // (--rows R: step t reads action row t % R, so R small keeps the actions cache-resident)
 // Config 3: the bundled map, the reference's 5 default ports; config 4: 64 ports on
 // water cells (any fixed set: this tool times, it does not check), auto-reset.
@@ -110,7 +111,9 @@ int main(int argc, char** argv) {
         std::vector<uint8_t> water(100 * 100);
         SE(a.map(jpg.data(), jpg.size(), 100, 100, water.data()));
         std::vector<int32_t> px, py, pf, pc;
-        if (config == 4) {
+        // config 4: 64 ports + auto-reset; 5: 64 ports, no auto-reset; 6: 5 ports + auto-reset
+        const bool p64 = config == 4 || config == 5, aut = config == 4 || config == 6;
+        if (p64) {
             for (int c = 0; c < 100 * 100 && (int)px.size() < 64; c += 37)
                 if (water[c]) {
                     px.push_back(c / 100);
@@ -129,7 +132,7 @@ int main(int argc, char** argv) {
         }
         se_env* env = nullptr;
         SE(a.create(&env, 0, n, 0, 100, 100, water.data(), (int32_t)px.size(), px.data(), py.data(),
-                    pf.data(), pc.data(), 2026, config == 4 ? SE_FLAG_AUTO_RESET : 0));
+                    pf.data(), pc.data(), 2026, aut ? SE_FLAG_AUTO_RESET : 0));
         se_state st{};
         st.x = (uint8_t*)dev(n);
         st.y = (uint8_t*)dev(n);
@@ -140,7 +143,7 @@ int main(int argc, char** argv) {
         st.fuel = (double*)dev(8 * n);
         st.cargo = (int32_t*)dev(4 * n);
         st.reward = (float*)dev(4 * n);
-        if (config == 4) {
+        if (aut) {
             int64_t stride = 0;
             int32_t segs = 0;
             SE(a.layout(env, &stride, &segs));
