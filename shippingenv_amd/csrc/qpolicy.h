@@ -29,12 +29,6 @@
 // 128 VGPRs with no spills and no scratch: check (-Rpass-analysis=kernel-resource-usage)
 // after any edit that adds register pressure.
 
-#ifndef SHIPENV_POLICY_DRAW2
-#define SHIPENV_POLICY_DRAW2 0  // 1: exploration draws for two tiles every other iteration (both lane halves)
-#endif
-#ifndef SHIPENV_POLICY_REGM
-#define SHIPENV_POLICY_REGM 1  // 0: the fc3 epilogue tests every register (no per-register uniform branch)
-#endif
 #ifndef SHIPENV_POLICY_ABL
 #define SHIPENV_POLICY_ABL 0  // timing-only ablations of the policy kernel (1: plain max epilogue, 2: no fc3)
 #endif
@@ -424,25 +418,9 @@ void policy_kernel(PolicyArgs A) {
     };
     int64_t tile = (int64_t)blockIdx.x * kPolicyWaves + (threadIdx.x >> 6);
     EnvIn nxt = load_env(tile < tiles ? tile : 0);
-#if SHIPENV_POLICY_DRAW2
-    // the exploration draw of an env (Philox, kSlotPolicy) is one block on one lane; a tile's
-    // 32 envs need 32 lanes, so every other iteration all 64 lanes draw: lanes h = 0 for this
-    // tile's envs, lanes h = 1 for the next tile's (the wave's next iteration), and that
-    // iteration's envs are finished on their h = 1 lanes (same draws, same decisions)
-    // the two words a decision uses wait in LDS (after the world image), not in registers
-    // live across the next tile's layers (two more VGPRs there spilled 12)
-    uint2* stash = reinterpret_cast<uint2*>(smem + qwords + A.dims.padded() / 4) + threadIdx.x;
-    int it = 0;
-#endif
     for (; tile < tiles; tile += stride) {
         const EnvIn cur_in = nxt;
         if (tile + stride < tiles) nxt = load_env(tile + stride);
-#if SHIPENV_POLICY_DRAW2
-        if (A.eps > 0.0 && (it & 1) == 0) {  // wave-uniform; at the top, where few registers are live
-            const U4 dd = draw(env_key(A.seed, A.env_base + (tile + h * stride) * 32 + r), A.t, kSlotPolicy);
-            *stash = make_uint2(dd.v[0], dd.v[1]);
-        }
-#endif
         const int64_t e = tile * 32 + r;
         const bool live = e < A.n;
         const int x = (int)cur_in.x, y = (int)cur_in.y;
@@ -573,14 +551,13 @@ void policy_kernel(PolicyArgs A) {
 #else
 #pragma unroll
             for (int reg = 0; reg < 16; ++reg) {
-                if (SHIPENV_POLICY_REGM && !((rm >> reg) & 1u)) continue;
+                if (!((rm >> reg) & 1u)) continue;
                 const int i = (reg & 3) + 8 * (reg >> 2);
                 const bool better = ((m >> i) & 1u) && c[reg] > best;  // ascending rows: first max
                 best = better ? c[reg] : best;
                 bidx = better ? base + 4 * h + i : bidx;
             }
 #endif
-            (void)rm;
             if (A.q_out && live) {
 #pragma unroll
                 for (int reg = 0; reg < 16; ++reg) {  // the full layout: row = action
@@ -596,21 +573,10 @@ void policy_kernel(PolicyArgs A) {
             best = ob2;
             bidx = oi;
         }
-#if SHIPENV_POLICY_DRAW2
-        const int fin_h = it & 1;
-        ++it;
-        if (h == fin_h && live) {
-#else
         if (h == 0 && live) {
-#endif
             int act = bidx == 0x7fffffff ? 0 : q.action_of_row(bidx);  // no valid action: 0 (:188-189)
             if (A.eps > 0.0) {
-#if SHIPENV_POLICY_DRAW2
-                const uint2 sd = *stash;
-                const U4 d{{sd.x, sd.y, 0u, 0u}};
-#else
                 const U4 d = draw(env_key(A.seed, A.env_base + e), A.t, kSlotPolicy);
-#endif
                 if (u32(d.v[0]) <= A.eps) {  // np.random.rand() <= epsilon (:191)
                     // random.choice(valid_actions) (:192): the k-th valid action, ascending
                     const int nsel = __popcll(sel);
@@ -931,7 +897,7 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
     DeviceGuard g(env->device);
     // the compact layout unless every row's Q is wanted
     const QnetDims& q = q_out ? qn->q : qn->qc;
-    const size_t lds = (size_t)q.bytes() + lds_bytes(env) + (SHIPENV_POLICY_DRAW2 ? kPolicyBlock * 8 : 0);
+    const size_t lds = (size_t)q.bytes() + lds_bytes(env);
     static std::atomic<uint64_t> lds_set{0};
     rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(policy_kernel), 160 * 1024, env->device);
     if (rc) return rc;

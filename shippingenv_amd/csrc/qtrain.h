@@ -93,6 +93,24 @@ __device__ __forceinline__ void st_part(float* p, float v) {
     if constexpr (SHIPENV_QT_NT != 0) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
+// T1's dW2 / dW3 partials as 16-byte stores (4 consecutive f1 / feature columns of one
+// row: the MFMAs take H1 / H2 as their A operand, so a lane's accumulator registers 4q..4q+3
+// are 4 adjacent columns). SHIPENV_QT_WT = 1: write-through (sc1), so the 12.6-16.8 MB of
+// partials are not left dirty in the XCDs' L2s for the kernel boundary to flush before T2
+// (MI355X_MICROARCH.md price list, "boundary" and "publish-large"); 0: plain stores.
+#ifndef SHIPENV_QT_WT
+#define SHIPENV_QT_WT 1
+#endif
+__device__ __forceinline__ void st_part4(float* base, uint32_t idx, float a, float b, float c, float d) {
+    const uint4 w = make_uint4(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b),
+                               __builtin_bit_cast(uint32_t, c), __builtin_bit_cast(uint32_t, d));
+    if constexpr (SHIPENV_QT_WT != 0) {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), r, 4u * idx, 0, 16);  // aux 16: sc1
+    } else {
+        *reinterpret_cast<uint4*>(base + idx) = w;
+    }
+}
 
 __device__ __forceinline__ int acc_r(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
 
@@ -111,6 +129,9 @@ struct Frags {
     }
 };
 
+#ifndef SHIPENV_QT_LATE_ADAM
+#define SHIPENV_QT_LATE_ADAM 1  // T2: Adam's constants after the sums' loads are issued (0: at the start)
+#endif
 #ifndef SHIPENV_QT_W3U
 #define SHIPENV_QT_W3U 16  // T2: dW3 rows gathered per thread and round (8 x kU rows per round)
 #endif
@@ -518,25 +539,28 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             const int f = wt * 32 + acc_r(r, lane);
             DZ1[f * kLS + c] = HA[f * kLS + c] > 0.0f ? acc[r] : 0.0f;
         }
-    } else {  // partial dW2[f2][f1] = sum_j dZ2[f2][j] h1[f1][j]: row tile wt, 4 column tiles
-        // the A operands (row tile wt of dZ2) once; each column tile's B operands read while
-        // the previous tile's chain runs
+    } else {  // partial dW2[f2][f1] = sum_j dZ2[f2][j] h1[f1][j]: f1 tile wt, 4 f2 tiles
+        // computed as its transpose H1 dZ2^T (A operands: f1 rows wt*32.. of h1, once; each
+        // f2 tile's B operands read while the previous tile's chain runs), so a lane's
+        // registers 4q..4q+3 are dW2[f2 = 32 ct + c][4 adjacent f1]: one 16-byte store each
         float* out = A.W.part_w2 + (int64_t)blockIdx.x * 128 * 128;
         float a2[16], b2[2][16];
 #pragma unroll
-        for (int s = 0; s < 16; ++s) a2[s] = DZ2[(wt * 32 + c) * kLS + 2 * s + h];
+        for (int s = 0; s < 16; ++s) a2[s] = HA[(wt * 32 + c) * kLS + 2 * s + h];
 #pragma unroll
-        for (int s = 0; s < 16; ++s) b2[0][s] = HA[c * kLS + 2 * s + h];
+        for (int s = 0; s < 16; ++s) b2[0][s] = DZ2[c * kLS + 2 * s + h];
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) {
             f32x16 acc = {};
 #pragma unroll
             for (int s = 0; s < 16; ++s) {
-                if (ct < 3) b2[(ct + 1) & 1][s] = HA[((ct + 1) * 32 + c) * kLS + 2 * s + h];
+                if (ct < 3) b2[(ct + 1) & 1][s] = DZ2[((ct + 1) * 32 + c) * kLS + 2 * s + h];
                 acc = mfma_f32(a2[s], b2[ct & 1][s], acc);
             }
 #pragma unroll
-            for (int r = 0; r < 16; ++r) st_part(out + (wt * 32 + acc_r(r, lane)) * 128 + ct * 32 + c, acc[r]);
+            for (int q = 0; q < 4; ++q)  // f1 = 32 wt + acc_r(4q + m, lane) = 32 wt + 8q + 4h + m
+                st_part4(out, (uint32_t)((ct * 32 + c) * 128 + wt * 32 + 8 * q + 4 * h), acc[4 * q], acc[4 * q + 1],
+                         acc[4 * q + 2], acc[4 * q + 3]);
         }
         // pinned order: the operands of tile 0, then per tile its chain with the next tile's
         // reads interleaved, then its stores (the compiler otherwise read each pair just
@@ -549,7 +573,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
                 if (ct < 3) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             }
-            __builtin_amdgcn_sched_group_barrier(0x040, 16, 0);
+            __builtin_amdgcn_sched_group_barrier(0x040, 4, 0);
         }
         // partial dW3 over the tile's distinct actions, column tile wt: row r (slot r) =
         // sum_j [first(j) = r] g_j h2[f][j]. A lane holds its 16 k-step samples' slots and g
@@ -565,15 +589,17 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             const int j = 2 * s + h;
             av[s] = FST[j] == c ? G[j] : 0.0f;
         }
+        // as its transpose H2 G^T: lane (c, h) holds slot c's features 32 wt + acc_r(r, lane),
+        // 4 adjacent per register quad (16-byte stores, only a live slot's lanes)
         f32x16 acc = {};
 #pragma unroll
-        for (int s = 0; s < 16; ++s) acc = mfma_f32(av[s], bv[s], acc);
+        for (int s = 0; s < 16; ++s) acc = mfma_f32(bv[s], av[s], acc);
         float* o3 = A.W.part_w3 + (int64_t)blockIdx.x * 32 * 128;
+        if ((slots >> c) & 1u)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = acc_r(r, lane);
-            if ((slots >> row) & 1u) st_part(o3 + row * 128 + wt * 32 + c, acc[r]);
-        }
+            for (int q = 0; q < 4; ++q)
+                st_part4(o3, (uint32_t)(c * 128 + wt * 32 + 8 * q + 4 * h), acc[4 * q], acc[4 * q + 1], acc[4 * q + 2],
+                         acc[4 * q + 3]);
         if (wt == 0) {  // db3 of slot c: the even samples' sum plus the odd samples' sum
             float s3 = 0.0f;
 #pragma unroll
@@ -670,9 +696,10 @@ __device__ __forceinline__ int row_of_action(const QnetDims& q, int a) {
 // p += m / ((sqrt(v) / sqrt(1 - b2^t) + eps) / (-lr / (1 - b1^t)))
 struct AdamStep {
     float b1, b2, eps, step_size, bc2_sqrt;
-    __device__ AdamStep(const QtAdamArgs& A) : b1(A.beta1), b2(A.beta2), eps(A.eps) {
-        // (no counter in mode 1, which stops before any Adam step)
-        const float t = A.step_dev ? (float)(*A.step_dev + (A.bumped ? 0 : 1)) : 1.0f;
+    // steps: *A.step_dev, loaded by the caller (no counter in mode 1, which stops before any
+    // Adam step)
+    __device__ AdamStep(const QtAdamArgs& A, int32_t steps) : b1(A.beta1), b2(A.beta2), eps(A.eps) {
+        const float t = A.step_dev ? (float)(steps + (A.bumped ? 0 : 1)) : 1.0f;
         step_size = 1.0f / ((powf(A.beta1, t) - 1.0f) / A.lr);
         bc2_sqrt = sqrtf(-(powf(A.beta2, t) - 1.0f));
     }
@@ -853,9 +880,18 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
     __shared__ int wtot[kQRBlock / 64];
     const int tid = threadIdx.x, in = A.d.in;
     QSTAMP(10);  // T2's stamps: slots 10-13 of the same rows (4 waves)
-    const AdamStep adam(A);
+    // the Adam count: its load is in flight while the sums' loads are issued; the step's
+    // constants (two powf) are formed where the first Adam step needs them, after the
+    // sums (SHIPENV_QT_LATE_ADAM; 0: at the kernel's start, ahead of every sum load)
+    const int32_t steps_dev = A.step_dev ? *A.step_dev : 0;
+#if SHIPENV_QT_LATE_ADAM
+#define QT_ADAM() AdamStep(A, steps_dev)
+#else
+    const AdamStep adam_early(A, steps_dev);
+#define QT_ADAM() adam_early
+#endif
     // every block has read the count; ctr[0] is read by the next update's T1 only
-    if (A.ctr_sync && blockIdx.x == 0 && tid == 0) *A.ctr_sync = *A.step_dev;
+    if (A.ctr_sync && blockIdx.x == 0 && tid == 0) *A.ctr_sync = steps_dev;
     // sum(w): this thread's share loads now, and the workgroup reduces it after its own
     // sum (inv is first needed by the Adam step), so the two round trips overlap
     const int mode = A.mode;  // block-uniform
@@ -932,6 +968,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             }
         }
         const float inv = weight_inv();
+        const AdamStep adam = QT_ADAM();
         QSTAMP(12);
         if (tid == 0)  // every thread holds the sums; the row loop below indexes them by column
 #pragma unroll
@@ -1022,6 +1059,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             }
         }
         const float inv = weight_inv();
+        const AdamStep adam = QT_ADAM();
         QSTAMP(12);
         if (tid < 64) {
             const int e = (int)e0 + tid, f1 = e & 127;
@@ -1084,6 +1122,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             }
         }
         const float inv = weight_inv();
+        const AdamStep adam = QT_ADAM();
         QSTAMP(12);
         if (row_live && tid <= 128) {
             const float p = adam(pw, g * inv, pm, pv);
@@ -1107,6 +1146,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         }
     }
     QSTAMP(13);
+#undef QT_ADAM
 }
 
 }  // namespace

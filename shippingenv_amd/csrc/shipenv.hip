@@ -41,7 +41,8 @@
 
 #ifndef SHIPENV_ABL4
 // timing-only auto-reset ablations (bits): 1 reset words without Philox, 2 no done
-// list, 4 no episode statistics, 8 no auto-reset at all (tools/build_ablation.sh)
+// list, 4 no episode statistics, 8 no auto-reset at all (tools/build_ablation.sh), 16 the
+// done list without its records' stores, 32 without its per-segment count stores
 #define SHIPENV_ABL4 0
 #endif
 #ifndef SHIPENV_PREFETCH
@@ -1653,6 +1654,9 @@ __device__ __forceinline__ void slab_add(double* p, double v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+#ifndef SHIPENV_DONE_PAD
+#define SHIPENV_DONE_PAD 8  // records per padded run (8 x 16 B = one 128-B line); 1 = no padding
+#endif
 // Done-list compaction of one iteration (auto-reset): no atomics, no LDS and no
 // barrier. A wave-exclusive prefix of the per-lane counts (0..4) comes from three
 // ballot bit-planes; the records go to this wave's own segment of the list in env
@@ -1662,15 +1666,25 @@ __device__ __forceinline__ void wave_compact(const StepArgs& A, const Finished& 
                                              int64_t segment) {
     const int nd = __popc(F.mask);
     const uint64_t b0 = __ballot(nd & 1), b1 = __ballot(nd & 2), b2 = __ballot(nd & 4);
-    if (nd) {
+    if ((SHIPENV_ABL4 & 16) == 0 && nd) {
         int64_t slot = segment * A.seg + (int32_t)(count_below(b0) + 2 * count_below(b1) + 4 * count_below(b2));
         const int32_t t = (int32_t)A.t;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             if ((F.mask >> j) & 1u) A.done_recs[slot++] = se_done_rec{(int32_t)(base + j), F.ret[j], F.len[j], t};
     }
-    if ((threadIdx.x & 63) == 0)
-        A.done_count[segment] = (int32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
+    const int32_t total = (int32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
+    if constexpr (SHIPENV_DONE_PAD > 1 && (SHIPENV_ABL4 & 16) == 0) {
+        // the wave's records padded to whole lines with filler records (env -1) past the
+        // count: a line of the list written in part by one wave left L2 as a partial-line
+        // write, and at N = 2^24 the ~1 record per wave cost config 4 ~11 us of ~192
+        // (SHIPENV_ABL4 = 16 ablation, profiles/r04/ab_c4parts.jsonl). A segment holds 256
+        // records, a multiple of the pad, so the filler stays inside it.
+        const int32_t pad = (-total) & (SHIPENV_DONE_PAD - 1), l = (int32_t)(threadIdx.x & 63);
+        if (total != 0 && l < pad)
+            A.done_recs[segment * A.seg + total + l] = se_done_rec{-1, 0.0f, 0, (int32_t)A.t};
+    }
+    if ((SHIPENV_ABL4 & 32) == 0 && (threadIdx.x & 63) == 0) A.done_count[segment] = total;
 }
 
 // Workgroup b owns the contiguous groups [b*iters*256, (b+1)*iters*256) (a group is
