@@ -97,10 +97,24 @@ __device__ __forceinline__ void st_part(float* p, float v) {
 // row: the MFMAs take H1 / H2 as their A operand, so a lane's accumulator registers 4q..4q+3
 // are 4 adjacent columns). SHIPENV_QT_WT = 1: write-through (sc1), so the 12.6-16.8 MB of
 // partials are not left dirty in the XCDs' L2s for the kernel boundary to flush before T2
-// (MI355X_MICROARCH.md price list, "boundary" and "publish-large"); 0: plain stores.
+// (MI355X_MICROARCH.md price list, "boundary" and "publish-large"); 2: the small partials
+// too; 0: plain stores. Update at B = 8192: 42.2 (4-byte plain stores) -> 41.3 (16-byte
+// plain) -> 39.65 us (16-byte write-through) (profiles/r04/ab_update_t1_wt.jsonl).
 #ifndef SHIPENV_QT_WT
 #define SHIPENV_QT_WT 1
 #endif
+// the small per-tile partials (dW1's 6 columns, db1, db2, db3, the slot map, the loss and
+// weight sums; 4.4 KB per tile) as 4-byte stores: write-through too at SHIPENV_QT_WT = 2
+template <typename T>
+__device__ __forceinline__ void st_part1(T* p, T v) {
+    static_assert(sizeof(T) == 4, "4-byte partials");
+    if constexpr (SHIPENV_QT_WT >= 2) {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, (short)0, 0x7fffffff, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, 0u, 0, 16);  // aux 16: sc1
+    } else {
+        *p = v;
+    }
+}
 __device__ __forceinline__ void st_part4(float* base, uint32_t idx, float a, float b, float c, float d) {
     const uint4 w = make_uint4(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b),
                                __builtin_bit_cast(uint32_t, c), __builtin_bit_cast(uint32_t, d));
@@ -606,8 +620,8 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             for (int s = 0; s < 16; ++s) s3 += av[s];
             const float x3 = __shfl_xor(s3, 32);
             if (h == 0) {
-                A.W.part_b3[(int64_t)blockIdx.x * 32 + c] = s3 + x3;
-                A.W.part_map[(int64_t)blockIdx.x * 32 + c] = live_slot ? ACT[c] : -1;
+                st_part1(A.W.part_b3 + (int64_t)blockIdx.x * 32 + c, s3 + x3);
+                st_part1(A.W.part_map + (int64_t)blockIdx.x * 32 + c, live_slot ? (int32_t)ACT[c] : (int32_t)-1);
             }
         }
     }
@@ -619,22 +633,22 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         for (int cc = c0; cc < c0 + 3; ++cc) {
             float s = 0.0f;
             for (int j = 0; j < 32; ++j) s += DZ1[f * kLS + j] * X[cc * kLS + j];
-            o[cc - c0] = s;
+            st_part1(o + (cc - c0), s);
         }
     } else {
         const int t = tid - 256;
         const float* src = t < 128 ? DZ2 + t * kLS : DZ1 + (t - 128) * kLS;
         float s = 0.0f;
         for (int j = 0; j < 32; ++j) s += src[j];
-        (t < 128 ? A.W.part_b2 : A.W.part_b1)[(int64_t)blockIdx.x * 128 + (t & 127)] = s;
+        st_part1((t < 128 ? A.W.part_b2 : A.W.part_b1) + (int64_t)blockIdx.x * 128 + (t & 127), s);
         if (t == 0) {
             float l = 0.0f, w = 0.0f;
             for (int j = 0; j < 32; ++j) {
                 l += LW[j];
                 w += WT[j];
             }
-            A.W.part_lw[2 * blockIdx.x] = l;
-            A.W.part_lw[2 * blockIdx.x + 1] = w;
+            st_part1(A.W.part_lw + 2 * blockIdx.x, l);
+            st_part1(A.W.part_lw + 2 * blockIdx.x + 1, w);
         }
     }
     QSTAMP(9);

@@ -569,6 +569,7 @@ struct StepArgs {
     se_done_rec* done_recs;  // this step's done list: per-(iteration, wave) segments of `seg` records
     int32_t* done_count;     // this step's per-segment record counts
     int64_t seg;             // segment stride (records) of one workgroup
+    int32_t done_pad;        // done-list records padded to runs of this many (1: none; wave_compact)
     int64_t iters;           // groups per thread (each workgroup owns iters * 256 groups)
     double* slab;            // per-wave {sum_ret, n_eps, sum_len, pad}
     StepRecord rec;          // step_kernel<..., kRec = true> only
@@ -1654,9 +1655,6 @@ __device__ __forceinline__ void slab_add(double* p, double v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-#ifndef SHIPENV_DONE_PAD
-#define SHIPENV_DONE_PAD 8  // records per padded run (8 x 16 B = one 128-B line); 1 = no padding
-#endif
 // Done-list compaction of one iteration (auto-reset): no atomics, no LDS and no
 // barrier. A wave-exclusive prefix of the per-lane counts (0..4) comes from three
 // ballot bit-planes; the records go to this wave's own segment of the list in env
@@ -1674,13 +1672,13 @@ __device__ __forceinline__ void wave_compact(const StepArgs& A, const Finished& 
             if ((F.mask >> j) & 1u) A.done_recs[slot++] = se_done_rec{(int32_t)(base + j), F.ret[j], F.len[j], t};
     }
     const int32_t total = (int32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
-    if constexpr (SHIPENV_DONE_PAD > 1 && (SHIPENV_ABL4 & 16) == 0) {
+    if ((SHIPENV_ABL4 & 16) == 0 && A.done_pad > 1) {  // launch-uniform (done_pad_records)
         // the wave's records padded to whole lines with filler records (env -1) past the
-        // count: a line of the list written in part by one wave left L2 as a partial-line
+        // count: a line of the list written in part by one wave leaves L2 as a partial-line
         // write, and at N = 2^24 the ~1 record per wave cost config 4 ~11 us of ~192
         // (SHIPENV_ABL4 = 16 ablation, profiles/r04/ab_c4parts.jsonl). A segment holds 256
         // records, a multiple of the pad, so the filler stays inside it.
-        const int32_t pad = (-total) & (SHIPENV_DONE_PAD - 1), l = (int32_t)(threadIdx.x & 63);
+        const int32_t pad = (-total) & (A.done_pad - 1), l = (int32_t)(threadIdx.x & 63);
         if (total != 0 && l < pad)
             A.done_recs[segment * A.seg + total + l] = se_done_rec{-1, 0.0f, 0, (int32_t)A.t};
     }
@@ -2481,6 +2479,15 @@ int step_block_cap() {
 // read and write the episode counters) are faster without them: config 4 at 2^20
 // 11.6 vs 12.5-12.7 us, equal from 2^21 to 2^24; the training loop's step + record
 // 16.0-16.3 vs 17.5-17.9 us.
+// The done list's records padded to whole 128-B lines (wave_compact) once the step's traffic
+// is beyond the Infinity Cache: config 4 at 2^24 -2.7 us per step (median of five alternating
+// rounds), at 2^20 +0.17 us (profiles/r04/ab_donepad.jsonl). SHIPENV_DONE_PAD overrides.
+int32_t done_pad_records(const se_env* env) {
+    const char* v = getenv("SHIPENV_DONE_PAD");
+    if (v) return atoi(v) == 0 ? 1 : 8;
+    return env->n > (int64_t)1 << 23 ? 8 : 1;
+}
+
 bool step_nt_loads(const se_env* env) {
     const char* v = getenv("SHIPENV_NT_LOADS");
     if (v) return atoi(v) != 0;
@@ -2610,6 +2617,7 @@ int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const 
         A.done_count = env->st.done_count + par * (size_t)env->nseg;
     }
     A.seg = env->seg;
+    A.done_pad = done_pad_records(env);
     A.iters = env->iters;
     A.slab = env->d_slab;
     const hipStream_t s = (hipStream_t)stream;
