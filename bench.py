@@ -916,6 +916,7 @@ def main():
             ports64 = random_water_ports(builtin_water(), 64, seed=3)
             el4b, k4b, st4b, _ = run_config(args.large_n, ports64, True, small, dist, "large-n-config4",
                                             preroll=args.preroll4)
+            t4b, src4b = pmc_traffic("step_kernel_auto_big_bytes_per_launch")
             out["large_n"]["config4"] = {
                 "value": round(args.large_n * small.steps / el4b, 1),
                 "ms_per_step": round(el4b / small.steps * 1e3, 5),
@@ -924,6 +925,9 @@ def main():
                 "episodes": st4b[1],
                 "preroll_steps": args.preroll4,
             }
+            if t4b:
+                out["large_n"]["config4"]["roofline"]["traffic"] = t4b
+                out["large_n"]["config4"]["roofline"]["traffic_source"] = src4b
         tb, srcb = pmc_traffic("step_kernel_big_bytes_per_launch")
         if tb:
             out["large_n"]["roofline"]["traffic"] = tb

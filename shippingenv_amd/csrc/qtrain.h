@@ -75,9 +75,9 @@ struct QtWork {
     float* c1[2];    // [128]: b1 + W1[:, 6:] . port
     float* portvec;  // [in - 6]: the preprocess_state port block
     float* part_w2;  // [tiles][128][128]
-    float* part_w1d; // [tiles][128][6]
-    float* part_b1;  // [tiles][128]
-    float* part_b2;  // [tiles][128]
+    float* part_w1d; // [128][tiles][6]: row f's partials contiguous (T2's W1 block f reads them coalesced)
+    float* part_b1;  // [128][tiles]
+    float* part_b2;  // [128][tiles]
     float* part_lw;  // [tiles][2]: sum w d^2, sum w
     // dW3 / db3 per distinct action of a tile: slot r sums the samples whose action first
     // occurs at sample r of the tile; part_map[t][r] is that action, or -1 (no such slot)
@@ -629,7 +629,8 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     // partial dW1 (dynamic columns), db1, db2, loss and weight sums
     if (tid < 256) {
         const int f = tid >> 1, c0 = (tid & 1) * 3;
-        float* o = A.W.part_w1d + ((int64_t)blockIdx.x * 128 + f) * 6 + c0;
+        const int64_t tiles = (A.B + kQT - 1) / kQT;
+        float* o = A.W.part_w1d + ((int64_t)f * tiles + blockIdx.x) * 6 + c0;
         for (int cc = c0; cc < c0 + 3; ++cc) {
             float s = 0.0f;
             for (int j = 0; j < 32; ++j) s += DZ1[f * kLS + j] * X[cc * kLS + j];
@@ -640,7 +641,8 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         const float* src = t < 128 ? DZ2 + t * kLS : DZ1 + (t - 128) * kLS;
         float s = 0.0f;
         for (int j = 0; j < 32; ++j) s += src[j];
-        st_part1((t < 128 ? A.W.part_b2 : A.W.part_b1) + (int64_t)blockIdx.x * 128 + (t & 127), s);
+        const int64_t tiles = (A.B + kQT - 1) / kQT;
+        st_part1((t < 128 ? A.W.part_b2 : A.W.part_b1) + (int64_t)(t & 127) * tiles + blockIdx.x, s);
         if (t == 0) {
             float l = 0.0f, w = 0.0f;
             for (int j = 0; j < 32; ++j) {
@@ -841,13 +843,12 @@ __device__ __forceinline__ float slot_row_sum(const float* w3, const float* b3, 
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
                 const int i = i0 + 8 * u;
-                const bool ok = i < total;
-                const int64_t row = c0 * 32 + (ok ? list[i] : 0);
-                v[u] = *reinterpret_cast<const float4*>(w3 + row * 128 + 4 * q);
-                vb[u] = b3[row];
-                if (!ok) {
-                    v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                    vb[u] = 0.0f;
+                v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                vb[u] = 0.0f;
+                if (i < total) {  // only the listed rows are loaded (a round past the list moves no bytes)
+                    const int64_t row = c0 * 32 + list[i];
+                    v[u] = *reinterpret_cast<const float4*>(w3 + row * 128 + 4 * q);
+                    vb[u] = b3[row];
                 }
             }
 #pragma unroll
@@ -955,10 +956,10 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             if (tid < in - 6) portbuf[tid] = port_c;  // visible after the barrier below
         } else {
             for (int64_t t = tid; t < A.tiles; t += kQRBlock) {
-                const float* p = A.W.part_w1d + (t * 128 + f) * 6;
+                const float* p = A.W.part_w1d + ((int64_t)f * A.tiles + t) * 6;
 #pragma unroll
                 for (int c = 0; c < 6; ++c) x[c] += p[c];
-                x[6] += A.W.part_b1[t * 128 + f];
+                x[6] += A.W.part_b1[(int64_t)f * A.tiles + t];
             }
             if (mode == 0 && tid < in - 6) portbuf[tid] = port_c;  // visible after block_sum's barrier
             block_sum<7>(x, red);
@@ -1065,7 +1066,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                 if (tid < 64) G[Grad::w2 + e0 + tid] = g;
                 if ((e0 & 127) == 0) {
                     float x = 0.0f;
-                    for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[t * 128 + f2];
+                    for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[(int64_t)f2 * A.tiles + t];
                     const float s2 = block_sum256(x, red);
                     if (tid == 0) G[Grad::b2 + f2] = s2;
                 }
@@ -1093,7 +1094,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                 s2 = G[Grad::b2 + f2];
             } else {
                 float x = 0.0f;
-                for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[t * 128 + f2];
+                for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[(int64_t)f2 * A.tiles + t];
                 s2 = block_sum256(x, red);
             }
             if (tid == 0) {

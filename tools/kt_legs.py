@@ -9,11 +9,13 @@ next dispatches of that leg's kernel instantiation in the trace:
              (--preroll3, bench.py's default 1000), then the step_py
              leg's P3 + W + K
              step_kernel<false, false, false, true, false, true> (the same code, se_step_seq):
-             the headline leg's W warm-up and K timed launches, and nothing else
+             the headline leg's W warm-up and K timed launches, then config3_literal's 10
+             warm-up and 1000 timed launches
   config 4   step_kernel<false, false, true, false, false, false> (auto-reset): launches P + W .. P + W + K
              after its P pre-roll steps (--preroll4, bench.py's default 1000)
   large_n    step_kernel<false, false, false, false, false, false> (N = 2^24): the from-reset leg's
              105 launches, then the steady leg's P3 pre-roll steps and its 105 (the last)
+  large_n config 4: the auto-reset kernel's last 105 launches (2^24, after its pre-roll)
 For each leg this prints the average kernel duration (end - start of the dispatch, as
 rocprofv3 records it) over the K timed launches, over the timed launches after the
 first, the per-launch list, the idle gaps between consecutive timed launches and
@@ -83,21 +85,26 @@ def main():
            "config3_step_py": leg(rows, C3, W + K + 2 * a.preroll3, W + K, K),
            "config4": leg(rows, C4, a.preroll4, W + K, K),
            "large_n_from_reset": leg(rows, BIG, 0, 2 * 105 + a.preroll3, 100, from_end=True, head=105),
-           "large_n": leg(rows, BIG, 0, 105, 100, from_end=True)}
-    for key, b in (("config3", 42), ("config3_from_reset", 42), ("config3_step_py", 42), ("config4", 58)):
+           "large_n": leg(rows, BIG, 0, 105, 100, from_end=True),
+           "config3_literal": leg(rows, C3S, W + K, 10 + 1000, 1000),
+           "large_n_config4": leg(rows, C4, 0, 105, 100, from_end=True)}
+    for key, b in (("config3", 42), ("config3_from_reset", 42), ("config3_step_py", 42), ("config4", 58),
+                   ("config3_literal", 42)):
         if out[key]:
             us = out[key]["avg_us_timed"]
             out[key]["frac_from_trace"] = round(b * a.n / (us * 1e-6) / 1e9 / PEAK, 4)
-    for key in ("large_n_from_reset", "large_n"):
+    for key, b in (("large_n_from_reset", 42), ("large_n", 42), ("large_n_config4", 58)):
         if out[key]:
             us = out[key]["avg_us_timed"]
-            out[key]["frac_from_trace"] = round(42 * (1 << 24) / (us * 1e-6) / 1e9 / PEAK, 4)
+            out[key]["frac_from_trace"] = round(b * (1 << 24) / (us * 1e-6) / 1e9 / PEAK, 4)
     if a.bench:
         with open(a.bench) as f:
             line = next(json.loads(x) for x in f if x.startswith("{"))
         out["bench"] = {"config3": line["roofline"],
                         "config4": line.get("config4", {}).get("roofline"),
-                        "large_n": line.get("large_n", {}).get("roofline")}
+                        "config3_literal": {k: line.get("config3_literal", {}).get(k) for k in ("kernel_ms", "frac")},
+                        "large_n": line.get("large_n", {}).get("roofline"),
+                        "large_n_config4": line.get("large_n", {}).get("config4", {}).get("roofline")}
     print(json.dumps(out, indent=1))
 
 

@@ -51,12 +51,12 @@ def main():
     b = os.path.join(src, "bench_under_rocprof.json")  # the bench's own line from the kt_bench run
     if os.path.exists(b):
         shutil.copy(b, os.path.join(dst, "bench_under_rocprof.json"))
-    for name in ("fetch_c3", "write_c3", "fetch_big", "write_big", "fetch_c4", "write_c4", "sq_c3",
-                 "sq2_c3"):
+    for name in ("fetch_c3", "write_c3", "fetch_big", "write_big", "fetch_c4", "write_c4", "fetch_c4big",
+                 "write_c4big", "sq_c3", "sq2_c3"):
         summary["pmc"][name] = counters(os.path.join(src, f"pmc_{name}_counter_collection.csv"))
-    n = {"c3": 1 << 20, "big": 1 << 24, "c4": 1 << 20}
+    n = {"c3": 1 << 20, "big": 1 << 24, "c4": 1 << 20, "c4big": 1 << 24}
     traffic = {}
-    for k in ("c3", "big", "c4"):
+    for k in ("c3", "big", "c4", "c4big"):
         fe = summary["pmc"].get(f"fetch_{k}", {}).get("FETCH_SIZE")
         wr = summary["pmc"].get(f"write_{k}", {}).get("WRITE_SIZE")
         if fe is not None and wr is not None:
@@ -80,6 +80,9 @@ def main():
                        "step_kernel_big_bytes_per_launch":
                            round(traffic["big"]["bytes_per_launch"]) if "big" in traffic else None,
                        "workload_big": "config 3, N=2^24 (the large_n leg)",
+                       "step_kernel_auto_big_bytes_per_launch":
+                           round(traffic["c4big"]["bytes_per_launch"]) if "c4big" in traffic else None,
+                       "workload_auto_big": "config 4, N=2^24 (the large_n config-4 leg)",
                        "correction": "FETCH_SIZE x2 (gfx950 half-count), WRITE_SIZE x1, KiB->B"},
                       f, indent=1)
     print(json.dumps({"traffic": traffic, "kernels": {k: {n: v["avg_us"] for n, v in d.items()
