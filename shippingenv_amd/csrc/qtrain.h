@@ -143,6 +143,9 @@ struct Frags {
     }
 };
 
+#ifndef SHIPENV_QT_EARLY_Q
+#define SHIPENV_QT_EARLY_Q 1  // T1: q_j from the online waves' fc2 registers while the target waves finish fc2
+#endif
 #ifndef SHIPENV_QT_LATE_ADAM
 #define SHIPENV_QT_LATE_ADAM 1  // T2: Adam's constants after the sums' loads are issued (0: at the start)
 #endif
@@ -339,6 +342,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     float* RW = WT + 64;            // [32] r_j
     float* DN = RW + 32;            // [32] done_j
     int* FST = reinterpret_cast<int*>(DN + 32);  // [32] first(j): the dW3 slot of sample j
+    float* QP = reinterpret_cast<float*>(FST + 32);  // [4][32] online fc3 row a_j, per fc2 row tile
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wt = wave & 3;
     const bool tgt = wave >= 4;
     const int64_t r0 = (int64_t)blockIdx.x * kQT;
@@ -411,6 +415,28 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) w3s[k] = w3r[k];
     }
+#if SHIPENV_QT_EARLY_Q
+    // the online waves' share of q_j = W3[a_j] . h2_j: lane (j, h) of wave wt holds h2 rows
+    // 32 wt + acc_r(r, lane) after fc2, so it loads W3[a_j] at those 16 columns (4 float4)
+    // now and sums them against its fc2 registers while the target waves finish their fc2
+    f32x4 w3q[4];
+    if (!tgt) {
+        const float* w3r = A.on.w3 + (int64_t)ACT[lane & 31] * 128 + wt * 32 + 4 * (lane >> 5);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w3q[q] = *reinterpret_cast<const f32x4*>(w3r + 8 * q);
+    }
+    // the first sample of the tile with sample qj's action (its dW3 slot), as below
+    {
+        const int aq = ACT[qj], k0 = 2 * qpart;
+        int fk = ACT[k0 + 1] == aq ? k0 + 1 : 32;
+        fk = ACT[k0] == aq ? k0 : fk;
+        fk = min(fk, __shfl_xor(fk, 1));
+        fk = min(fk, __shfl_xor(fk, 2));
+        fk = min(fk, __shfl_xor(fk, 4));
+        fk = min(fk, __shfl_xor(fk, 8));
+        if (qpart == 0) FST[qj] = fk;
+    }
+#endif
 
     // fc1, fc2 of both networks: online on states, target on next_states
     store_relu(tgt ? TA : HA, wt, gemm_lds(f1, tgt ? XN : X, acc1, lane), lane);
@@ -430,6 +456,18 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         __builtin_amdgcn_sched_barrier(0);
         acc = gemm_lds<64, 2, 64>(fa, tgt ? TA : HA, acc, lane);
         store_relu(tgt ? TB : HB, wt, acc, lane);
+#if SHIPENV_QT_EARLY_Q
+        if (!tgt) {  // sum over this lane's 16 rows, then the two lane halves of sample lane & 31
+            float qp = 0.0f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float x = acc[r];
+                qp += (x > 0.0f ? x : 0.0f) * w3q[r >> 2][r & 3];
+            }
+            qp += __shfl_xor(qp, 32);
+            if (lane < 32) QP[wt * 32 + lane] = qp;
+        }
+#endif
     }
     QSTAMP(14);  // this wave's fc2 done (its relu stores wait for the chain's last MFMA)
     __syncthreads(); QSTAMP(3);
@@ -499,10 +537,19 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         const int64_t row = r0 + tid;
         float mx = QM[tid];
         for (int w = 1; w < 8; ++w) mx = fmaxf(mx, QM[w * 32 + tid]);
-        Y[tid] = row < A.B ? RW[tid] + (A.gamma * mx) * (1.0f - DN[tid]) : 0.0f;
+        const float y = row < A.B ? RW[tid] + (A.gamma * mx) * (1.0f - DN[tid]) : 0.0f;
+        Y[tid] = y;
+#if SHIPENV_QT_EARLY_Q
+        // q_j = the four row tiles' shares + b3[a_j]; g_j = 2 w_j (q_j - y_j)
+        const float q = ((QP[tid] + QP[32 + tid]) + (QP[64 + tid] + QP[96 + tid])) + A.on.b3[ACT[tid]];
+        const float d = q - y;
+        G[tid] = 2.0f * WT[tid] * d;
+        LW[tid] = WT[tid] * d * d;
+#endif
     }
     __syncthreads(); QSTAMP(5);
 
+#if !SHIPENV_QT_EARLY_Q
     // q_j = W3[a_j] . h2_j + b3[a_j]; g_j = 2 w_j (q_j - y_j): 16 threads per sample
     {
         float s = 0.0f;
@@ -533,6 +580,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         }
     }
     __syncthreads(); QSTAMP(6);
+#endif
     // dZ2 = (h2 > 0) g_j W3[a_j] (into the target's dead h1 buffer)
     {
         const float g = G[qj];
@@ -1311,7 +1359,7 @@ int qtrain_step(se_qtrain* q, se_qnet* qn, int64_t batch, const float* obs, cons
     DeviceGuard g(q->device);
     const hipStream_t s = (hipStream_t)stream;
     const int64_t tiles = (batch + kQT - 1) / kQT;
-    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 8 * 32) * 4;
+    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 8 * 32 + 4 * 32) * 4;
     static std::atomic<uint64_t> lds_set{0};
     rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(qtrain_tile_kernel), (int)lds, q->device);
     if (rc) return rc;
