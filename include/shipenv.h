@@ -394,9 +394,7 @@ int se_clear_stats(se_env* env, void* stream);
  * finished, in env order, into its own segment; no global atomics, so the list is
  * deterministic. se_done_layout gives the segment stride and count the done_recs /
  * done_count buffers must be sized for (2 * segments * seg_stride records,
- * 2 * segments counts). Within one parity's records, record k of segment s is at
- * s * 8 + k for k < 8 (every segment's first 8 in one dense block) and at
- * segments * 8 + s * (seg_stride - 8) + k - 8 beyond. se_done_list gives where the most recent step wrote
+ * 2 * segments counts). se_done_list gives where the most recent step wrote
  * (record offset of its buffer, offset of its counts); that list stays intact
  * while the following step runs. se_done_compact copies it contiguously
  * (out: up to n records, out_count: 1 int) on the stream. */

@@ -75,9 +75,9 @@ struct QtWork {
     float* c1[2];    // [128]: b1 + W1[:, 6:] . port
     float* portvec;  // [in - 6]: the preprocess_state port block
     float* part_w2;  // [tiles][128][128]
-    float* part_w1d; // [128][tiles][6]: row f's partials contiguous (T2's W1 block f reads them coalesced)
-    float* part_b1;  // [128][tiles]
-    float* part_b2;  // [128][tiles]
+    float* part_w1d; // [tiles][128][6]
+    float* part_b1;  // [tiles][128]
+    float* part_b2;  // [tiles][128]
     float* part_lw;  // [tiles][2]: sum w d^2, sum w
     // dW3 / db3 per distinct action of a tile: slot r sums the samples whose action first
     // occurs at sample r of the tile; part_map[t][r] is that action, or -1 (no such slot)
@@ -143,9 +143,6 @@ struct Frags {
     }
 };
 
-#ifndef SHIPENV_QT_EARLY_Q
-#define SHIPENV_QT_EARLY_Q 1  // T1: q_j from the online waves' fc2 registers while the target waves finish fc2
-#endif
 #ifndef SHIPENV_QT_LATE_ADAM
 #define SHIPENV_QT_LATE_ADAM 1  // T2: Adam's constants after the sums' loads are issued (0: at the start)
 #endif
@@ -342,7 +339,6 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     float* RW = WT + 64;            // [32] r_j
     float* DN = RW + 32;            // [32] done_j
     int* FST = reinterpret_cast<int*>(DN + 32);  // [32] first(j): the dW3 slot of sample j
-    float* QP = reinterpret_cast<float*>(FST + 32);  // [4][32] online fc3 row a_j, per fc2 row tile
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wt = wave & 3;
     const bool tgt = wave >= 4;
     const int64_t r0 = (int64_t)blockIdx.x * kQT;
@@ -415,28 +411,6 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) w3s[k] = w3r[k];
     }
-#if SHIPENV_QT_EARLY_Q
-    // the online waves' share of q_j = W3[a_j] . h2_j: lane (j, h) of wave wt holds h2 rows
-    // 32 wt + acc_r(r, lane) after fc2, so it loads W3[a_j] at those 16 columns (4 float4)
-    // now and sums them against its fc2 registers while the target waves finish their fc2
-    f32x4 w3q[4];
-    if (!tgt) {
-        const float* w3r = A.on.w3 + (int64_t)ACT[lane & 31] * 128 + wt * 32 + 4 * (lane >> 5);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) w3q[q] = *reinterpret_cast<const f32x4*>(w3r + 8 * q);
-    }
-    // the first sample of the tile with sample qj's action (its dW3 slot), as below
-    {
-        const int aq = ACT[qj], k0 = 2 * qpart;
-        int fk = ACT[k0 + 1] == aq ? k0 + 1 : 32;
-        fk = ACT[k0] == aq ? k0 : fk;
-        fk = min(fk, __shfl_xor(fk, 1));
-        fk = min(fk, __shfl_xor(fk, 2));
-        fk = min(fk, __shfl_xor(fk, 4));
-        fk = min(fk, __shfl_xor(fk, 8));
-        if (qpart == 0) FST[qj] = fk;
-    }
-#endif
 
     // fc1, fc2 of both networks: online on states, target on next_states
     store_relu(tgt ? TA : HA, wt, gemm_lds(f1, tgt ? XN : X, acc1, lane), lane);
@@ -456,18 +430,6 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         __builtin_amdgcn_sched_barrier(0);
         acc = gemm_lds<64, 2, 64>(fa, tgt ? TA : HA, acc, lane);
         store_relu(tgt ? TB : HB, wt, acc, lane);
-#if SHIPENV_QT_EARLY_Q
-        if (!tgt) {  // sum over this lane's 16 rows, then the two lane halves of sample lane & 31
-            float qp = 0.0f;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float x = acc[r];
-                qp += (x > 0.0f ? x : 0.0f) * w3q[r >> 2][r & 3];
-            }
-            qp += __shfl_xor(qp, 32);
-            if (lane < 32) QP[wt * 32 + lane] = qp;
-        }
-#endif
     }
     QSTAMP(14);  // this wave's fc2 done (its relu stores wait for the chain's last MFMA)
     __syncthreads(); QSTAMP(3);
@@ -537,19 +499,10 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         const int64_t row = r0 + tid;
         float mx = QM[tid];
         for (int w = 1; w < 8; ++w) mx = fmaxf(mx, QM[w * 32 + tid]);
-        const float y = row < A.B ? RW[tid] + (A.gamma * mx) * (1.0f - DN[tid]) : 0.0f;
-        Y[tid] = y;
-#if SHIPENV_QT_EARLY_Q
-        // q_j = the four row tiles' shares + b3[a_j]; g_j = 2 w_j (q_j - y_j)
-        const float q = ((QP[tid] + QP[32 + tid]) + (QP[64 + tid] + QP[96 + tid])) + A.on.b3[ACT[tid]];
-        const float d = q - y;
-        G[tid] = 2.0f * WT[tid] * d;
-        LW[tid] = WT[tid] * d * d;
-#endif
+        Y[tid] = row < A.B ? RW[tid] + (A.gamma * mx) * (1.0f - DN[tid]) : 0.0f;
     }
     __syncthreads(); QSTAMP(5);
 
-#if !SHIPENV_QT_EARLY_Q
     // q_j = W3[a_j] . h2_j + b3[a_j]; g_j = 2 w_j (q_j - y_j): 16 threads per sample
     {
         float s = 0.0f;
@@ -580,7 +533,6 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         }
     }
     __syncthreads(); QSTAMP(6);
-#endif
     // dZ2 = (h2 > 0) g_j W3[a_j] (into the target's dead h1 buffer)
     {
         const float g = G[qj];
@@ -677,8 +629,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     // partial dW1 (dynamic columns), db1, db2, loss and weight sums
     if (tid < 256) {
         const int f = tid >> 1, c0 = (tid & 1) * 3;
-        const int64_t tiles = (A.B + kQT - 1) / kQT;
-        float* o = A.W.part_w1d + ((int64_t)f * tiles + blockIdx.x) * 6 + c0;
+        float* o = A.W.part_w1d + ((int64_t)blockIdx.x * 128 + f) * 6 + c0;
         for (int cc = c0; cc < c0 + 3; ++cc) {
             float s = 0.0f;
             for (int j = 0; j < 32; ++j) s += DZ1[f * kLS + j] * X[cc * kLS + j];
@@ -689,8 +640,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         const float* src = t < 128 ? DZ2 + t * kLS : DZ1 + (t - 128) * kLS;
         float s = 0.0f;
         for (int j = 0; j < 32; ++j) s += src[j];
-        const int64_t tiles = (A.B + kQT - 1) / kQT;
-        st_part1((t < 128 ? A.W.part_b2 : A.W.part_b1) + (int64_t)(t & 127) * tiles + blockIdx.x, s);
+        st_part1((t < 128 ? A.W.part_b2 : A.W.part_b1) + (int64_t)blockIdx.x * 128 + (t & 127), s);
         if (t == 0) {
             float l = 0.0f, w = 0.0f;
             for (int j = 0; j < 32; ++j) {
@@ -891,12 +841,13 @@ __device__ __forceinline__ float slot_row_sum(const float* w3, const float* b3, 
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
                 const int i = i0 + 8 * u;
-                v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                vb[u] = 0.0f;
-                if (i < total) {  // only the listed rows are loaded (a round past the list moves no bytes)
-                    const int64_t row = c0 * 32 + list[i];
-                    v[u] = *reinterpret_cast<const float4*>(w3 + row * 128 + 4 * q);
-                    vb[u] = b3[row];
+                const bool ok = i < total;
+                const int64_t row = c0 * 32 + (ok ? list[i] : 0);
+                v[u] = *reinterpret_cast<const float4*>(w3 + row * 128 + 4 * q);
+                vb[u] = b3[row];
+                if (!ok) {
+                    v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                    vb[u] = 0.0f;
                 }
             }
 #pragma unroll
@@ -1004,10 +955,10 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             if (tid < in - 6) portbuf[tid] = port_c;  // visible after the barrier below
         } else {
             for (int64_t t = tid; t < A.tiles; t += kQRBlock) {
-                const float* p = A.W.part_w1d + ((int64_t)f * A.tiles + t) * 6;
+                const float* p = A.W.part_w1d + (t * 128 + f) * 6;
 #pragma unroll
                 for (int c = 0; c < 6; ++c) x[c] += p[c];
-                x[6] += A.W.part_b1[(int64_t)f * A.tiles + t];
+                x[6] += A.W.part_b1[t * 128 + f];
             }
             if (mode == 0 && tid < in - 6) portbuf[tid] = port_c;  // visible after block_sum's barrier
             block_sum<7>(x, red);
@@ -1114,7 +1065,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                 if (tid < 64) G[Grad::w2 + e0 + tid] = g;
                 if ((e0 & 127) == 0) {
                     float x = 0.0f;
-                    for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[(int64_t)f2 * A.tiles + t];
+                    for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[t * 128 + f2];
                     const float s2 = block_sum256(x, red);
                     if (tid == 0) G[Grad::b2 + f2] = s2;
                 }
@@ -1142,7 +1093,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                 s2 = G[Grad::b2 + f2];
             } else {
                 float x = 0.0f;
-                for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[(int64_t)f2 * A.tiles + t];
+                for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[t * 128 + f2];
                 s2 = block_sum256(x, red);
             }
             if (tid == 0) {
@@ -1359,7 +1310,7 @@ int qtrain_step(se_qtrain* q, se_qnet* qn, int64_t batch, const float* obs, cons
     DeviceGuard g(q->device);
     const hipStream_t s = (hipStream_t)stream;
     const int64_t tiles = (batch + kQT - 1) / kQT;
-    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 8 * 32 + 4 * 32) * 4;
+    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 8 * 32) * 4;
     static std::atomic<uint64_t> lds_set{0};
     rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(qtrain_tile_kernel), (int)lds, q->device);
     if (rc) return rc;

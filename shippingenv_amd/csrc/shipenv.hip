@@ -568,8 +568,7 @@ struct StepArgs {
     se_tape* tape;           // replay: variates in, used flags out
     se_done_rec* done_recs;  // this step's done list: per-(iteration, wave) segments of `seg` records
     int32_t* done_count;     // this step's per-segment record counts
-    int64_t seg;             // records per done-list segment (one per iteration and wave)
-    int64_t nseg;            // done-list segments (done_slot)
+    int64_t seg;             // segment stride (records) of one workgroup
     int32_t done_pad;        // done-list records padded to runs of this many (1: none; wave_compact)
     int64_t iters;           // groups per thread (each workgroup owns iters * 256 groups)
     double* slab;            // per-wave {sum_ret, n_eps, sum_len, pad}
@@ -1656,17 +1655,6 @@ __device__ __forceinline__ void slab_add(double* p, double v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Where record k of done-list segment s lives in a parity's buffer (nseg segments of seg
-// records): the first kDoneDense records of every segment in one dense block, segment after
-// segment (s * 8 + k), the rest (a wave that finished more than 8 envs in one step) after
-// it (nseg * 8 + s * (seg - 8) + k - 8). With ~1 record per wave in steady state the step's
-// records land in consecutive 128-B lines instead of one line per 4 KB segment: scattered
-// across 256 MB per step at N = 2^24, those writes cost config 4 ~11 us of ~185.
-constexpr int64_t kDoneDense = 8;
-__host__ __device__ __forceinline__ int64_t done_slot(int64_t s, int64_t k, int64_t nseg, int64_t seg) {
-    return k < kDoneDense ? s * kDoneDense + k : nseg * kDoneDense + s * (seg - kDoneDense) + (k - kDoneDense);
-}
-
 // Done-list compaction of one iteration (auto-reset): no atomics, no LDS and no
 // barrier. A wave-exclusive prefix of the per-lane counts (0..4) comes from three
 // ballot bit-planes; the records go to this wave's own segment of the list in env
@@ -1677,20 +1665,22 @@ __device__ __forceinline__ void wave_compact(const StepArgs& A, const Finished& 
     const int nd = __popc(F.mask);
     const uint64_t b0 = __ballot(nd & 1), b1 = __ballot(nd & 2), b2 = __ballot(nd & 4);
     if ((SHIPENV_ABL4 & 16) == 0 && nd) {
-        int64_t k = (int32_t)(count_below(b0) + 2 * count_below(b1) + 4 * count_below(b2));
+        int64_t slot = segment * A.seg + (int32_t)(count_below(b0) + 2 * count_below(b1) + 4 * count_below(b2));
         const int32_t t = (int32_t)A.t;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            if ((F.mask >> j) & 1u)
-                A.done_recs[done_slot(segment, k++, A.nseg, A.seg)] = se_done_rec{(int32_t)(base + j), F.ret[j], F.len[j], t};
+            if ((F.mask >> j) & 1u) A.done_recs[slot++] = se_done_rec{(int32_t)(base + j), F.ret[j], F.len[j], t};
     }
     const int32_t total = (int32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
     if ((SHIPENV_ABL4 & 16) == 0 && A.done_pad > 1) {  // launch-uniform (done_pad_records)
-        // the segment's dense run filled to its whole 128-B line with filler records (env
-        // -1) past the count, so no line of the list leaves L2 written in part
-        const int32_t pad = total < kDoneDense ? (int32_t)kDoneDense - total : 0, l = (int32_t)(threadIdx.x & 63);
+        // the wave's records padded to whole lines with filler records (env -1) past the
+        // count: a line of the list written in part by one wave leaves L2 as a partial-line
+        // write, and at N = 2^24 the ~1 record per wave cost config 4 ~11 us of ~192
+        // (SHIPENV_ABL4 = 16 ablation, profiles/r04/ab_c4parts.jsonl). A segment holds 256
+        // records, a multiple of the pad, so the filler stays inside it.
+        const int32_t pad = (-total) & (A.done_pad - 1), l = (int32_t)(threadIdx.x & 63);
         if (total != 0 && l < pad)
-            A.done_recs[segment * kDoneDense + total + l] = se_done_rec{-1, 0.0f, 0, (int32_t)A.t};
+            A.done_recs[segment * A.seg + total + l] = se_done_rec{-1, 0.0f, 0, (int32_t)A.t};
     }
     if ((SHIPENV_ABL4 & 32) == 0 && (threadIdx.x & 63) == 0) A.done_count[segment] = total;
 }
@@ -1872,7 +1862,7 @@ __global__ __launch_bounds__(64) void step_tail_kernel(StepArgs A) {
         int32_t c = (g & 63) == 0 ? 0 : A.done_count[b];  // a fresh segment: step_kernel wrote none
         for (int j = 0; j < 4; ++j)
             if ((F.mask >> j) & 1u)
-                A.done_recs[done_slot(b, c++, A.nseg, A.seg)] = se_done_rec{(int32_t)(at.base + j), F.ret[j], F.len[j], (int32_t)A.t};
+                A.done_recs[b * A.seg + c++] = se_done_rec{(int32_t)(at.base + j), F.ret[j], F.len[j], (int32_t)A.t};
         A.done_count[b] = c;
         if (bs.eps != 0) {
             // the slab entry of the wave that owns group g
@@ -1938,7 +1928,7 @@ __global__ __launch_bounds__(kBlock) void done_copy_kernel(const se_done_rec* __
     const int64_t s = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     if (s >= nseg) return;
     const int32_t cnt = counts[s], start = offsets[s];
-    for (int i = threadIdx.x & 63; i < cnt; i += 64) out[start + i] = recs[done_slot(s, i, nseg, seg)];
+    for (int i = threadIdx.x & 63; i < cnt; i += 64) out[start + i] = recs[s * seg + i];
 }
 
 // ------------------------------------------------------------------ reset kernel
@@ -2627,7 +2617,6 @@ int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const 
         A.done_count = env->st.done_count + par * (size_t)env->nseg;
     }
     A.seg = env->seg;
-    A.nseg = env->nseg;
     A.done_pad = done_pad_records(env);
     A.iters = env->iters;
     A.slab = env->d_slab;
