@@ -135,8 +135,8 @@ def spawn_ranks(n, argv, script=None, env=None, grace_s=30.0):
     """Run `script argv` as N fresh processes, rank r with RANK = LOCAL_RANK = r (GPU r),
     WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and a free MASTER_PORT, as torchrun would. The
     parent makes no GPU or HIP call (it only imports torch, which initialises nothing).
-    Rank 0's stdout (the one JSON line) is forwarded to stdout; every rank's stderr is
-    inherited. If a rank exits non-zero the others get `grace_s` seconds, then SIGTERM
+    Rank 0's JSON line is forwarded to stdout (its other stdout lines to stderr); every
+    rank's stderr is inherited. If a rank exits non-zero the others get `grace_s` seconds, then SIGTERM
     (SIGKILL 10 s later): a rank left waiting in a collective for a dead peer would hang.
     Returns 0 if every rank succeeded, else the first non-zero exit status (1 for a signal)."""
     import socket
@@ -189,7 +189,10 @@ def spawn_ranks(n, argv, script=None, env=None, grace_s=30.0):
         c = first_bad[1] if first_bad else bad[0]
         return c if c > 0 else 1
     out0.seek(0)
-    sys.stdout.write(out0.read().decode())
+    # the driver reads one JSON line: rank 0's other stdout text (a library's own chatter,
+    # e.g. gloo's "[Gloo] Rank 0 is connected to ...") goes to stderr
+    for line in out0.read().decode().splitlines(keepends=True):
+        (sys.stdout if line.startswith("{") else sys.stderr).write(line)
     sys.stdout.flush()
     return 0
 

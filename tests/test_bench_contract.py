@@ -64,6 +64,8 @@ rank = int(os.environ["RANK"])
 mode = sys.argv[1]
 if mode == "ok":
     if rank == 0:
+        # a library's own chatter on stdout (gloo prints "[Gloo] Rank 0 is connected ...")
+        print("[Gloo] Rank 0 is connected to 2 peer ranks.", flush=True)
         print(json.dumps({"rank": rank, "world": int(os.environ["WORLD_SIZE"]),
                           "local": int(os.environ["LOCAL_RANK"]), "argv": sys.argv[1:],
                           "master": [os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"]],
