@@ -628,13 +628,21 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     __syncthreads(); QSTAMP(8);  // dZ1 complete
     // partial dW1 (dynamic columns), db1, db2, loss and weight sums
     if (tid < 256) {
+        // the three columns side by side: each dZ1 value is read once and the three sums
+        // are independent chains (each still sums j = 0..31 in order)
         const int f = tid >> 1, c0 = (tid & 1) * 3;
         float* o = A.W.part_w1d + ((int64_t)blockIdx.x * 128 + f) * 6 + c0;
-        for (int cc = c0; cc < c0 + 3; ++cc) {
-            float s = 0.0f;
-            for (int j = 0; j < 32; ++j) s += DZ1[f * kLS + j] * X[cc * kLS + j];
-            st_part1(o + (cc - c0), s);
+        float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
+#pragma unroll 8
+        for (int j = 0; j < 32; ++j) {
+            const float d = DZ1[f * kLS + j];
+            s0 += d * X[c0 * kLS + j];
+            s1 += d * X[(c0 + 1) * kLS + j];
+            s2 += d * X[(c0 + 2) * kLS + j];
         }
+        st_part1(o, s0);
+        st_part1(o + 1, s1);
+        st_part1(o + 2, s2);
     } else {
         const int t = tid - 256;
         const float* src = t < 128 ? DZ2 + t * kLS : DZ1 + (t - 128) * kLS;
