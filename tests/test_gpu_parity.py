@@ -313,12 +313,17 @@ def test_config3_full_mix_vs_oracle(oracle_mod, monkeypatch, blocks, nt):
     env.close()
 
 
-@pytest.mark.parametrize("n,blocks,nt", [(8192, None, None), (8195, "3", None), (8192, None, "1")])
-def test_config4_autoreset_64_ports_vs_oracle(oracle_mod, water, monkeypatch, n, blocks, nt):
+@pytest.mark.parametrize("n,blocks,nt,pad", [(8192, None, None, None), (8195, "3", None, None),
+                                             (8192, None, "1", None), (8195, "3", None, "1")])
+def test_config4_autoreset_64_ports_vs_oracle(oracle_mod, water, monkeypatch, n, blocks, nt, pad):
     """blocks="3": 3 workgroups, several groups per thread (double-buffered loads),
     a partial last workgroup and a tail group appended to its done segment. nt="1": the
-    variant with nontemporal loads (off by default with auto-reset)."""
+    variant with nontemporal loads (off by default with auto-reset). pad="1": the done
+    list's records padded to whole lines (the form beyond 2^23 envs, forced)."""
     from shippingenv_amd.vec import random_water_ports
+
+    if pad:
+        monkeypatch.setenv("SHIPENV_DONE_PAD", pad)
 
     if blocks:
         monkeypatch.setenv("SHIPENV_STEP_BLOCKS", blocks)
@@ -491,18 +496,23 @@ def test_shard_invariance(oracle_mod):
     part.close()
 
 
-@pytest.mark.parametrize("blocks", [None, "64"])
-def test_done_list_full_size_segments(monkeypatch, blocks):
+@pytest.mark.parametrize("blocks,pad", [(None, None), ("64", None), (None, "1"), ("64", "1")])
+def test_done_list_full_size_segments(monkeypatch, blocks, pad):
     """N = 2^20 + 3 (tail group) with auto-reset: the compacted done list of every
     step lists exactly the envs that reported done, in env order, with the
     returns / lengths the stats slab accumulates. blocks="64": 17 iterations per
-    thread, so 4,352 (iteration, wave) segments go through se_done_compact's scan."""
+    thread, so 4,352 (iteration, wave) segments go through se_done_compact's scan.
+    pad="1": each wave's records padded with filler records to the segment's 128-B line
+    (the form beyond 2^23 envs, forced here): the tail group's records overwrite the
+    filler past its segment's count."""
     from shippingenv_amd.vec import random_water_ports
 
     from conftest import golden_water
 
     if blocks:
         monkeypatch.setenv("SHIPENV_STEP_BLOCKS", blocks)
+    if pad:
+        monkeypatch.setenv("SHIPENV_DONE_PAD", pad)
     n = (1 << 20) + 3
     env = VecEnv(n, seed=11, ports=random_water_ports(golden_water(), 64, seed=3), auto_reset=True)
     env.reset()
