@@ -103,6 +103,9 @@ __device__ __forceinline__ void st_part(float* p, float v) {
 #ifndef SHIPENV_QT_WT
 #define SHIPENV_QT_WT 1
 #endif
+#ifndef SHIPENV_QT_ABL
+#define SHIPENV_QT_ABL 0  // timing-only ablations of T1 (1: no dW2 partial stores, 2: no dW3 partial stores)
+#endif
 // the small per-tile partials (dW1's 6 columns, db1, db2, db3, the slot map, the loss and
 // weight sums; 4.4 KB per tile) as 4-byte stores: write-through too at SHIPENV_QT_WT = 2
 template <typename T>
@@ -573,6 +576,9 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q)  // f1 = 32 wt + acc_r(4q + m, lane) = 32 wt + 8q + 4h + m
+#if SHIPENV_QT_ABL & 1  // timing only: the dW2 partials computed, not stored
+                if (A.B < 0)
+#endif
                 st_part4(out, (uint32_t)((ct * 32 + c) * 128 + wt * 32 + 8 * q + 4 * h), acc[4 * q], acc[4 * q + 1],
                          acc[4 * q + 2], acc[4 * q + 3]);
         }
@@ -609,6 +615,9 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
 #pragma unroll
         for (int s = 0; s < 16; ++s) acc = mfma_f32(bv[s], av[s], acc);
         float* o3 = A.W.part_w3 + (int64_t)blockIdx.x * 32 * 128;
+#if SHIPENV_QT_ABL & 2  // timing only: the dW3 partials computed, not stored
+        if (A.B < 0)
+#endif
         if ((slots >> c) & 1u)
 #pragma unroll
             for (int q = 0; q < 4; ++q)
