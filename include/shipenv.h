@@ -17,6 +17,8 @@
  *  - Per-environment failures are not API errors: they are reported per env in
  *    err[i] (SE_ERR_*), exactly where the reference raises an exception; such an
  *    env's state is left untouched with reward 0 and done 0.
+ *  - n = 0 (an empty batch) is valid: the env's calls then launch nothing and accept
+ *    null N-sized buffers; a step still advances the step counter.
  */
 #ifndef SHIPENV_H
 #define SHIPENV_H

@@ -890,7 +890,7 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
     if (!qn->packed) return fail(SE_ESTATE, "se_qnet_set_weights has not been called");
     if (qn->world_version != env->world_version)
         return fail(SE_ESTATE, "ports changed since se_qnet_set_weights (the port block is folded into fc1)");
-    if (!actions) return fail(SE_EINVAL, "null actions");
+    if (!actions && env->n > 0) return fail(SE_EINVAL, "null actions");
     if (q_out && ldq < qn->q.A) return fail(SE_EINVAL, "ldq < number of actions");
     if (!(epsilon >= 0.0)) return fail(SE_EINVAL, "epsilon must be >= 0");
     if (env->n == 0) return SE_OK;
@@ -943,7 +943,7 @@ int launch_policy_f32(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t,
     if (!qn->packed) return fail(SE_ESTATE, "se_qnet_set_weights has not been called");
     if (qn->world_version != env->world_version)
         return fail(SE_ESTATE, "ports changed since se_qnet_set_weights (the port block is folded into fc1)");
-    if (!actions) return fail(SE_EINVAL, "null actions");
+    if (!actions && env->n > 0) return fail(SE_EINVAL, "null actions");
     if (q_out && ldq < qn->q.A) return fail(SE_EINVAL, "ldq < number of actions");
     if (!(epsilon >= 0.0)) return fail(SE_EINVAL, "epsilon must be >= 0");
     if (env->n == 0) return SE_OK;

@@ -2590,7 +2590,7 @@ int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const 
                 bool seq = false) {
     int rc = check_ready(env);
     if (rc) return rc;
-    if (!act || (typed && (!a || !b)) || (replay && !tape))
+    if (env->n > 0 && (!act || (typed && (!a || !b)) || (replay && !tape)))  // n = 0: an empty batch
         return fail(SE_EINVAL, "null action/tape pointer");
     if (!aligned16(act) || (typed && (!aligned16(a) || !aligned16(b))))
         return fail(SE_EINVAL, "action buffers must be 16-byte aligned");
@@ -2745,7 +2745,7 @@ int se_bind(se_env* env, const se_state* st) {
         if (!aligned16(p)) return fail(SE_EINVAL, "state buffers must be 16-byte aligned");
     }
     if (env->flags & SE_FLAG_AUTO_RESET) {
-        if (!st->ep_return || !st->ep_len || !st->done_recs || !st->done_count)
+        if ((env->n > 0 && (!st->ep_return || !st->ep_len)) || !st->done_recs || !st->done_count)
             return fail(SE_EINVAL, "auto-reset needs ep_return, ep_len, done_recs and done_count");
         if (!aligned16(st->ep_return) || !aligned16(st->ep_len) || !aligned16(st->done_recs))
             return fail(SE_EINVAL, "state buffers must be 16-byte aligned");
@@ -2776,7 +2776,7 @@ int se_reset_to(se_env* env, const uint8_t* mask, const int32_t* origin, const i
                 void* stream) {
     int rc = check_ready(env);
     if (rc) return rc;
-    if (!origin || !dest) return fail(SE_EINVAL, "null origin/dest");
+    if (env->n > 0 && (!origin || !dest)) return fail(SE_EINVAL, "null origin/dest");
     DeviceGuard g(env->device);
     ResetArgs A{env->d_world, env->dims, env->n, env->env_base, env->seed,
                 (uint32_t)env->epoch, env->st, mask, origin, dest};
@@ -2831,7 +2831,7 @@ int se_step_agent_replay(se_env* env, const int32_t* actions, se_tape* tape, voi
 int se_observe(se_env* env, float* obs, int64_t ld, void* stream) {
     int rc = check_ready(env);
     if (rc) return rc;
-    if (!obs || ld < 6 + 4 * (int64_t)env->dims.P) return fail(SE_EINVAL, "bad obs buffer / ld");
+    if ((env->n > 0 && !obs) || ld < 6 + 4 * (int64_t)env->dims.P) return fail(SE_EINVAL, "bad obs buffer / ld");
     DeviceGuard g(env->device);
     ObsArgs A{env->d_world, env->dims, env->n, ld, env->st, obs};
     const int64_t W = 6 + 4 * (int64_t)env->dims.P;
@@ -2851,7 +2851,7 @@ int se_observe(se_env* env, float* obs, int64_t ld, void* stream) {
 int se_valid_mask(se_env* env, uint8_t* bits, void* stream) {
     int rc = check_ready(env);
     if (rc) return rc;
-    if (!bits) return fail(SE_EINVAL, "null bits");
+    if (env->n > 0 && !bits) return fail(SE_EINVAL, "null bits");
     DeviceGuard g(env->device);
     const int32_t stride = (4 + env->dims.P + 250 + 7) / 8;
     MaskArgs A{env->d_world, env->dims, env->n, stride, env->st, bits};
@@ -2868,7 +2868,7 @@ int se_valid_mask(se_env* env, uint8_t* bits, void* stream) {
 }
 
 int se_gen_actions(se_env* env, int32_t* actions, uint32_t t, void* stream) {
-    if (!env || !actions) return fail(SE_EINVAL, "null argument");
+    if (!env || (!actions && env->n > 0)) return fail(SE_EINVAL, "null argument");
     if (!aligned16(actions)) return fail(SE_EINVAL, "actions must be 16-byte aligned");
     if (env->dims.P < 1) return fail(SE_EINVAL, "the synthetic agent needs ports");
     DeviceGuard g(env->device);
@@ -2883,8 +2883,8 @@ int se_gen_actions(se_env* env, int32_t* actions, uint32_t t, void* stream) {
 int se_sample_actions(se_env* env, int32_t* type, int32_t* a, int32_t* b, uint32_t t, void* stream) {
     int rc = check_ready(env);
     if (rc) return rc;
-    if (!type || !a || !b) return fail(SE_EINVAL, "null output pointer");
     if (env->n == 0) return SE_OK;
+    if (!type || !a || !b) return fail(SE_EINVAL, "null output pointer");
     DeviceGuard g(env->device);
     SampleArgs A{env->d_world, env->dims, env->n, env->env_base, env->seed, t, env->st, type, a, b};
     sample_kernel<<<grid_for(env->n), kBlock, SHIPENV_SAMPLE_STAGE ? lds_bytes(env) : 0, (hipStream_t)stream>>>(A);

@@ -205,18 +205,19 @@ class VecEnv:
         a = actions
         if not (type(a) is torch.Tensor and a.dtype is torch.int32 and a.is_cuda and a.dim() == 2
                 and a.get_device() == self._dev_index and a.shape[1] == self.n and a.stride(1) == 1
-                and a.data_ptr() % 16 == 0 and (a.shape[0] < 2 or a.stride(0) % 4 == 0)):
+                and a.data_ptr() % 16 == 0 and (a.shape[0] < 2 or a.stride(0) % 4 == 0 or self.n == 0)):
             raise ValueError("step_seq needs an int32 [K, n] device tensor with 16-byte aligned rows")
+        ld = a.stride(0) if self.n else 0  # an empty batch: no rows to stride over
         if mark is not None:
             if mark.cuda_event == 0:  # torch creates the HIP event on its first record
                 mark.record()
-            rc = N.lib().se_step_seq_mark(self._h, a.data_ptr(), a.stride(0), a.shape[0],
+            rc = N.lib().se_step_seq_mark(self._h, a.data_ptr(), ld, a.shape[0],
                                           _raw_stream(self._dev_index), mark.cuda_event, int(mark_after))
             if rc:
                 N.check(rc)
             self._keep = a
             return self.reward, self.done, self.err
-        rc = self._se_step_seq(self._h, a.data_ptr(), a.stride(0), a.shape[0], _raw_stream(self._dev_index))
+        rc = self._se_step_seq(self._h, a.data_ptr(), ld, a.shape[0], _raw_stream(self._dev_index))
         if rc:
             N.check(rc)
         self._keep = a

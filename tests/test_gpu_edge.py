@@ -1,0 +1,127 @@
+"""Edge cases of the batched path: the empty batch and the smallest
+ragged ones, through the C-ABI against the oracle.
+
+* n = 0: every call is a no-op that accepts null buffers (include/shipenv.h,
+  "Conventions"); a step still advances the step counter.
+* n = 1, 2, 3 (the tail kernel alone: no full group of 4) and 5, 7 (one full group and a
+  tail), with and without auto-reset: bit-exact against the oracle on every step, the done
+  list and the episode statistics included.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("x", "y", "fuel", "cargo", "origin", "dest")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from shippingenv_amd import build
+
+    build.build(verbose=False)
+
+
+def _state(env):
+    torch.cuda.synchronize()
+    out = {}
+    for f in FIELDS:
+        v = getattr(env, f).cpu().numpy()
+        if f in ("origin", "dest"):
+            v = np.where(v == 255, -1, v.astype(np.int32))
+        elif f == "fuel":
+            v = v.view(np.int64)
+        else:
+            v = v.astype(np.int32)
+        out[f] = v
+    return out
+
+
+def _assert_vs_oracle(env, st, what):
+    got = _state(env)
+    for f in FIELDS:
+        want = np.asarray(getattr(st, f))
+        if f == "fuel":
+            want = want.view(np.int64)
+        np.testing.assert_array_equal(got[f], want, err_msg=f"{what}: {f}")
+
+
+@pytest.mark.parametrize("auto", [False, True])
+def test_empty_batch_is_a_noop(auto):
+    from shippingenv_amd.policy import DQNNetwork, QPolicy
+    from shippingenv_amd.vec import VecEnv
+
+    env = VecEnv(0, seed=3, auto_reset=auto, device="cuda:0")
+    env.reset()
+    env.reset_to(np.zeros(0, np.int32), np.zeros(0, np.int32))
+    empty = torch.empty(0, dtype=torch.int32, device=env.device)
+    r, d, e = env.step(empty)
+    assert r.numel() == d.numel() == e.numel() == 0
+    env.step(env.gen_actions(1))
+    env.step_seq(torch.empty((3, 0), dtype=torch.int32, device=env.device))
+    assert env.counters[0] == 5  # 1 + 1 + 3 steps, each with nothing to launch
+    assert tuple(env.observe().shape) == (0, env.obs_size)
+    assert env.valid_mask().shape[0] == 0
+    ty, a, b = env.sample_actions(0)
+    assert ty.numel() == a.numel() == b.numel() == 0
+    ret, steps, status = env.rollout(np.zeros(0, np.int32), max_steps=10)
+    assert ret.numel() == steps.numel() == status.numel() == 0
+    torch.manual_seed(0)
+    pol = QPolicy(env, DQNNetwork(env.obs_size, env.action_space_size))
+    for precision in ("bf16", "f32"):
+        assert pol.act(0.5, 7, precision=precision).numel() == 0
+    np.testing.assert_array_equal(env.episode_stats().cpu().numpy(), np.zeros(3))
+    if auto:
+        ids, ret, length, step = env.done_list()
+        assert ids.numel() == ret.numel() == length.numel() == step.numel() == 0
+    env.close()
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 7])
+@pytest.mark.parametrize("auto", [False, True])
+def test_tiny_batches_vs_oracle(oracle_mod, n, auto):
+    """Config 3's action mix on n envs from reset, 600 steps, every step against the oracle
+    (auto-reset: the done list and the statistics too)."""
+    from shippingenv_amd.vec import VecEnv
+
+    O = oracle_mod
+    seed = 97 + n
+    env = VecEnv(n, seed=seed, auto_reset=auto, device="cuda:0")
+    world = O.OracleWorld(env.water, env.port_x, env.port_y, env.port_fuel, env.port_cargo)
+    st = O.OracleState(n)
+    env.reset()
+    O.reset(world, st, seed=seed, epoch=0)
+    _assert_vs_oracle(env, st, "reset")
+    stats, dones, errs = np.zeros(3), 0, set()
+    for t in range(600):
+        acts = env.gen_actions(t)
+        ref = O.gen_actions(n, env.P, seed, 0, t)
+        np.testing.assert_array_equal(acts.cpu().numpy(), ref)
+        r, d, e = env.step(acts)
+        if auto:
+            O.step_autoreset(world, st, ref, seed=seed, t=t, stats=stats)
+        else:
+            O.step(world, st, actions=ref, seed=seed, t=t)
+        np.testing.assert_array_equal(r.cpu().numpy(), st.reward.astype(np.float32), err_msg=f"t={t}")
+        np.testing.assert_array_equal(d.cpu().numpy().astype(np.int32), st.done, err_msg=f"t={t}")
+        np.testing.assert_array_equal(e.cpu().numpy().astype(np.int32), st.err, err_msg=f"t={t}")
+        _assert_vs_oracle(env, st, f"t={t}")
+        errs |= set(np.unique(st.err).tolist())
+        if auto:
+            ids, ret, length, step = env.done_list()
+            want = np.nonzero(st.done)[0]
+            np.testing.assert_array_equal(ids.cpu().numpy(), want, err_msg=f"t={t}")
+            assert (step.cpu().numpy() == t).all()
+            dones += len(want)
+            np.testing.assert_array_equal(env.ep_return.cpu().numpy(), st.ep_return)
+            np.testing.assert_array_equal(env.ep_len.cpu().numpy(), st.ep_len)
+    assert len(errs) > 1  # the mix's invalid actions showed up
+    if auto:
+        got = env.episode_stats().cpu().numpy()
+        assert got[1] == stats[1] == dones
+        assert got[2] == stats[2]
+        np.testing.assert_allclose(got[0], stats[0], rtol=1e-12)
+    env.close()
