@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-4 evidence on the final code: the GPU suite, smoke(), the driver's bench command twice,
 # its rocprofv3 kernel trace (tools/trace_driver.sh -> kt_legs.json) and the PMC traffic passes
-# (tools/pmc_r04.sh), all from one box
+# (tools/pmc_r04.sh), the size sweep and the update / policy SQ counters, all from one box
 set -u
 TAG=${1:-r04z}
 OUT=gpurun_out/$TAG
@@ -12,3 +12,11 @@ timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_d
 timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_drv2.json 2> $OUT/bench_drv2.err || exit $?
 bash tools/trace_driver.sh $TAG || exit $?
 bash tools/pmc_r04.sh $TAG || exit $?
+# throughput against N (config 3: 2^14..2^25, config 4: 2^18..2^24), then the SQ counters of the
+# DQN update's kernels and of the bf16 policy kernel (one pass each)
+timeout -k 10 400 python3 tools/size_sweep.py --out $OUT/size_sweep.json > $OUT/size_sweep.log 2>&1 || exit $?
+bash tools/pmc_update.sh $TAG || exit $?
+R=$(pwd)
+(export TMPDIR=/tmp && cd /tmp &&
+ timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_SALU \
+   --output-format csv -d "$R/$OUT" -o pmc_pol -- python3 "$R/tools/time_policy.py" --launches 3 > "$R/$OUT/pmc_pol.log" 2>&1) || exit $?
