@@ -103,6 +103,15 @@ __device__ __forceinline__ void st_part(float* p, float v) {
 #ifndef SHIPENV_QT_WT
 #define SHIPENV_QT_WT 1
 #endif
+// T1's second-dispatched half (waves 4-7, the target net's) at issue priority 1 for the whole
+// kernel: each SIMD holds one online and one target wave, and at equal priority the older
+// (online) wave wins every VALU arbitration, so the target waves finished fc2 2.3 us after the
+// online ones (profiles/r04/qtrace_t1_t2_r04.jsonl). MI355X_MICROARCH.md "Two waves per SIMD"
+// item 4, cdna_hip_programming.md T5 static form. 39.95 -> 39.6 us per update (median of 12,
+// alternating builds, profiles/r04/ab_prio.jsonl); 0 = off.
+#ifndef SHIPENV_QT_PRIO
+#define SHIPENV_QT_PRIO 1
+#endif
 #ifndef SHIPENV_QT_ABL
 #define SHIPENV_QT_ABL 0  // timing-only ablations of T1 (1: no dW2 partial stores, 2: no dW3 partial stores)
 #endif
@@ -347,6 +356,9 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     const int64_t r0 = (int64_t)blockIdx.x * kQT;
     const int in = A.d.in;
     QSTAMP(0);
+#if SHIPENV_QT_PRIO  // the younger half at issue priority 1 (a wave-uniform guard: s_setprio ignores EXEC)
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= kQTBlock / 2) __builtin_amdgcn_s_setprio(1);
+#endif
     if (A.bump && blockIdx.x == 0 && tid == 0)  // no return value: the wave does not wait on it
         __hip_atomic_fetch_add(A.bump, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
