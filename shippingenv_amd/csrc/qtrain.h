@@ -103,6 +103,12 @@ __device__ __forceinline__ void st_part(float* p, float v) {
 #ifndef SHIPENV_QT_WT
 #define SHIPENV_QT_WT 1
 #endif
+// the 16-byte partial stores' cache bits (buffer-store aux): 16 = sc1, write-through. Per update
+// at B = 8192 (profiles/r04/ab_update_t1_aux.jsonl, medians of 12 alternating runs): 16 39.3 us,
+// 17 (sc0 + sc1) 39.25, 2 (nt) 40.8, 18 (sc1 + nt) 46.35
+#ifndef SHIPENV_QT_AUX
+#define SHIPENV_QT_AUX 16
+#endif
 // T1's second-dispatched half (waves 4-7, the target net's) at issue priority 1 for the whole
 // kernel: each SIMD holds one online and one target wave, and at equal priority the older
 // (online) wave wins every VALU arbitration, so the target waves finished fc2 2.3 us after the
@@ -132,7 +138,7 @@ __device__ __forceinline__ void st_part4(float* base, uint32_t idx, float a, flo
                                __builtin_bit_cast(uint32_t, c), __builtin_bit_cast(uint32_t, d));
     if constexpr (SHIPENV_QT_WT != 0) {
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), r, 4u * idx, 0, 16);  // aux 16: sc1
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), r, 4u * idx, 0, SHIPENV_QT_AUX);
     } else {
         *reinterpret_cast<uint4*>(base + idx) = w;
     }
