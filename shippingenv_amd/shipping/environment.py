@@ -114,6 +114,8 @@ def _port_key(positions):
 
 def _category(c):
     """`match action_category` compares by equality (:364-374)."""
+    if type(c) is int and 1 <= c <= 4:  # the plain ints of ActionType
+        return c
     for t in (ActionType.MOVE_SHIP, ActionType.SELECT_PORT, ActionType.TAKE_FUEL,
               ActionType.TAKE_CARGO):
         try:
@@ -306,7 +308,9 @@ class Environment:
         x, y = self._ship_xy()
         cell = None  # the one grid cell this step reads: a move's target (:293)
         if act_type == ActionType.MOVE_SHIP:
-            H, W = np.shape(self.np_game)[:2]
+            g = self.np_game
+            shp = g.shape if type(g) is np.ndarray else np.shape(g)
+            H, W = shp[0], shp[1]
             if 0 <= x + a < H and 0 <= y + b < W:
                 cell = (x + a, y + b)
         stepper = self._world(cell)
