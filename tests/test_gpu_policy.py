@@ -168,6 +168,23 @@ def test_explore_is_uniform_over_valid_actions(steps, ports):
     assert 0.2 < (u <= 0.3).mean() < 0.4
 
 
+@pytest.mark.parametrize("n", [1, 5, 31, 33])
+def test_tiny_batches_choose_as_the_rule(n):
+    """One partial 32-env tile (n < 32) or a full tile and a partial one (33): both policy
+    kernels choose the first masked maximum of their own Q at epsilon 0, and the Philox
+    choice among the valid actions at epsilon 1."""
+    env, model, pol = make(n, steps=0, scale=20.0)
+    A = env.action_space_size
+    valid = valid_bool(env)
+    want_explore, _ = explore_expected(env, valid, 9)
+    for precision in ("bf16", "f32"):
+        q_out = torch.empty((n, A), dtype=torch.float32, device=env.device)
+        act = pol.act(0.0, 5, q_out=q_out, precision=precision).cpu().numpy()
+        np.testing.assert_array_equal(act, first_masked_argmax(q_out.cpu().numpy(), valid), err_msg=precision)
+        np.testing.assert_array_equal(pol.act(1.0, 9, precision=precision).cpu().numpy(), want_explore,
+                                      err_msg=precision)
+
+
 def test_stale_packing_is_refused():
     from shippingenv_amd import _native as N
     from shippingenv_amd.vec import DEFAULT_PORTS
