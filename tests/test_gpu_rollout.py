@@ -92,13 +92,15 @@ def test_rollouts_vs_oracle_on_reference_states():
     env.close()
 
 
-def test_rollouts_from_stepped_states_and_sampled_policy():
+@pytest.mark.parametrize("n,k", [(2048, 4), (1, 5), (3, 2)])
+def test_rollouts_from_stepped_states_and_sampled_policy(n, k):
     """Envs driven by the batched random policy (sample -> step_typed), then K
-    rollouts per env, as MCTS batches its simulations."""
+    rollouts per env, as MCTS batches its simulations (also for one env and for three,
+    the smallest batches)."""
     from shippingenv_amd.vec import random_water_ports
     from conftest import golden_water
 
-    seed, n = 19, 2048
+    seed = 19
     ports = random_water_ports(golden_water(), 12, seed=4)
     env = VecEnv(n, seed=seed, ports=ports)
     env.reset()
@@ -114,7 +116,6 @@ def test_rollouts_from_stepped_states_and_sampled_policy():
         env.step_typed(torch.as_tensor(rt, device=env.device), a, b)
         O.step(world, st, act_type=rt, act_a=ra, act_b=rb, seed=seed, t=t)
         np.testing.assert_array_equal(env.reward.cpu().numpy(), st.reward.astype(np.float32))
-    k = 4
     src = np.repeat(np.arange(n, dtype=np.int32), k)
     ret, steps, status = env.rollout(src, max_steps=100, rollout_base=7 * n)
     r = O.rollout(world, oracle_state(env), src, max_steps=100, max_attempts=800, seed=seed,
@@ -123,6 +124,7 @@ def test_rollouts_from_stepped_states_and_sampled_policy():
     np.testing.assert_array_equal(steps.cpu().numpy(), r[1])
     np.testing.assert_array_equal(status.cpu().numpy(), r[2])
     # rollouts of one env differ (independent streams) but share the start state
-    rr = ret.cpu().numpy().reshape(n, k)
-    assert (rr.std(axis=1) > 0).mean() > 0.5
+    if n >= 64:
+        rr = ret.cpu().numpy().reshape(n, k)
+        assert (rr.std(axis=1) > 0).mean() > 0.5
     env.close()
