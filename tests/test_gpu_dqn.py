@@ -222,7 +222,7 @@ class _Ref64:
             assert bool((dv <= vb).all()), (what, name, "exp_avg_sq")
 
 
-@pytest.mark.parametrize("n,ports64,batch", [(2048, False, 256), (4099, True, 300)])
+@pytest.mark.parametrize("n,ports64,batch", [(2048, False, 256), (4099, True, 300), (4, False, 3), (64, False, 33)])
 def test_fused_update_matches_reference_update(n, ports64, batch):
     """Per update k: from our parameters and Adam moments before it, the reference's update
     (agents/dqn.py:226-242: nn.MSELoss, torch.optim.Adam) in float64 on the minibatch the
