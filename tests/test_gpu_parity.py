@@ -442,13 +442,15 @@ def test_fuel_cost_sqrt_is_correctly_rounded(oracle_mod):
 
 
 # ---------------------------------------------------------------- full size
-def test_full_size_invariants_and_sampled_exactness(oracle_mod):
-    """N = 2^20 (BASELINE config 3): every ship on a non-ground cell, indices in
+@pytest.mark.parametrize("n", [1 << 20, (1 << 26) + 3])
+def test_full_size_invariants_and_sampled_exactness(oracle_mod, n):
+    """N = 2^20 (BASELINE config 3) and 2^26 + 3 (the largest size tested: two groups per
+    thread at the default grid cap, and a tail): every ship on a non-ground cell, indices in
     range, and 512 sampled quads (2048 envs) bit-exact against the oracle run with
     the same global ids (shard invariance of the Philox key: draws are keyed by the
     quad, and a LOSS_r block goes to the r-th firing env of its quad)."""
     O = oracle_mod
-    n, seed, T = 1 << 20, 2024, 40
+    seed, T = 2024, 40
     env = VecEnv(n, seed=seed)
     env.reset()
     rng = np.random.default_rng(1)
@@ -458,12 +460,13 @@ def test_full_size_invariants_and_sampled_exactness(oracle_mod):
     sts = [O.OracleState(4) for _ in quads]
     for st, q in zip(sts, quads):
         O.reset(world, st, seed=seed, env_id_base=int(4 * q), epoch=0)
+    ids_dev = torch.as_tensor(ids, device=env.device)
     for t in range(T):
         acts = env.gen_actions(t)
         env.step(acts)
-        a_host = acts.cpu().numpy()
-        for st, q in zip(sts, quads):
-            O.step(world, st, actions=a_host[4 * q:4 * q + 4], seed=seed, env_id_base=int(4 * q), t=t)
+        a_host = acts[ids_dev].cpu().numpy()  # the sampled quads' actions only
+        for j, (st, q) in enumerate(zip(sts, quads)):
+            O.step(world, st, actions=a_host[4 * j:4 * j + 4], seed=seed, env_id_base=int(4 * q), t=t)
     got = get_state(env)
     nonground = world.nonground.astype(bool)
     assert nonground[got["x"], got["y"]].all()
@@ -496,15 +499,18 @@ def test_shard_invariance(oracle_mod):
     part.close()
 
 
-@pytest.mark.parametrize("blocks,pad", [(None, None), ("64", None), (None, "1"), ("64", "1")])
-def test_done_list_full_size_segments(monkeypatch, blocks, pad):
+@pytest.mark.parametrize("blocks,pad,n", [(None, None, (1 << 20) + 3), ("64", None, (1 << 20) + 3),
+                                          (None, "1", (1 << 20) + 3), ("64", "1", (1 << 20) + 3),
+                                          (None, None, (1 << 26) + 3)])
+def test_done_list_full_size_segments(monkeypatch, blocks, pad, n):
     """N = 2^20 + 3 (tail group) with auto-reset: the compacted done list of every
     step lists exactly the envs that reported done, in env order, with the
     returns / lengths the stats slab accumulates. blocks="64": 17 iterations per
     thread, so 4,352 (iteration, wave) segments go through se_done_compact's scan.
     pad="1": each wave's records padded with filler records to the segment's 128-B line
     (the form beyond 2^23 envs, forced here): the tail group's records overwrite the
-    filler past its segment's count."""
+    filler past its segment's count. n = 2^26 + 3: the largest size tested, with the default
+    padding (on beyond 2^23 envs) and two groups per thread at the default grid cap."""
     from shippingenv_amd.vec import random_water_ports
 
     from conftest import golden_water
@@ -513,7 +519,6 @@ def test_done_list_full_size_segments(monkeypatch, blocks, pad):
         monkeypatch.setenv("SHIPENV_STEP_BLOCKS", blocks)
     if pad:
         monkeypatch.setenv("SHIPENV_DONE_PAD", pad)
-    n = (1 << 20) + 3
     env = VecEnv(n, seed=11, ports=random_water_ports(golden_water(), 64, seed=3), auto_reset=True)
     env.reset()
     tot_ret, tot_eps, tot_len = 0.0, 0, 0
