@@ -39,7 +39,10 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-leve
 #   state x,y,origin,dest u8 + cargo i32 + fuel f64 = 16 B, read and written;
 #   action i32 4 B read; reward f32 4 B, done u8 1 B, err i8 1 B written.
 BYTES_STEP = 16 + 16 + 4 + 4 + 1 + 1  # 42
-BYTES_STEP_AUTO = BYTES_STEP + 4 + 4 + 4 + 4  # + ep_return f32 and ep_len i32, read and written
+# + ep_return f32, read and written. Since round 5 the running length is an episode-start
+# stamp (se_state.ep_start) read and written only for the ~1 in 240 envs that finish, like
+# the done-list records (excluded); it was ep_len i32 read and written per env (58 B).
+BYTES_STEP_AUTO = BYTES_STEP + 4 + 4  # 50
 # the survey's canonical widths (x, y, origin, dest, cargo i32; fuel f64): 66 / 82 B
 CANONICAL_STEP, CANONICAL_STEP_AUTO = 66, 82
 
@@ -669,7 +672,7 @@ KERNEL_MS_BASIS = ("HIP events on the launch stream, one right before launch 1 a
 
 def roofline(bytes_per_step, n, k_ms, canonical):
     """The roofline object of one leg. achieved = this build's algorithmic bytes per
-    env-step (42 / 58 B) x n / the per-launch kernel time; the
+    env-step (42 / 50 B) x n / the per-launch kernel time; the
     survey's canonical field widths (66 / 82 B) are given as a byte count only: the
     kernel does not move them, so no rate is derived from them."""
     achieved = bytes_per_step * n / (k_ms * 1e-3) / 1e9
@@ -812,7 +815,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64+int (fuel/reward f64, positions/cargo int)",
+        "dtype": "f64+int (fuel f64; reward computed in f64, stored f32 after one rounding; positions/cargo int)",
         "data": "synthetic (Philox agent actions resident in HBM; reference map and ports)",
         "config": {
             "workload": "BASELINE configs[2]: N=2^20 envs/GPU, full step, default 5 ports; steady state "

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define SHIPENV_ABI_VERSION 1
+#define SHIPENV_ABI_VERSION 2  /* 2: se_state.ep_start (episode-start stamps) replaces ep_len */
 
 /* API status codes */
 #define SE_OK 0
@@ -77,7 +77,10 @@ typedef struct se_done_rec {
 } se_done_rec;
 
 /* Per-env SoA state, one entry per environment, all device pointers (16-B aligned).
- * ep_return, ep_len, done_recs and done_count may be NULL unless SE_FLAG_AUTO_RESET. */
+ * ep_return, ep_start, done_recs and done_count may be NULL unless SE_FLAG_AUTO_RESET.
+ * All calls on one env must be ordered on one stream (or externally synchronised):
+ * the step kernel updates each wave's statistics-slab entry and the done lists with
+ * plain loads and stores, which assumes no other launch on the same env overlaps it. */
 typedef struct se_state {
     uint8_t* x;         /* ship_position[0], row of np_game      (environment.py:37,:241,:297) */
     uint8_t* y;         /* ship_position[1], column of np_game */
@@ -89,7 +92,13 @@ typedef struct se_state {
     uint8_t* done;      /* step() done                                                     :376 */
     int8_t* err;        /* SE_ERR_* per env */
     float* ep_return;   /* running episode return (auto-reset) */
-    int32_t* ep_len;    /* running episode length in step calls (auto-reset) */
+    int32_t* ep_start;  /* auto-reset: the step-counter value (mod 2^32) at which the env's
+                           current episode began; its running length in step calls is
+                           (step counter - ep_start) mod 2^32. A step writes it only for
+                           the envs it resets (about 1 in 240 per step), where a running
+                           length was read and written for every env on every step.
+                           se_reset / se_reset_to stamp the counter's current value; a
+                           checkpoint restores it together with se_set_counters. */
     struct se_done_rec* done_recs; /* auto-reset done lists: 2 * segments * seg_stride records
                                       (se_done_layout), double-buffered by step parity */
     int32_t* done_count;           /* auto-reset per-segment counts: 2 * segments entries */
@@ -291,7 +300,7 @@ int se_replay_begin(se_replay* r, const int32_t* actions, void* stream);
 /* Record reward, done and s' after se_step: appends n transitions (FIFO eviction). A
  * step that raised (err != 0) is stored flagged and never sampled: the reference's loop
  * breaks before remember (:304-309). cut (optional, device u8[n]): 1 where the episode must
- * restart, i.e. the step raised or ep_len >= max_steps (max_steps > 0 needs an auto-reset
+ * restart, i.e. the step raised or the episode length (step counter - ep_start) >= max_steps (max_steps > 0 needs an auto-reset
  * env, :281); pass it to se_reset. */
 int se_replay_end(se_replay* r, uint8_t* cut, int32_t max_steps, void* stream);
 /* The training loop's fused forms (one launch each instead of two):
@@ -398,8 +407,11 @@ int se_clear_stats(se_env* env, void* stream);
  * done_count buffers must be sized for (2 * segments * seg_stride records,
  * 2 * segments counts). se_done_list gives where the most recent step wrote
  * (record offset of its buffer, offset of its counts); that list stays intact
- * while the following step runs. se_done_compact copies it contiguously
- * (out: up to n records, out_count: 1 int) on the stream. */
+ * while the following step runs. Only the first done_count[s] records of segment s
+ * are valid: records past the count may be stale, or filler records (env == -1,
+ * step == the step counter) that pad a segment's records to whole 128-byte lines
+ * (above 2^23 envs, or SHIPENV_DONE_PAD=1 at se_create). se_done_compact copies the
+ * valid records contiguously (out: up to n records, out_count: 1 int) on the stream. */
 int se_done_layout(se_env* env, int64_t* seg_stride, int32_t* segments);
 int se_done_list(se_env* env, int64_t* rec_offset, int64_t* count_offset);
 int se_done_compact(se_env* env, se_done_rec* out, int32_t* out_count, void* stream);

@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 # SHIPENV_LIB names another build of the same library (an A/B variant under _lib/abl)
 LIB_PATH = os.environ.get("SHIPENV_LIB") or os.path.join(HERE, "_lib", "libshipenv_hip.so")
-ABI_VERSION = 1
+ABI_VERSION = 2  # include/shipenv.h SHIPENV_ABI_VERSION
 
 SE_FLAG_AUTO_RESET = 1
 SE_NONE = 255
@@ -59,7 +59,7 @@ class ShipEnvError(RuntimeError):
 class SeState(C.Structure):
     _fields_ = [(name, C.c_void_p) for name in (
         "x", "y", "fuel", "cargo", "origin", "dest", "reward", "done", "err", "ep_return",
-        "ep_len", "done_recs", "done_count", "reward64")]
+        "ep_start", "done_recs", "done_count", "reward64")]
 
 
 class SeDoneRec(C.Structure):
@@ -159,6 +159,9 @@ def lib():
     # library's HIP later found no device once torch's runtime had initialised
     # (tests/test_compat_gpu.py::test_library_loaded_before_torch).
     import torch  # noqa: F401
+    if os.environ.get("SHIPENV_LIB"):  # an A/B variant replaces the product library: say so
+        import sys
+        print(f"shippingenv_amd: SHIPENV_LIB overrides the library: {LIB_PATH}", file=sys.stderr, flush=True)
     try:
         handle = C.CDLL(LIB_PATH)
     except OSError as e:

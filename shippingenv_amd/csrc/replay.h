@@ -61,6 +61,8 @@ struct RecordArgs {
     uint64_t seed;
     int64_t env_base;
     uint32_t epoch;
+    uint32_t t;  // the step counter after the recorded step (the next step's index): an
+                 // episode's length is t - ep_start, and a restarted one starts at t
 };
 
 // s and a of every env, before se_step (remember's state, action)
@@ -87,7 +89,7 @@ __global__ __launch_bounds__(kBlock) void replay_end_kernel(RecordArgs A) {
         A.ring.n_pos[slot] = pack_pos(A.st, i);
         A.ring.n_fuel[slot] = (float)A.st.fuel[i];
         if (!A.cut) continue;
-        const bool cut = raised | (A.max_steps > 0 && A.st.ep_len[i] >= A.max_steps);
+        const bool cut = raised | (A.max_steps > 0 && (int32_t)(A.t - (uint32_t)A.st.ep_start[i]) >= A.max_steps);
         A.cut[i] = (uint8_t)cut;
         if (A.world && cut) {  // reset_kernel's body for this env
             const LdsWorld w = world_view(A.dims, A.world);
@@ -101,7 +103,7 @@ __global__ __launch_bounds__(kBlock) void replay_end_kernel(RecordArgs A) {
             A.st.origin[i] = (uint8_t)s.origin;
             A.st.dest[i] = (uint8_t)s.dest;
             if (A.st.ep_return) A.st.ep_return[i] = 0.0f;
-            if (A.st.ep_len) A.st.ep_len[i] = 0;
+            if (A.st.ep_start) A.st.ep_start[i] = (int32_t)A.t;
             A.st.done[i] = 0;
             A.st.err[i] = 0;
             A.st.reward[i] = 0.0f;
@@ -148,9 +150,11 @@ __global__ __launch_bounds__(kBlock) void replay_end4_kernel(RecordArgs A) {
             make_float4((float)f01.x, (float)f01.y, (float)f23.x, (float)f23.y);
         if (!A.cut) continue;
         if (A.max_steps > 0) {
-            const int4 len = *reinterpret_cast<const int4*>(A.st.ep_len + i0);
-            cut4 |= (uint32_t)(len.x >= A.max_steps) | (uint32_t)(len.y >= A.max_steps) << 8 |
-                    (uint32_t)(len.z >= A.max_steps) << 16 | (uint32_t)(len.w >= A.max_steps) << 24;
+            const uint4 st4 = *reinterpret_cast<const uint4*>(A.st.ep_start + i0);
+            const int32_t lx = (int32_t)(A.t - st4.x), ly = (int32_t)(A.t - st4.y);
+            const int32_t lz = (int32_t)(A.t - st4.z), lw = (int32_t)(A.t - st4.w);
+            cut4 |= (uint32_t)(lx >= A.max_steps) | (uint32_t)(ly >= A.max_steps) << 8 |
+                    (uint32_t)(lz >= A.max_steps) << 16 | (uint32_t)(lw >= A.max_steps) << 24;
         }
         *reinterpret_cast<uint32_t*>(A.cut + i0) = cut4;
         if (!A.world || !cut4) continue;
@@ -169,7 +173,7 @@ __global__ __launch_bounds__(kBlock) void replay_end4_kernel(RecordArgs A) {
             A.st.origin[i] = (uint8_t)sh.origin;
             A.st.dest[i] = (uint8_t)sh.dest;
             if (A.st.ep_return) A.st.ep_return[i] = 0.0f;
-            if (A.st.ep_len) A.st.ep_len[i] = 0;
+            if (A.st.ep_start) A.st.ep_start[i] = (int32_t)A.t;
             A.st.done[i] = 0;
             A.st.err[i] = 0;
             A.st.reward[i] = 0.0f;
@@ -381,7 +385,7 @@ int se_replay_begin(se_replay* r, const int32_t* actions, void* stream) {
     if (r->open) return fail(SE_ESTATE, "se_replay_begin twice without se_replay_end");
     se_env* env = r->env;
     DeviceGuard g(env->device);
-    RecordArgs A{env->n, r->cap, r->head, 0, env->st, actions, r->ring, nullptr, 0, nullptr, {}, 0, 0, 0};
+    RecordArgs A{env->n, r->cap, r->head, 0, env->st, actions, r->ring, nullptr, 0, nullptr, {}, 0, 0, 0, 0};
     if (env->n > 0) {
         replay_begin_kernel<<<grid_for(env->n), kBlock, 0, (hipStream_t)stream>>>(A);
         HIP_TRY(hipGetLastError());
@@ -399,15 +403,15 @@ int replay_end(se_replay* r, uint8_t* cut, int32_t max_steps, bool reset_cut, vo
     if (rc) return rc;
     if (!r->open) return fail(SE_ESTATE, "se_replay_end without se_replay_begin");
     se_env* env = r->env;
-    if (max_steps > 0 && (!cut || !env->st.ep_len))
-        return fail(SE_EINVAL, "max_steps needs a cut buffer and an auto-reset env (ep_len)");
+    if (max_steps > 0 && (!cut || !env->st.ep_start))
+        return fail(SE_EINVAL, "max_steps needs a cut buffer and an auto-reset env (ep_start)");
     if (reset_cut && !cut) return fail(SE_EINVAL, "se_replay_end_reset needs a cut buffer");
     if (reset_cut && env->dims.P < 2) return fail(SE_EINVAL, "reset needs at least two ports");
     DeviceGuard g(env->device);
     const int64_t new_size = std::min(r->size + env->n, r->cap);
     RecordArgs A{env->n, r->cap, r->head, new_size, env->st, nullptr, r->ring, cut, max_steps,
                  reset_cut ? env->d_world : nullptr, env->dims, env->seed, env->env_base,
-                 (uint32_t)env->epoch};
+                 (uint32_t)env->epoch, (uint32_t)env->step_t};
     if (env->n % 4 == 0 && r->head % 4 == 0 && r->cap % 4 == 0 && ((uintptr_t)cut & 3u) == 0)
         replay_end4_kernel<<<grid_for(std::max<int64_t>(env->n / 4, 1)), kBlock, 0, (hipStream_t)stream>>>(A);
     else
@@ -438,7 +442,7 @@ int se_step_record(se_replay* r, const int32_t* actions, uint8_t* cut, int32_t m
     if (!r->open) return fail(SE_ESTATE, "se_step_record without se_replay_begin / se_policy_record");
     if (!cut) return fail(SE_EINVAL, "se_step_record needs a cut buffer");
     se_env* env = r->env;
-    if (!(env->flags & SE_FLAG_AUTO_RESET) || !env->st.ep_len)
+    if (!(env->flags & SE_FLAG_AUTO_RESET) || !env->st.ep_start)
         return fail(SE_EINVAL, "se_step_record needs an auto-reset env");
     if (env->dims.P < 2) return fail(SE_EINVAL, "reset needs at least two ports");
     if (!actions || !aligned16(actions)) return fail(SE_EINVAL, "actions must be a 16-byte aligned buffer");

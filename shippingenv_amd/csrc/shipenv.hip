@@ -42,8 +42,15 @@
 #ifndef SHIPENV_ABL4
 // timing-only auto-reset ablations (bits): 1 reset words without Philox, 2 no done
 // list, 4 no episode statistics, 8 no auto-reset at all (tools/build_ablation.sh), 16 the
-// done list without its records' stores, 32 without its per-segment count stores
+// done list without its records' stores, 32 without its per-segment count stores, 64
+// without the episode-start stamps' loads, 128 without their stores
 #define SHIPENV_ABL4 0
+#endif
+#ifndef SHIPENV_STAMP_ST
+#define SHIPENV_STAMP_ST 0  // 1 = the stamps' stores temporal (experiment; default nontemporal)
+#endif
+#ifndef SHIPENV_STAMP_GRAIN
+#define SHIPENV_STAMP_GRAIN 1  // lanes (16 B each) whose stamps load / store together (1, 2 or 4)
 #endif
 #ifndef SHIPENV_PREFETCH
 #define SHIPENV_PREFETCH 0  // 1 = load the next group before computing this one (step kernel)
@@ -724,9 +731,6 @@ struct At {
 };
 
 // The inputs of the 4 envs of one group.
-#ifndef SHIPENV_EP_EARLY
-#define SHIPENV_EP_EARLY 0  // 1 = auto-reset: the episode counters load with the group (experiment)
-#endif
 template <bool kTyped, bool kAuto, bool kNt = false>
 struct Group {
     uint32_t x, y, org, dst;  // packed u8 x4
@@ -735,7 +739,7 @@ struct Group {
     int32_t a[4];             // agent index / action type
     int32_t p[4], q[4];       // typed: values a, b
     float e[4];               // ep_return
-    int32_t l[4];             // ep_len
+    uint32_t l[4];            // ep_start: the step counter when the episode began
 
     // lane: the group within the block's row (threadIdx.x; the kernel's first load
     // clamps it into range instead of branching around the load)
@@ -754,10 +758,6 @@ struct Group {
                 ld4_full<kNt>(A.act_a, at.g0, p, lane);
                 ld4_full<kNt>(A.act_b, at.g0, q, lane);
             }
-            if (kAuto && SHIPENV_EP_EARLY) {
-                ld4_full<kNt>(S.ep_return, at.g0, e, lane);
-                ld4_full<kNt>(S.ep_len, at.g0, l, lane);
-            }
         } else {
             x = ld4u8_tail(S.x, at.base, at.n);
             y = ld4u8_tail(S.y, at.base, at.n);
@@ -772,19 +772,63 @@ struct Group {
             }
             if (kAuto) {
                 ld4_tail(S.ep_return, at.base, at.n, e);
-                ld4_tail(S.ep_len, at.base, at.n, l);
+                ld4_tail(reinterpret_cast<const uint32_t*>(S.ep_start), at.base, at.n, l);
             }
         }
     }
-    // episode counters of a full group: loaded late (step_group), they would
-    // otherwise hold 8 registers across the whole step
-    __device__ __forceinline__ void load_episode(const StepArgs& A, At<true> at) {
-        if (SHIPENV_EP_EARLY) return;
+    // episode counters of a full group, loaded late (step_group), where they would
+    // otherwise hold 8 registers across the whole step: the running return of every
+    // env, and the episode-start stamps only where they are needed, i.e. in the lanes
+    // with an env that finishes in this step (`any`; about 1 env in 240 per step) or
+    // for every env (kAll: se_step_record's max_steps cut). The stamps of other lanes
+    // are never read or written, so a running length costs no traffic per step.
+    template <bool kAll = false>
+    __device__ __forceinline__ void load_episode(const StepArgs& A, At<true> at, bool any) {
         ld4_full<kNt>(A.st.ep_return, at.g0, e);
-        ld4_full<kNt>(A.st.ep_len, at.g0, l);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) l[j] = 0u;
+        if ((SHIPENV_ABL4 & 64) == 0 && (kAll || any))
+            ld4_full<kNt>(reinterpret_cast<const uint32_t*>(A.st.ep_start), at.g0, l);
     }
-    __device__ __forceinline__ void load_episode(const StepArgs&, At<false>) {}  // loaded with the rest
+    template <bool kAll = false>
+    __device__ __forceinline__ void load_episode(const StepArgs&, At<false>, bool) {}  // loaded with the rest
 };
+
+// Whether this lane's stamps move: one of its envs finished, or (SHIPENV_STAMP_GRAIN > 1)
+// one of the lanes of its aligned run of GRAIN lanes, so the run's stores cover a whole
+// 32- or 64-byte span.
+__device__ __forceinline__ bool stamp_lane(uint32_t fin) {
+    if constexpr (SHIPENV_STAMP_GRAIN <= 1) {
+        return fin != 0;
+    } else {
+        const uint64_t b = __ballot(fin != 0);
+        const uint32_t g = (threadIdx.x & 63) & ~(uint32_t)(SHIPENV_STAMP_GRAIN - 1);
+        return ((b >> g) & ((1ull << SHIPENV_STAMP_GRAIN) - 1)) != 0;
+    }
+}
+
+// ep_start of a group after a step at counter t: t + 1 for the envs that finished (the
+// next step starts their new episode), unchanged for the others. A full group stores
+// its lane's 16 bytes only when one of its envs finished; the partial last group
+// stores its live envs.
+template <bool kFull>
+__device__ __forceinline__ void store_stamps(const se_state& S, At<kFull> at, const uint32_t (&l)[4],
+                                             uint32_t fin, uint32_t t, bool any) {
+    uint32_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = ((fin >> j) & 1u) ? t + 1u : l[j];
+    if constexpr (kFull) {
+        if ((SHIPENV_ABL4 & 128) == 0 && any) {
+            if constexpr (SHIPENV_STAMP_ST == 0) {
+                st4_full(reinterpret_cast<uint32_t*>(S.ep_start), at.g0, v);
+            } else {  // experiment: temporal 16-byte store
+                reinterpret_cast<uint4*>(slab_of(S.ep_start, at.g0))[threadIdx.x] = make_uint4(v[0], v[1], v[2], v[3]);
+            }
+        }
+    } else {
+        st4_tail(reinterpret_cast<uint32_t*>(S.ep_start), at.base, at.n, v);
+    }
+}
 
 template <bool kFull, typename T>
 __device__ __forceinline__ void store4(T* p, At<kFull> at, const T (&v)[4]) {
@@ -843,11 +887,10 @@ __device__ __forceinline__ void store_moved(const se_state& S, At<kFull> at, con
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// cargo, origin, dest, reward (+ the episode counters): final after the second half.
+// cargo, origin, dest, reward (+ the running returns): final after the second half.
 template <bool kAuto, bool kFull>
 __device__ __forceinline__ void store_rest(const se_state& S, At<kFull> at, const Ship (&s)[4],
-                                           const float (&rw)[4], const float (&epr)[4],
-                                           const int32_t (&epl)[4]) {
+                                           const float (&rw)[4], const float (&epr)[4]) {
     uint32_t oo = 0, od = 0;
     int32_t cargo[4];
 #pragma unroll
@@ -861,10 +904,7 @@ __device__ __forceinline__ void store_rest(const se_state& S, At<kFull> at, cons
     store4u8(S.dest, at, od);
     store4(S.cargo, at, cargo);
     store4(S.reward, at, rw);
-    if constexpr (kAuto) {
-        store4(S.ep_return, at, epr);
-        store4(S.ep_len, at, epl);
-    }
+    if constexpr (kAuto) store4(S.ep_return, at, epr);
 }
 
 // Step the 4 envs 4k..4k+3 of one group (base = 4k). Production draws are Philox
@@ -916,14 +956,12 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
     (void)F;
     store_moved(S, at, s, p);
     float rw[4], epr[4];
-    int32_t epl[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         rw[j] = (float)p[j].r;
         epr[j] = kAuto ? G.e[j] + rw[j] : 0.0f;
-        epl[j] = kAuto ? G.l[j] + 1 : 0;
     }
-    store_rest<kAuto>(S, at, s, rw, epr, epl);
+    store_rest<kAuto>(S, at, s, rw, epr);
 #else
     if constexpr (kReplay) {
         // one env at a time; a missing variate (NEED_DRAW) leaves its env untouched
@@ -941,10 +979,9 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
         }
         store_moved(S, at, s, p);
         float rw[4], none[4] = {0.f, 0.f, 0.f, 0.f};
-        int32_t zero[4] = {0, 0, 0, 0};
 #pragma unroll
         for (int j = 0; j < 4; ++j) rw[j] = (float)p[j].r;
-        store_rest<false>(S, at, s, rw, none, zero);
+        store_rest<false>(S, at, s, rw, none);
         (void)bs;
         (void)F;
     } else {
@@ -1018,7 +1055,7 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
                     s[j].fuel = f ? r.fuel : s[j].fuel;
                 }
             }
-            G.load_episode(late_args(), at);
+            G.load_episode(late_args(), at, stamp_lane(fin));
         }
         store_moved(S, at, s, p);
 
@@ -1066,7 +1103,6 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
         U4 ab{{0u, 0u, 0u, 0u}};
         if (arrive) ab = draw(qk, t, kSlotArrive);
         float rw[4], epr[4];
-        int32_t epl[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             // beta = the median of the three words * 2^-32 (the conversion is monotone)
@@ -1076,25 +1112,24 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
                        (fire >> j) & 1u, (arrive >> j) & 1u);
             rw[j] = (float)p[j].r;  // one rounding of the reference's f64 reward
             epr[j] = 0.0f;
-            epl[j] = 0;
             if constexpr (kAuto) {
                 const bool f = (fin >> j) & 1u;
                 F.ret[j] = G.e[j] + rw[j];
-                F.len[j] = G.l[j] + 1;
+                F.len[j] = (int32_t)(t + 1u - G.l[j]);  // stamps are loaded where fin
                 if ((SHIPENV_ABL4 & 4) == 0 && f) {
                     bs.ret += (double)F.ret[j];
                     bs.eps += 1;
                     bs.len += F.len[j];
                 }
                 epr[j] = f ? 0.0f : F.ret[j];
-                epl[j] = f ? 0 : F.len[j];
                 s[j].cargo = f ? 0 : s[j].cargo;
                 s[j].origin = f ? byte_of(reset_o, j) : s[j].origin;
                 s[j].dest = f ? byte_of(reset_d, j) : s[j].dest;
             }
         }
         if constexpr (kAuto) F.mask = fin;
-        store_rest<kAuto>(late_args().st, at, s, rw, epr, epl);
+        store_rest<kAuto>(late_args().st, at, s, rw, epr);
+        if constexpr (kAuto) store_stamps(late_args().st, at, G.l, fin, t, stamp_lane(fin));
     }
 #endif
 }
@@ -1191,7 +1226,7 @@ __device__ __forceinline__ void record_restart(const StepArgs& A, const LdsWorld
         S.origin[i] = (uint8_t)sh.origin;
         S.dest[i] = (uint8_t)sh.dest;
         S.ep_return[i] = 0.0f;
-        S.ep_len[i] = 0;
+        S.ep_start[i] = (int32_t)(A.t + 1u);  // its first step is the next one
         S.done[i] = 0;
         S.err[i] = 0;
         S.reward[i] = 0.0f;
@@ -1412,7 +1447,7 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
                 f[j] = fj ? kFuelInit : f[j];
             }
         }
-        G.load_episode(late_args(), at);
+        G.template load_episode<kRec>(late_args(), at, stamp_lane(fin));
     }
     // x, y, fuel, done and err are final here (cargo loss and arrival change none)
     uint32_t rec_x = 0, rec_y = 0, rec_cut = 0;
@@ -1535,7 +1570,7 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
         }
     }
     float rw[4], epr[4];
-    int32_t epl[4];
+    int32_t epl[4];  // kRec: the running length after this step (0 for a finished episode)
     uint32_t oo = 0, od = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -1545,7 +1580,7 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
         if constexpr (kAuto) {
             const bool fj = (fin >> j) & 1u;
             F.ret[j] = G.e[j] + rw[j];
-            F.len[j] = G.l[j] + 1;
+            F.len[j] = (int32_t)(t + 1u - G.l[j]);  // stamps are loaded where fin (kRec: everywhere)
             if ((SHIPENV_ABL4 & 4) == 0 && fj) {
                 bs.ret += (double)F.ret[j];
                 bs.eps += 1;
@@ -1568,7 +1603,7 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
     store4(S.reward, at, rw);
     if constexpr (kAuto) {
         store4(S.ep_return, at, epr);
-        store4(S.ep_len, at, epl);
+        store_stamps(S, at, G.l, fin, t, stamp_lane(fin));
     }
     if constexpr (kRec) F.cut = record_group(late_args(), base, rw, rec_x, rec_y, oo, od, rec_cut, epl);
     if constexpr (kReplay) {
@@ -1938,6 +1973,7 @@ struct ResetArgs {
     int64_t n, env_base;
     uint64_t seed;
     uint32_t epoch;
+    uint32_t t;  // the step counter: the first step of the new episodes
     se_state st;
     const uint8_t* mask;
     const int32_t* origin_in;  // explicit values (se_reset_to) or NULL
@@ -1971,7 +2007,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(ResetArgs A) {
         A.st.origin[i] = (uint8_t)s.origin;
         A.st.dest[i] = (uint8_t)s.dest;
         if (A.st.ep_return) A.st.ep_return[i] = 0.0f;
-        if (A.st.ep_len) A.st.ep_len[i] = 0;
+        if (A.st.ep_start) A.st.ep_start[i] = (int32_t)A.t;
         A.st.done[i] = 0;
         A.st.err[i] = 0;
         A.st.reward[i] = 0.0f;
@@ -2197,6 +2233,151 @@ __global__ __launch_bounds__(kBlock) void valid_mask_tiled_kernel(MaskArgs A) {
     }
 }
 
+// Row templates (round 5). A row of is_valid_action bits depends on the ship's state only
+// through (cur, origin): cur = the first port on the ship's cell (-1 at sea) fixes the
+// TAKE_* amounts (its stocks) and the SELECT rows (every port on its cell), and the origin
+// clears its own SELECT bit when it stands on that cell (dqn.py:152-161). So every row is
+// one of 1 + P + sum_p |same[p]| templates: template 0 the moves alone, 1 + p port p's
+// cell with no origin on it, and 1 + P + pbase[p] + rank(o) port p's cell with origin o
+// cleared. mask_tmpl_kernel builds them once per world image into a device buffer:
+//   [0, 512)    same[64]: bit q of same[p] = port q stands on port p's cell
+//   [512, 772)  pbase[65]: prefix counts of |same[p]|
+//   [1024, ...) ntmpl blocks of TB bytes: 16 zero bytes, the S row bytes in np.packbits
+//               order, then zeros to the block's end (TB = round16(S + 35))
+// so that a 16-byte window read at any byte offset of [0, 16 + S) of a block holds the
+// row's bytes from that offset on, zeros before the row and after it.
+constexpr int kMaskHdr = 1024;
+__host__ __device__ constexpr int mask_tb(int S) { return (S + 35 + 15) & ~15; }
+constexpr int kMaskTmplMax = 320;  // templates held in LDS (P = 64 on distinct cells: 129)
+
+// the bits of actions [b, b + 32) of a row (bit o = action b + o), in packbits byte order
+__device__ __forceinline__ uint32_t mask_word(int b, int cur, int cst, int fst, uint64_t sel, int P) {
+    uint32_t m = bits_in(-b, 3 - b);  // moves: always
+    if (cur >= 0) {
+        const int c_lo = 5 + P, f_lo = 55 + P;  // TAKE_CARGO / TAKE_FUEL amount 1
+        m |= bits_in(c_lo - b, c_lo + min(cst, 49) - 1 - b) | bits_in(f_lo - b, f_lo + min(fst, 199) - 1 - b);
+        const int sh = b - 4;  // rows 4 + p: sel shifted by 4 - b
+        m |= (uint32_t)(sh < 0 ? (-sh < 64 ? sel << -sh : 0ull) : (sh < 64 ? sel >> sh : 0ull));
+    }
+    return __builtin_amdgcn_perm(0u, __builtin_bitreverse32(m), 0x00010203u);
+}
+
+__global__ __launch_bounds__(kBlock) void mask_tmpl_kernel(const uint32_t* world, WorldDims d, int S,
+                                                           uint8_t* buf) {
+    const LdsWorld w = world_view(d, world);
+    const int P = w.P, TB = mask_tb(S);
+    __shared__ uint64_t same[64];
+    __shared__ uint32_t pbase[65];
+    if ((int)threadIdx.x < P) {
+        uint64_t m = 0;
+        for (int q = 0; q < P; ++q) m |= (uint64_t)(w.pos[q] == w.pos[threadIdx.x]) << q;
+        same[threadIdx.x] = m;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        pbase[0] = 0;
+        for (int p = 0; p < P; ++p) pbase[p + 1] = pbase[p] + (uint32_t)__popcll(same[p]);
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < 64) reinterpret_cast<uint64_t*>(buf)[threadIdx.x] = (int)threadIdx.x < P ? same[threadIdx.x] : 0ull;
+    if ((int)threadIdx.x <= 64) reinterpret_cast<uint32_t*>(buf + 512)[threadIdx.x] = (int)threadIdx.x <= P ? pbase[threadIdx.x] : 0u;
+    const int ntmpl = 1 + P + (int)pbase[P], wpt = TB / 4;
+    uint32_t* out = reinterpret_cast<uint32_t*>(buf + kMaskHdr);
+    for (int k = threadIdx.x; k < ntmpl * wpt; k += kBlock) {
+        const int t = k / wpt, c = 4 * (k - t * wpt) - 16;  // the word's first row byte
+        int cur = -1;
+        uint64_t sel = 0;
+        if (t >= 1 && t <= P) {
+            cur = t - 1;
+            sel = same[cur];
+        } else if (t > P) {
+            const uint32_t j = (uint32_t)(t - 1 - P);
+            int p = 0;
+            while (pbase[p + 1] <= j) ++p;
+            uint64_t m = same[p];
+            for (uint32_t r = j - pbase[p]; r > 0; --r) m &= m - 1;  // the rank-th port of the cell
+            cur = p;
+            sel = same[p] & ~(m & (~m + 1));
+        }
+        uint32_t word = 0;
+        if (c >= 0 && c < S) {
+            word = mask_word(8 * c, cur, cur >= 0 ? w.pcargo(cur) : 0, cur >= 0 ? w.pfuel(cur) : 0, sel, P);
+            const int keep = S - c;  // bytes of the word inside the row
+            if (keep < 4) word &= (1u << (8 * keep)) - 1u;
+        }
+        out[k] = word;
+    }
+}
+
+// 16 bytes of LDS from any byte offset (the blocks leave 4 spare bytes past every window)
+__device__ __forceinline__ uint4 lds_window(const uint32_t* l, uint32_t off) {
+    const uint32_t a = off >> 2, sh = off & 3u;
+    const uint32_t w0 = l[a], w1 = l[a + 1], w2 = l[a + 2], w3 = l[a + 3], w4 = l[a + 4];
+    return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                      __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+}
+
+// is_valid_action bits from the row templates: per 256-row tile, one thread per row looks up
+// its template (desc: the block's byte offset in LDS), then one thread per 16-byte chunk of
+// the tile's dense output ORs the windows of the (at most two) rows the chunk covers and
+// stores it: S and 256 * S are such that a chunk never spans three rows or two tiles.
+__global__ __launch_bounds__(kBlock) void valid_mask_tmpl_kernel(MaskArgs A, const uint8_t* __restrict__ buf,
+                                                                 int ntmpl, uint32_t magic) {
+    extern __shared__ uint32_t tl[];  // [ntmpl * TB / 4] templates
+    __shared__ uint64_t same[64];
+    __shared__ uint32_t pbase[64];
+    __shared__ uint32_t desc[kTileRows + 1];
+    const LdsWorld w = world_view(A.dims, A.world);
+    const int P = w.P, S = A.stride, TB = mask_tb(S);
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(buf + kMaskHdr);
+        uint4* dst = reinterpret_cast<uint4*>(tl);
+        for (int k = threadIdx.x; k < ntmpl * TB / 16; k += kBlock) dst[k] = src[k];
+        if (threadIdx.x < 64) {
+            same[threadIdx.x] = reinterpret_cast<const uint64_t*>(buf)[threadIdx.x];
+            pbase[threadIdx.x] = reinterpret_cast<const uint32_t*>(buf + 512)[threadIdx.x];
+        }
+    }
+    for (int64_t r0 = (int64_t)blockIdx.x * kTileRows; r0 < A.n; r0 += (int64_t)gridDim.x * kTileRows) {
+        const int rows = (int)min((int64_t)kTileRows, A.n - r0);
+        __syncthreads();  // the templates are in; the previous tile's chunks have read desc
+        {
+            uint32_t id = 0;
+            if ((int)threadIdx.x < rows) {
+                const int64_t i = r0 + threadIdx.x;
+                const int cur = w.port_at(A.st.x[i], A.st.y[i]);
+                const int o = A.st.origin[i];  // SE_NONE (255) is never on a cell
+                if (cur >= 0) {
+                    const uint64_t sm = same[cur];
+                    const bool on = o < 64 && ((sm >> o) & 1ull);
+                    id = on ? 1u + (uint32_t)P + pbase[cur] + (uint32_t)__popcll(sm & ((1ull << o) - 1ull))
+                            : 1u + (uint32_t)cur;
+                }
+            }
+            desc[threadIdx.x] = id * (uint32_t)TB;
+            if (threadIdx.x == 0) desc[kTileRows] = 0;
+        }
+        __syncthreads();
+        const uint32_t nb = (uint32_t)(rows * S);
+        uint8_t* out = A.bits + r0 * S;
+        for (uint32_t q = threadIdx.x; 16 * q < nb; q += kBlock) {
+            const uint32_t c = 16 * q, r = div_tile(c, magic), c0 = c - r * (uint32_t)S;
+            const uint4 a = lds_window(tl, desc[r] + 16u + c0);
+            // the next row's bytes land at chunk offset S - c0; a window from before that
+            // row's start reads its zero prefix (-16 at most: otherwise the chunk ends first)
+            const int nx = max((int)c0 - S, -16);
+            const uint4 b = lds_window(tl, desc[r + 1] + (uint32_t)(16 + nx));
+            const uint4 v = make_uint4(a.x | b.x, a.y | b.y, a.z | b.z, a.w | b.w);
+            if (c + 16 <= nb) {
+                st_stream(reinterpret_cast<uint4*>(out + c), v);
+            } else {  // the ragged tail of the last tile
+                const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+                for (uint32_t k = 0; c + k < nb; ++k) out[c + k] = (uint8_t)(vv[k >> 2] >> (8 * (k & 3)));
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ synthetic agent
 __global__ __launch_bounds__(kBlock) void gen_actions_kernel(int64_t n, int64_t env_base,
                                                              uint64_t seed, uint32_t t, int32_t P,
@@ -2409,6 +2590,13 @@ struct se_env {
     int grid = 0;
     int64_t nseg = 0;   // done-list segments: one per (iteration, wave) of the step kernel
     int64_t nslab = 0;  // stats slab entries: one per step-kernel wave
+    uint8_t* d_mask_tmpl = nullptr;  // se_valid_mask's row templates (mask_tmpl_kernel), lazily built
+    size_t mask_tmpl_cap = 0;
+    uint64_t mask_tmpl_version = 0;  // world_version they were built from (0: none)
+    int mask_ntmpl = 0;              // 1 + P + sum_p |ports on p's cell| (upload_world)
+    bool mask_tiled = false;         // SHIPENV_MASK_TILED=1 at se_create: the round-4 tiled kernel
+    int32_t done_pad = 1;   // done-list records padded to runs of this many (done_pad_records)
+    bool nt_loads = false;  // nontemporal state loads in the step kernel (step_nt_loads)
 };
 
 // A host-resident world (se_host_*): no device, no HIP call. It steps envs whose SoA
@@ -2475,23 +2663,29 @@ int step_block_cap() {
 // Nontemporal state loads for the kernels without auto-reset while one step's traffic
 // (~42 B per env) stays inside or near the 256 MiB Infinity Cache. Forced on vs off at
 // the 32768-workgroup cap (profiles/r02h/nt_sweep, two runs each): config 3 at 2^20
-// 8.5-8.8 vs 9.1-9.2 us, at 2^24 131-134 vs 123 us. The auto-reset kernels (which also
-// read and write the episode counters) are faster without them: config 4 at 2^20
-// 11.6 vs 12.5-12.7 us, equal from 2^21 to 2^24; the training loop's step + record
-// 16.0-16.3 vs 17.5-17.9 us.
+// 8.5-8.8 vs 9.1-9.2 us, at 2^24 131-134 vs 123 us. The auto-reset kernels are faster
+// without them up to 2^21 envs (config 4 at 2^20 11.6 vs 12.5 us; the training loop's step
+// + record 16.0-16.3 vs 17.5-17.9 us) and with them beyond (below).
 // The done list's records padded to whole 128-B lines (wave_compact) once the step's traffic
 // is beyond the Infinity Cache: config 4 at 2^24 -2.7 us per step (median of five alternating
 // rounds), at 2^20 +0.17 us (profiles/r04/ab_donepad.jsonl). SHIPENV_DONE_PAD overrides.
+// Both settings are resolved once, by se_create (se_env::done_pad / nt_loads): a launch
+// reads no environment variable, and the layout cannot change between two steps.
 int32_t done_pad_records(const se_env* env) {
     const char* v = getenv("SHIPENV_DONE_PAD");
     if (v) return atoi(v) == 0 ? 1 : 8;
     return env->n > (int64_t)1 << 23 ? 8 : 1;
 }
 
+// Round 5 (episode-start stamps): the auto-reset kernel's few scattered stamp accesses per
+// wave are cheap while the state streams do not evict them from the Infinity Cache, which
+// the streams' nontemporal loads achieve. Config 4, alternating (profiles/r05/nt_sweep_c4.jsonl):
+// 2^20 11.6 (temporal) vs 12.5 us (nontemporal), 2^22 43.6 vs 43.3, 2^23 83.0 vs 80.4,
+// 2^24 173.4 vs 157.3, 2^25 339.5 vs 310.6; so nontemporal above 2^21 envs.
 bool step_nt_loads(const se_env* env) {
     const char* v = getenv("SHIPENV_NT_LOADS");
     if (v) return atoi(v) != 0;
-    if (env->flags & SE_FLAG_AUTO_RESET) return false;
+    if (env->flags & SE_FLAG_AUTO_RESET) return env->n > (int64_t)1 << 21;
     return env->n <= (int64_t)1 << 23;
 }
 
@@ -2574,6 +2768,9 @@ int upload_world(se_env* env, int32_t P, const int32_t* px, const int32_t* py, c
         env->fmax = std::max(env->fmax, std::min(pf[i], 199));
     }
     env->world_version += 1;
+    env->mask_ntmpl = 1 + P;  // se_valid_mask's row templates (mask_tmpl_kernel)
+    for (int p = 0; p < P; ++p)
+        for (int q = 0; q < P; ++q) env->mask_ntmpl += (px[p] == px[q] && py[p] == py[q]) ? 1 : 0;
     return SE_OK;
 }
 
@@ -2617,13 +2814,13 @@ int launch_step(se_env* env, bool typed, bool replay, const int32_t* act, const 
         A.done_count = env->st.done_count + par * (size_t)env->nseg;
     }
     A.seg = env->seg;
-    A.done_pad = done_pad_records(env);
+    A.done_pad = env->done_pad;
     A.iters = env->iters;
     A.slab = env->d_slab;
     const hipStream_t s = (hipStream_t)stream;
     const size_t lds = lds_bytes(env);
     const int grid = env->grid;
-    const bool ntl = step_nt_loads(env);
+    const bool ntl = env->nt_loads;
     if (rec) {  // se_step_record: the caller checked agent actions, auto-reset, n % 4 == 0, n > 0
         A.rec = *rec;
         if (ntl) step_kernel<false, false, true, true, true><<<grid, kStepBlock, lds, s>>>(A);
@@ -2715,6 +2912,10 @@ int se_create(se_env** out, int device, int64_t n, int64_t env_id_base, int32_t 
         env->seg = 64 * kEnvsPerThread;  // one done-list segment per (iteration, wave)
         env->nseg = (int64_t)env->grid * env->iters * (kStepBlock / 64);
         env->nslab = (int64_t)env->grid * (kStepBlock / 64);  // stats: one entry per wave
+        env->done_pad = done_pad_records(env);
+        env->nt_loads = step_nt_loads(env);
+        const char* mv = getenv("SHIPENV_MASK_TILED");
+        env->mask_tiled = mv && atoi(mv) != 0;
     }
     hipError_t e = hipMalloc(&env->d_slab, (size_t)env->nslab * 4 * sizeof(double));
     if (e == hipSuccess) e = hipMemset(env->d_slab, 0, (size_t)env->nslab * 4 * sizeof(double));
@@ -2745,9 +2946,9 @@ int se_bind(se_env* env, const se_state* st) {
         if (!aligned16(p)) return fail(SE_EINVAL, "state buffers must be 16-byte aligned");
     }
     if (env->flags & SE_FLAG_AUTO_RESET) {
-        if ((env->n > 0 && (!st->ep_return || !st->ep_len)) || !st->done_recs || !st->done_count)
-            return fail(SE_EINVAL, "auto-reset needs ep_return, ep_len, done_recs and done_count");
-        if (!aligned16(st->ep_return) || !aligned16(st->ep_len) || !aligned16(st->done_recs))
+        if ((env->n > 0 && (!st->ep_return || !st->ep_start)) || !st->done_recs || !st->done_count)
+            return fail(SE_EINVAL, "auto-reset needs ep_return, ep_start, done_recs and done_count");
+        if (!aligned16(st->ep_return) || !aligned16(st->ep_start) || !aligned16(st->done_recs))
             return fail(SE_EINVAL, "state buffers must be 16-byte aligned");
         DeviceGuard g(env->device);
         HIP_TRY(hipMemset(st->done_count, 0, 2 * (size_t)env->nseg * sizeof(int32_t)));
@@ -2763,7 +2964,7 @@ int se_reset(se_env* env, const uint8_t* mask, void* stream) {
     if (env->dims.P < 2) return fail(SE_EINVAL, "reset needs at least two ports");
     DeviceGuard g(env->device);
     ResetArgs A{env->d_world, env->dims, env->n, env->env_base, env->seed,
-                (uint32_t)env->epoch, env->st, mask, nullptr, nullptr};
+                (uint32_t)env->epoch, (uint32_t)env->step_t, env->st, mask, nullptr, nullptr};
     if (env->n > 0) {
         reset_kernel<<<grid_for(env->n), kBlock, 0, (hipStream_t)stream>>>(A);
         HIP_TRY(hipGetLastError());
@@ -2779,7 +2980,7 @@ int se_reset_to(se_env* env, const uint8_t* mask, const int32_t* origin, const i
     if (env->n > 0 && (!origin || !dest)) return fail(SE_EINVAL, "null origin/dest");
     DeviceGuard g(env->device);
     ResetArgs A{env->d_world, env->dims, env->n, env->env_base, env->seed,
-                (uint32_t)env->epoch, env->st, mask, origin, dest};
+                (uint32_t)env->epoch, (uint32_t)env->step_t, env->st, mask, origin, dest};
     if (env->n > 0) {
         reset_kernel<<<grid_for(env->n), kBlock, 0, (hipStream_t)stream>>>(A);
         HIP_TRY(hipGetLastError());
@@ -2857,9 +3058,31 @@ int se_valid_mask(se_env* env, uint8_t* bits, void* stream) {
     MaskArgs A{env->d_world, env->dims, env->n, stride, env->st, bits};
     const int64_t total = env->n * stride;
     if (total == 0) return SE_OK;
-    if (aligned16(bits)) {  // the tiled kernel (rows are always dense here)
+    const hipStream_t s = (hipStream_t)stream;
+    const int tb = mask_tb(stride);
+    if (aligned16(bits) && env->dims.P <= 64 && env->mask_ntmpl <= kMaskTmplMax && !env->mask_tiled) {
+        // the row templates, rebuilt when the world image changed
+        const size_t need = (size_t)kMaskHdr + (size_t)env->mask_ntmpl * tb;
+        if (need > env->mask_tmpl_cap) {
+            if (env->d_mask_tmpl) HIP_TRY(hipFree(env->d_mask_tmpl));
+            env->d_mask_tmpl = nullptr;
+            env->mask_tmpl_cap = 0;
+            HIP_TRY(hipMalloc(&env->d_mask_tmpl, need));
+            env->mask_tmpl_cap = need;
+            env->mask_tmpl_version = 0;
+        }
+        if (env->mask_tmpl_version != env->world_version) {
+            mask_tmpl_kernel<<<1, kBlock, 0, s>>>(env->d_world, env->dims, stride, env->d_mask_tmpl);
+            HIP_TRY(hipGetLastError());
+            env->mask_tmpl_version = env->world_version;
+        }
+        const uint32_t magic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)stride - 1) / (uint64_t)stride);
+        const size_t lds = (size_t)env->mask_ntmpl * tb;
+        valid_mask_tmpl_kernel<<<grid_for(env->n, lds > 4096 ? 1024 : kMaxBlocks), kBlock, lds, s>>>(
+            A, env->d_mask_tmpl, env->mask_ntmpl, magic);
+    } else if (aligned16(bits)) {  // the tiled kernel (rows are always dense here)
         const size_t lds = ((size_t)kTileRows * stride + 15) & ~(size_t)15;
-        valid_mask_tiled_kernel<<<grid_for(env->n), kBlock, lds, (hipStream_t)stream>>>(A);
+        valid_mask_tiled_kernel<<<grid_for(env->n), kBlock, lds, s>>>(A);
     } else {
         valid_mask_kernel<<<grid_for(total), kBlock, lds_bytes(env), (hipStream_t)stream>>>(A);
     }
@@ -2993,6 +3216,7 @@ int se_destroy(se_env* env) {
     if (env->d_world) (void)hipFree(env->d_world);
     if (env->d_slab) (void)hipFree(env->d_slab);
     if (env->d_offsets) (void)hipFree(env->d_offsets);
+    if (env->d_mask_tmpl) (void)hipFree(env->d_mask_tmpl);
     delete env;
     return SE_OK;
 }
@@ -3072,7 +3296,7 @@ int se_host_reset_to(se_host* h, int64_t n, const se_state* st, const uint8_t* m
         st->origin[i] = (uint8_t)origin[i];
         st->dest[i] = (uint8_t)dest[i];
         if (st->ep_return) st->ep_return[i] = 0.0f;
-        if (st->ep_len) st->ep_len[i] = 0;
+        if (st->ep_start) st->ep_start[i] = 0;  // a host world has no step counter
         st->done[i] = 0;
         st->err[i] = 0;
         st->reward[i] = 0.0f;

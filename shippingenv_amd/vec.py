@@ -102,7 +102,9 @@ class VecEnv:
         self.done = torch.zeros(n, dtype=torch.uint8, **kw)
         self.err = torch.zeros(n, dtype=torch.int8, **kw)
         self.ep_return = torch.zeros(n, dtype=torch.float32, **kw)
-        self.ep_len = torch.zeros(n, dtype=torch.int32, **kw)
+        # episode-start stamps on the step counter (include/shipenv.h se_state.ep_start);
+        # the running lengths are the property ep_len
+        self.ep_start = torch.zeros(n, dtype=torch.int32, **kw)
         self._h = C.c_void_p()
         flags = N.SE_FLAG_AUTO_RESET if self.auto_reset else 0
         with torch.cuda.device(self.device):
@@ -123,7 +125,7 @@ class VecEnv:
         self._done_out = None
         self._state = N.SeState(*[t.data_ptr() for t in (
             self.x, self.y, self.fuel, self.cargo, self.origin, self.dest, self.reward,
-            self.done, self.err, self.ep_return, self.ep_len, self.done_recs, self.done_count)] + [None])
+            self.done, self.err, self.ep_return, self.ep_start, self.done_recs, self.done_count)] + [None])
         N.check(lib.se_bind(self._h, C.byref(self._state)))
         self._se_step = lib.se_step
         self._se_step_seq = lib.se_step_seq
@@ -139,6 +141,14 @@ class VecEnv:
     @property
     def obs_size(self):
         return 6 + 4 * self.P
+
+    @property
+    def ep_len(self):
+        """Running episode lengths in step calls (auto-reset): (step counter - ep_start)
+        mod 2^32, as a new int32 device tensor computed on the current stream."""
+        t = self.counters[0] & 0xFFFFFFFF
+        d = (t - self.ep_start.to(torch.int64)) & 0xFFFFFFFF
+        return torch.where(d >= 2**31, d - 2**32, d).to(torch.int32)
 
     def _stream(self):
         return C.c_void_p(_raw_stream(self._dev_index))
@@ -196,12 +206,13 @@ class VecEnv:
         self._keep = a
         return self.reward, self.done, self.err
 
-    def step_seq(self, actions, mark=None, mark_after=1):
+    def step_seq(self, actions, mark=None, mark_after=0):
         """len(actions) consecutive step() calls issued from native code (se_step_seq):
         actions is an int32 device tensor [K, n] (rows contiguous, 16-byte aligned), row k
         the actions of step k. mark: a torch.cuda.Event recorded on the current stream right
-        after launch `mark_after` (se_step_seq_mark), a timer mark inside the one native
-        call. Returns the last step's (reward, done, err)."""
+        after launch `mark_after` (se_step_seq_mark; 0 = before launch 1, the timed loop's
+        form; at most K), a timer mark inside the one native call. Returns the last
+        step's (reward, done, err)."""
         a = actions
         if not (type(a) is torch.Tensor and a.dtype is torch.int32 and a.is_cuda and a.dim() == 2
                 and a.get_device() == self._dev_index and a.shape[1] == self.n and a.stride(1) == 1
@@ -210,7 +221,13 @@ class VecEnv:
         ld = a.stride(0) if self.n else 0  # an empty batch: no rows to stride over
         if mark is not None:
             if mark.cuda_event == 0:  # torch creates the HIP event on its first record
-                mark.record()
+                with torch.cuda.device(self.device):
+                    mark.record()
+            ev_dev = getattr(mark, "device", None)
+            if ev_dev is not None and ev_dev.index is not None and ev_dev.index != self._dev_index:
+                raise ValueError(f"mark event is on {ev_dev}, the env on cuda:{self._dev_index}")
+            if not 0 <= int(mark_after) <= a.shape[0]:
+                raise ValueError(f"mark_after must be in [0, {a.shape[0]}], got {mark_after}")
             rc = N.lib().se_step_seq_mark(self._h, a.data_ptr(), ld, a.shape[0],
                                           _raw_stream(self._dev_index), mark.cuda_event, int(mark_after))
             if rc:

@@ -421,6 +421,61 @@ def test_observe_and_valid_mask_vs_golden(water):
     env.close()
 
 
+@pytest.mark.parametrize("case", ["default", "ports64", "shared_cells", "ports100", "tiled_forced"])
+def test_valid_mask_row_templates(oracle_mod, water, monkeypatch, case):
+    """se_valid_mask's template kernel (round 5): every row is one of 1 + P + sum_p |ports on
+    p's cell| templates (the moves alone; a port's cell; a port's cell without the origin's
+    SELECT row). The states put ships on every port cell with every origin, None included,
+    and at sea; n is ragged (3 tiles + 77 rows). 18 ports with three shared cells exercise the
+    same-cell templates; P = 100 (> 64) and SHIPENV_MASK_TILED=1 take the round-4 tiled kernel.
+    All equal the oracle (agents/dqn.py:125-175); after set_ports (new stocks) the templates
+    are rebuilt and the rows follow."""
+    from shippingenv_amd.vec import draw_port_stocks, random_water_ports
+
+    O = oracle_mod
+    if case == "default":
+        ports = None
+    elif case in ("ports64", "tiled_forced"):
+        ports = random_water_ports(water, 64, seed=4)
+    elif case == "shared_cells":
+        base = random_water_ports(water, 12, seed=6)
+        ports = base + [base[0], base[0], base[3], base[7], base[7], base[7]]
+    else:
+        ports = random_water_ports(water, 100, seed=7)
+    if case == "tiled_forced":
+        monkeypatch.setenv("SHIPENV_MASK_TILED", "1")
+    n = 3 * 256 + 77
+    env = VecEnv(n, seed=3, ports=ports)
+    P = env.P
+    rng = np.random.default_rng(11)
+    at_port = rng.random(n) < 0.85
+    k = rng.integers(0, P, n)
+    cells = np.argwhere(env.water != 0)
+    sea = cells[rng.integers(0, len(cells), n)]
+    x = np.where(at_port, env.port_x[k], sea[:, 0]).astype(np.int32)
+    y = np.where(at_port, env.port_y[k], sea[:, 1]).astype(np.int32)
+    # origin: the port itself, another port of the same cell, any port, or None
+    same = np.array([[env.port_x[a] == env.port_x[b] and env.port_y[a] == env.port_y[b] for b in range(P)]
+                     for a in range(P)])
+    alt = np.array([rng.choice(np.nonzero(same[i])[0]) for i in k])
+    u = rng.random(n)
+    origin = np.where(u < 0.4, k, np.where(u < 0.7, alt, np.where(u < 0.9, rng.integers(0, P, n), -1)))
+    for stock_seed in (None, 99):
+        if stock_seed is not None:
+            f, c = draw_port_stocks(P, stock_seed)
+            env.set_ports([[int(a), int(b)] for a, b in zip(env.port_x, env.port_y)], f, c)
+        world, st = _oracle_pair(O, env)
+        st.x[:], st.y[:], st.origin[:] = x, y, origin
+        env.x.copy_(torch.from_numpy(x.astype(np.uint8)))
+        env.y.copy_(torch.from_numpy(y.astype(np.uint8)))
+        env.origin.copy_(torch.from_numpy(np.where(origin < 0, 255, origin).astype(np.uint8)))
+        want = O.valid_mask(world, st)
+        got = env.valid_mask().cpu().numpy()
+        np.testing.assert_array_equal(got, want, err_msg=f"{case} stocks {stock_seed}")
+        assert want[:, :1].any() and (want.sum(axis=1) > 1).mean() > 0.5  # moves, and port rows
+    env.close()
+
+
 def test_fuel_cost_sqrt_is_correctly_rounded(oracle_mod):
     """Typed moves (dx, dy) from (0, 0) over the whole grid: fuel bits use
     np.sqrt of every reachable squared distance (shipping/util.py:4)."""

@@ -33,7 +33,11 @@ def test_exports_every_declared_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.se_abi_version() == 1
+    import re
+    from shippingenv_amd import _native
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "shipenv.h")).read()
+    want = int(re.search(r"#define SHIPENV_ABI_VERSION (\d+)", hdr).group(1))
+    assert lib.se_abi_version() == want == _native.ABI_VERSION == 2
 
 
 def test_library_is_gfx950():

@@ -148,7 +148,7 @@ int main(int argc, char** argv) {
             int32_t segs = 0;
             SE(a.layout(env, &stride, &segs));
             st.ep_return = (float*)dev(4 * n);
-            st.ep_len = (int32_t*)dev(4 * n);
+            st.ep_start = (int32_t*)dev(4 * n);
             st.done_recs = (se_done_rec*)dev(2 * (size_t)segs * stride * sizeof(se_done_rec));
             st.done_count = (int32_t*)dev(2 * (size_t)segs * sizeof(int32_t));
         }
@@ -209,7 +209,7 @@ int main(int argc, char** argv) {
         SE(a.destroy(env));
         for (void* p : {(void*)st.x, (void*)st.y, (void*)st.origin, (void*)st.dest, (void*)st.done,
                         (void*)st.err, (void*)st.fuel, (void*)st.cargo, (void*)st.reward,
-                        (void*)st.ep_return, (void*)st.ep_len, (void*)st.done_recs,
+                        (void*)st.ep_return, (void*)st.ep_start, (void*)st.done_recs,
                         (void*)st.done_count, (void*)acts})
             if (p) CK(hipFree(p));
         CK(hipStreamDestroy(s));
