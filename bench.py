@@ -227,13 +227,13 @@ def timed_loop(env, acts, first, steps, dist, reduce_every=0, counter=None, step
         e.record(stream)
     # the step's action rows as views made before the clock starts: indexing the
     # [steps, n] table inside the loop is harness work (1.4 us of host time per step,
-    # tools/diag/host_step_cost.py), not the step's
+    # tools/archive/diag/host_step_cost.py), not the step's
     if not step_seq:
         chunks = [acts[first + k] for k in range(steps)]
     else:  # runs that end where an all-reduce follows; the first run records ef right before
         # its launch 1 from native code (se_step_seq_mark, mark_after = 0): splitting the run
         # after launch 1 for a Python record cost ~0.7 us per step over the driver's 20, and a
-        # native record there 0.2-0.4 (tools/diag/wall_forms.py, profiles/r04/wall_forms*)
+        # native record there 0.2-0.4 (tools/archive/diag/wall_forms.py, profiles/r04/wall_forms*)
         cuts = sorted({0, steps} | ({k for k in range(reduce_every, steps, reduce_every)}
                                     if reduce_every else set()))
         chunks = [acts[first + a:first + b] for a, b in zip(cuts, cuts[1:])]

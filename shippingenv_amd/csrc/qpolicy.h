@@ -810,6 +810,254 @@ __global__ __launch_bounds__(kPolicyF32Block) void policy_f32_kernel(PolicyF32Ar
     }
 }
 
+// ------------------------------------------------------------------ the split-bf16 f32 step
+// The fp32-faithful step on bf16 MFMA (round 5; se_policy_f32's default). fc2 and fc3 run
+// on v_mfma_f32_32x32x16_bf16 with every f32 operand split into three bf16 parts,
+// w = w0 + w1 + w2 and x = x0 + x1 + x2 (each part the round-to-nearest bf16 of what the
+// parts before it leave; three 8-bit significands hold an f32's 24 bits), and the six
+// products whose parts sum to at most 2, w0x2 + w1x1 + w2x0 + w0x1 + w1x0 + w0x0, smallest
+// first, into one f32 accumulator. The dropped products (w1x2, w2x1, w2x2) are below
+// 2^-23 of |w x|: a simulation of this datapath against float64 (MFMA = one f32 rounding
+// per instruction) errs like the f32 MFMA path and torch's fp32 GEMM.
+// Six bf16 MFMAs (32 cycles each) per 16-deep k-step where the f32 datapath runs eight
+// v_mfma_f32_32x32x2_f32 (64 cycles each): 2.7x fewer MFMA cycles. fc1 (6 live inputs)
+// stays on f32 MFMA. Relu'd activations are split once per layer (registers 8s..8s+7 of
+// tile kt are k-step (kt, s)'s B operand, as in the bf16 kernel) and held as 24 bf16x8
+// parts. Image: the f32 image's fc1 and biases, fc2 and fc3 as three bf16 fragments per
+// (tile, kt, s): 96 KB + 24 KB per fc3 tile, so the world is read in place (L2), not
+// staged, and fc3 comes from global memory when it does not fit (the full layout).
+struct QnetX3Dims {
+    QnetDims q;
+    __host__ __device__ int w1() const { return 0; }                    // f32 fc1, as QnetF32Dims (3 KB)
+    __host__ __device__ int w2() const { return 4096; }                 // [mt][kt][s][part] bf16 fragments: 96 KB
+    __host__ __device__ int b1() const { return w2() + 96 * 1024; }
+    __host__ __device__ int b2() const { return b1() + 4 * kQHidden; }
+    __host__ __device__ int b3() const { return b2() + 4 * kQHidden; }  // mt3 * 32 f32
+    __host__ __device__ int same() const { return b3() + q.mt3 * 128; }
+    __host__ __device__ int regm() const { return same() + 8 * q.P; }
+    __host__ __device__ int w3() const { return (regm() + 4 * q.mt3 + 15) & ~15; }  // mt3 x 24 KB, last
+    __host__ __device__ int bytes() const { return w3() + q.mt3 * 24 * 1024; }
+};
+
+// v = p0 + p1 + p2, each the bf16 rounding of the remainder (exact f32 subtractions)
+__device__ __forceinline__ void split3(float v, __bf16& p0, __bf16& p1, __bf16& p2) {
+    p0 = (__bf16)v;
+    const float r1 = v - (float)p0;
+    p1 = (__bf16)r1;
+    p2 = (__bf16)(r1 - (float)p1);
+}
+
+struct PackX3Args {
+    const float *w1, *b1, *w2, *b2, *w3, *b3;
+    const uint32_t* world;
+    WorldDims dims;
+    QnetX3Dims d;
+    uint8_t* img;
+};
+
+// One thread per (fragment, lane) of fc2 / fc3 (its 8 elements' three parts), per fc1 float,
+// bias entry, same-cell mask and epilogue register mask (the latter as qnet_pack_f32_kernel).
+__global__ __launch_bounds__(256) void qnet_pack_x3_kernel(PackX3Args A) {
+    const QnetX3Dims d = A.d;
+    const QnetDims q = d.q;
+    uint8_t* const img = A.img;
+    const int in1 = q.in1();
+    const int n_w1 = 4 * 3 * 64, n_w2 = 32 * 64, n_w3 = q.mt3 * 8 * 64;
+    const int total = n_w1 + n_w2 + n_w3 + 2 * kQHidden + q.mt3 * 32 + q.P + q.mt3;
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        if (t < n_w1) {  // fc1 in f32: (mt, s, lane) = W1[mt*32 + r][2s + h] (qnet_pack_f32_kernel)
+            const int lane = t & 63, st = t >> 6, s = st % 3, mt = st / 3;
+            reinterpret_cast<float*>(img + d.w1())[t] = A.w1[(mt * 32 + (lane & 31)) * in1 + 2 * s + (lane >> 5)];
+            continue;
+        }
+        if (t < n_w1 + n_w2 + n_w3) {  // fragment f = (mt*4 + kt)*2 + s, lane: W[row][kt*32 + acc_row(s, j, h)]
+            const bool second = t < n_w1 + n_w2;
+            const int u = t - (second ? n_w1 : n_w1 + n_w2);
+            const int f = u >> 6, lane = u & 63, r = lane & 31, h = lane >> 5;
+            const int s = f & 1, kt = (f >> 1) & 3, mt = f >> 3;
+            const int row = mt * 32 + r;
+            const bool in = second || row < q.rows;
+            const float* W = second ? A.w2 : A.w3;
+            const int wrow = second ? row : q.action_of_row(row);
+            bf16x8 p[3];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float v = in ? W[wrow * kQHidden + kt * 32 + acc_row(s, j, h)] : 0.0f;
+                __bf16 a, b, c;
+                split3(v, a, b, c);
+                p[0][j] = a;
+                p[1][j] = b;
+                p[2][j] = c;
+            }
+            uint8_t* dst = img + (second ? d.w2() : d.w3()) + f * 3 * 1024 + lane * 16;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) *reinterpret_cast<bf16x8*>(dst + k * 1024) = p[k];
+            continue;
+        }
+        int u = t - (n_w1 + n_w2 + n_w3);
+        const LdsWorld wv = world_view(A.dims, A.world);
+        const int P = q.P;
+        if (u < kQHidden) {  // b1 + fc1 over the constant port block, in f64 then f32
+            double acc = (double)A.b1[u];
+            for (int p = 0; p < P; ++p) {
+                const float* w = A.w1 + u * in1 + 6 + 4 * p;
+                acc += (double)w[0] * (double)wv.px(p) + (double)w[1] * (double)wv.py(p) +
+                       (double)w[2] * (double)wv.pfuel(p) + (double)w[3] * (double)wv.pcargo(p);
+            }
+            reinterpret_cast<float*>(img + d.b1())[u] = (float)acc;
+        } else if ((u -= kQHidden) < kQHidden) {
+            reinterpret_cast<float*>(img + d.b2())[u] = A.b2[u];
+        } else if ((u -= kQHidden) < q.mt3 * 32) {
+            reinterpret_cast<float*>(img + d.b3())[u] = u < q.rows ? A.b3[q.action_of_row(u)] : 0.0f;
+        } else if ((u -= q.mt3 * 32) < P) {
+            uint64_t same = 0;
+            for (int p = 0; p < P; ++p)
+                if (wv.pos[p] == wv.pos[u]) same |= 1ull << p;
+            reinterpret_cast<uint64_t*>(img + d.same())[u] = same;
+        } else {
+            const int mt = u - P, base = mt * 32;
+            int cmax = 0, fmax = 0;
+            for (int p = 0; p < P; ++p) {
+                cmax = max(cmax, min(wv.pcargo(p), 49));
+                fmax = max(fmax, min(wv.pfuel(p), 199));
+            }
+            const int c_lo = 5 + P, c_hi = 4 + P + cmax, f_lo = 55 + P, f_hi = 54 + P + fmax;
+            uint32_t rm = 0;
+            for (int reg = 0; reg < 16; ++reg)
+                for (int h = 0; h < 2; ++h) {
+                    const int row = base + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                    const int a = q.action_of_row(row);
+                    const bool ok = row < q.rows && (a < 4 + P || (a >= c_lo && a <= c_hi) || (a >= f_lo && a <= f_hi));
+                    rm |= (uint32_t)ok << reg;
+                }
+            reinterpret_cast<uint32_t*>(img + d.regm())[mt] = rm;
+        }
+    }
+}
+
+// relu of one 32-row f32 tile, split into the three bf16 B fragments of its two k-steps
+__device__ __forceinline__ void relu_split3(const f32x16& c, bf16x8 (&out)[2][3]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const f32x2 v{fmaxf(c[8 * s + 2 * p], 0.0f), fmaxf(c[8 * s + 2 * p + 1], 0.0f)};
+            const bf16x2 a = __builtin_convertvector(v, bf16x2);
+            const f32x2 r1 = v - __builtin_convertvector(a, f32x2);
+            const bf16x2 b = __builtin_convertvector(r1, bf16x2);
+            const bf16x2 e = __builtin_convertvector(r1 - __builtin_convertvector(b, f32x2), bf16x2);
+            out[s][0][2 * p] = a[0];
+            out[s][0][2 * p + 1] = a[1];
+            out[s][1][2 * p] = b[0];
+            out[s][1][2 * p + 1] = b[1];
+            out[s][2][2 * p] = e[0];
+            out[s][2][2 * p + 1] = e[1];
+        }
+}
+
+__device__ __forceinline__ f32x16 mfma_bf16(const bf16x8& a, const bf16x8& b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// c + W x over one k-step: the six part products, smallest first
+__device__ __forceinline__ f32x16 kstep_x3(const bf16x8* Wf, int lane, const bf16x8 (&x)[3], f32x16 c) {
+    const bf16x8 w0 = Wf[lane], w1 = Wf[64 + lane], w2 = Wf[128 + lane];
+    c = mfma_bf16(w0, x[2], c);
+    c = mfma_bf16(w1, x[1], c);
+    c = mfma_bf16(w2, x[0], c);
+    c = mfma_bf16(w0, x[1], c);
+    c = mfma_bf16(w1, x[0], c);
+    c = mfma_bf16(w0, x[0], c);
+    return c;
+}
+
+constexpr int kPolicyX3Block = 512;
+constexpr int kPolicyX3Waves = kPolicyX3Block / 64;
+
+template <bool kW3Global>
+__global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args F, QnetX3Dims D) {
+    extern __shared__ uint4 smem[];
+    const PolicyArgs& A = F.p;
+    const QnetDims q = D.q;
+    const int staged = (kW3Global ? D.w3() : D.bytes()) / 16;
+    for (int i = threadIdx.x; i < staged; i += kPolicyX3Block) smem[i] = A.qimg[i];
+    __syncthreads();
+    const LdsWorld w = world_view(A.dims, A.world);  // port_at / stocks read in place (L2)
+    const uint8_t* qb = reinterpret_cast<const uint8_t*>(smem);
+    const float* W1 = reinterpret_cast<const float*>(qb + D.w1());
+    const bf16x8* W2 = reinterpret_cast<const bf16x8*>(qb + D.w2());
+    const bf16x8* W3 = reinterpret_cast<const bf16x8*>((kW3Global ? reinterpret_cast<const uint8_t*>(A.qimg) : qb) + D.w3());
+    const float* B1 = reinterpret_cast<const float*>(qb + D.b1());
+    const float* B2 = reinterpret_cast<const float*>(qb + D.b2());
+    const float* B3 = reinterpret_cast<const float*>(qb + D.b3());
+    const uint64_t* SAME = reinterpret_cast<const uint64_t*>(qb + D.same());
+    const uint32_t* REGM = reinterpret_cast<const uint32_t*>(qb + D.regm());
+
+    const int lane = threadIdx.x & 63, h = lane >> 5;
+    const int P = q.P;
+    const int64_t tiles = (A.n + 31) >> 5;
+    const int64_t stride = (int64_t)gridDim.x * kPolicyX3Waves;
+    // the env state of the wave's next tile is loaded while this one computes (no HBM round
+    // trip at the top of a tile), and its validity (the port on the ship's cell and that
+    // port's stocks, two dependent L2 reads of the world image) resolved during fc3
+    struct EnvIn {
+        double fuel;
+        uint32_t x8, y8, o8, d8;
+    };
+    auto load_env = [&](int64_t t) {
+        const int64_t ei = min(t * 32 + (lane & 31), A.n - 1);
+        return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei]};
+    };
+    int64_t tile = (int64_t)blockIdx.x * kPolicyX3Waves + (threadIdx.x >> 6);
+    EnvIn nxt = load_env(tile < tiles ? tile : 0);
+    EnvValid vnxt = env_valid(w, q, SAME, (int)nxt.x8, (int)nxt.y8, nxt.o8 == SE_NONE ? -1 : (int)nxt.o8);
+    for (; tile < tiles; tile += stride) {
+        const EnvIn in = nxt;
+        const EnvValid v = vnxt;
+        const bool more = tile + stride < tiles;
+        if (more) nxt = load_env(tile + stride);
+        const int64_t e = tile * 32 + (lane & 31);
+        const bool live = e < A.n;
+        const double fuel = in.fuel;
+        const uint32_t x8 = in.x8, y8 = in.y8, o8 = in.o8, d8 = in.d8;
+        const int origin = o8 == SE_NONE ? -1 : (int)o8, dest = d8 == SE_NONE ? -1 : (int)d8;
+        const float ff = (float)fuel;  // the preprocess_state row as torch's FloatTensor holds it
+        const float in0 = h ? (float)y8 : (float)x8, in2 = h ? (float)dest : (float)origin;
+        bf16x8 X1[4][2][3], X2[4][2][3];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {  // fc1 on f32 MFMA (x, y | fuel, fuel | origin, dest), relu, split
+            f32x16 c = bias_frag(B1 + mt * 32 + 4 * h);
+            c = mfma32(W1[(mt * 3 + 0) * 64 + lane], in0, c);
+            c = mfma32(W1[(mt * 3 + 1) * 64 + lane], ff, c);
+            c = mfma32(W1[(mt * 3 + 2) * 64 + lane], in2, c);
+            relu_split3(c, X1[mt]);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {  // fc2 row tile mt = fc3's k-tile mt
+            f32x16 c = bias_frag(B2 + mt * 32 + 4 * h);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) c = kstep_x3(W2 + ((mt * 4 + (k >> 1)) * 2 + (k & 1)) * 192, lane, X1[k >> 1][k & 1], c);
+            relu_split3(c, X2[mt]);
+        }
+        if (more) vnxt = env_valid(w, q, SAME, (int)nxt.x8, (int)nxt.y8, nxt.o8 == SE_NONE ? -1 : (int)nxt.o8);
+        float best = -INFINITY;
+        int bidx = 0x7fffffff;
+#pragma nounroll
+        for (int mt = 0; mt < q.mt3; ++mt) {  // fc3 + the masked first-maximum argmax
+            const int base = mt * 32;
+            if (!A.q_out && !__any(tile_maybe(v, mt, P))) continue;
+            const uint32_t m = tile_mask(v, mt, P);
+            const uint32_t rm = __builtin_amdgcn_readfirstlane(REGM[mt]);
+            f32x16 c = bias_frag(B3 + mt * 32 + 4 * h);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) c = kstep_x3(W3 + ((mt * 4 + (k >> 1)) * 2 + (k & 1)) * 192, lane, X2[k >> 1][k & 1], c);
+            tile_argmax(c, m, rm, base, h, best, bidx);
+            if (A.q_out && live) tile_q_out(A.q_out, A.ldq, q.rows, c, e, base, h);
+        }
+        FINISH_ENV(v, e, live, h, best, bidx, x8, y8, o8, d8, ff);
+    }
+}
+
 }  // namespace
 
 struct se_qnet {
@@ -824,6 +1072,8 @@ struct se_qnet {
     bool packed = false;
     uint8_t* d_img32 = nullptr;  // se_policy_f32's image, repacked from w[] at every call
     int img32_bytes = 0;
+    bool f32_mfma = false;  // SHIPENV_POLICY_F32=mfma at se_qnet_create: the f32-MFMA datapath
+                            // (policy_f32_kernel) instead of the split-bf16 one (policy_x3_kernel)
 };
 
 extern "C" {
@@ -836,6 +1086,8 @@ int se_qnet_create(se_qnet** out, se_env* env) {
     se_qnet* qn = new se_qnet;
     qn->env = env;
     qn->device = env->device;
+    const char* mode = getenv("SHIPENV_POLICY_F32");
+    qn->f32_mfma = mode && std::string(mode) == "mfma";
     *out = qn;
     return SE_OK;
 }
@@ -934,6 +1186,65 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }
+// the split-bf16 datapath (policy_x3_kernel); the caller checked the arguments
+int launch_policy_x3(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, float* q_out, int64_t ldq,
+                     const PolicyRecord* rec, void* stream) {
+    se_env* env = qn->env;
+    QnetX3Dims d;
+    d.q = q_out ? qn->q : qn->qc;  // the compact rows unless every row's Q is wanted
+    if (d.bytes() > qn->img32_bytes) {
+        if (qn->d_img32) HIP_TRY(hipFree(qn->d_img32));
+        qn->d_img32 = nullptr;
+        HIP_TRY(hipMalloc(&qn->d_img32, (size_t)d.bytes()));
+        qn->img32_bytes = d.bytes();
+    }
+    const hipStream_t s = (hipStream_t)stream;
+    // the image from the current weights (in place updates by an optimizer or T2 included)
+    PackX3Args pk{qn->w[0], qn->w[1], qn->w[2], qn->w[3], qn->w[4], qn->w[5], env->d_world, env->dims, d,
+                  qn->d_img32};
+    qnet_pack_x3_kernel<<<128, 256, 0, s>>>(pk);
+    HIP_TRY(hipGetLastError());
+    const bool w3_global = d.bytes() > 160 * 1024;
+    const size_t lds = (size_t)(w3_global ? d.w3() : d.bytes());
+    if (lds > 160 * 1024) return fail(SE_EINVAL, "split-bf16 network exceeds the 160 KB LDS");
+    static std::atomic<uint64_t> lds_set0{0}, lds_set1{0};
+    int rc = allow_dynamic_lds(lds_set0, reinterpret_cast<const void*>(policy_x3_kernel<false>), 160 * 1024, env->device);
+    if (!rc) rc = allow_dynamic_lds(lds_set1, reinterpret_cast<const void*>(policy_x3_kernel<true>), 160 * 1024, env->device);
+    if (rc) return rc;
+    int dev_cus = 256;
+    if (hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, env->device) != hipSuccess)
+        dev_cus = 256;
+    const int64_t tiles = (env->n + 31) / 32;
+    const int64_t want = (tiles + kPolicyX3Waves - 1) / kPolicyX3Waves;
+    const int grid = (int)(want < dev_cus ? want : dev_cus);
+    PolicyF32Args F{};
+    PolicyArgs& A = F.p;
+    A.world = env->d_world;
+    A.dims = env->dims;
+    A.qimg = reinterpret_cast<const uint4*>(qn->d_img32);
+    A.q = d.q;
+    A.n = env->n;
+    A.env_base = env->env_base;
+    A.seed = env->seed;
+    A.t = t;
+    A.eps = epsilon;
+    A.st = env->st;
+    A.actions = actions;
+    A.q_out = q_out;
+    A.ldq = ldq;
+    if (rec) {
+        A.rec_pos = rec->pos;
+        A.rec_fuel = rec->fuel;
+        A.rec_act = rec->act;
+        A.rec_head = rec->head;
+        A.rec_cap = rec->cap;
+    }
+    if (w3_global) policy_x3_kernel<true><<<grid, kPolicyX3Block, lds, s>>>(F, d);
+    else policy_x3_kernel<false><<<grid, kPolicyX3Block, lds, s>>>(F, d);
+    HIP_TRY(hipGetLastError());
+    return SE_OK;
+}
+
 int launch_policy_f32(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, float* q_out, int64_t ldq,
                       const PolicyRecord* rec, void* stream) {
     if (!qn) return fail(SE_EINVAL, "null qnet");
@@ -948,6 +1259,7 @@ int launch_policy_f32(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t,
     if (!(epsilon >= 0.0)) return fail(SE_EINVAL, "epsilon must be >= 0");
     if (env->n == 0) return SE_OK;
     DeviceGuard g(env->device);
+    if (!qn->f32_mfma) return launch_policy_x3(qn, actions, epsilon, t, q_out, ldq, rec, stream);
     QnetF32Dims d;
     d.q = q_out ? qn->q : qn->qc;  // the compact rows unless every row's Q is wanted
     if (d.bytes() > qn->img32_bytes) {

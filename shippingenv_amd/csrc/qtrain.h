@@ -319,7 +319,7 @@ struct QtStepArgs {
 };
 
 #ifndef SHIPENV_QTRACE
-#define SHIPENV_QTRACE 0  // 1 = diagnostic build: per-wave phase stamps of T1 (tools/qtrain_trace.py)
+#define SHIPENV_QTRACE 0  // 1 = diagnostic build: per-wave phase stamps of T1 (tools/archive/qtrain_trace.py)
 #endif
 #if SHIPENV_QTRACE
 constexpr int kQTraceWg = 1024, kQTraceStamps = 16;

@@ -36,12 +36,12 @@
 #include "philox.h"
 
 #ifndef SHIPENV_TRACE
-#define SHIPENV_TRACE 0  // 1 = diagnostic build: per-wave phase timestamps (tools/wave_trace.py)
+#define SHIPENV_TRACE 0  // 1 = diagnostic build: per-wave phase timestamps (tools/archive/wave_trace.py)
 #endif
 
 #ifndef SHIPENV_ABL4
 // timing-only auto-reset ablations (bits): 1 reset words without Philox, 2 no done
-// list, 4 no episode statistics, 8 no auto-reset at all (tools/build_ablation.sh), 16 the
+// list, 4 no episode statistics, 8 no auto-reset at all (tools/archive/build_ablation.sh), 16 the
 // done list without its records' stores, 32 without its per-segment count stores, 64
 // without the episode-start stamps' loads, 128 without their stores
 #define SHIPENV_ABL4 0
@@ -62,7 +62,7 @@
 #define SHIPENV_STAGE_ORDER 0  // 1 = write the world image to LDS before issuing the group's loads (experiment)
 #endif
 #ifndef SHIPENV_ABLATE
-#define SHIPENV_ABLATE 0  // 0 = the product; 1 = timing-only memory-traffic build, 2 = also no staging (tools/build_ablation.sh, tools/ablate_libs.sh)
+#define SHIPENV_ABLATE 0  // 0 = the product; 1 = timing-only memory-traffic build, 2 = also no staging (tools/archive/build_ablation.sh, tools/archive/ablate_libs.sh)
 #endif
 
 using namespace shipenv;
@@ -77,7 +77,7 @@ constexpr int kStepBlock = SHIPENV_STEP_BLOCK;  // step kernel workgroup (one LD
 constexpr int kEnvsPerThread = 4; // one 4-byte / 16-byte lane access per field
 constexpr int kMaxBlocks = 2048;  // 256 CUs x 8; grid-stride beyond
 // step kernel default workgroup cap (SHIPENV_STEP_BLOCKS overrides): one group of 4 envs per
-// thread up to 2^25 envs. Measured against 2048 (iters = 8 at 2^24; tools/blk_sweep.sh,
+// thread up to 2^25 envs. Measured against 2048 (iters = 8 at 2^24; tools/archive/blk_sweep.sh,
 // profiles/r02h/blk_sweep): 2^24 129 -> 123 us, 2^25 293 -> 253 us, config 4 at 2^24
 // 200 -> 182 us; 2^20 (grid 1024 either way) unchanged
 constexpr int kStepBlocks = 32768;
@@ -942,7 +942,7 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
     const uint32_t t = A.t;
     Pending p[4];
 
-#if SHIPENV_ABLATE  // timing-only build (tools/build_ablation.sh, tools/ablate_libs.sh): memory traffic, no logic or draws
+#if SHIPENV_ABLATE  // timing-only build (tools/archive/build_ablation.sh, tools/archive/ablate_libs.sh): memory traffic, no logic or draws
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         s[j].x ^= ty[j] & 1;

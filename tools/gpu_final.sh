@@ -1,9 +1,9 @@
 #!/bin/bash
-# round-4 evidence on the final code: the GPU suite, smoke(), the driver's bench command twice,
+# the round's evidence on the final code: the GPU suite, smoke(), the driver's bench command twice,
 # its rocprofv3 kernel trace (tools/trace_driver.sh -> kt_legs.json) and the PMC traffic passes
-# (tools/pmc_r04.sh), the size sweep and the update / policy SQ counters, all from one box
+# (tools/pmc_traffic.sh), the size sweep and the update / policy SQ counters, all from one box
 set -u
-TAG=${1:-r04z}
+TAG=${1:-r05z}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu > $OUT/tests_gpu.log 2>&1 || exit $?
@@ -11,7 +11,7 @@ timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smo
 timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_drv.json 2> $OUT/bench_drv.err || exit $?
 timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_drv2.json 2> $OUT/bench_drv2.err || exit $?
 bash tools/trace_driver.sh $TAG || exit $?
-bash tools/pmc_r04.sh $TAG || exit $?
+bash tools/pmc_traffic.sh $TAG || exit $?
 # throughput against N (config 3: 2^14..2^25, config 4: 2^18..2^24), then the SQ counters of the
 # DQN update's kernels and of the bf16 policy kernel (one pass each)
 timeout -k 10 400 python3 tools/size_sweep.py --out $OUT/size_sweep.json > $OUT/size_sweep.log 2>&1 || exit $?

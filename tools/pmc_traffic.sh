@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-4 PMC traffic passes (one counter per pass; FETCH_SIZE and WRITE_SIZE apart, MI355X_MICROARCH
+# PMC traffic passes (one counter per pass; FETCH_SIZE and WRITE_SIZE apart, MI355X_MICROARCH
 # §HBM) for config 3 and config 4 at 2^20 and 2^24 (tools/prof_step.py), then the SQ counters of
 # config 3, into gpurun_out/prof_<tag>/ (tools/summarize_profiles.py condenses it)
 set -u

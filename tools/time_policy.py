@@ -21,6 +21,7 @@ def main():
     p.add_argument("--steps", type=int, default=20, help="policy+step iterations before timing")
     p.add_argument("--eps", type=float, default=0.1)
     p.add_argument("--lib", default=None)
+    p.add_argument("--precision", default="bf16", choices=("bf16", "f32"))
     a = p.parse_args()
     if a.lib:
         from shippingenv_amd import _native
@@ -43,10 +44,11 @@ def main():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for k in range(a.launches):
-        pol.act(a.eps, 1000 + k)
+        pol.act(a.eps, 1000 + k, precision=a.precision)
     e1.record()
     torch.cuda.synchronize()
-    print(json.dumps({"lib": os.path.basename(a.lib or "default"), "n": a.n, "ms_per_launch": round(e0.elapsed_time(e1) / a.launches, 4),
+    print(json.dumps({"lib": os.path.basename(a.lib or "default"), "precision": a.precision,
+                      "f32_mode": os.environ.get("SHIPENV_POLICY_F32", "split-bf16"), "n": a.n, "ms_per_launch": round(e0.elapsed_time(e1) / a.launches, 4),
                       "at_port": float(at.float().mean()), "wave32_with_port": float(waves_any)}))
 
 
