@@ -289,6 +289,22 @@ __device__ __forceinline__ EnvValid env_valid(const LdsWorld& w, const QnetDims&
     return v;
 }
 
+// env_valid from the ship's cell code and the stocks of its first port (read earlier, so
+// the two dependent world reads are in flight during MFMA work)
+__device__ __forceinline__ EnvValid env_valid_from(const LdsWorld& w, const QnetDims& q, const uint64_t* SAME, int code,
+                                                   int2 stock, int origin) {
+    EnvValid v;
+    v.cur = w.port_of_code(code);
+    v.cst = v.cur >= 0 ? min(stock.y, 49) : 0;
+    v.fst = v.cur >= 0 ? min(stock.x, 199) : 0;
+    v.c_lo = q.cargo_row1();
+    v.c_hi = v.c_lo + v.cst - 1;
+    v.f_lo = q.fuel_row1();
+    v.f_hi = v.f_lo + v.fst - 1;
+    v.sel = v.cur >= 0 ? SAME[max(v.cur, 0)] & ~(origin >= 0 ? 1ull << origin : 0ull) : 0ull;
+    return v;
+}
+
 // can any row of tile mt be valid for this env (a tile no env of the wave can choose from
 // is skipped, MFMAs included)
 __device__ __forceinline__ bool tile_maybe(const EnvValid& v, int mt, int P) {
@@ -935,13 +951,20 @@ __global__ __launch_bounds__(256) void qnet_pack_x3_kernel(PackX3Args A) {
     }
 }
 
+// relu as a signed integer max with 0 on the f32 pattern (a non-negative float orders like
+// its int pattern; a negative one, -0 included, becomes +0): one v_max_i32, where fmaxf
+// also canonicalised its operand (two v_max_f32 per element)
+__device__ __forceinline__ float relu_bits(float x) {
+    return __builtin_bit_cast(float, max(__builtin_bit_cast(int, x), 0));
+}
+
 // relu of one 32-row f32 tile, split into the three bf16 B fragments of its two k-steps
 __device__ __forceinline__ void relu_split3(const f32x16& c, bf16x8 (&out)[2][3]) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-            const f32x2 v{fmaxf(c[8 * s + 2 * p], 0.0f), fmaxf(c[8 * s + 2 * p + 1], 0.0f)};
+            const f32x2 v{relu_bits(c[8 * s + 2 * p]), relu_bits(c[8 * s + 2 * p + 1])};
             const bf16x2 a = __builtin_convertvector(v, bf16x2);
             const f32x2 r1 = v - __builtin_convertvector(a, f32x2);
             const bf16x2 b = __builtin_convertvector(r1, bf16x2);
@@ -971,10 +994,113 @@ __device__ __forceinline__ f32x16 kstep_x3(const bf16x8* Wf, int lane, const bf1
     return c;
 }
 
+#ifndef SHIPENV_X3_ABL
+#define SHIPENV_X3_ABL 0  // timing-only ablations of policy_x3_kernel: 1 no epilogue, 2 fc3 tile 0 only,
+                          // 4 no fragment re-reads, 8 no splits
+#endif
+#ifndef SHIPENV_X3_STAGGER
+#define SHIPENV_X3_STAGGER 0  // experiment: waves 4-7 sleep this many x 6400 cycles first
+#endif
+#ifndef SHIPENV_X3_PRIO
+#define SHIPENV_X3_PRIO 0  // experiment: waves 4-7 at issue priority 1
+#endif
+#ifndef SHIPENV_X3_SCHED
+#define SHIPENV_X3_SCHED 1  // 0: the layers in plain order (the scheduler's own interleave)
+#endif
+// chunk q (0..15) of the relu + 3-way split of tile c into out (relu_split3 in 16 pieces of
+// about five VALU): pair q >> 1 (elements 2p, 2p + 1 of k-step s), stage q & 1 (the bf16
+// rounding x0 and the remainder, then x1 and x2); r holds the remainders between stages
+__device__ __forceinline__ void split_chunk(const f32x16& c, bf16x8 (&out)[2][3], f32x2 (&r)[8], int q) {
+    const int pr = q >> 1, s = pr >> 2, p = pr & 3;
+#if SHIPENV_X3_ABL & 8  // timing only: the splits dropped (stage 0 keeps x0 = bf16(c))
+    if (q & 1) return;
+    out[s][0][2 * p] = (__bf16)c[8 * s + 2 * p];
+    out[s][0][2 * p + 1] = (__bf16)c[8 * s + 2 * p + 1];
+    out[s][1] = out[s][2] = out[s][0];
+    return;
+#endif
+    if ((q & 1) == 0) {
+        const f32x2 v{relu_bits(c[8 * s + 2 * p]), relu_bits(c[8 * s + 2 * p + 1])};
+        const bf16x2 a = __builtin_convertvector(v, bf16x2);
+        out[s][0][2 * p] = a[0];
+        out[s][0][2 * p + 1] = a[1];
+        r[pr] = v - __builtin_convertvector(a, f32x2);
+    } else {
+        const bf16x2 b = __builtin_convertvector(r[pr], bf16x2);
+        const bf16x2 e = __builtin_convertvector(r[pr] - __builtin_convertvector(b, f32x2), bf16x2);
+        out[s][1][2 * p] = b[0];
+        out[s][1][2 * p + 1] = b[1];
+        out[s][2][2 * p] = e[0];
+        out[s][2][2 * p + 1] = e[1];
+    }
+}
+
+// the three part fragments of fragment f (image order [f][part][lane])
+__device__ __forceinline__ void x3_frags(const bf16x8* W, int f, int lane, bf16x8 (&wf)[3]) {
+#if SHIPENV_X3_ABL & 4  // timing only: fragment reads after the first k-step dropped
+    if (f != 0) return;
+#endif
+    wf[0] = W[f * 192 + lane];
+    wf[1] = W[f * 192 + 64 + lane];
+    wf[2] = W[f * 192 + 128 + lane];
+}
+
+// half of one k-step's six part products, in kstep_x3's order
+__device__ __forceinline__ f32x16 khalf_x3(const bf16x8 (&w)[3], const bf16x8 (&x)[3], f32x16 c, int half) {
+    if (half == 0) {
+        c = mfma_bf16(w[0], x[2], c);
+        c = mfma_bf16(w[1], x[1], c);
+        c = mfma_bf16(w[2], x[0], c);
+    } else {
+        c = mfma_bf16(w[0], x[1], c);
+        c = mfma_bf16(w[1], x[0], c);
+        c = mfma_bf16(w[0], x[0], c);
+    }
+    return c;
+}
+
+// bias rows of a fc3 tile, -inf where bit (reg & 3) + 8 (reg >> 2) of m is clear (the row
+// is invalid for this env): its Q stays -inf through the MFMAs and never wins the argmax
+__device__ __forceinline__ f32x16 masked_bias(const float* b, uint32_t m) {
+    f32x16 c = bias_frag(b);
+    uint32_t x = m & 0x0f0f0f0fu;  // register reg's bit to bit reg
+    x = (x | (x >> 4)) & 0x00ff00ffu;
+    x = (x | (x >> 8)) & 0x0000ffffu;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) c[reg] = ((x >> reg) & 1u) ? c[reg] : -INFINITY;
+    return c;
+}
+
+// the first maximum over registers 4j..4j+3 of a masked tile (invalid rows are -inf), the
+// row recorded without the lane half's 4h (added once at the end): one compare and two
+// selects per register, no validity test and no per-register branch
+__device__ __forceinline__ void argmax_masked_part(const f32x16& c, int base, float& best, int& bidx, int j) {
+#pragma unroll
+    for (int reg = 4 * j; reg < 4 * j + 4; ++reg) {
+        const bool better = c[reg] > best;
+        best = better ? c[reg] : best;
+        bidx = better ? base + (reg & 3) + 8 * (reg >> 2) : bidx;
+    }
+}
+
+// tile_argmax over registers 4j..4j+3 only (j = 0..3 in order is tile_argmax)
+__device__ __forceinline__ void tile_argmax_part(const f32x16& c, uint32_t m, uint32_t rm, int base, int h,
+                                                 float& best, int& bidx, int j) {
+    m >>= 4 * h;
+#pragma unroll
+    for (int reg = 4 * j; reg < 4 * j + 4; ++reg) {
+        if (!((rm >> reg) & 1u)) continue;
+        const int i = (reg & 3) + 8 * (reg >> 2);
+        const bool better = ((m >> i) & 1u) && c[reg] > best;
+        best = better ? c[reg] : best;
+        bidx = better ? base + 4 * h + i : bidx;
+    }
+}
+
 constexpr int kPolicyX3Block = 512;
 constexpr int kPolicyX3Waves = kPolicyX3Block / 64;
 
-template <bool kW3Global>
+template <bool kW3Global, bool kQout = false>
 __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args F, QnetX3Dims D) {
     extern __shared__ uint4 smem[];
     const PolicyArgs& A = F.p;
@@ -1009,6 +1135,17 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
         return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei]};
     };
     int64_t tile = (int64_t)blockIdx.x * kPolicyX3Waves + (threadIdx.x >> 6);
+#if SHIPENV_X3_PRIO
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
+#if SHIPENV_X3_STAGGER
+    // waves 4-7 (each SIMD's second wave) start later, so the two waves' VALU-only
+    // stretches (the per-tile epilogue) fall beside the partner's MFMA phases
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4) {
+#pragma unroll
+        for (int i = 0; i < SHIPENV_X3_STAGGER; ++i) __builtin_amdgcn_s_sleep(100);
+    }
+#endif
     EnvIn nxt = load_env(tile < tiles ? tile : 0);
     EnvValid vnxt = env_valid(w, q, SAME, (int)nxt.x8, (int)nxt.y8, nxt.o8 == SE_NONE ? -1 : (int)nxt.o8);
     for (; tile < tiles; tile += stride) {
@@ -1024,6 +1161,132 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
         const float ff = (float)fuel;  // the preprocess_state row as torch's FloatTensor holds it
         const float in0 = h ? (float)y8 : (float)x8, in2 = h ? (float)dest : (float)origin;
         bf16x8 X1[4][2][3], X2[4][2][3];
+        float best = -INFINITY;
+        int bidx = 0x7fffffff;
+#if SHIPENV_X3_SCHED
+        // The same arithmetic, hand-interleaved: the MFMAs go in groups of three (half a
+        // k-step), and beside each group, fenced by sched_barrier so the compiler cannot
+        // cluster them again, about five VALU of work that does not feed those MFMAs (a
+        // chunk of a split of the layer's other tiles, or of the previous fc3 tile's
+        // argmax). A wave's VALU then issues while its own MFMAs occupy the matrix pipe
+        // (32 cycles each) instead of between MFMA phases. fc2 runs k-tile by k-tile over
+        // its four row tiles (four accumulators), so k-tile kt + 1 is split during k-tile kt;
+        // its last k-tile runs row tile by row tile, so the finished row tiles split beside
+        // the rest; fc3's first tile splits fc2's last one. Fragments are read one k-step
+        // ahead. Bit-identical to the plain order (the same operations on the same values).
+        f32x2 rs[8];
+        f32x16 c1[4], acc[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {  // fc1 on f32 MFMA (x, y | fuel, fuel | origin, dest)
+            c1[mt] = bias_frag(B1 + mt * 32 + 4 * h);
+            c1[mt] = mfma32(W1[(mt * 3 + 0) * 64 + lane], in0, c1[mt]);
+            c1[mt] = mfma32(W1[(mt * 3 + 1) * 64 + lane], ff, c1[mt]);
+            c1[mt] = mfma32(W1[(mt * 3 + 2) * 64 + lane], in2, c1[mt]);
+            if (mt == 0) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[i] = bias_frag(B2 + i * 32 + 4 * h);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 6; ++j)
+                    if ((mt - 1) * 6 + j < 16) split_chunk(c1[0], X1[0], rs, (mt - 1) * 6 + j);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        bf16x8 wf[2][3];
+        x3_frags(W2, 0, lane, wf[0]);
+        // the next tile's two dependent world reads (its cell code, then that port's stocks)
+        // go out during fc2, so their round trips overlap the MFMAs
+        int ncode = 0;
+        int2 nstock = make_int2(0, 0);
+        // fc2: 32 k-steps (k-tile kt, row tile mt, step s2), 64 groups
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            const int kt = i >> 3, mt = (i >> 1) & 3, s2 = i & 1;
+            if (i == 4 && more) ncode = w.code((int)nxt.x8, (int)nxt.y8);
+            if (i == 20 && more) nstock = w.stock[max(w.port_of_code(ncode), 0)];
+            if (i + 1 < 32) {
+                const int nk = (i + 1) >> 3, nm = ((i + 1) >> 1) & 3, ns = (i + 1) & 1;
+                x3_frags(W2, (nm * 4 + nk) * 2 + ns, lane, wf[(i + 1) & 1]);
+            } else {
+                x3_frags(W3, 0, lane, wf[0]);  // fc3 tile 0, k-step 0
+            }
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                acc[mt] = khalf_x3(wf[i & 1], X1[kt][s2], acc[mt], half);
+                const int g = 2 * (i & 7) + half;  // group within the k-tile, 0..15
+                if (kt < 3) {
+                    split_chunk(c1[kt + 1], X1[kt + 1], rs, g);
+                } else if (mt > 0) {  // the previous row tile's split, 4 chunks per group
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) split_chunk(acc[mt - 1], X2[mt - 1], rs, 4 * (g - 4 * mt) + j);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        // fc3 tile 0 (the moves: every env can choose from it), fc2's last row tile split
+        // beside its first 12 groups (done before k-step 6 reads it). Without q_out, a row
+        // no action of this env can take starts at -inf (masked_bias), so the argmax needs
+        // no validity test and never picks it.
+        f32x16 c = kQout ? bias_frag(B3 + 4 * h) : masked_bias(B3 + 4 * h, tile_mask(v, 0, P) >> (4 * h));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k + 1 < 8) x3_frags(W3, k + 1, lane, wf[(k + 1) & 1]);
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                c = khalf_x3(wf[k & 1], X2[k >> 1][k & 1], c, half);
+                const int g = 2 * k + half;
+                if (g < 4) {
+                    split_chunk(acc[3], X2[3], rs, 2 * g);
+                    split_chunk(acc[3], X2[3], rs, 2 * g + 1);
+                } else if (g < 12) {
+                    split_chunk(acc[3], X2[3], rs, g + 4);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        // the next tile's validity from the world reads issued during fc2 (ncode, nstock)
+        if (more) vnxt = env_valid_from(w, q, SAME, ncode, nstock, nxt.o8 == SE_NONE ? -1 : (int)nxt.o8);
+        // fc3 tiles 1..: the previous tile's argmax beside each chain, 4 registers a group
+        int pbase = 0;
+        uint32_t pm = tile_mask(v, 0, P), prm = __builtin_amdgcn_readfirstlane(REGM[0]);
+        if (kQout && live) tile_q_out(A.q_out, A.ldq, q.rows, c, e, 0, h);
+#pragma nounroll
+        for (int mt = 1; mt < ((SHIPENV_X3_ABL & 2) ? 1 : q.mt3); ++mt) {  // (ABL & 2: timing only, fc3 tile 0 alone)
+            const int base = mt * 32;
+            if (!kQout && !__any(tile_maybe(v, mt, P))) continue;
+            const bf16x8* W3t = W3 + mt * 8 * 192;
+            f32x16 c3 = kQout ? bias_frag(B3 + mt * 32 + 4 * h)
+                              : masked_bias(B3 + mt * 32 + 4 * h, tile_mask(v, mt, P) >> (4 * h));
+            x3_frags(W3t, 0, lane, wf[0]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (k + 1 < 8) x3_frags(W3t, k + 1, lane, wf[(k + 1) & 1]);
+#pragma unroll
+                for (int half = 0; half < 2; ++half) {
+                    c3 = khalf_x3(wf[k & 1], X2[k >> 1][k & 1], c3, half);
+                    const int g = 2 * k + half;
+                    if (g < 4) {
+                        if (kQout) tile_argmax_part(c, pm, prm, pbase, h, best, bidx, g);
+                        else argmax_masked_part(c, pbase, best, bidx, g);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            c = c3;
+            pbase = base;
+            pm = tile_mask(v, mt, P);
+            prm = __builtin_amdgcn_readfirstlane(REGM[mt]);
+            if (kQout && live) tile_q_out(A.q_out, A.ldq, q.rows, c, e, base, h);
+        }
+        if (kQout) {
+            tile_argmax(c, pm, prm, pbase, h, best, bidx);
+        } else {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) argmax_masked_part(c, pbase, best, bidx, g);
+            bidx += bidx == 0x7fffffff ? 0 : 4 * h;  // the lane half's rows (argmax_masked_part omits 4h)
+        }
+#else
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {  // fc1 on f32 MFMA (x, y | fuel, fuel | origin, dest), relu, split
             f32x16 c = bias_frag(B1 + mt * 32 + 4 * h);
@@ -1040,8 +1303,6 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
             relu_split3(c, X2[mt]);
         }
         if (more) vnxt = env_valid(w, q, SAME, (int)nxt.x8, (int)nxt.y8, nxt.o8 == SE_NONE ? -1 : (int)nxt.o8);
-        float best = -INFINITY;
-        int bidx = 0x7fffffff;
 #pragma nounroll
         for (int mt = 0; mt < q.mt3; ++mt) {  // fc3 + the masked first-maximum argmax
             const int base = mt * 32;
@@ -1054,7 +1315,12 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
             tile_argmax(c, m, rm, base, h, best, bidx);
             if (A.q_out && live) tile_q_out(A.q_out, A.ldq, q.rows, c, e, base, h);
         }
+#endif
+#if SHIPENV_X3_ABL & 1  // timing only: no epilogue (the chosen row stored as the action)
+        if (h == 0 && live) A.actions[e] = bidx;
+#else
         FINISH_ENV(v, e, live, h, best, bidx, x8, y8, o8, d8, ff);
+#endif
     }
 }
 
@@ -1208,8 +1474,10 @@ int launch_policy_x3(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, 
     const size_t lds = (size_t)(w3_global ? d.w3() : d.bytes());
     if (lds > 160 * 1024) return fail(SE_EINVAL, "split-bf16 network exceeds the 160 KB LDS");
     static std::atomic<uint64_t> lds_set0{0}, lds_set1{0};
+    static std::atomic<uint64_t> lds_set2{0};
     int rc = allow_dynamic_lds(lds_set0, reinterpret_cast<const void*>(policy_x3_kernel<false>), 160 * 1024, env->device);
     if (!rc) rc = allow_dynamic_lds(lds_set1, reinterpret_cast<const void*>(policy_x3_kernel<true>), 160 * 1024, env->device);
+    if (!rc) rc = allow_dynamic_lds(lds_set2, reinterpret_cast<const void*>(policy_x3_kernel<true, true>), 160 * 1024, env->device);
     if (rc) return rc;
     int dev_cus = 256;
     if (hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, env->device) != hipSuccess)
@@ -1239,8 +1507,14 @@ int launch_policy_x3(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, 
         A.rec_head = rec->head;
         A.rec_cap = rec->cap;
     }
-    if (w3_global) policy_x3_kernel<true><<<grid, kPolicyX3Block, lds, s>>>(F, d);
-    else policy_x3_kernel<false><<<grid, kPolicyX3Block, lds, s>>>(F, d);
+    if (q_out) {  // the full layout (fc3 from global memory): unmasked Q rows for q_out
+        if (!w3_global) return fail(SE_EINVAL, "q_out: the full fc3 layout is expected in global memory");
+        policy_x3_kernel<true, true><<<grid, kPolicyX3Block, lds, s>>>(F, d);
+    } else if (w3_global) {
+        policy_x3_kernel<true><<<grid, kPolicyX3Block, lds, s>>>(F, d);
+    } else {
+        policy_x3_kernel<false><<<grid, kPolicyX3Block, lds, s>>>(F, d);
+    }
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }

@@ -6,8 +6,8 @@ in torch. ``QPolicy`` packs its weights for the fused kernel (bf16 MFMA, f32
 accumulation), which computes for every env of a VecEnv the observation row,
 Q = DQNNetwork(obs), the first maximum over the valid actions and epsilon-greedy
 exploration (choose_action, :177-203) in one launch, without writing Q to HBM.
-``act(precision="f32")`` runs the same step with the network in fp32 (f32 MFMA), the
-precision the reference's agent evaluates it in.
+``act(precision="f32")`` runs the same step with the network in fp32 (bf16 MFMA on
+3-way operand splits, or f32 MFMA), the precision the reference's agent evaluates it in.
 """
 from __future__ import annotations
 
@@ -88,7 +88,9 @@ class QPolicy:
         q_out: optional f32 [n, >= A] to receive the Q rows (testing / inspection).
         precision: "bf16" (se_policy: bf16 weights and activations on bf16 MFMA, f32
         accumulation) or "f32" (se_policy_f32: the network in fp32 as agents/dqn.py runs
-        it, on f32 MFMA; about 6x the time)."""
+        it; fc2 and fc3 on bf16 MFMA with every f32 operand split into three bf16 parts,
+        about 4x the bf16 policy's time; SHIPENV_POLICY_F32=mfma at QPolicy creation selects
+        the f32-MFMA kernel instead)."""
         if precision not in ("bf16", "f32"):
             raise ValueError("precision must be 'bf16' or 'f32'")
         fn = N.lib().se_policy if precision == "bf16" else N.lib().se_policy_f32

@@ -1,5 +1,5 @@
 set -u
-O=gpurun_out/r05f; mkdir -p $O
+O=gpurun_out/${1:-r05f}; mkdir -p $O
 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_policy.py > $O/tests_policy.log 2>&1; rc=$?
 tail -30 $O/tests_policy.log
 for r in 1 2; do
