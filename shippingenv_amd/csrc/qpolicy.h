@@ -998,6 +998,9 @@ __device__ __forceinline__ f32x16 kstep_x3(const bf16x8* Wf, int lane, const bf1
 #define SHIPENV_X3_ABL 0  // timing-only ablations of policy_x3_kernel: 1 no epilogue, 2 fc3 tile 0 only,
                           // 4 no fragment re-reads, 8 no splits
 #endif
+#ifndef SHIPENV_X3_LOOKAHEAD
+#define SHIPENV_X3_LOOKAHEAD 2  // k-steps ahead that fc2 / fc3's fragments are read
+#endif
 #ifndef SHIPENV_X3_STAGGER
 #define SHIPENV_X3_STAGGER 0  // experiment: waves 4-7 sleep this many x 6400 cycles first
 #endif
@@ -1033,6 +1036,29 @@ __device__ __forceinline__ void split_chunk(const f32x16& c, bf16x8 (&out)[2][3]
         out[s][2][2 * p] = e[0];
         out[s][2][2 * p + 1] = e[1];
     }
+}
+
+// pair q (0..7) of the relu + 3-way split of tile c into out: elements 2p, 2p + 1 of
+// k-step s (q = 4s + p), both stages (relu_split3 in 8 pieces of about 11 VALU)
+__device__ __forceinline__ void split_pair(const f32x16& c, bf16x8 (&out)[2][3], int q) {
+    const int s = q >> 2, p = q & 3;
+#if SHIPENV_X3_ABL & 8  // timing only: the splits dropped (x0 = bf16(c) for every part)
+    out[s][0][2 * p] = (__bf16)c[8 * s + 2 * p];
+    out[s][0][2 * p + 1] = (__bf16)c[8 * s + 2 * p + 1];
+    if (p == 3) out[s][1] = out[s][2] = out[s][0];
+    return;
+#endif
+    const f32x2 v{relu_bits(c[8 * s + 2 * p]), relu_bits(c[8 * s + 2 * p + 1])};
+    const bf16x2 a = __builtin_convertvector(v, bf16x2);
+    const f32x2 r1 = v - __builtin_convertvector(a, f32x2);
+    const bf16x2 b = __builtin_convertvector(r1, bf16x2);
+    const bf16x2 e = __builtin_convertvector(r1 - __builtin_convertvector(b, f32x2), bf16x2);
+    out[s][0][2 * p] = a[0];
+    out[s][0][2 * p + 1] = a[1];
+    out[s][1][2 * p] = b[0];
+    out[s][1][2 * p + 1] = b[1];
+    out[s][2][2 * p] = e[0];
+    out[s][2][2 * p + 1] = e[1];
 }
 
 // the three part fragments of fragment f (image order [f][part][lane])
@@ -1174,7 +1200,6 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
         // its last k-tile runs row tile by row tile, so the finished row tiles split beside
         // the rest; fc3's first tile splits fc2's last one. Fragments are read one k-step
         // ahead. Bit-identical to the plain order (the same operations on the same values).
-        f32x2 rs[8];
         f32x16 c1[4], acc[4];
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {  // fc1 on f32 MFMA (x, y | fuel, fuel | origin, dest)
@@ -1185,62 +1210,59 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
             if (mt == 0) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) acc[i] = bias_frag(B2 + i * 32 + 4 * h);
-            } else {
+            } else {  // X1[0]'s 8 pairs beside fc1's other row tiles: 3, 3, 2
 #pragma unroll
-                for (int j = 0; j < 6; ++j)
-                    if ((mt - 1) * 6 + j < 16) split_chunk(c1[0], X1[0], rs, (mt - 1) * 6 + j);
+                for (int j = 0; j < 3; ++j)
+                    if ((mt - 1) * 3 + j < 8) split_pair(c1[0], X1[0], (mt - 1) * 3 + j);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
-        bf16x8 wf[2][3];
-        x3_frags(W2, 0, lane, wf[0]);
+        // fragments read kLa k-steps ahead over the flat k-step sequence: fc2's 32 (k-tile
+        // kt, row tile mt, step s2), then fc3 tile 0's 8
+        constexpr int kLa = SHIPENV_X3_LOOKAHEAD;
+        bf16x8 wf[kLa + 1][3];
+        auto frag_of = [&](int j, bf16x8 (&dst)[3]) {
+            if (j < 32) x3_frags(W2, (((j >> 1) & 3) * 4 + (j >> 3)) * 2 + (j & 1), lane, dst);
+            else x3_frags(W3, j - 32, lane, dst);
+        };
+#pragma unroll
+        for (int j = 0; j < kLa; ++j) frag_of(j, wf[j]);
         // the next tile's two dependent world reads (its cell code, then that port's stocks)
         // go out during fc2, so their round trips overlap the MFMAs
         int ncode = 0;
         int2 nstock = make_int2(0, 0);
-        // fc2: 32 k-steps (k-tile kt, row tile mt, step s2), 64 groups
 #pragma unroll
         for (int i = 0; i < 32; ++i) {
             const int kt = i >> 3, mt = (i >> 1) & 3, s2 = i & 1;
             if (i == 4 && more) ncode = w.code((int)nxt.x8, (int)nxt.y8);
             if (i == 20 && more) nstock = w.stock[max(w.port_of_code(ncode), 0)];
-            if (i + 1 < 32) {
-                const int nk = (i + 1) >> 3, nm = ((i + 1) >> 1) & 3, ns = (i + 1) & 1;
-                x3_frags(W2, (nm * 4 + nk) * 2 + ns, lane, wf[(i + 1) & 1]);
-            } else {
-                x3_frags(W3, 0, lane, wf[0]);  // fc3 tile 0, k-step 0
-            }
+            frag_of(i + kLa, wf[(i + kLa) % (kLa + 1)]);
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
-                acc[mt] = khalf_x3(wf[i & 1], X1[kt][s2], acc[mt], half);
+                acc[mt] = khalf_x3(wf[i % (kLa + 1)], X1[kt][s2], acc[mt], half);
                 const int g = 2 * (i & 7) + half;  // group within the k-tile, 0..15
                 if (kt < 3) {
-                    split_chunk(c1[kt + 1], X1[kt + 1], rs, g);
-                } else if (mt > 0) {  // the previous row tile's split, 4 chunks per group
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) split_chunk(acc[mt - 1], X2[mt - 1], rs, 4 * (g - 4 * mt) + j);
+                    if (half == 0) split_pair(c1[kt + 1], X1[kt + 1], g >> 1);  // 8 pairs over 16 groups
+                } else if (mt > 0) {  // the previous row tile's 8 pairs over this row tile's 4 groups
+                    split_pair(acc[mt - 1], X2[mt - 1], 2 * (g - 4 * mt));
+                    split_pair(acc[mt - 1], X2[mt - 1], 2 * (g - 4 * mt) + 1);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
         // fc3 tile 0 (the moves: every env can choose from it), fc2's last row tile split
-        // beside its first 12 groups (done before k-step 6 reads it). Without q_out, a row
+        // beside its first 8 groups (done before k-step 6 reads it). Without q_out, a row
         // no action of this env can take starts at -inf (masked_bias), so the argmax needs
         // no validity test and never picks it.
         f32x16 c = kQout ? bias_frag(B3 + 4 * h) : masked_bias(B3 + 4 * h, tile_mask(v, 0, P) >> (4 * h));
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            if (k + 1 < 8) x3_frags(W3, k + 1, lane, wf[(k + 1) & 1]);
+            if (32 + k + kLa < 40) frag_of(32 + k + kLa, wf[(32 + k + kLa) % (kLa + 1)]);
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
-                c = khalf_x3(wf[k & 1], X2[k >> 1][k & 1], c, half);
+                c = khalf_x3(wf[(32 + k) % (kLa + 1)], X2[k >> 1][k & 1], c, half);
                 const int g = 2 * k + half;
-                if (g < 4) {
-                    split_chunk(acc[3], X2[3], rs, 2 * g);
-                    split_chunk(acc[3], X2[3], rs, 2 * g + 1);
-                } else if (g < 12) {
-                    split_chunk(acc[3], X2[3], rs, g + 4);
-                }
+                if (g < 8) split_pair(acc[3], X2[3], g);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -1257,14 +1279,15 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
             const bf16x8* W3t = W3 + mt * 8 * 192;
             f32x16 c3 = kQout ? bias_frag(B3 + mt * 32 + 4 * h)
                               : masked_bias(B3 + mt * 32 + 4 * h, tile_mask(v, mt, P) >> (4 * h));
-            x3_frags(W3t, 0, lane, wf[0]);
+#pragma unroll
+            for (int j = 0; j < kLa; ++j) x3_frags(W3t, j, lane, wf[j]);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                if (k + 1 < 8) x3_frags(W3t, k + 1, lane, wf[(k + 1) & 1]);
+                if (k + kLa < 8) x3_frags(W3t, k + kLa, lane, wf[(k + kLa) % (kLa + 1)]);
 #pragma unroll
                 for (int half = 0; half < 2; ++half) {
-                    c3 = khalf_x3(wf[k & 1], X2[k >> 1][k & 1], c3, half);
+                    c3 = khalf_x3(wf[k % (kLa + 1)], X2[k >> 1][k & 1], c3, half);
                     const int g = 2 * k + half;
                     if (g < 4) {
                         if (kQout) tile_argmax_part(c, pm, prm, pbase, h, best, bidx, g);
