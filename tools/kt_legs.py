@@ -15,12 +15,14 @@ next dispatches of that leg's kernel instantiation in the trace:
              after its P pre-roll steps (--preroll4, bench.py's default 1000)
   large_n    step_kernel<false, false, false, false, false, false> (N = 2^24): the from-reset leg's
              105 launches, then the steady leg's P3 pre-roll steps and its 105 (the last)
-  large_n config 4: the auto-reset kernel's last 105 launches (2^24, after its pre-roll)
+  large_n config 4: the auto-reset kernel's last 105 launches (2^24, after its pre-roll); since
+             round 5 that is the nontemporal-load instantiation (C4NT)
 For each leg this prints the average kernel duration (end - start of the dispatch, as
 rocprofv3 records it) over the K timed launches, over the timed launches after the
 first, the per-launch list, the idle gaps between consecutive timed launches and
 (end of launch K - end of launch 1) / (K - 1), the span bench.py's events measure; with --bench, the bench line's own kernel_ms and frac
-beside the figure recomputed from the trace (42 / 58 B per env-step over 8 TB/s).
+beside the figure recomputed from the trace (42 / 50 B per env-step over 8 TB/s; config 4 was 58 B
+before round 5's episode-start stamps).
 """
 from __future__ import annotations
 
@@ -31,6 +33,7 @@ import json
 C3 = "step_kernel<false, false, false, true, false, false>"
 C3S = "step_kernel<false, false, false, true, false, true>"
 C4 = "step_kernel<false, false, true, false, false, false>"
+C4NT = "step_kernel<false, false, true, true, false, false>"  # auto-reset with nontemporal loads (N > 2^21, round 5)
 BIG = "step_kernel<false, false, false, false, false, false>"
 PEAK = 8000.0
 
@@ -87,13 +90,13 @@ def main():
            "large_n_from_reset": leg(rows, BIG, 0, 2 * 105 + a.preroll3, 100, from_end=True, head=105),
            "large_n": leg(rows, BIG, 0, 105, 100, from_end=True),
            "config3_literal": leg(rows, C3S, W + K, 10 + 1000, 1000),
-           "large_n_config4": leg(rows, C4, 0, 105, 100, from_end=True)}
-    for key, b in (("config3", 42), ("config3_from_reset", 42), ("config3_step_py", 42), ("config4", 58),
+           "large_n_config4": leg(rows, C4NT, 0, 105, 100, from_end=True)}
+    for key, b in (("config3", 42), ("config3_from_reset", 42), ("config3_step_py", 42), ("config4", 50),
                    ("config3_literal", 42)):
         if out[key]:
             us = out[key]["avg_us_timed"]
             out[key]["frac_from_trace"] = round(b * a.n / (us * 1e-6) / 1e9 / PEAK, 4)
-    for key, b in (("large_n_from_reset", 42), ("large_n", 42), ("large_n_config4", 58)):
+    for key, b in (("large_n_from_reset", 42), ("large_n", 42), ("large_n_config4", 50)):
         if out[key]:
             us = out[key]["avg_us_timed"]
             out[key]["frac_from_trace"] = round(b * (1 << 24) / (us * 1e-6) / 1e9 / PEAK, 4)

@@ -4,7 +4,7 @@
 
 For each (N, config): K back-to-back se_step launches over action rows resident in HBM
 (the bench's synthetic agent), timed by wall clock between synchronizes, as bench.py
-does. frac = algorithmic bytes (42 B per env-step for config 3, 58 B for config 4;
+does. frac = algorithmic bytes (42 B per env-step for config 3, 50 B for config 4 (58 before round 5);
 DESIGN.md section 3) x N / time per step / 8 TB/s. It shows the regimes of DESIGN.md
 section 5: launch-bound below ~2^18, VALU-issue- and launch-bound while the working
 set sits in the 256 MiB Infinity Cache (N <= 2^21), HBM-bound beyond.
@@ -20,7 +20,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-BYTES = {3: 42, 4: 58}
+BYTES = {3: 42, 4: 50}
 PEAK = 8000.0  # GB/s, MI355X HBM3E
 
 
