@@ -340,6 +340,30 @@ __device__ __forceinline__ void tile_argmax(const f32x16& c, uint32_t m, uint32_
     }
 }
 
+// bias rows of a fc3 tile, -inf where bit (reg & 3) + 8 (reg >> 2) of m is clear (the row
+// is invalid for this env): its Q stays -inf through the MFMAs and never wins the argmax
+__device__ __forceinline__ f32x16 masked_bias(const float* b, uint32_t m) {
+    f32x16 c = bias_frag(b);
+    uint32_t x = m & 0x0f0f0f0fu;  // register reg's bit to bit reg
+    x = (x | (x >> 4)) & 0x00ff00ffu;
+    x = (x | (x >> 8)) & 0x0000ffffu;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) c[reg] = ((x >> reg) & 1u) ? c[reg] : -INFINITY;
+    return c;
+}
+
+// the first maximum over registers 4j..4j+3 of a masked tile (invalid rows are -inf), the
+// row recorded without the lane half's 4h (added once at the end): one compare and two
+// selects per register, no validity test and no per-register branch
+__device__ __forceinline__ void argmax_masked_part(const f32x16& c, int base, float& best, int& bidx, int j) {
+#pragma unroll
+    for (int reg = 4 * j; reg < 4 * j + 4; ++reg) {
+        const bool better = c[reg] > best;
+        best = better ? c[reg] : best;
+        bidx = better ? base + (reg & 3) + 8 * (reg >> 2) : bidx;
+    }
+}
+
 __device__ __forceinline__ void tile_q_out(float* q_out, int64_t ldq, int rows, const f32x16& c, int64_t e, int base,
                                            int h) {
 #pragma unroll
@@ -397,6 +421,10 @@ __device__ __forceinline__ void finish_env(const QnetDims& q, const EnvValid& v,
     }
 }
 
+#ifndef SHIPENV_POLICY_MASKED
+#define SHIPENV_POLICY_MASKED 1  // 0: the round-4 epilogue (per-register validity tests and skips)
+#endif
+template <bool kQout>
 __global__ __launch_bounds__(kPolicyBlock)
 #if SHIPENV_POLICY_WAVES_PER_EU
 __attribute__((amdgpu_waves_per_eu(SHIPENV_POLICY_WAVES_PER_EU)))
@@ -542,7 +570,7 @@ void policy_kernel(PolicyArgs A) {
             const bool maybe = (mt == 0) | ((cur >= 0) & (base < 4 + P)) |
                                ((cst > 0) & (c_lo <= top) & (c_hi >= base)) |
                                ((fst > 0) & (f_lo <= top) & (f_hi >= base));
-            if (!A.q_out && !__any(maybe)) continue;
+            if (!kQout && !__any(maybe)) continue;
             uint32_t m = range_bits(-base, 3 - base) | range_bits(c_lo - base, c_hi - base) |
                          range_bits(f_lo - base, f_hi - base);
             if (base < 4 + P) {  // SELECT rows 4 + p live in this tile (uniform): sel shifted by 4 - base
@@ -554,7 +582,10 @@ void policy_kernel(PolicyArgs A) {
             bf16x8 wf[8];  // the tile's 8 fragments, read before the chain consumes them
 #pragma unroll
             for (int k = 0; k < 8; ++k) wf[k] = W3f[(mt * 8 + k) * 64 + lane];
-            f32x16 c = bias_frag(B3 + mt * 32 + 4 * h);
+            // without q_out (round 5): rows this env cannot take start at -inf (masked_bias), so
+            // the first maximum below needs no validity test and no per-register branch
+            constexpr bool kMasked = !kQout && SHIPENV_POLICY_MASKED;
+            f32x16 c = kMasked ? masked_bias(B3 + mt * 32 + 4 * h, m >> (4 * h)) : bias_frag(B3 + mt * 32 + 4 * h);
 #pragma unroll
             for (int k = 0; k < 8; ++k)
                 c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k], h2[k >> 1][k & 1], c, 0, 0, 0);
@@ -565,16 +596,21 @@ void policy_kernel(PolicyArgs A) {
             for (int reg = 0; reg < 16; ++reg) best = fmaxf(best, c[reg]);
             bidx = base;
 #else
+            if constexpr (kMasked) {
 #pragma unroll
-            for (int reg = 0; reg < 16; ++reg) {
-                if (!((rm >> reg) & 1u)) continue;
-                const int i = (reg & 3) + 8 * (reg >> 2);
-                const bool better = ((m >> i) & 1u) && c[reg] > best;  // ascending rows: first max
-                best = better ? c[reg] : best;
-                bidx = better ? base + 4 * h + i : bidx;
+                for (int j = 0; j < 4; ++j) argmax_masked_part(c, base, best, bidx, j);  // rows without 4h
+            } else {
+#pragma unroll
+                for (int reg = 0; reg < 16; ++reg) {
+                    if (!((rm >> reg) & 1u)) continue;
+                    const int i = (reg & 3) + 8 * (reg >> 2);
+                    const bool better = ((m >> i) & 1u) && c[reg] > best;  // ascending rows: first max
+                    best = better ? c[reg] : best;
+                    bidx = better ? base + 4 * h + i : bidx;
+                }
             }
 #endif
-            if (A.q_out && live) {
+            if (kQout && live) {
 #pragma unroll
                 for (int reg = 0; reg < 16; ++reg) {  // the full layout: row = action
                     const int row = base + 4 * h + (reg & 3) + 8 * (reg >> 2);
@@ -582,6 +618,7 @@ void policy_kernel(PolicyArgs A) {
                 }
             }
         }
+        if (!kQout && SHIPENV_POLICY_MASKED) bidx += bidx == 0x7fffffff ? 0 : 4 * h;  // the lane half's rows
         // the two lane halves hold the same env: larger value, then lower index
         const float ob2 = __shfl_xor(best, 32);
         const int oi = __shfl_xor(bidx, 32);
@@ -842,10 +879,13 @@ __global__ __launch_bounds__(kPolicyF32Block) void policy_f32_kernel(PolicyF32Ar
 // parts. Image: the f32 image's fc1 and biases, fc2 and fc3 as three bf16 fragments per
 // (tile, kt, s): 96 KB + 24 KB per fc3 tile, so the world is read in place (L2), not
 // staged, and fc3 comes from global memory when it does not fit (the full layout).
+#ifndef SHIPENV_X3_FC1
+#define SHIPENV_X3_FC1 1  // 1: fc1 as two split-bf16 MFMAs per row tile (x3_fc1_slot); 0: f32 MFMA
+#endif
 struct QnetX3Dims {
     QnetDims q;
-    __host__ __device__ int w1() const { return 0; }                    // f32 fc1, as QnetF32Dims (3 KB)
-    __host__ __device__ int w2() const { return 4096; }                 // [mt][kt][s][part] bf16 fragments: 96 KB
+    __host__ __device__ int w1() const { return 0; }  // fc1: bf16 fragments [mt][2 steps][lane] (8 KB), or f32 (3 KB)
+    __host__ __device__ int w2() const { return 8192; }                 // [mt][kt][s][part] bf16 fragments: 96 KB
     __host__ __device__ int b1() const { return w2() + 96 * 1024; }
     __host__ __device__ int b2() const { return b1() + 4 * kQHidden; }
     __host__ __device__ int b3() const { return b2() + 4 * kQHidden; }  // mt3 * 32 f32
@@ -863,6 +903,22 @@ __device__ __forceinline__ void split3(float v, __bf16& p0, __bf16& p1, __bf16& 
     p2 = (__bf16)(r1 - (float)p1);
 }
 
+// fc1 on bf16 MFMA (SHIPENV_X3_FC1): the six dynamic columns' products as 24 of the 32 k
+// slots of two v_mfma_f32_32x32x16_bf16 per row tile. Slot k (step k >> 4, lane half
+// (k >> 3) & 1, element k & 7) holds weight part wp of column col times input part xp:
+// x, y, origin, dest are exact in bf16 (|v| <= 255), so they take w0 x + w1 x + w2 x; the
+// fuel column (2) and the "cargo" = fuel column (3, environment.py:206) take the six split
+// products of w and the fuel f32. Columns: 0 x, 1 y, 2 fuel, 3 cargo, 4 origin, 5 dest.
+struct Fc1Slot {
+    int8_t col, wp, xp;  // xp: -1 = the exact input, else the fuel part
+};
+__host__ __device__ constexpr Fc1Slot x3_fc1_slot(int k) {
+    constexpr Fc1Slot t[24] = {{0, 0, -1}, {1, 0, -1}, {4, 0, -1}, {5, 0, -1}, {0, 1, -1}, {1, 1, -1}, {4, 1, -1}, {5, 1, -1},
+                               {0, 2, -1}, {1, 2, -1}, {4, 2, -1}, {5, 2, -1}, {2, 0, 0},  {2, 0, 1},  {2, 1, 0},  {2, 0, 2},
+                               {2, 1, 1},  {2, 2, 0},  {3, 0, 0},  {3, 0, 1},  {3, 1, 0},  {3, 0, 2},  {3, 1, 1},  {3, 2, 0}};
+    return k < 24 ? t[k] : Fc1Slot{-1, 0, 0};
+}
+
 struct PackX3Args {
     const float *w1, *b1, *w2, *b2, *w3, *b3;
     const uint32_t* world;
@@ -873,17 +929,32 @@ struct PackX3Args {
 
 // One thread per (fragment, lane) of fc2 / fc3 (its 8 elements' three parts), per fc1 float,
 // bias entry, same-cell mask and epilogue register mask (the latter as qnet_pack_f32_kernel).
-__global__ __launch_bounds__(256) void qnet_pack_x3_kernel(PackX3Args A) {
+// items [first, total) step `stride` of the split image into img (global memory for
+// qnet_pack_x3_kernel, the workgroup's LDS for policy_x3_kernel's own prologue)
+__device__ __forceinline__ void pack_x3_items(const PackX3Args& A, uint8_t* img, int first, int stride) {
     const QnetX3Dims d = A.d;
     const QnetDims q = d.q;
-    uint8_t* const img = A.img;
     const int in1 = q.in1();
-    const int n_w1 = 4 * 3 * 64, n_w2 = 32 * 64, n_w3 = q.mt3 * 8 * 64;
+    const int n_w1 = SHIPENV_X3_FC1 ? 4 * 2 * 64 : 4 * 3 * 64, n_w2 = 32 * 64, n_w3 = q.mt3 * 8 * 64;
     const int total = n_w1 + n_w2 + n_w3 + 2 * kQHidden + q.mt3 * 32 + q.P + q.mt3;
-    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-        if (t < n_w1) {  // fc1 in f32: (mt, s, lane) = W1[mt*32 + r][2s + h] (qnet_pack_f32_kernel)
-            const int lane = t & 63, st = t >> 6, s = st % 3, mt = st / 3;
-            reinterpret_cast<float*>(img + d.w1())[t] = A.w1[(mt * 32 + (lane & 31)) * in1 + 2 * s + (lane >> 5)];
+    for (int t = first; t < total; t += stride) {
+        if (t < n_w1) {
+            const int lane = t & 63;
+            if (SHIPENV_X3_FC1) {  // fc1 fragment (mt, step, lane): element j = slot 16 step + 8h + j
+                const int st = (t >> 6) & 1, mt = t >> 7, row = mt * 32 + (lane & 31);
+                bf16x8 v;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const Fc1Slot sl = x3_fc1_slot(16 * st + 8 * (lane >> 5) + j);
+                    __bf16 p0 = (__bf16)0.0f, p1 = p0, p2 = p0;
+                    if (sl.col >= 0) split3(A.w1[row * in1 + sl.col], p0, p1, p2);
+                    v[j] = sl.wp == 0 ? p0 : (sl.wp == 1 ? p1 : p2);
+                }
+                reinterpret_cast<bf16x8*>(img + d.w1())[t] = v;
+            } else {  // fc1 in f32: (mt, s, lane) = W1[mt*32 + r][2s + h] (qnet_pack_f32_kernel)
+                const int st = t >> 6, s = st % 3, mt = st / 3;
+                reinterpret_cast<float*>(img + d.w1())[t] = A.w1[(mt * 32 + (lane & 31)) * in1 + 2 * s + (lane >> 5)];
+            }
             continue;
         }
         if (t < n_w1 + n_w2 + n_w3) {  // fragment f = (mt*4 + kt)*2 + s, lane: W[row][kt*32 + acc_row(s, j, h)]
@@ -951,6 +1022,10 @@ __global__ __launch_bounds__(256) void qnet_pack_x3_kernel(PackX3Args A) {
     }
 }
 
+__global__ __launch_bounds__(256) void qnet_pack_x3_kernel(PackX3Args A) {
+    pack_x3_items(A, A.img, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
+}
+
 // relu as a signed integer max with 0 on the f32 pattern (a non-negative float orders like
 // its int pattern; a negative one, -0 included, becomes +0): one v_max_i32, where fmaxf
 // also canonicalised its operand (two v_max_f32 per element)
@@ -1009,6 +1084,9 @@ __device__ __forceinline__ f32x16 kstep_x3(const bf16x8* Wf, int lane, const bf1
 #endif
 #ifndef SHIPENV_X3_SCHED
 #define SHIPENV_X3_SCHED 1  // 0: the layers in plain order (the scheduler's own interleave)
+#endif
+#if !SHIPENV_X3_SCHED && SHIPENV_X3_FC1
+#error "SHIPENV_X3_SCHED=0 is written for the f32 fc1 image: build it with SHIPENV_X3_FC1=0"
 #endif
 // chunk q (0..15) of the relu + 3-way split of tile c into out (relu_split3 in 16 pieces of
 // about five VALU): pair q >> 1 (elements 2p, 2p + 1 of k-step s), stage q & 1 (the bf16
@@ -1085,30 +1163,6 @@ __device__ __forceinline__ f32x16 khalf_x3(const bf16x8 (&w)[3], const bf16x8 (&
     return c;
 }
 
-// bias rows of a fc3 tile, -inf where bit (reg & 3) + 8 (reg >> 2) of m is clear (the row
-// is invalid for this env): its Q stays -inf through the MFMAs and never wins the argmax
-__device__ __forceinline__ f32x16 masked_bias(const float* b, uint32_t m) {
-    f32x16 c = bias_frag(b);
-    uint32_t x = m & 0x0f0f0f0fu;  // register reg's bit to bit reg
-    x = (x | (x >> 4)) & 0x00ff00ffu;
-    x = (x | (x >> 8)) & 0x0000ffffu;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) c[reg] = ((x >> reg) & 1u) ? c[reg] : -INFINITY;
-    return c;
-}
-
-// the first maximum over registers 4j..4j+3 of a masked tile (invalid rows are -inf), the
-// row recorded without the lane half's 4h (added once at the end): one compare and two
-// selects per register, no validity test and no per-register branch
-__device__ __forceinline__ void argmax_masked_part(const f32x16& c, int base, float& best, int& bidx, int j) {
-#pragma unroll
-    for (int reg = 4 * j; reg < 4 * j + 4; ++reg) {
-        const bool better = c[reg] > best;
-        best = better ? c[reg] : best;
-        bidx = better ? base + (reg & 3) + 8 * (reg >> 2) : bidx;
-    }
-}
-
 // tile_argmax over registers 4j..4j+3 only (j = 0..3 in order is tile_argmax)
 __device__ __forceinline__ void tile_argmax_part(const f32x16& c, uint32_t m, uint32_t rm, int base, int h,
                                                  float& best, int& bidx, int j) {
@@ -1127,12 +1181,19 @@ constexpr int kPolicyX3Block = 512;
 constexpr int kPolicyX3Waves = kPolicyX3Block / 64;
 
 template <bool kW3Global, bool kQout = false>
-__global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args F, QnetX3Dims D) {
+__global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args F, QnetX3Dims D, PackX3Args PK) {
     extern __shared__ uint4 smem[];
     const PolicyArgs& A = F.p;
     const QnetDims q = D.q;
-    const int staged = (kW3Global ? D.w3() : D.bytes()) / 16;
-    for (int i = threadIdx.x; i < staged; i += kPolicyX3Block) smem[i] = A.qimg[i];
+    if constexpr (kW3Global) {  // fc3 stays in the packed global image: copy the rest
+        const int staged = D.w3() / 16;
+        for (int i = threadIdx.x; i < staged; i += kPolicyX3Block) smem[i] = A.qimg[i];
+    } else {
+        // the whole image fits: each workgroup splits the f32 weights into its own LDS copy
+        // (about 93 KB of f32 reads per workgroup at P = 5 where the packed image is 152 KB),
+        // so no pack kernel runs before the policy and in-place weight updates are seen
+        pack_x3_items(PK, reinterpret_cast<uint8_t*>(smem), threadIdx.x, kPolicyX3Block);
+    }
     __syncthreads();
     const LdsWorld w = world_view(A.dims, A.world);  // port_at / stocks read in place (L2)
     const uint8_t* qb = reinterpret_cast<const uint8_t*>(smem);
@@ -1185,7 +1246,9 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
         const uint32_t x8 = in.x8, y8 = in.y8, o8 = in.o8, d8 = in.d8;
         const int origin = o8 == SE_NONE ? -1 : (int)o8, dest = d8 == SE_NONE ? -1 : (int)d8;
         const float ff = (float)fuel;  // the preprocess_state row as torch's FloatTensor holds it
+#if !SHIPENV_X3_FC1
         const float in0 = h ? (float)y8 : (float)x8, in2 = h ? (float)dest : (float)origin;
+#endif
         bf16x8 X1[4][2][3], X2[4][2][3];
         float best = -INFINITY;
         int bidx = 0x7fffffff;
@@ -1201,12 +1264,37 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
         // the rest; fc3's first tile splits fc2's last one. Fragments are read one k-step
         // ahead. Bit-identical to the plain order (the same operations on the same values).
         f32x16 c1[4], acc[4];
+#if SHIPENV_X3_FC1
+        bf16x8 xin[2];  // fc1's B operands: slot 16 step + 8h + j of x3_fc1_slot
+        {
+            __bf16 f0, f1, f2;
+            split3(ff, f0, f1, f2);
+            const __bf16 fp[3] = {f0, f1, f2};
+            const __bf16 ex[6] = {(__bf16)(float)x8, (__bf16)(float)y8, f0, f0, (__bf16)(float)origin,
+                                  (__bf16)(float)dest};  // exact inputs by column (2, 3 unused)
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {  // fc1 on f32 MFMA (x, y | fuel, fuel | origin, dest)
+            for (int st = 0; st < 2; ++st)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const Fc1Slot a = x3_fc1_slot(16 * st + j), b = x3_fc1_slot(16 * st + 8 + j);
+                    const __bf16 va = a.col < 0 ? (__bf16)0.0f : (a.xp < 0 ? ex[a.col] : fp[a.xp]);
+                    const __bf16 vb = b.col < 0 ? (__bf16)0.0f : (b.xp < 0 ? ex[b.col] : fp[b.xp]);
+                    xin[st][j] = h ? vb : va;
+                }
+        }
+        const bf16x8* W1b = reinterpret_cast<const bf16x8*>(W1);
+#endif
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {  // fc1 (x, y | fuel, fuel | origin, dest)
             c1[mt] = bias_frag(B1 + mt * 32 + 4 * h);
+#if SHIPENV_X3_FC1
+            c1[mt] = mfma_bf16(W1b[(mt * 2 + 0) * 64 + lane], xin[0], c1[mt]);
+            c1[mt] = mfma_bf16(W1b[(mt * 2 + 1) * 64 + lane], xin[1], c1[mt]);
+#else
             c1[mt] = mfma32(W1[(mt * 3 + 0) * 64 + lane], in0, c1[mt]);
             c1[mt] = mfma32(W1[(mt * 3 + 1) * 64 + lane], ff, c1[mt]);
             c1[mt] = mfma32(W1[(mt * 3 + 2) * 64 + lane], in2, c1[mt]);
+#endif
             if (mt == 0) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) acc[i] = bias_frag(B2 + i * 32 + 4 * h);
@@ -1440,7 +1528,9 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
     const QnetDims& q = q_out ? qn->q : qn->qc;
     const size_t lds = (size_t)q.bytes() + lds_bytes(env);
     static std::atomic<uint64_t> lds_set{0};
-    rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(policy_kernel), 160 * 1024, env->device);
+    static std::atomic<uint64_t> lds_set_q{0};
+    rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(policy_kernel<false>), 160 * 1024, env->device);
+    if (!rc) rc = allow_dynamic_lds(lds_set_q, reinterpret_cast<const void*>(policy_kernel<true>), 160 * 1024, env->device);
     if (rc) return rc;
     if (lds > 160 * 1024) return fail(SE_EINVAL, "network + world image exceed the 160 KB LDS");
     int dev_cus = 256;
@@ -1471,7 +1561,8 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
         A.rec_head = rec->head;
         A.rec_cap = rec->cap;
     }
-    policy_kernel<<<grid, kPolicyBlock, lds, (hipStream_t)stream>>>(A);
+    if (q_out) policy_kernel<true><<<grid, kPolicyBlock, lds, (hipStream_t)stream>>>(A);
+    else policy_kernel<false><<<grid, kPolicyBlock, lds, (hipStream_t)stream>>>(A);
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }
@@ -1491,9 +1582,11 @@ int launch_policy_x3(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, 
     // the image from the current weights (in place updates by an optimizer or T2 included)
     PackX3Args pk{qn->w[0], qn->w[1], qn->w[2], qn->w[3], qn->w[4], qn->w[5], env->d_world, env->dims, d,
                   qn->d_img32};
-    qnet_pack_x3_kernel<<<128, 256, 0, s>>>(pk);
-    HIP_TRY(hipGetLastError());
     const bool w3_global = d.bytes() > 160 * 1024;
+    if (w3_global) {  // fc3's fragments are read from a packed global image
+        qnet_pack_x3_kernel<<<128, 256, 0, s>>>(pk);
+        HIP_TRY(hipGetLastError());
+    }
     const size_t lds = (size_t)(w3_global ? d.w3() : d.bytes());
     if (lds > 160 * 1024) return fail(SE_EINVAL, "split-bf16 network exceeds the 160 KB LDS");
     static std::atomic<uint64_t> lds_set0{0}, lds_set1{0};
@@ -1532,11 +1625,11 @@ int launch_policy_x3(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, 
     }
     if (q_out) {  // the full layout (fc3 from global memory): unmasked Q rows for q_out
         if (!w3_global) return fail(SE_EINVAL, "q_out: the full fc3 layout is expected in global memory");
-        policy_x3_kernel<true, true><<<grid, kPolicyX3Block, lds, s>>>(F, d);
+        policy_x3_kernel<true, true><<<grid, kPolicyX3Block, lds, s>>>(F, d, pk);
     } else if (w3_global) {
-        policy_x3_kernel<true><<<grid, kPolicyX3Block, lds, s>>>(F, d);
+        policy_x3_kernel<true><<<grid, kPolicyX3Block, lds, s>>>(F, d, pk);
     } else {
-        policy_x3_kernel<false><<<grid, kPolicyX3Block, lds, s>>>(F, d);
+        policy_x3_kernel<false><<<grid, kPolicyX3Block, lds, s>>>(F, d, pk);
     }
     HIP_TRY(hipGetLastError());
     return SE_OK;
