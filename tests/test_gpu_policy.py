@@ -327,3 +327,29 @@ def test_f32_explore_and_record_paths_match_bf16_form(steps, ports):
     np.testing.assert_array_equal(act, first_masked_argmax(q_out.cpu().numpy(), valid_bool(env)))
     compact = pol.act(0.0, 5, precision="f32").cpu().numpy()
     np.testing.assert_array_equal(compact, act)
+
+
+@pytest.mark.parametrize("ports", [None, "64"])
+def test_f32_sees_in_place_weight_updates(ports):
+    """se_policy_f32 splits the f32 weights at every call: in the policy kernel's own LDS when
+    the split image fits (P = 5), or through the packed global image when fc3 does not fit
+    (P = 64's compact rows, and the full layout of q_out). After the weight tensors the
+    policy was built on change in place (an optimizer step), the greedy actions are the
+    first masked maximum of the new Q rows and differ from the old ones."""
+    from conftest import golden_water
+    from shippingenv_amd.vec import random_water_ports
+
+    if ports == "64":
+        ports = random_water_ports(golden_water(), 64, seed=3)
+    env, model, pol = make(4096 + 33, ports=ports, steps=5, scale=20.0)
+    valid = valid_bool(env)
+    before = pol.act(0.0, 7, precision="f32").clone()
+    with torch.no_grad():
+        for w in pol._w:  # the device tensors se_qnet_set_weights bound
+            w.mul_(-1.0)
+    q_out = torch.empty((env.n, env.action_space_size), dtype=torch.float32, device=env.device)
+    full = pol.act(0.0, 7, q_out=q_out, precision="f32").cpu().numpy()
+    compact = pol.act(0.0, 7, precision="f32").cpu().numpy()
+    np.testing.assert_array_equal(full, first_masked_argmax(q_out.cpu().numpy(), valid))
+    np.testing.assert_array_equal(compact, full)
+    assert (compact != before.cpu().numpy()).mean() > 0.1
