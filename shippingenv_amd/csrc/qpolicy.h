@@ -422,7 +422,7 @@ __device__ __forceinline__ void finish_env(const QnetDims& q, const EnvValid& v,
 }
 
 #ifndef SHIPENV_POLICY_MASKED
-#define SHIPENV_POLICY_MASKED 1  // 0: the round-4 epilogue (per-register validity tests and skips)
+#define SHIPENV_POLICY_MASKED 0  // 1: masked -inf fc3 bias + branch-free argmax (63.5 vs 63.4 us, profiles/r05/ab_policy_bf16_masked.jsonl: not kept); 0: the round-4 epilogue
 #endif
 template <bool kQout>
 __global__ __launch_bounds__(kPolicyBlock)

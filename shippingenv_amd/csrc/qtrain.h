@@ -220,6 +220,93 @@ __device__ __forceinline__ void store_relu(float* dst, int tile, const f32x16& a
     }
 }
 
+// T1's forward GEMMs (fc2 of both nets, the target's fc3) on v_mfma_f32_32x32x16_bf16 with
+// every f32 operand split into three bf16 parts (split3 in qpolicy.h: round to nearest, exact
+// remainders) and the six part products of order <= 2, smallest first: the policy's
+// fp32-faithful datapath (§10), at 6 x 32 MFMA cycles per K = 16 where the f32 MFMA takes
+// 8 x 64. The weights stay f32 in global memory, in the order the bf16 A operand reads them
+// (x3_index; 32 B per lane and k-step, the f32 image's bytes), and are split in registers;
+// the activations are split once, by the wave that produced them, into LDS B fragments.
+// 0: the f32 MFMA forward of round 4.
+#ifndef SHIPENV_QT_X3
+#define SHIPENV_QT_X3 1
+#endif
+#ifndef SHIPENV_QT_X3_SCHED
+#define SHIPENV_QT_X3_SCHED 1  // the next k-step's splits between the MFMAs of this one, fenced (0: the compiler's order)
+#endif
+
+// f32 image index of W[row][k] (128 columns) for the split-bf16 A operand: [row tile][k-step
+// g][lane][8], element j of lane (r, h) = W[32 tile + r][32 (g >> 1) + acc_row(g & 1, j, h)],
+// the column order in which a 32 x 32 accumulator's registers 8s..8s+7 are the B fragment of
+// k-step s (qnet_pack_kernel's acc_row)
+__host__ __device__ __forceinline__ int x3_index(int row, int k) {
+    const int kk = k & 31, g = 2 * (k >> 5) + (kk >> 4), h = (kk >> 2) & 1, j = 4 * ((kk >> 3) & 1) + (kk & 3);
+    return (((row >> 5) * 8 + g) * 64 + (row & 31) + 32 * h) * 8 + j;
+}
+
+// parts p0 .. p1 - 1 of eight f32 weights (a, b) -> their bf16 splits w[0..2] (split3)
+__device__ __forceinline__ void split8_half(const float4& a, const float4& b, bf16x8 (&w)[3], int half) {
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int q = 2 * half; q < 2 * half + 2; ++q) {
+        const f32x2 x{v[2 * q], v[2 * q + 1]};
+        const bf16x2 p0 = __builtin_convertvector(x, bf16x2);
+        const f32x2 r1 = x - __builtin_convertvector(p0, f32x2);
+        const bf16x2 p1 = __builtin_convertvector(r1, bf16x2);
+        const bf16x2 p2 = __builtin_convertvector(r1 - __builtin_convertvector(p1, f32x2), bf16x2);
+        w[0][2 * q] = p0[0];
+        w[0][2 * q + 1] = p0[1];
+        w[1][2 * q] = p1[0];
+        w[1][2 * q + 1] = p1[1];
+        w[2][2 * q] = p2[0];
+        w[2][2 * q + 1] = p2[1];
+    }
+}
+
+// acc + W X over k-steps [g0, g0 + G): W from f32 registers wa[2 (g - g0)], [2 (g - g0) + 1]
+// (split here), X the LDS B fragments S[g][part][lane]. Step g + 1's splits and LDS reads are
+// issued between step g's MFMAs (SHIPENV_QT_X3_SCHED fences: left alone the scheduler
+// clustered the VALU ahead of the chain, as in the policy's x3 kernel).
+template <int G>
+__device__ __forceinline__ f32x16 gemm_x3(const float4* wa, const bf16x8* S, int g0, f32x16 acc, int lane) {
+    bf16x8 w[2][3], x[2][3];
+    split8_half(wa[0], wa[1], w[0], 0);
+    split8_half(wa[0], wa[1], w[0], 1);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) x[0][p] = S[(g0 * 3 + p) * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+        const int c = i & 1, n = c ^ 1;
+        if (i + 1 < G)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) x[n][p] = S[((g0 + i + 1) * 3 + p) * 64 + lane];
+        acc = mfma_bf16(w[c][0], x[c][2], acc);
+        acc = mfma_bf16(w[c][1], x[c][1], acc);
+        acc = mfma_bf16(w[c][2], x[c][0], acc);
+        if (SHIPENV_QT_X3_SCHED) __builtin_amdgcn_sched_barrier(0);
+        if (i + 1 < G) split8_half(wa[2 * i + 2], wa[2 * i + 3], w[n], 0);
+        if (SHIPENV_QT_X3_SCHED) __builtin_amdgcn_sched_barrier(0);
+        acc = mfma_bf16(w[c][0], x[c][1], acc);
+        acc = mfma_bf16(w[c][1], x[c][0], acc);
+        acc = mfma_bf16(w[c][0], x[c][0], acc);
+        if (SHIPENV_QT_X3_SCHED) __builtin_amdgcn_sched_barrier(0);
+        if (i + 1 < G) split8_half(wa[2 * i + 2], wa[2 * i + 3], w[n], 1);
+        if (SHIPENV_QT_X3_SCHED) __builtin_amdgcn_sched_barrier(0);
+    }
+    return acc;
+}
+
+// relu of a 32-row accumulator tile `tile` of a layer's output, split into the LDS B
+// fragments of k-steps 2 tile, 2 tile + 1 (each lane its own slots: see x3_index)
+__device__ __forceinline__ void store_split(bf16x8* S, int tile, const f32x16& acc, int lane) {
+    bf16x8 sp[2][3];
+    relu_split3(acc, sp);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) S[((2 * tile + s) * 3 + p) * 64 + lane] = sp[s][p];
+}
+
 // Sum over a wave in a fixed butterfly of __shfl_xor: lane i and lane i^m add the same
 // two values, so every lane ends with the same bits.
 __device__ __forceinline__ float wave_sum_f32(float x) {
@@ -283,16 +370,29 @@ __global__ __launch_bounds__(kQABlock) void qtrain_pack_kernel(QtPackArgs A) {
             const int row = tile * 32 + (lane & 31), k = 2 * s + (lane >> 5);
             A.W.pw1[A.which][e] = A.net.w1[(int64_t)row * in + k];
         } else if (e < n1 + n2) {
-            const int i = e - n1, lane = i & 63, s = (i >> 6) & 63, tile = i >> 12;
+            const int i = e - n1;
+#if SHIPENV_QT_X3  // [tile][g][lane][j] (x3_index)
+            const int j = i & 7, lane = (i >> 3) & 63, g = (i >> 9) & 7, tile = i >> 12;
+            A.W.pw2[A.which][i] = A.net.w2[(tile * 32 + (lane & 31)) * 128 + 32 * (g >> 1) + acc_row(g & 1, j, lane >> 5)];
+#else
+            const int lane = i & 63, s = (i >> 6) & 63, tile = i >> 12;
             A.W.pw2[A.which][i] = A.net.w2[(tile * 32 + (lane & 31)) * 128 + 2 * s + (lane >> 5)];
+#endif
         } else if (e < n1 + 2 * n2) {
             if (A.which) continue;  // the transposed image is the online net's (backward)
             const int i = e - n1 - n2, lane = i & 63, s = (i >> 6) & 63, tile = i >> 12;
             A.W.pw2t[i] = A.net.w2[(2 * s + (lane >> 5)) * 128 + tile * 32 + (lane & 31)];
         } else {
-            const int i = e - n1 - 2 * n2, lane = i & 63, s = (i >> 6) & 63, tile = i >> 12;
+            const int i = e - n1 - 2 * n2;
+#if SHIPENV_QT_X3
+            const int j = i & 7, lane = (i >> 3) & 63, g = (i >> 9) & 7, tile = i >> 12;
+            const int row = tile * 32 + (lane & 31);
+            A.W.pw3t[i] = row < A.d.A ? A.net.w3[row * 128 + 32 * (g >> 1) + acc_row(g & 1, j, lane >> 5)] : 0.0f;
+#else
+            const int lane = i & 63, s = (i >> 6) & 63, tile = i >> 12;
             const int row = tile * 32 + (lane & 31);
             A.W.pw3t[i] = row < A.d.A ? A.net.w3[row * 128 + 2 * s + (lane >> 5)] : 0.0f;
+#endif
         }
     }
 }
@@ -357,6 +457,14 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     float* RW = WT + 64;            // [32] r_j
     float* DN = RW + 32;            // [32] done_j
     int* FST = reinterpret_cast<int*>(DN + 32);  // [32] first(j): the dW3 slot of sample j
+#if SHIPENV_QT_X3
+    // split-bf16 B fragments [k-step][part][lane]: h1 of both nets, the target's h2; fc3's
+    // partial accumulators of the tiles past the eighth ([tile - 8][wt][reg][lane] f32) reuse
+    // the h1 fragments once fc2 is done
+    bf16x8* SH1 = reinterpret_cast<bf16x8*>(FST + 32);  // [2][8][3][64]
+    bf16x8* SH2 = SH1 + 2 * 8 * 3 * 64;                  // [8][3][64]
+    float* XP = reinterpret_cast<float*>(SH1);
+#endif
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wt = wave & 3;
     const bool tgt = wave >= 4;
     const int64_t r0 = (int64_t)blockIdx.x * kQT;
@@ -371,10 +479,23 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     // fc1's operands and fc2's fragments do not depend on the batch: their loads are in
     // flight while the inputs are staged
     const int net = tgt ? 1 : 0;
+#if SHIPENV_QT_X3
+    Frags<64> fb;   // W^2T (dH1), loaded during fc3
+    float4 wa[16];  // fc2's f32 A operands in x3_index order, then fc3's
+    {
+        const float4* p = reinterpret_cast<const float4*>(A.W.pw2[net]) + wt * 8 * 64 * 2;
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            wa[2 * g] = p[(g * 64 + lane) * 2];
+            wa[2 * g + 1] = p[(g * 64 + lane) * 2 + 1];
+        }
+    }
+#else
     Frags<64> fa, fb;  // fc2, then fc3 / W2^T: each loaded one layer ahead
+    fa.load(A.W.pw2[net] + wt * 64 * 64, lane);
+#endif
     Frags<3> f1;
     f1.load(A.W.pw1[net] + wt * 3 * 64, lane);
-    fa.load(A.W.pw2[net] + wt * 64 * 64, lane);
     f32x16 acc1 = bias_init(A.W.c1[net], wt, lane, 128);
 
     if (A.from_ring) {  // the sampler's pick of row r0 + tid, straight into the tiles
@@ -433,6 +554,72 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         for (int k = 0; k < 8; ++k) w3s[k] = w3r[k];
     }
 
+#if SHIPENV_QT_X3
+    // fc1 (f32 MFMA, K = 6), then its relu split into the h1 fragments (the online net's
+    // f32 h1 is kept too, for the backward)
+    {
+        const f32x16 a1 = gemm_lds(f1, tgt ? XN : X, acc1, lane);
+        if (!tgt) store_relu(HA, wt, a1, lane);
+        store_split(SH1 + net * 8 * 3 * 64, wt, a1, lane);
+    }
+    __syncthreads(); QSTAMP(2);
+    // fc2 of row tile wt; fc3's A operands (tile `wave`) load behind its first k-step,
+    // into the registers fc2's consumed k-steps free
+    float4 wb[16];
+    f32x16 acc = bias_init(tgt ? A.tg.b2 : A.on.b2, wt, lane, 128);
+    {
+        const bf16x8* S = SH1 + net * 8 * 3 * 64;
+        acc = gemm_x3<1>(wa, S, 0, acc, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        const float4* p = reinterpret_cast<const float4*>(A.W.pw3t) + wave * 8 * 64 * 2;
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            wb[2 * g] = p[(g * 64 + lane) * 2];
+            wb[2 * g + 1] = p[(g * 64 + lane) * 2 + 1];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        acc = gemm_x3<7>(wa + 2, S, 1, acc, lane);
+        if (tgt) store_split(SH2, wt, acc, lane);
+        else store_relu(HB, wt, acc, lane);
+    }
+    QSTAMP(14);
+    __syncthreads(); QSTAMP(3);
+    // target fc3: tile `wave` on each wave (mt3 >= 9), and the mt3 - 8 (at most 2) tiles past
+    // the eighth split over K: tile 8 on waves 4-7, tile 9 on waves 0-3, two k-steps each, so
+    // every SIMD runs the same MFMA cycles; their partial accumulators meet in LDS (XP) and
+    // wave 0 sums them in a fixed order below
+    {
+        const int xt = tgt ? 8 : 9;
+        const bool extra = xt < A.d.mt3;  // wave-uniform
+        float4 wx[4];
+        f32x16 accx = {};
+        if (extra) {
+            const float4* p = reinterpret_cast<const float4*>(A.W.pw3t) + xt * 8 * 64 * 2;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                wx[2 * u] = p[((2 * wt + u) * 64 + lane) * 2];
+                wx[2 * u + 1] = p[((2 * wt + u) * 64 + lane) * 2 + 1];
+            }
+            if (wt == 0) accx = bias_init(A.tg.b3, xt, lane, A.d.A);
+        }
+        f32x16 acc3 = bias_init(A.tg.b3, wave, lane, A.d.A);
+        acc3 = gemm_x3<8>(wb, SH2, 0, acc3, lane);
+        if (!tgt) fb.load(A.W.pw2t + wt * 64 * 64, lane);  // dH1's operands
+        float m = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if (wave * 32 + acc_r(r, lane) < A.d.A) m = fmaxf(m, acc3[r]);
+        m = fmaxf(m, __shfl_xor(m, 32));  // lane & 31 = sample
+        if (lane < 32) QM[wave * 32 + lane] = m;
+        if (extra) {
+            accx = gemm_x3<2>(wx, SH2, 2 * wt, accx, lane);
+            float* o = XP + ((xt - 8) * 4 + wt) * 16 * 64;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[r * 64 + lane] = accx[r];
+        }
+    }
+    QSTAMP(15);
+#else
     // fc1, fc2 of both networks: online on states, target on next_states
     store_relu(tgt ? TA : HA, wt, gemm_lds(f1, tgt ? XN : X, acc1, lane), lane);
     __syncthreads(); QSTAMP(2);
@@ -515,12 +702,28 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         if (lane < 32) QM[wave * 32 + lane] = m;
     }
     QSTAMP(15);  // this wave's fc3 done
+#endif
     __syncthreads(); QSTAMP(4);
-    if (tid < 32) {
-        const int64_t row = r0 + tid;
-        float mx = QM[tid];
-        for (int w = 1; w < 8; ++w) mx = fmaxf(mx, QM[w * 32 + tid]);
-        Y[tid] = row < A.B ? RW[tid] + (A.gamma * mx) * (1.0f - DN[tid]) : 0.0f;
+    if (tid < 64) {
+        float mx = -INFINITY;
+#if SHIPENV_QT_X3
+        // the tiles past the eighth: the four K-partials of each in a fixed order
+        for (int xt = 8; xt < A.d.mt3; ++xt) {
+            const float* o = XP + (xt - 8) * 4 * 16 * 64;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float v = (o[r * 64 + lane] + o[(16 + r) * 64 + lane]) +
+                                (o[(32 + r) * 64 + lane] + o[(48 + r) * 64 + lane]);
+                if (xt * 32 + acc_r(r, lane) < A.d.A) mx = fmaxf(mx, v);
+            }
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+#endif
+        if (tid < 32) {
+            const int64_t row = r0 + tid;
+            for (int w = 0; w < 8; ++w) mx = fmaxf(mx, QM[w * 32 + tid]);
+            Y[tid] = row < A.B ? RW[tid] + (A.gamma * mx) * (1.0f - DN[tid]) : 0.0f;
+        }
     }
     __syncthreads(); QSTAMP(5);
 
@@ -1116,7 +1319,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             A.m.w2[e] = pm;
             A.v.w2[e] = pv;
             A.on.w2[e] = p;
-            A.W.pw2[0][frag_index(f2, f1)] = p;
+            A.W.pw2[0][SHIPENV_QT_X3 ? x3_index(f2, f1) : frag_index(f2, f1)] = p;
             A.W.pw2t[frag_index(f1, f2)] = p;
             if (A.img[0])
 #pragma unroll
@@ -1345,7 +1548,7 @@ int qtrain_step(se_qtrain* q, se_qnet* qn, int64_t batch, const float* obs, cons
     DeviceGuard g(q->device);
     const hipStream_t s = (hipStream_t)stream;
     const int64_t tiles = (batch + kQT - 1) / kQT;
-    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 8 * 32) * 4;
+    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 8 * 32) * 4 + (SHIPENV_QT_X3 ? 3 * 8 * 3 * 64 * 16 : 0);
     static std::atomic<uint64_t> lds_set{0};
     rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(qtrain_tile_kernel), (int)lds, q->device);
     if (rc) return rc;
