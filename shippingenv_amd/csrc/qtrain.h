@@ -231,6 +231,17 @@ __device__ __forceinline__ void store_relu(float* dst, int tile, const f32x16& a
 #ifndef SHIPENV_QT_X3
 #define SHIPENV_QT_X3 1
 #endif
+#ifndef SHIPENV_QT_X3B
+// 1: the backward's MFMAs too (dH1 on dZ2 fragments split by its producer; dW2 / dW3 with both
+// operands read from the f32 LDS tiles and split in registers). Measured slower: update 38.8 ->
+// 41.1 us, backward phase 6.8 -> 8.2 us (profiles/r05/ab_update_x3_backward.jsonl,
+// qtrace_x3_backward.jsonl): the splits of operands that are read once cost more than the MFMA
+// cycles they save. Needs SHIPENV_QT_X3.
+#define SHIPENV_QT_X3B 0
+#endif
+#if SHIPENV_QT_X3B && !SHIPENV_QT_X3
+#error "SHIPENV_QT_X3B needs SHIPENV_QT_X3 (its fragments reuse the forward's LDS)"
+#endif
 #ifndef SHIPENV_QT_X3_SCHED
 #define SHIPENV_QT_X3_SCHED 1  // the next k-step's splits between the MFMAs of this one, fenced (0: the compiler's order)
 #endif
@@ -381,7 +392,15 @@ __global__ __launch_bounds__(kQABlock) void qtrain_pack_kernel(QtPackArgs A) {
         } else if (e < n1 + 2 * n2) {
             if (A.which) continue;  // the transposed image is the online net's (backward)
             const int i = e - n1 - n2, lane = i & 63, s = (i >> 6) & 63, tile = i >> 12;
+#if SHIPENV_QT_X3B  // W2^T in x3_index order: element (f1, f2) = W2[f2][f1]
+            {
+                const int j = i & 7, ln = (i >> 3) & 63, g = (i >> 9) & 7, tl = i >> 12;
+                (void)lane; (void)s; (void)tile;
+                A.W.pw2t[i] = A.net.w2[(32 * (g >> 1) + acc_row(g & 1, j, ln >> 5)) * 128 + tl * 32 + (ln & 31)];
+            }
+#else
             A.W.pw2t[i] = A.net.w2[(2 * s + (lane >> 5)) * 128 + tile * 32 + (lane & 31)];
+#endif
         } else {
             const int i = e - n1 - 2 * n2;
 #if SHIPENV_QT_X3
@@ -480,7 +499,11 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     // flight while the inputs are staged
     const int net = tgt ? 1 : 0;
 #if SHIPENV_QT_X3
-    Frags<64> fb;   // W^2T (dH1), loaded during fc3
+#if SHIPENV_QT_X3B
+    float4 wd[16];  // W2^T (dH1) in x3_index order, loaded during fc3
+#else
+    Frags<64> fb;   // W2^T (dH1), loaded during fc3
+#endif
     float4 wa[16];  // fc2's f32 A operands in x3_index order, then fc3's
     {
         const float4* p = reinterpret_cast<const float4*>(A.W.pw2[net]) + wt * 8 * 64 * 2;
@@ -547,12 +570,27 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     // this thread's slice of W3[a_j] (q_j and dZ2 below): sample j = tid >> 4, features
     // 8 (tid & 15) .. + 7
     const int qj = tid >> 4, qpart = tid & 15;
+#if SHIPENV_QT_X3B
+    // (SHIPENV_QT_X3B) features 16 g + 4 h + {0..3, 8..11} of slot (g, h) = (qpart >> 1,
+    // qpart & 1): the elements of lane (qj, h)'s split-bf16 B fragment of dZ2's k-step g
+    const int qf0 = 16 * (qpart >> 1) + 4 * (qpart & 1);
+    auto qfeat = [&](int k) { return qf0 + (k & 3) + 8 * (k >> 2); };
+    float w3s[8];
+    {
+        const float4* w3r = reinterpret_cast<const float4*>(A.on.w3 + (int64_t)ACT[qj] * 128 + qf0);
+        const float4 u = w3r[0], v = w3r[2];
+        w3s[0] = u.x; w3s[1] = u.y; w3s[2] = u.z; w3s[3] = u.w;
+        w3s[4] = v.x; w3s[5] = v.y; w3s[6] = v.z; w3s[7] = v.w;
+    }
+#else
+    auto qfeat = [&](int k) { return qpart * 8 + k; };
     float w3s[8];
     {
         const float* w3r = A.on.w3 + (int64_t)ACT[qj] * 128 + qpart * 8;
 #pragma unroll
         for (int k = 0; k < 8; ++k) w3s[k] = w3r[k];
     }
+#endif
 
 #if SHIPENV_QT_X3
     // fc1 (f32 MFMA, K = 6), then its relu split into the h1 fragments (the online net's
@@ -604,7 +642,18 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         }
         f32x16 acc3 = bias_init(A.tg.b3, wave, lane, A.d.A);
         acc3 = gemm_x3<8>(wb, SH2, 0, acc3, lane);
+#if SHIPENV_QT_X3B
+        if (!tgt) {  // dH1's A operands (W2^T, x3_index order)
+            const float4* p = reinterpret_cast<const float4*>(A.W.pw2t) + wt * 8 * 64 * 2;
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                wd[2 * g] = p[(g * 64 + lane) * 2];
+                wd[2 * g + 1] = p[(g * 64 + lane) * 2 + 1];
+            }
+        }
+#else
         if (!tgt) fb.load(A.W.pw2t + wt * 64 * 64, lane);  // dH1's operands
+#endif
         float m = -INFINITY;
 #pragma unroll
         for (int r = 0; r < 16; ++r)
@@ -731,7 +780,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     {
         float s = 0.0f;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) s += w3s[k] * HB[(qpart * 8 + k) * kLS + qj];
+        for (int k = 0; k < 8; ++k) s += w3s[k] * HB[qfeat(k) * kLS + qj];
         s += __shfl_xor(s, 1);
         s += __shfl_xor(s, 2);
         s += __shfl_xor(s, 4);
@@ -757,27 +806,125 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         }
     }
     __syncthreads(); QSTAMP(6);
-    // dZ2 = (h2 > 0) g_j W3[a_j] (into the target's dead h1 buffer)
+    // dZ2 = (h2 > 0) g_j W3[a_j] (into the target's dead h1 buffer; with SHIPENV_QT_X3B also
+    // split into dH1's B fragments, in the target h2's dead fragments)
     {
         const float g = G[qj];
+        float d[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const int f = qpart * 8 + k;
-            DZ2[f * kLS + qj] = HB[f * kLS + qj] > 0.0f ? g * w3s[k] : 0.0f;
+            const int f = qfeat(k);
+            d[k] = HB[f * kLS + qj] > 0.0f ? g * w3s[k] : 0.0f;
+            DZ2[f * kLS + qj] = d[k];
         }
+#if SHIPENV_QT_X3B
+        bf16x8 sp[3];
+        split8_half(make_float4(d[0], d[1], d[2], d[3]), make_float4(d[4], d[5], d[6], d[7]), sp, 0);
+        split8_half(make_float4(d[0], d[1], d[2], d[3]), make_float4(d[4], d[5], d[6], d[7]), sp, 1);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) SH2[((qpart >> 1) * 3 + p) * 64 + qj + 32 * (qpart & 1)] = sp[p];
+#endif
     }
     __syncthreads(); QSTAMP(7);
 
     const int h = lane >> 5, c = lane & 31;
     if (!tgt) {  // dH1 = W2^T dZ2 -> dZ1 = (h1 > 0) dH1
         f32x16 acc = {};
+#if SHIPENV_QT_X3B
+        acc = gemm_x3<8>(wd, SH2, 0, acc, lane);
+#else
         acc = gemm_lds(fb, DZ2, acc, lane);
+#endif
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int f = wt * 32 + acc_r(r, lane);
             DZ1[f * kLS + c] = HA[f * kLS + c] > 0.0f ? acc[r] : 0.0f;
         }
-    } else {  // partial dW2[f2][f1] = sum_j dZ2[f2][j] h1[f1][j]: f1 tile wt, 4 f2 tiles
+    } else {
+#if SHIPENV_QT_X3B
+        // partial dW2 (as H1 dZ2^T, f1 tile wt, 4 f2 tiles) and dW3 (as H2 G^T over the tile's
+        // slots) on split-bf16 MFMAs over K = 32 samples (two k-steps of 16): lane (r, h) of an
+        // operand holds samples 16 u + 8 h + 0..7 of its row, read from the f32 LDS tiles and
+        // split here. The accumulators are laid out as before, so are the stores.
+        auto row8 = [&](const float* src, int u, bf16x8 (&w)[3]) {
+            const float* q = src + 16 * u + 8 * h;
+            const float4 x = make_float4(q[0], q[1], q[2], q[3]), y = make_float4(q[4], q[5], q[6], q[7]);
+            split8_half(x, y, w, 0);
+            split8_half(x, y, w, 1);
+        };
+        auto x3_k32 = [&](const bf16x8 (&a)[2][3], const bf16x8 (&b)[2][3]) {
+            f32x16 acc = {};
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                acc = mfma_bf16(a[u][0], b[u][2], acc);
+                acc = mfma_bf16(a[u][1], b[u][1], acc);
+                acc = mfma_bf16(a[u][2], b[u][0], acc);
+                acc = mfma_bf16(a[u][0], b[u][1], acc);
+                acc = mfma_bf16(a[u][1], b[u][0], acc);
+                acc = mfma_bf16(a[u][0], b[u][0], acc);
+            }
+            return acc;
+        };
+        float* out = A.W.part_w2 + (int64_t)blockIdx.x * 128 * 128;
+        bf16x8 a2[2][3], b2[2][3];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) row8(HA + (wt * 32 + c) * kLS, u, a2[u]);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) row8(DZ2 + (ct * 32 + c) * kLS, u, b2[u]);
+            const f32x16 acc = x3_k32(a2, b2);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)  // f1 = 32 wt + acc_r(4q + m, lane) = 32 wt + 8q + 4h + m
+#if SHIPENV_QT_ABL & 1  // timing only: the dW2 partials computed, not stored
+                if (A.B < 0)
+#endif
+                st_part4(out, (uint32_t)((ct * 32 + c) * 128 + wt * 32 + 8 * q + 4 * h), acc[4 * q], acc[4 * q + 1],
+                         acc[4 * q + 2], acc[4 * q + 3]);
+        }
+        // dW3: slot r = sum_j [first(j) = r] g_j h2[f][j]; B lane (c, h): sample j's g where
+        // slot c is first(j), else 0 (the split of the selected value)
+        const bool live_slot = FST[c] == c && r0 + c < A.B;
+        const uint32_t slots = (uint32_t)__ballot(live_slot);  // lanes 0-31 = slots 0-31
+        float av[16];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int j = 16 * u + 8 * h + k;
+                av[8 * u + k] = FST[j] == c ? G[j] : 0.0f;
+            }
+        bf16x8 bv[2][3], gv[2][3];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            row8(HB + (wt * 32 + c) * kLS, u, bv[u]);
+            const float4 x = make_float4(av[8 * u], av[8 * u + 1], av[8 * u + 2], av[8 * u + 3]);
+            const float4 y = make_float4(av[8 * u + 4], av[8 * u + 5], av[8 * u + 6], av[8 * u + 7]);
+            split8_half(x, y, gv[u], 0);
+            split8_half(x, y, gv[u], 1);
+        }
+        const f32x16 acc = x3_k32(bv, gv);
+        float* o3 = A.W.part_w3 + (int64_t)blockIdx.x * 32 * 128;
+#if SHIPENV_QT_ABL & 2  // timing only: the dW3 partials computed, not stored
+        if (A.B < 0)
+#endif
+        if ((slots >> c) & 1u)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                st_part4(o3, (uint32_t)(c * 128 + wt * 32 + 8 * q + 4 * h), acc[4 * q], acc[4 * q + 1], acc[4 * q + 2],
+                         acc[4 * q + 3]);
+        if (wt == 0) {  // db3 of slot c: this lane half's 16 samples, then the other half's
+            float s3 = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) s3 += av[k];
+            const float x3 = __shfl_xor(s3, 32);
+            if (h == 0) {
+                st_part1(A.W.part_b3 + (int64_t)blockIdx.x * 32 + c, s3 + x3);
+                st_part1(A.W.part_map + (int64_t)blockIdx.x * 32 + c, live_slot ? (int32_t)ACT[c] : (int32_t)-1);
+            }
+        }
+#else
+  // partial dW2[f2][f1] = sum_j dZ2[f2][j] h1[f1][j]: f1 tile wt, 4 f2 tiles
         // computed as its transpose H1 dZ2^T (A operands: f1 rows wt*32.. of h1, once; each
         // f2 tile's B operands read while the previous tile's chain runs), so a lane's
         // registers 4q..4q+3 are dW2[f2 = 32 ct + c][4 adjacent f1]: one 16-byte store each
@@ -854,6 +1001,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
                 st_part1(A.W.part_map + (int64_t)blockIdx.x * 32 + c, live_slot ? (int32_t)ACT[c] : (int32_t)-1);
             }
         }
+#endif
     }
     __syncthreads(); QSTAMP(8);  // dZ1 complete
     // partial dW1 (dynamic columns), db1, db2, loss and weight sums
@@ -1320,7 +1468,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             A.v.w2[e] = pv;
             A.on.w2[e] = p;
             A.W.pw2[0][SHIPENV_QT_X3 ? x3_index(f2, f1) : frag_index(f2, f1)] = p;
-            A.W.pw2t[frag_index(f1, f2)] = p;
+            A.W.pw2t[SHIPENV_QT_X3B ? x3_index(f1, f2) : frag_index(f1, f2)] = p;
             if (A.img[0])
 #pragma unroll
                 for (int l = 0; l < 2; ++l) put_bf16(A.img[l] + A.q[l].w2() + pol_offset(f2, f1), p);
