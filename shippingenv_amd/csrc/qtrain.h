@@ -242,6 +242,18 @@ __device__ __forceinline__ void store_relu(float* dst, int tile, const f32x16& a
 #if SHIPENV_QT_X3B && !SHIPENV_QT_X3
 #error "SHIPENV_QT_X3B needs SHIPENV_QT_X3 (its fragments reuse the forward's LDS)"
 #endif
+// 1: fc2 / fc3's weights pre-split in global memory (three bf16 parts, [tile][k-step][part][lane]
+// bf16x8, kstep_x3's layout; 6 B per weight instead of 4), so T1 runs no weight splits; 0: f32
+// weights split in registers
+#ifndef SHIPENV_QT_X3W
+#define SHIPENV_QT_X3W 1
+#endif
+#if SHIPENV_QT_X3W && !SHIPENV_QT_X3
+#error "SHIPENV_QT_X3W needs SHIPENV_QT_X3"
+#endif
+#ifndef SHIPENV_QT_PICK_FIRST
+#define SHIPENV_QT_PICK_FIRST 1  // T1: the minibatch picks' first ring loads ahead of the weight loads (0: after)
+#endif
 #ifndef SHIPENV_QT_X3_SCHED
 #define SHIPENV_QT_X3_SCHED 1  // the next k-step's splits between the MFMAs of this one, fenced (0: the compiler's order)
 #endif
@@ -253,6 +265,36 @@ __device__ __forceinline__ void store_relu(float* dst, int tile, const f32x16& a
 __host__ __device__ __forceinline__ int x3_index(int row, int k) {
     const int kk = k & 31, g = 2 * (k >> 5) + (kk >> 4), h = (kk >> 2) & 1, j = 4 * ((kk >> 3) & 1) + (kk & 3);
     return (((row >> 5) * 8 + g) * 64 + (row & 31) + 32 * h) * 8 + j;
+}
+
+// bf16 index of part 0 of W[row][k] in a pre-split image (SHIPENV_QT_X3W): [row tile][k-step g]
+// [part][lane][8], elements as x3_index; part p is 512 p further
+__host__ __device__ __forceinline__ int x3w_index(int row, int k) {
+    const int kk = k & 31, g = 2 * (k >> 5) + (kk >> 4), h = (kk >> 2) & 1, j = 4 * ((kk >> 3) & 1) + (kk & 3);
+    return (((row >> 5) * 8 + g) * 3 * 64 + (row & 31) + 32 * h) * 8 + j;
+}
+
+// acc + W X over k-steps [g0, g0 + G) with pre-split weights w[i][part] and the LDS B fragments
+// S[g][part][lane] (the next k-step's read while this one's MFMAs run)
+template <int G>
+__device__ __forceinline__ f32x16 gemm_x3w(const bf16x8 (*w)[3], const bf16x8* S, int g0, f32x16 acc, int lane) {
+    bf16x8 x[2][3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) x[0][p] = S[(g0 * 3 + p) * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+        const int c = i & 1, n = c ^ 1;
+        if (i + 1 < G)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) x[n][p] = S[((g0 + i + 1) * 3 + p) * 64 + lane];
+        acc = mfma_bf16(w[i][0], x[c][2], acc);
+        acc = mfma_bf16(w[i][1], x[c][1], acc);
+        acc = mfma_bf16(w[i][2], x[c][0], acc);
+        acc = mfma_bf16(w[i][0], x[c][1], acc);
+        acc = mfma_bf16(w[i][1], x[c][0], acc);
+        acc = mfma_bf16(w[i][0], x[c][0], acc);
+    }
+    return acc;
 }
 
 // parts p0 .. p1 - 1 of eight f32 weights (a, b) -> their bf16 splits w[0..2] (split3)
@@ -381,6 +423,7 @@ __global__ __launch_bounds__(kQABlock) void qtrain_pack_kernel(QtPackArgs A) {
             const int row = tile * 32 + (lane & 31), k = 2 * s + (lane >> 5);
             A.W.pw1[A.which][e] = A.net.w1[(int64_t)row * in + k];
         } else if (e < n1 + n2) {
+            if (SHIPENV_QT_X3W) continue;  // the split images: below
             const int i = e - n1;
 #if SHIPENV_QT_X3  // [tile][g][lane][j] (x3_index)
             const int j = i & 7, lane = (i >> 3) & 63, g = (i >> 9) & 7, tile = i >> 12;
@@ -402,6 +445,7 @@ __global__ __launch_bounds__(kQABlock) void qtrain_pack_kernel(QtPackArgs A) {
             A.W.pw2t[i] = A.net.w2[(2 * s + (lane >> 5)) * 128 + tile * 32 + (lane & 31)];
 #endif
         } else {
+            if (SHIPENV_QT_X3W) continue;
             const int i = e - n1 - 2 * n2;
 #if SHIPENV_QT_X3
             const int j = i & 7, lane = (i >> 3) & 63, g = (i >> 9) & 7, tile = i >> 12;
@@ -414,6 +458,30 @@ __global__ __launch_bounds__(kQABlock) void qtrain_pack_kernel(QtPackArgs A) {
 #endif
         }
     }
+#if SHIPENV_QT_X3W
+    // fc2 (and the target's fc3) pre-split: one item per (tile, k-step, lane), its 8 weights'
+    // three parts
+    const int m2 = 4 * 8 * 64, m3 = A.which ? A.d.mt3 * 8 * 64 : 0;
+    for (int e = blockIdx.x * kQABlock + threadIdx.x; e < m2 + m3; e += gridDim.x * kQABlock) {
+        const bool two = e < m2;
+        const int i = two ? e : e - m2, lane = i & 63, g = (i >> 6) & 7, tile = i >> 9;
+        const int row = tile * 32 + (lane & 31);
+        bf16x8 p[3];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 32 * (g >> 1) + acc_row(g & 1, j, lane >> 5);
+            const float v = two ? A.net.w2[row * 128 + k] : (row < A.d.A ? A.net.w3[row * 128 + k] : 0.0f);
+            __bf16 a, b, c;
+            split3(v, a, b, c);
+            p[0][j] = a;
+            p[1][j] = b;
+            p[2][j] = c;
+        }
+        bf16x8* dst = reinterpret_cast<bf16x8*>(two ? A.W.pw2[A.which] : A.W.pw3t) + (tile * 8 + g) * 3 * 64 + lane;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) dst[q * 64] = p[q];
+    }
+#endif
 }
 
 struct QtStepArgs {
@@ -498,12 +566,36 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     // fc1's operands and fc2's fragments do not depend on the batch: their loads are in
     // flight while the inputs are staged
     const int net = tgt ? 1 : 0;
+#if SHIPENV_QT_PICK_FIRST
+    // the first try of wave 0's minibatch picks: its ring loads go out ahead of the weights'
+    // (the vector memory counter is in order: behind ~24 KB of fragments per wave they waited)
+    PickFirst pf{{-1, 0u, 0u, 0.0f, 0.0f, 0.0f, 0, 0}, -1};
+    U4 pkey{};
+    int64_t psize = 0;
+    uint32_t pt = 0;
+    if (A.from_ring && tid < 32) {
+        psize = A.size_host >= 0 ? A.size_host : *A.ring.d_size;
+        pt = A.t_host >= 0 ? (uint32_t)A.t_host : (uint32_t)A.ctr[0];
+        pkey = draw(env_key(A.seed, kReplayKeyId), pt, kSlotReplay);
+        if (r0 + tid < A.B) pf = pick_issue(A.ring, psize, pkey, feistel_half((uint32_t)psize), r0 + tid);
+    }
+#endif
 #if SHIPENV_QT_X3
 #if SHIPENV_QT_X3B
     float4 wd[16];  // W2^T (dH1) in x3_index order, loaded during fc3
 #else
     Frags<64> fb;   // W2^T (dH1), loaded during fc3
 #endif
+#if SHIPENV_QT_X3W
+    bf16x8 wa[8][3];  // fc2's pre-split A operands
+    {
+        const bf16x8* p = reinterpret_cast<const bf16x8*>(A.W.pw2[net]) + wt * 8 * 3 * 64;
+#pragma unroll
+        for (int g = 0; g < 8; ++g)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) wa[g][q] = p[(g * 3 + q) * 64 + lane];
+    }
+#else
     float4 wa[16];  // fc2's f32 A operands in x3_index order, then fc3's
     {
         const float4* p = reinterpret_cast<const float4*>(A.W.pw2[net]) + wt * 8 * 64 * 2;
@@ -513,6 +605,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             wa[2 * g + 1] = p[(g * 64 + lane) * 2 + 1];
         }
     }
+#endif
 #else
     Frags<64> fa, fb;  // fc2, then fc3 / W2^T: each loaded one layer ahead
     fa.load(A.W.pw2[net] + wt * 64 * 64, lane);
@@ -524,12 +617,17 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     if (A.from_ring) {  // the sampler's pick of row r0 + tid, straight into the tiles
         if (tid < 32) {
             const Ring& ring = A.ring;
+            const int64_t row = r0 + tid;
+            Pick pk{-1, 0u, 0u, 0.0f, 0.0f, 0.0f, 0, 0};
+#if SHIPENV_QT_PICK_FIRST
+            const uint32_t t = pt;
+            if (row < A.B) pk = pick_resolve(pf, ring, psize, pkey, feistel_half((uint32_t)psize), row, A.B);
+#else
             const int64_t size = A.size_host >= 0 ? A.size_host : *ring.d_size;
             const uint32_t t = A.t_host >= 0 ? (uint32_t)A.t_host : (uint32_t)A.ctr[0];
             const U4 key = draw(env_key(A.seed, kReplayKeyId), t, kSlotReplay);
-            const int64_t row = r0 + tid;
-            Pick pk{-1, 0u, 0u, 0.0f, 0.0f, 0.0f, 0, 0};
             if (row < A.B) pk = pick_transition(ring, size, key, feistel_half((uint32_t)size), row, A.B);
+#endif
             const bool ok = pk.slot >= 0;
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
@@ -603,6 +701,38 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     __syncthreads(); QSTAMP(2);
     // fc2 of row tile wt; fc3's A operands (tile `wave`) load behind its first k-step,
     // into the registers fc2's consumed k-steps free
+#if SHIPENV_QT_X3W
+    // fc3's pre-split A operands of k-step g load once fc2's k-step g has consumed its own
+    // (fenced, so that at most one k-step's worth more is live)
+    bf16x8 wb[8][3];
+    f32x16 acc = bias_init(tgt ? A.tg.b2 : A.on.b2, wt, lane, 128);
+    {
+        const bf16x8* S = SH1 + net * 8 * 3 * 64;
+        const bf16x8* P3 = reinterpret_cast<const bf16x8*>(A.W.pw3t) + wave * 8 * 3 * 64;
+        bf16x8 x[2][3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) x[0][q] = S[q * 64 + lane];
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            const int c = g & 1;
+            if (g + 1 < 8)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) x[c ^ 1][q] = S[((g + 1) * 3 + q) * 64 + lane];
+            acc = mfma_bf16(wa[g][0], x[c][2], acc);
+            acc = mfma_bf16(wa[g][1], x[c][1], acc);
+            acc = mfma_bf16(wa[g][2], x[c][0], acc);
+            acc = mfma_bf16(wa[g][0], x[c][1], acc);
+            acc = mfma_bf16(wa[g][1], x[c][0], acc);
+            acc = mfma_bf16(wa[g][0], x[c][0], acc);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) wb[g][q] = P3[(g * 3 + q) * 64 + lane];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (tgt) store_split(SH2, wt, acc, lane);
+        else store_relu(HB, wt, acc, lane);
+    }
+#else
     float4 wb[16];
     f32x16 acc = bias_init(tgt ? A.tg.b2 : A.on.b2, wt, lane, 128);
     {
@@ -620,6 +750,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         if (tgt) store_split(SH2, wt, acc, lane);
         else store_relu(HB, wt, acc, lane);
     }
+#endif
     QSTAMP(14);
     __syncthreads(); QSTAMP(3);
     // target fc3: tile `wave` on each wave (mt3 >= 9), and the mt3 - 8 (at most 2) tiles past
@@ -629,6 +760,20 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     {
         const int xt = tgt ? 8 : 9;
         const bool extra = xt < A.d.mt3;  // wave-uniform
+#if SHIPENV_QT_X3W
+        bf16x8 wx[2][3];
+        f32x16 accx = {};
+        if (extra) {
+            const bf16x8* p = reinterpret_cast<const bf16x8*>(A.W.pw3t) + xt * 8 * 3 * 64;
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) wx[u][q] = p[((2 * wt + u) * 3 + q) * 64 + lane];
+            if (wt == 0) accx = bias_init(A.tg.b3, xt, lane, A.d.A);
+        }
+        f32x16 acc3 = bias_init(A.tg.b3, wave, lane, A.d.A);
+        acc3 = gemm_x3w<8>(wb, SH2, 0, acc3, lane);
+#else
         float4 wx[4];
         f32x16 accx = {};
         if (extra) {
@@ -642,6 +787,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         }
         f32x16 acc3 = bias_init(A.tg.b3, wave, lane, A.d.A);
         acc3 = gemm_x3<8>(wb, SH2, 0, acc3, lane);
+#endif
 #if SHIPENV_QT_X3B
         if (!tgt) {  // dH1's A operands (W2^T, x3_index order)
             const float4* p = reinterpret_cast<const float4*>(A.W.pw2t) + wt * 8 * 64 * 2;
@@ -661,7 +807,11 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         m = fmaxf(m, __shfl_xor(m, 32));  // lane & 31 = sample
         if (lane < 32) QM[wave * 32 + lane] = m;
         if (extra) {
+#if SHIPENV_QT_X3W
+            accx = gemm_x3w<2>(wx, SH2, 2 * wt, accx, lane);
+#else
             accx = gemm_x3<2>(wx, SH2, 2 * wt, accx, lane);
+#endif
             float* o = XP + ((xt - 8) * 4 + wt) * 16 * 64;
 #pragma unroll
             for (int r = 0; r < 16; ++r) o[r * 64 + lane] = accx[r];
@@ -1040,6 +1190,35 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     QSTAMP(9);
 }
 
+#ifndef SHIPENV_QT_T2FIX
+#define SHIPENV_QT_T2FIX 1  // T2: the step count as a vector load, no per-lane pointer reloads (0: round 4)
+#endif
+// sum over t = tid, tid + kQRBlock, ... < tiles of p[t * stride]: the first load issued with no
+// wait (its value is added where the sum is used), the rest (more than kQRBlock tiles) looped
+struct StridedSum {
+    float first = 0.0f, rest = 0.0f;
+    __device__ __forceinline__ void issue(const float* p, int64_t stride, int64_t tiles) {
+        const int64_t t = threadIdx.x;
+        first = t < tiles ? p[t * stride] : 0.0f;
+        for (int64_t u = t + kQRBlock; u < tiles; u += kQRBlock) rest += p[u * stride];
+    }
+    __device__ __forceinline__ float value() const { return first + rest; }
+};
+// a pointer materialised in SGPRs and opaque to the optimiser (no select-of-loads rewrite into
+// a per-lane load of the kernel argument)
+template <typename T>
+__device__ __forceinline__ T* sgpr_ptr(T* p) {
+    asm volatile("" : "+s"(p));
+    return p;
+}
+// a 4-byte load through the vector memory path (a VGPR offset the compiler cannot fold)
+__device__ __forceinline__ int32_t vload_i32(const int32_t* p) {
+    int z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(p), (short)0, 4, 0x00020000);
+    return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)z, 0, 0);
+}
+
 struct QtAdamArgs {
     QtWork W;
     Mlp on, m, v;
@@ -1283,7 +1462,14 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
     // the Adam count: its load is in flight while the sums' loads are issued; the step's
     // constants (two powf) are formed where the first Adam step needs them, after the
     // sums (SHIPENV_QT_LATE_ADAM; 0: at the kernel's start, ahead of every sum load)
+#if SHIPENV_QT_T2FIX
+    // a vector load (vmcnt): as a scalar load of a line T1 has just written, its wait
+    // (lgkmcnt(0), which every later kernel-argument load shares) held each block ~1.4 us
+    // before its first partial-sum load
+    const int32_t steps_dev = A.step_dev ? vload_i32(A.step_dev) : 0;
+#else
     const int32_t steps_dev = A.step_dev ? *A.step_dev : 0;
+#endif
 #if SHIPENV_QT_LATE_ADAM
 #define QT_ADAM() AdamStep(A, steps_dev)
 #else
@@ -1291,11 +1477,25 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
 #define QT_ADAM() adam_early
 #endif
     // every block has read the count; ctr[0] is read by the next update's T1 only
+#if !SHIPENV_QT_T2FIX
     if (A.ctr_sync && blockIdx.x == 0 && tid == 0) *A.ctr_sync = steps_dev;
+#endif
     // sum(w): this thread's share loads now, and the workgroup reduces it after its own
     // sum (inv is first needed by the Adam step), so the two round trips overlap
     const int mode = A.mode;  // block-uniform
     float* G = A.grad;
+#if SHIPENV_QT_T2FIX
+    // (the first load of each strided sum is not waited for here: in a loop its s_waitcnt held
+    // the block one round trip before its partial sums' loads were issued)
+    StridedSum ws, ls;  // ls: the loss sum, W1 block 0 (mode 0) only
+    if (mode == 0 || (mode == 1 && blockIdx.x == 0)) {
+        ws.issue(A.W.part_lw + 1, 2, A.tiles);
+        if (mode == 0 && blockIdx.x == 0) ls.issue(A.W.part_lw, 2, A.tiles);
+    }
+    auto weight_inv = [&]() {
+        return 1.0f / fmaxf(mode == 2 ? G[Grad::lw(A.d) + 1] : block_sum256(ws.value(), red), 1.0f);
+    };
+#else
     float wsum = 0.0f, lsum = 0.0f;  // lsum: the loss sum, W1 block 0 (mode 0) only
     if (mode == 0 || (mode == 1 && blockIdx.x == 0))
         for (int64_t t = tid; t < A.tiles; t += kQRBlock) {
@@ -1305,6 +1505,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
     auto weight_inv = [&]() {
         return 1.0f / fmaxf(mode == 2 ? G[Grad::lw(A.d) + 1] : block_sum256(wsum, red), 1.0f);
     };
+#endif
     QSTAMP(11);
     const int b = blockIdx.x;
     if (b < 128) {  // W1 row f: 6 dynamic columns + db1 reduced over the tiles, the port columns
@@ -1357,11 +1558,15 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                 if (f == 0) {  // the loss and weight sums
                     float l = 0.0f;
                     for (int64_t t = tid; t < A.tiles; t += kQRBlock) l += A.W.part_lw[2 * t];
-                    const float ls = block_sum256(l, red);
-                    const float ws = block_sum256(wsum, red);
+                    const float lsm = block_sum256(l, red);
+#if SHIPENV_QT_T2FIX
+                    const float wsm = block_sum256(ws.value(), red);
+#else
+                    const float wsm = block_sum256(wsum, red);
+#endif
                     if (tid == 0) {
-                        G[Grad::lw(A.d)] = ls;
-                        G[Grad::lw(A.d) + 1] = ws;
+                        G[Grad::lw(A.d)] = lsm;
+                        G[Grad::lw(A.d) + 1] = wsm;
                     }
                 }
                 return;
@@ -1369,6 +1574,9 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         }
         const float inv = weight_inv();
         const AdamStep adam = QT_ADAM();
+#if SHIPENV_QT_T2FIX
+        if (A.ctr_sync && f == 0 && tid == 0) *A.ctr_sync = steps_dev;  // the next update's T1 reads it
+#endif
         QSTAMP(12);
         if (tid == 0)  // every thread holds the sums; the row loop below indexes them by column
 #pragma unroll
@@ -1421,7 +1629,11 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         if (f == 0) {  // the loss: sum w d^2 / sum w
             float loss;
             // (mode 0: this thread's share was loaded at the start, with the weight sum)
+#if SHIPENV_QT_T2FIX
+            loss = mode == 2 ? G[Grad::lw(A.d)] : block_sum256(ls.value(), red);
+#else
             loss = mode == 2 ? G[Grad::lw(A.d)] : block_sum256(lsum, red);
+#endif
             if (tid == 0) *A.loss_out = loss * inv;
         }
     } else if (b < 384) {  // W2 elements e0 .. e0 + 63 (row-major [f2][f1])
@@ -1443,6 +1655,10 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             }
         }
         float g;
+#if SHIPENV_QT_T2FIX
+        StridedSum b2s;  // a row's first block: its db2 partials, issued ahead of dW2's
+        if (mode != 2 && (e0 & 127) == 0) b2s.issue(A.W.part_b2 + f2, 128, A.tiles);
+#endif
         if (mode == 2) {
             g = tid < 64 ? G[Grad::w2 + e0 + tid] : 0.0f;
         } else {
@@ -1450,8 +1666,12 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             if (mode == 1) {
                 if (tid < 64) G[Grad::w2 + e0 + tid] = g;
                 if ((e0 & 127) == 0) {
+#if SHIPENV_QT_T2FIX
+                    const float x = b2s.value();
+#else
                     float x = 0.0f;
                     for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[t * 128 + f2];
+#endif
                     const float s2 = block_sum256(x, red);
                     if (tid == 0) G[Grad::b2 + f2] = s2;
                 }
@@ -1467,7 +1687,18 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             A.m.w2[e] = pm;
             A.v.w2[e] = pv;
             A.on.w2[e] = p;
+#if SHIPENV_QT_X3W
+            {
+                __bf16 p0, p1, p2;
+                split3(p, p0, p1, p2);
+                __bf16* img = reinterpret_cast<__bf16*>(A.W.pw2[0]) + x3w_index(f2, f1);
+                img[0] = p0;
+                img[512] = p1;
+                img[1024] = p2;
+            }
+#else
             A.W.pw2[0][SHIPENV_QT_X3 ? x3_index(f2, f1) : frag_index(f2, f1)] = p;
+#endif
             A.W.pw2t[SHIPENV_QT_X3B ? x3_index(f1, f2) : frag_index(f1, f2)] = p;
             if (A.img[0])
 #pragma unroll
@@ -1478,8 +1709,12 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             if (mode == 2) {
                 s2 = G[Grad::b2 + f2];
             } else {
+#if SHIPENV_QT_T2FIX
+                const float x = b2s.value();
+#else
                 float x = 0.0f;
                 for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[t * 128 + f2];
+#endif
                 s2 = block_sum256(x, red);
             }
             if (tid == 0) {
@@ -1498,6 +1733,20 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         const int f3 = tid;  // threads < 128: element f3 of the row; thread 128: b3
         const int64_t i3 = (int64_t)a3 * 128 + f3;
         float pw = 0.f, pm = 0.f, pv = 0.f;  // the Adam operands, loaded ahead of the sums
+#if SHIPENV_QT_T2FIX
+        // the six pointers held in SGPRs (opaque), and every thread loads both candidates: the
+        // compiler otherwise merged the two branches' loads (and the stores below) into one
+        // through a pointer it re-read from the kernel arguments per lane, a dependent round trip
+        float *ow3 = sgpr_ptr(A.on.w3), *ob3 = sgpr_ptr(A.on.b3), *mw3 = sgpr_ptr(A.m.w3), *mb3 = sgpr_ptr(A.m.b3),
+              *vw3 = sgpr_ptr(A.v.w3), *vb3 = sgpr_ptr(A.v.b3);
+        if (mode != 1 && row_live) {
+            const int64_t iw = (int64_t)a3 * 128 + (tid & 127);
+            const float w_ = ow3[iw], m_ = mw3[iw], v_ = vw3[iw], bw_ = ob3[a3], bm_ = mb3[a3], bv_ = vb3[a3];
+            pw = tid < 128 ? w_ : bw_;
+            pm = tid < 128 ? m_ : bm_;
+            pv = tid < 128 ? v_ : bv_;
+        }
+#else
         if (mode != 1 && row_live) {
             if (tid < 128) {
                 pw = A.on.w3[i3];
@@ -1509,6 +1758,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                 pv = A.v.b3[a3];
             }
         }
+#endif
         float g = 0.0f;  // dW3[a3][tid] (tid < 128) or db3[a3] (tid = 128)
         if (mode == 2) {
             if (tid < 128) g = G[Grad::w3 + i3];
@@ -1526,6 +1776,14 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         QSTAMP(12);
         if (row_live && tid <= 128) {
             const float p = adam(pw, g * inv, pm, pv);
+#if SHIPENV_QT_T2FIX
+            float* dm = tid < 128 ? mw3 + i3 : mb3 + a3;
+            float* dv = tid < 128 ? vw3 + i3 : vb3 + a3;
+            float* dp = tid < 128 ? ow3 + i3 : ob3 + a3;
+            *dm = pm;
+            *dv = pv;
+            *dp = p;
+#else
             if (tid < 128) {
                 A.m.w3[i3] = pm;
                 A.v.w3[i3] = pv;
@@ -1535,6 +1793,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                 A.v.b3[a3] = pv;
                 A.on.b3[a3] = p;
             }
+#endif
             if (A.img[0])
 #pragma unroll
                 for (int l = 0; l < 2; ++l) {
@@ -1598,8 +1857,9 @@ int se_qtrain_create(se_qtrain** out, se_env* env, int64_t max_batch) {
     q->max_tiles = (max_batch + kQT - 1) / kQT;
     const size_t T = (size_t)q->max_tiles;
     const size_t mt3 = (size_t)q->d.mt3;
-    const size_t sizes[] = {4 * 3 * 64, 4 * 3 * 64, 4 * 64 * 64, 4 * 64 * 64, 4 * 64 * 64,
-                            mt3 * 64 * 64, 128, 128, (size_t)(4 * P),
+    constexpr size_t kW = SHIPENV_QT_X3W ? 6 : 4;  // bytes per weight of fc2 / fc3's MFMA images
+    const size_t sizes[] = {4 * 3 * 64, 4 * 3 * 64, 4 * 64 * 16 * kW, 4 * 64 * 16 * kW, 4 * 64 * 64,
+                            mt3 * 16 * 64 * kW, 128, 128, (size_t)(4 * P),
                             T * 128 * 128, T * 128 * 6, T * 128, T * 128, T * 2, T * 32 * 128,
                             T * 32, T * 32};
     size_t total = 0, off[17];

@@ -255,9 +255,9 @@ struct Pick {
 };
 
 __device__ __forceinline__ Pick pick_transition(const Ring& ring, int64_t size, const U4& key, uint32_t h,
-                                                int64_t j, int64_t B) {
+                                                int64_t j, int64_t B, int k0 = 0) {
     Pick p{-1, 0u, 0u, 0.0f, 0.0f, 0.0f, 0, 0};
-    for (int k = 0; k < kReplayTries; ++k) {
+    for (int k = k0; k < kReplayTries; ++k) {
         const int64_t pos = j + (int64_t)k * B;
         if (pos >= size) break;
         const uint32_t l = feistel_perm((uint32_t)pos, (uint32_t)size, h, key.v);
@@ -274,6 +274,39 @@ __device__ __forceinline__ Pick pick_transition(const Ring& ring, int64_t size, 
         }
     }
     return p;
+}
+
+// pick_transition split in two: the first try's loads issued (no wait, so that loads issued
+// after them need not be waited for first), then the result, with the later tries only when
+// the first candidate is flagged. Same picks, bit for bit.
+struct PickFirst {
+    Pick p;
+    int64_t l;  // the first candidate's slot, -1 if row j has none (j >= size)
+};
+__device__ __forceinline__ PickFirst pick_issue(const Ring& ring, int64_t size, const U4& key, uint32_t h, int64_t j) {
+    PickFirst f{{-1, 0u, 0u, 0.0f, 0.0f, 0.0f, 0, 0}, -1};
+    if (j < size) {
+        const uint32_t l = feistel_perm((uint32_t)j, (uint32_t)size, h, key.v);
+        f.l = l;
+        f.p.fl = ring.flags[l];
+        f.p.sp = ring.s_pos[l];
+        f.p.sf = ring.s_fuel[l];
+        f.p.np = ring.n_pos[l];
+        f.p.nf = ring.n_fuel[l];
+        f.p.ac = ring.act[l];
+        f.p.rw = ring.rew[l];
+    }
+    return f;
+}
+__device__ __forceinline__ Pick pick_resolve(const PickFirst& f, const Ring& ring, int64_t size, const U4& key,
+                                             uint32_t h, int64_t j, int64_t B) {
+    if (f.l < 0) return f.p;  // slot -1
+    if (!(f.p.fl & kRecInvalid)) {
+        Pick p = f.p;
+        p.slot = f.l;
+        return p;
+    }
+    return pick_transition(ring, size, key, h, j, B, 1);  // (a slot -1 pick's fields are not read)
 }
 
 // kSampleRows transitions per workgroup. The first wave picks the slots, loading each

@@ -5,8 +5,8 @@ set -u
 O=gpurun_out/${1:-r05r}; mkdir -p $O
 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_policy.py tests/test_gpu_dqn.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
-PREC=bf16 ROUNDS=3 tools/ab_policy_r05.sh > $O/ab_policy_bf16.jsonl 2>$O/ab.err || exit 1
-PREC=f32 ROUNDS=3 tools/ab_policy_r05.sh > $O/ab_policy_f32.jsonl 2>>$O/ab.err || exit 1
+: > $O/ab.err
+PREC=f32 ROUNDS=2 bash tools/ab_policy_r05.sh > $O/ab_policy_f32.jsonl 2>>$O/ab.err || exit 1
 L=shippingenv_amd/_lib/libshipenv_hip.so
 for rep in 1 2; do
   for c in 3 5 6 4; do
