@@ -84,6 +84,10 @@ struct QtWork {
     float* part_w3;  // [tiles][32][128]: only the rows of live slots are stored
     float* part_b3;  // [tiles][32]
     int32_t* part_map; // [tiles][32]
+    // SHIPENV_QT_SLOT_TABLE: part_slot[a][t] = the slot of action a in tile t (0..31), 0xff when
+    // the tile has none; row stride slot_ld (the workspace's tile capacity)
+    uint8_t* part_slot;
+    int64_t slot_ld;
 };
 
 #ifndef SHIPENV_QT_NT
@@ -253,6 +257,18 @@ __device__ __forceinline__ void store_relu(float* dst, int tile, const f32x16& a
 #endif
 #ifndef SHIPENV_QT_PICK_FIRST
 #define SHIPENV_QT_PICK_FIRST 1  // T1: the minibatch picks' first ring loads ahead of the weight loads (0: after)
+#endif
+#ifndef SHIPENV_QT_BIAS_LATE
+#define SHIPENV_QT_BIAS_LATE 1  // T1: fc1's operands loaded first, fc2 / fc3's bias added after the chain (0: as initial values)
+#endif
+// T1 also writes each tile's action -> slot table column, so a W3 block of T2 reads one
+// coalesced 256-byte row of it instead of scanning every tile's 32-entry slot map (9.4 MB of
+// map lines across the W3 blocks at B = 8192); 0: the scan
+#ifndef SHIPENV_QT_SLOT_TABLE
+#define SHIPENV_QT_SLOT_TABLE SHIPENV_QT_X3
+#endif
+#if SHIPENV_QT_SLOT_TABLE && !SHIPENV_QT_X3
+#error "SHIPENV_QT_SLOT_TABLE needs SHIPENV_QT_X3 (its LDS map lives past the split fragments)"
 #endif
 #ifndef SHIPENV_QT_X3_SCHED
 #define SHIPENV_QT_X3_SCHED 1  // the next k-step's splits between the MFMAs of this one, fenced (0: the compiler's order)
@@ -551,6 +567,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     bf16x8* SH1 = reinterpret_cast<bf16x8*>(FST + 32);  // [2][8][3][64]
     bf16x8* SH2 = SH1 + 2 * 8 * 3 * 64;                  // [8][3][64]
     float* XP = reinterpret_cast<float*>(SH1);
+    int* MAPL = reinterpret_cast<int*>(SH2 + 8 * 3 * 64);  // [32] the tile's slot map
 #endif
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wt = wave & 3;
     const bool tgt = wave >= 4;
@@ -566,6 +583,12 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     // fc1's operands and fc2's fragments do not depend on the batch: their loads are in
     // flight while the inputs are staged
     const int net = tgt ? 1 : 0;
+#if SHIPENV_QT_BIAS_LATE
+    // fc1's operands first: behind the fragment loads, fc1 waited for all of them
+    Frags<3> f1;
+    f1.load(A.W.pw1[net] + wt * 3 * 64, lane);
+    f32x16 acc1 = bias_init(A.W.c1[net], wt, lane, 128);
+#endif
 #if SHIPENV_QT_PICK_FIRST
     // the first try of wave 0's minibatch picks: its ring loads go out ahead of the weights'
     // (the vector memory counter is in order: behind ~24 KB of fragments per wave they waited)
@@ -610,9 +633,11 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     Frags<64> fa, fb;  // fc2, then fc3 / W2^T: each loaded one layer ahead
     fa.load(A.W.pw2[net] + wt * 64 * 64, lane);
 #endif
+#if !SHIPENV_QT_BIAS_LATE
     Frags<3> f1;
     f1.load(A.W.pw1[net] + wt * 3 * 64, lane);
     f32x16 acc1 = bias_init(A.W.c1[net], wt, lane, 128);
+#endif
 
     if (A.from_ring) {  // the sampler's pick of row r0 + tid, straight into the tiles
         if (tid < 32) {
@@ -705,7 +730,14 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     // fc3's pre-split A operands of k-step g load once fc2's k-step g has consumed its own
     // (fenced, so that at most one k-step's worth more is live)
     bf16x8 wb[8][3];
+#if SHIPENV_QT_BIAS_LATE
+    // the chain starts at 0 and the bias is added after it, so its loads' round trip hides
+    // under the chain instead of holding its first MFMA
+    const f32x16 bias2 = bias_init(tgt ? A.tg.b2 : A.on.b2, wt, lane, 128);
+    f32x16 acc = {};
+#else
     f32x16 acc = bias_init(tgt ? A.tg.b2 : A.on.b2, wt, lane, 128);
+#endif
     {
         const bf16x8* S = SH1 + net * 8 * 3 * 64;
         const bf16x8* P3 = reinterpret_cast<const bf16x8*>(A.W.pw3t) + wave * 8 * 3 * 64;
@@ -729,6 +761,9 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             for (int q = 0; q < 3; ++q) wb[g][q] = P3[(g * 3 + q) * 64 + lane];
             __builtin_amdgcn_sched_barrier(0);
         }
+#if SHIPENV_QT_BIAS_LATE
+        acc += bias2;
+#endif
         if (tgt) store_split(SH2, wt, acc, lane);
         else store_relu(HB, wt, acc, lane);
     }
@@ -771,8 +806,13 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
                 for (int q = 0; q < 3; ++q) wx[u][q] = p[((2 * wt + u) * 3 + q) * 64 + lane];
             if (wt == 0) accx = bias_init(A.tg.b3, xt, lane, A.d.A);
         }
+#if SHIPENV_QT_BIAS_LATE
+        const f32x16 bias3 = bias_init(A.tg.b3, wave, lane, A.d.A);
+        f32x16 acc3 = gemm_x3w<8>(wb, SH2, 0, f32x16{}, lane) + bias3;
+#else
         f32x16 acc3 = bias_init(A.tg.b3, wave, lane, A.d.A);
         acc3 = gemm_x3w<8>(wb, SH2, 0, acc3, lane);
+#endif
 #else
         float4 wx[4];
         f32x16 accx = {};
@@ -1071,6 +1111,9 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             if (h == 0) {
                 st_part1(A.W.part_b3 + (int64_t)blockIdx.x * 32 + c, s3 + x3);
                 st_part1(A.W.part_map + (int64_t)blockIdx.x * 32 + c, live_slot ? (int32_t)ACT[c] : (int32_t)-1);
+#if SHIPENV_QT_SLOT_TABLE
+                MAPL[c] = live_slot ? (int32_t)ACT[c] : (int32_t)-1;
+#endif
             }
         }
 #else
@@ -1149,6 +1192,9 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             if (h == 0) {
                 st_part1(A.W.part_b3 + (int64_t)blockIdx.x * 32 + c, s3 + x3);
                 st_part1(A.W.part_map + (int64_t)blockIdx.x * 32 + c, live_slot ? (int32_t)ACT[c] : (int32_t)-1);
+#if SHIPENV_QT_SLOT_TABLE
+                MAPL[c] = live_slot ? (int32_t)ACT[c] : (int32_t)-1;
+#endif
             }
         }
 #endif
@@ -1187,6 +1233,21 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             st_part1(A.W.part_lw + 2 * blockIdx.x + 1, w);
         }
     }
+#if SHIPENV_QT_SLOT_TABLE
+    if (tid < 32 * A.d.mt3) {  // this tile's column of the action -> slot table
+        const int4* m4 = reinterpret_cast<const int4*>(MAPL);
+        int sl = 0xff;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int4 v = m4[i];
+            sl = v.x == tid ? 4 * i : sl;
+            sl = v.y == tid ? 4 * i + 1 : sl;
+            sl = v.z == tid ? 4 * i + 2 : sl;
+            sl = v.w == tid ? 4 * i + 3 : sl;
+        }
+        A.W.part_slot[(int64_t)tid * A.W.slot_ld + blockIdx.x] = (uint8_t)sl;
+    }
+#endif
     QSTAMP(9);
 }
 
@@ -1368,14 +1429,17 @@ __device__ __forceinline__ float tile_sum64(const float* src, int64_t stride, in
 // sums at most one partial per tile. Thread t < 128 returns dW3[a][t], thread 128 db3[a].
 template <int kU>
 __device__ __forceinline__ float slot_row_sum(const float* w3, const float* b3, const int32_t* map, int64_t tiles,
-                                              int a, float4* red, int* list, int* wtot) {
+                                              int a, float4* red, int* list, int* wtot, const uint8_t* slot_row) {
     const int t = threadIdx.x, q = t & 31, grp = t >> 5, lane = t & 63, w = t >> 6;
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     float accb = 0.0f;
     for (int64_t c0 = 0; c0 < tiles; c0 += kQRBlock) {
         const int64_t tt = c0 + t;
         int slot = -1;
-        if (tt < tiles) {
+        if (slot_row) {  // SHIPENV_QT_SLOT_TABLE: row a of the action -> slot table
+            const int v = tt < tiles ? (int)slot_row[tt] : 0xff;
+            slot = v == 0xff ? -1 : v;
+        } else if (tt < tiles) {
             const int4* mp = reinterpret_cast<const int4*>(map + tt * 32);
             int4 v[8];
 #pragma unroll
@@ -1764,7 +1828,8 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             if (tid < 128) g = G[Grad::w3 + i3];
             else if (tid == 128) g = G[Grad::b3(A.d) + a3];
         } else {
-            g = slot_row_sum<SHIPENV_QT_W3U>(A.W.part_w3, A.W.part_b3, A.W.part_map, A.tiles, a3, red4, list, wtot);
+            g = slot_row_sum<SHIPENV_QT_W3U>(A.W.part_w3, A.W.part_b3, A.W.part_map, A.tiles, a3, red4, list, wtot,
+                                             SHIPENV_QT_SLOT_TABLE ? A.W.part_slot + (int64_t)a3 * A.W.slot_ld : nullptr);
             if (mode == 1) {
                 if (tid < 128) G[Grad::w3 + i3] = g;
                 else if (tid == 128) G[Grad::b3(A.d) + a3] = g;
@@ -1861,9 +1926,9 @@ int se_qtrain_create(se_qtrain** out, se_env* env, int64_t max_batch) {
     const size_t sizes[] = {4 * 3 * 64, 4 * 3 * 64, 4 * 64 * 16 * kW, 4 * 64 * 16 * kW, 4 * 64 * 64,
                             mt3 * 16 * 64 * kW, 128, 128, (size_t)(4 * P),
                             T * 128 * 128, T * 128 * 6, T * 128, T * 128, T * 2, T * 32 * 128,
-                            T * 32, T * 32};
-    size_t total = 0, off[17];
-    for (int i = 0; i < 17; ++i) {
+                            T * 32, T * 32, (mt3 * 32 * T + 3) / 4};
+    size_t total = 0, off[18];
+    for (int i = 0; i < 18; ++i) {
         off[i] = total;
         total += (sizes[i] * 4 + 255) & ~(size_t)255;
     }
@@ -1875,7 +1940,7 @@ int se_qtrain_create(se_qtrain** out, se_env* env, int64_t max_batch) {
     auto at = [&](int i) { return b + off[i] / 4; };
     q->W = QtWork{{at(0), at(1)}, {at(2), at(3)}, at(4), at(5), {at(6), at(7)}, at(8),
                   at(9), at(10), at(11), at(12), at(13), at(14), at(15),
-                  reinterpret_cast<int32_t*>(at(16))};
+                  reinterpret_cast<int32_t*>(at(16)), reinterpret_cast<uint8_t*>(at(17)), (int64_t)T};
     *out = q;
     return SE_OK;
 }
@@ -1956,7 +2021,7 @@ int qtrain_step(se_qtrain* q, se_qnet* qn, int64_t batch, const float* obs, cons
     DeviceGuard g(q->device);
     const hipStream_t s = (hipStream_t)stream;
     const int64_t tiles = (batch + kQT - 1) / kQT;
-    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 8 * 32) * 4 + (SHIPENV_QT_X3 ? 3 * 8 * 3 * 64 * 16 : 0);
+    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 8 * 32) * 4 + (SHIPENV_QT_X3 ? 3 * 8 * 3 * 64 * 16 + 32 * 4 : 0);
     static std::atomic<uint64_t> lds_set{0};
     rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(qtrain_tile_kernel), (int)lds, q->device);
     if (rc) return rc;
