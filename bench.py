@@ -663,10 +663,11 @@ def run_dqn_train(n, args, dist):
         "stream_ms_per_step": round(kern_ms, 4),
         "update_ms": round(upd_ms, 4),
         "updates_per_s": round(1e3 / upd_ms, 1),
-        "update_roofline": {"bound": "mfma (f32)", "achieved": round(upd_tf, 2), "peak": F32_MFMA_PEAK_TFLOPS,
+        "update_roofline": {"bound": "mfma (f32 arithmetic; T1's forward on split-bf16 MFMA, its backward on f32 MFMA)",
+                            "achieved": round(upd_tf, 2), "peak": F32_MFMA_PEAK_TFLOPS,
                             "unit": "TFLOP/s", "frac": round(upd_tf / F32_MFMA_PEAK_TFLOPS, 4),
                             "flop_per_sample": flop,
-                            "note": "whole update: 2 kernels (T1 also draws the minibatch from the ring and advances the counter, T2 also rewrites the policy images)"},
+                            "note": "whole update: 2 kernels (T1 also draws the minibatch from the ring and advances the counter, T2 also rewrites the policy images); peak = the f32 MFMA peak, the precision the update computes in"},
         "batch": args.train_batch,
         "global_batch": args.train_batch * dist.world,
         "data_parallel": (f"dp{dist.world}: gradient SUM all-reduce of {agent._grad.numel()} f32 per update"
