@@ -30,7 +30,13 @@
 // after any edit that adds register pressure.
 
 #ifndef SHIPENV_POLICY_ABL
-#define SHIPENV_POLICY_ABL 0  // timing-only ablations of the policy kernel (1: plain max epilogue, 2: no fc3)
+#define SHIPENV_POLICY_ABL 0  // timing-only ablations of the policy kernel (1: plain max epilogue, 2: no fc3,
+                              // 4: no bias reads, 8: fc2 reads one fragment)
+#endif
+#if SHIPENV_POLICY_ABL == 4
+#define PBIAS(b) (f32x16{})
+#else
+#define PBIAS(b) bias_frag(b)
 #endif
 
 namespace {
@@ -488,7 +494,7 @@ void policy_kernel(PolicyArgs A) {
         bf16x8 h1[4][2], h2[4][2];
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {  // fc1 + relu
-            f32x16 c = bias_frag(B1 + mt * 32 + 4 * h);
+            f32x16 c = PBIAS(B1 + mt * 32 + 4 * h);
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(W1f[mt * 64 + lane], ob, c, 0, 0, 0);
             relu_pack(c, h1[mt]);
         }
@@ -507,7 +513,7 @@ void policy_kernel(PolicyArgs A) {
         for (int pass = 0; pass < SHIPENV_FC2_SPLIT; ++pass) {
             f32x16 c2[kFc2Tiles];
 #pragma unroll
-            for (int i = 0; i < kFc2Tiles; ++i) c2[i] = bias_frag(B2 + (pass * kFc2Tiles + i) * 32 + 4 * h);
+            for (int i = 0; i < kFc2Tiles; ++i) c2[i] = PBIAS(B2 + (pass * kFc2Tiles + i) * 32 + 4 * h);
 #if SHIPENV_POLICY_LOOKAHEAD > 0
             static_assert(kFc2Tiles == 1, "the fragment lookahead is written for one tile per pass");
             // the tile's 8 fragments read SHIPENV_POLICY_LOOKAHEAD k-steps ahead of their MFMA,
@@ -516,10 +522,10 @@ void policy_kernel(PolicyArgs A) {
             constexpr int L = SHIPENV_POLICY_LOOKAHEAD;
             bf16x8 wf[8];
 #pragma unroll
-            for (int k = 0; k < L; ++k) wf[k] = W2f[(pass * 8 + k) * 64 + lane];
+            for (int k = 0; k < L; ++k) wf[k] = W2f[(SHIPENV_POLICY_ABL == 8 ? 0 : (pass * 8 + k)) * 64 + lane];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                if (k + L < 8) wf[k + L] = W2f[(pass * 8 + k + L) * 64 + lane];
+                if (k + L < 8) wf[k + L] = W2f[(SHIPENV_POLICY_ABL == 8 ? 0 : (pass * 8 + k + L)) * 64 + lane];
                 c2[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k], h1[k >> 1][k & 1], c2[0], 0, 0, 0);
             }
 #pragma unroll
@@ -585,7 +591,7 @@ void policy_kernel(PolicyArgs A) {
             // without q_out (round 5): rows this env cannot take start at -inf (masked_bias), so
             // the first maximum below needs no validity test and no per-register branch
             constexpr bool kMasked = !kQout && SHIPENV_POLICY_MASKED;
-            f32x16 c = kMasked ? masked_bias(B3 + mt * 32 + 4 * h, m >> (4 * h)) : bias_frag(B3 + mt * 32 + 4 * h);
+            f32x16 c = kMasked ? masked_bias(B3 + mt * 32 + 4 * h, m >> (4 * h)) : PBIAS(B3 + mt * 32 + 4 * h);
 #pragma unroll
             for (int k = 0; k < 8; ++k)
                 c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k], h2[k >> 1][k & 1], c, 0, 0, 0);
@@ -912,11 +918,19 @@ __device__ __forceinline__ void split3(float v, __bf16& p0, __bf16& p1, __bf16& 
 struct Fc1Slot {
     int8_t col, wp, xp;  // xp: -1 = the exact input, else the fuel part
 };
+// SHIPENV_X3_BFOLD = 1: slots 24-26 hold the three bf16 parts of fc1's bias (b1 with the port
+// block folded, the image's f32 b1) times an input of 1.0 (col -2), so the chains start at 0 and
+// no bias is read from LDS (4 x 16-byte reads per row tile and env tile). Measured even or
+// slower (0.2776 vs 0.2751 ms per call, medians of 4 alternating runs,
+// profiles/r05/ab_policy_f32_bias_fold.jsonl): not kept.
+#ifndef SHIPENV_X3_BFOLD
+#define SHIPENV_X3_BFOLD 0
+#endif
 __host__ __device__ constexpr Fc1Slot x3_fc1_slot(int k) {
     constexpr Fc1Slot t[24] = {{0, 0, -1}, {1, 0, -1}, {4, 0, -1}, {5, 0, -1}, {0, 1, -1}, {1, 1, -1}, {4, 1, -1}, {5, 1, -1},
                                {0, 2, -1}, {1, 2, -1}, {4, 2, -1}, {5, 2, -1}, {2, 0, 0},  {2, 0, 1},  {2, 1, 0},  {2, 0, 2},
                                {2, 1, 1},  {2, 2, 0},  {3, 0, 0},  {3, 0, 1},  {3, 1, 0},  {3, 0, 2},  {3, 1, 1},  {3, 2, 0}};
-    return k < 24 ? t[k] : Fc1Slot{-1, 0, 0};
+    return k < 24 ? t[k] : (SHIPENV_X3_BFOLD && k < 27 ? Fc1Slot{-2, (int8_t)(k - 24), -1} : Fc1Slot{-1, 0, 0});
 }
 
 struct PackX3Args {
@@ -931,6 +945,19 @@ struct PackX3Args {
 // bias entry, same-cell mask and epilogue register mask (the latter as qnet_pack_f32_kernel).
 // items [first, total) step `stride` of the split image into img (global memory for
 // qnet_pack_x3_kernel, the workgroup's LDS for policy_x3_kernel's own prologue)
+// b1[f] + W1[f, 6:] . the port block, in f64 then f32 (qnet_pack_kernel's fold)
+__device__ __forceinline__ float x3_fold_b1(const PackX3Args& A, int f) {
+    const LdsWorld wv = world_view(A.dims, A.world);
+    const int in1 = A.d.q.in1();
+    double acc = (double)A.b1[f];
+    for (int p = 0; p < A.d.q.P; ++p) {
+        const float* w = A.w1 + f * in1 + 6 + 4 * p;
+        acc += (double)w[0] * (double)wv.px(p) + (double)w[1] * (double)wv.py(p) + (double)w[2] * (double)wv.pfuel(p) +
+               (double)w[3] * (double)wv.pcargo(p);
+    }
+    return (float)acc;
+}
+
 __device__ __forceinline__ void pack_x3_items(const PackX3Args& A, uint8_t* img, int first, int stride) {
     const QnetX3Dims d = A.d;
     const QnetDims q = d.q;
@@ -943,11 +970,14 @@ __device__ __forceinline__ void pack_x3_items(const PackX3Args& A, uint8_t* img,
             if (SHIPENV_X3_FC1) {  // fc1 fragment (mt, step, lane): element j = slot 16 step + 8h + j
                 const int st = (t >> 6) & 1, mt = t >> 7, row = mt * 32 + (lane & 31);
                 bf16x8 v;
+                float b1f = 0.0f;  // the row's fc1 bias (as the image's b1 below), for the folded slots
+                if (SHIPENV_X3_BFOLD && st == 1 && (lane >> 5)) b1f = x3_fold_b1(A, row);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const Fc1Slot sl = x3_fc1_slot(16 * st + 8 * (lane >> 5) + j);
                     __bf16 p0 = (__bf16)0.0f, p1 = p0, p2 = p0;
                     if (sl.col >= 0) split3(A.w1[row * in1 + sl.col], p0, p1, p2);
+                    else if (sl.col == -2) split3(b1f, p0, p1, p2);
                     v[j] = sl.wp == 0 ? p0 : (sl.wp == 1 ? p1 : p2);
                 }
                 reinterpret_cast<bf16x8*>(img + d.w1())[t] = v;
@@ -985,13 +1015,7 @@ __device__ __forceinline__ void pack_x3_items(const PackX3Args& A, uint8_t* img,
         const LdsWorld wv = world_view(A.dims, A.world);
         const int P = q.P;
         if (u < kQHidden) {  // b1 + fc1 over the constant port block, in f64 then f32
-            double acc = (double)A.b1[u];
-            for (int p = 0; p < P; ++p) {
-                const float* w = A.w1 + u * in1 + 6 + 4 * p;
-                acc += (double)w[0] * (double)wv.px(p) + (double)w[1] * (double)wv.py(p) +
-                       (double)w[2] * (double)wv.pfuel(p) + (double)w[3] * (double)wv.pcargo(p);
-            }
-            reinterpret_cast<float*>(img + d.b1())[u] = (float)acc;
+            reinterpret_cast<float*>(img + d.b1())[u] = x3_fold_b1(A, u);
         } else if ((u -= kQHidden) < kQHidden) {
             reinterpret_cast<float*>(img + d.b2())[u] = A.b2[u];
         } else if ((u -= kQHidden) < q.mt3 * 32) {
@@ -1200,7 +1224,7 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
     const float* W1 = reinterpret_cast<const float*>(qb + D.w1());
     const bf16x8* W2 = reinterpret_cast<const bf16x8*>(qb + D.w2());
     const bf16x8* W3 = reinterpret_cast<const bf16x8*>((kW3Global ? reinterpret_cast<const uint8_t*>(A.qimg) : qb) + D.w3());
-    const float* B1 = reinterpret_cast<const float*>(qb + D.b1());
+    [[maybe_unused]] const float* B1 = reinterpret_cast<const float*>(qb + D.b1());
     const float* B2 = reinterpret_cast<const float*>(qb + D.b2());
     const float* B3 = reinterpret_cast<const float*>(qb + D.b3());
     const uint64_t* SAME = reinterpret_cast<const uint64_t*>(qb + D.same());
@@ -1277,8 +1301,8 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const Fc1Slot a = x3_fc1_slot(16 * st + j), b = x3_fc1_slot(16 * st + 8 + j);
-                    const __bf16 va = a.col < 0 ? (__bf16)0.0f : (a.xp < 0 ? ex[a.col] : fp[a.xp]);
-                    const __bf16 vb = b.col < 0 ? (__bf16)0.0f : (b.xp < 0 ? ex[b.col] : fp[b.xp]);
+                    const __bf16 va = a.col == -2 ? (__bf16)1.0f : a.col < 0 ? (__bf16)0.0f : (a.xp < 0 ? ex[a.col] : fp[a.xp]);
+                    const __bf16 vb = b.col == -2 ? (__bf16)1.0f : b.col < 0 ? (__bf16)0.0f : (b.xp < 0 ? ex[b.col] : fp[b.xp]);
                     xin[st][j] = h ? vb : va;
                 }
         }
@@ -1286,7 +1310,11 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
 #endif
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {  // fc1 (x, y | fuel, fuel | origin, dest)
+#if SHIPENV_X3_FC1 && SHIPENV_X3_BFOLD
+            c1[mt] = f32x16{};  // the bias is in the fragments (slots 24-26)
+#else
             c1[mt] = bias_frag(B1 + mt * 32 + 4 * h);
+#endif
 #if SHIPENV_X3_FC1
             c1[mt] = mfma_bf16(W1b[(mt * 2 + 0) * 64 + lane], xin[0], c1[mt]);
             c1[mt] = mfma_bf16(W1b[(mt * 2 + 1) * 64 + lane], xin[1], c1[mt]);
