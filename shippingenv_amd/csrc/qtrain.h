@@ -255,6 +255,20 @@ __device__ __forceinline__ void store_relu(float* dst, int tile, const f32x16& a
 #if SHIPENV_QT_X3W && !SHIPENV_QT_X3
 #error "SHIPENV_QT_X3W needs SHIPENV_QT_X3"
 #endif
+// 1: dW2 and dW3 (the target waves' part of the backward) on split-bf16 MFMA over K = 32
+// samples, with operands split once into sample-major LDS tiles by transposing passes in
+// phases that already exist (h1 and h2 in the q / g phase, dZ2 by the dZ2 phase itself, which
+// then takes one feature and 8 samples per thread): 12 MFMAs of 32 cycles per 32 x 32 tile
+// where the f32 MFMA ran 16 of 64. dH1 stays on f32 MFMA. Needs SHIPENV_QT_X3, not _X3B.
+// Measured slower: 34.0 -> 37.3 us per update back to back, the backward phase 6.9 -> 9.0 us
+// in the stamped build, and the untouched input / fc1 phases slower too
+// (profiles/r05/time_update_x3bt.jsonl, qtrace_x3bt.jsonl): not kept.
+#ifndef SHIPENV_QT_X3BT
+#define SHIPENV_QT_X3BT 0
+#endif
+#if SHIPENV_QT_X3BT && (!SHIPENV_QT_X3 || SHIPENV_QT_X3B)
+#error "SHIPENV_QT_X3BT needs SHIPENV_QT_X3 and excludes SHIPENV_QT_X3B"
+#endif
 #ifndef SHIPENV_QT_PICK_FIRST
 #define SHIPENV_QT_PICK_FIRST 1  // T1: the minibatch picks' first ring loads ahead of the weight loads (0: after)
 #endif
@@ -330,6 +344,30 @@ __device__ __forceinline__ void split8_half(const float4& a, const float4& b, bf
         w[2][2 * q] = p2[0];
         w[2][2 * q + 1] = p2[1];
     }
+}
+
+// sample-major split tiles: [part][feature][32 samples] bf16, 64-byte rows of four 16-byte chunks
+// (8 samples each), chunk k of row r stored at chunk slot k ^ ((r >> 2) & 3), so that 16
+// consecutive rows' chunk k (one 16-lane pass of a fragment read) fall in 16 distinct bank groups
+__device__ __forceinline__ int tslot(int row, int chunk) { return row * 4 + (chunk ^ ((row >> 2) & 3)); }
+constexpr int kTS = 32;
+// eight f32 values -> their three bf16 parts, stored as chunk slot `slot` of the three parts'
+// sample-major split tiles (parts 128 x 32 elements apart)
+__device__ __forceinline__ void t_split8(const float (&v)[8], __bf16* T, int slot) {
+    __bf16* dst = T + 8 * slot;
+    bf16x8 w[3];
+    const float4 x = make_float4(v[0], v[1], v[2], v[3]), y = make_float4(v[4], v[5], v[6], v[7]);
+    split8_half(x, y, w, 0);
+    split8_half(x, y, w, 1);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) *reinterpret_cast<bf16x8*>(dst + p * 128 * kTS) = w[p];
+}
+// the same from eight consecutive floats of an f32 LDS tile row
+__device__ __forceinline__ void t_split_row(const float* src, __bf16* T, int slot) {
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = src[i];
+    t_split8(v, T, slot);
 }
 
 // acc + W X over k-steps [g0, g0 + G): W from f32 registers wa[2 (g - g0)], [2 (g - g0) + 1]
@@ -566,8 +604,21 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     // the h1 fragments once fc2 is done
     bf16x8* SH1 = reinterpret_cast<bf16x8*>(FST + 32);  // [2][8][3][64]
     bf16x8* SH2 = SH1 + 2 * 8 * 3 * 64;                  // [8][3][64]
+#if SHIPENV_QT_X3BT
+    float* XP = TA;  // TA and TB (33.8 KB) are unused until dZ2 in this form; SH1 takes the transposes
+#else
     float* XP = reinterpret_cast<float*>(SH1);
+#endif
     int* MAPL = reinterpret_cast<int*>(SH2 + 8 * 3 * 64);  // [32] the tile's slot map
+#if SHIPENV_QT_X3BT
+    // sample-major split tiles [part][feature][32 samples] bf16 (64 B rows): h1 and h2 of the
+    // online net in the h1 fragments' space once fc2 and fc3 are done, dZ2 in the target h2
+    // fragments' space; g's parts [part][32]
+    __bf16* HTs = reinterpret_cast<__bf16*>(SH1);
+    __bf16* H2Ts = HTs + 3 * 128 * kTS;
+    __bf16* DZ2Ts = reinterpret_cast<__bf16*>(SH2);
+    __bf16* GS = reinterpret_cast<__bf16*>(MAPL + 32);
+#endif
 #endif
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wt = wave & 3;
     const bool tgt = wave >= 4;
@@ -713,6 +764,13 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) w3s[k] = w3r[k];
     }
+#endif
+#if SHIPENV_QT_X3BT
+    // the dZ2 phase's slice: feature tf = tid >> 2 of samples 8 tg .. 8 tg + 7
+    const int tf = tid >> 2, tg = tid & 3;
+    float w3g[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w3g[i] = A.on.w3[(int64_t)ACT[8 * tg + i] * 128 + tf];
 #endif
 
 #if SHIPENV_QT_X3
@@ -964,6 +1022,14 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             Y[tid] = row < A.B ? RW[tid] + (A.gamma * mx) * (1.0f - DN[tid]) : 0.0f;
         }
     }
+#if SHIPENV_QT_X3BT
+    else {  // the idle waves: h1 and h2 (online, relu'd f32 tiles) into the sample-major split tiles
+        for (int it = tid - 64; it < 2 * 512; it += kQTBlock - 64) {
+            const int which = it >> 9, f = (it >> 2) & 127, g8 = it & 3;
+            t_split_row((which ? HB : HA) + f * kLS + 8 * g8, which ? H2Ts : HTs, tslot(f, g8));
+        }
+    }
+#endif
     __syncthreads(); QSTAMP(5);
 
     // q_j = W3[a_j] . h2_j + b3[a_j]; g_j = 2 w_j (q_j - y_j): 16 threads per sample
@@ -993,11 +1059,30 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             const float d = (s + A.on.b3[ACT[qj]]) - Y[qj];
             G[qj] = 2.0f * WT[qj] * d;
             LW[qj] = WT[qj] * d * d;
+#if SHIPENV_QT_X3BT
+            __bf16 g0, g1, g2;
+            split3(G[qj], g0, g1, g2);
+            GS[qj] = g0;
+            GS[32 + qj] = g1;
+            GS[64 + qj] = g2;
+#endif
         }
     }
     __syncthreads(); QSTAMP(6);
     // dZ2 = (h2 > 0) g_j W3[a_j] (into the target's dead h1 buffer; with SHIPENV_QT_X3B also
     // split into dH1's B fragments, in the target h2's dead fragments)
+#if SHIPENV_QT_X3BT
+    {  // feature tf of samples 8 tg .. + 7: the f32 tile (dH1, db2) and its sample-major split (dW2)
+        float d[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int j = 8 * tg + i;
+            d[i] = HB[tf * kLS + j] > 0.0f ? G[j] * w3g[i] : 0.0f;
+            DZ2[tf * kLS + j] = d[i];
+        }
+        t_split8(d, DZ2Ts, tslot(tf, tg));
+    }
+#else
     {
         const float g = G[qj];
         float d[8];
@@ -1015,6 +1100,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         for (int p = 0; p < 3; ++p) SH2[((qpart >> 1) * 3 + p) * 64 + qj + 32 * (qpart & 1)] = sp[p];
 #endif
     }
+#endif
     __syncthreads(); QSTAMP(7);
 
     const int h = lane >> 5, c = lane & 31;
@@ -1107,6 +1193,92 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             float s3 = 0.0f;
 #pragma unroll
             for (int k = 0; k < 16; ++k) s3 += av[k];
+            const float x3 = __shfl_xor(s3, 32);
+            if (h == 0) {
+                st_part1(A.W.part_b3 + (int64_t)blockIdx.x * 32 + c, s3 + x3);
+                st_part1(A.W.part_map + (int64_t)blockIdx.x * 32 + c, live_slot ? (int32_t)ACT[c] : (int32_t)-1);
+#if SHIPENV_QT_SLOT_TABLE
+                MAPL[c] = live_slot ? (int32_t)ACT[c] : (int32_t)-1;
+#endif
+            }
+        }
+#elif SHIPENV_QT_X3BT
+        // partial dW2 (as H1 dZ2^T: f1 tile wt, 4 f2 tiles) and dW3 (as H2 G^T over the tile's
+        // slots) on split-bf16 MFMAs over K = 32 samples (two k-steps of 16): lane (r, h) of an
+        // operand holds samples 16 u + 8 h + 0..7 of its row, three 16-byte reads of the
+        // sample-major split tiles. The accumulators are laid out as before, so are the stores.
+        auto tfrag = [&](const __bf16* T, int row, int u, bf16x8 (&w)[3]) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                w[p] = *reinterpret_cast<const bf16x8*>(T + p * 128 * kTS + 8 * tslot(row, 2 * u + h));
+        };
+        auto x3_k32 = [&](const bf16x8 (&a)[2][3], const bf16x8 (&b)[2][3]) {
+            f32x16 acc = {};
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                acc = mfma_bf16(a[u][0], b[u][2], acc);
+                acc = mfma_bf16(a[u][1], b[u][1], acc);
+                acc = mfma_bf16(a[u][2], b[u][0], acc);
+                acc = mfma_bf16(a[u][0], b[u][1], acc);
+                acc = mfma_bf16(a[u][1], b[u][0], acc);
+                acc = mfma_bf16(a[u][0], b[u][0], acc);
+            }
+            return acc;
+        };
+        float* out = A.W.part_w2 + (int64_t)blockIdx.x * 128 * 128;
+        bf16x8 a2[2][3], b2[2][3];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) tfrag(HTs, wt * 32 + c, u, a2[u]);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) tfrag(DZ2Ts, ct * 32 + c, u, b2[u]);
+            const f32x16 acc = x3_k32(a2, b2);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)  // f1 = 32 wt + acc_r(4q + m, lane) = 32 wt + 8q + 4h + m
+#if SHIPENV_QT_ABL & 1  // timing only: the dW2 partials computed, not stored
+                if (A.B < 0)
+#endif
+                st_part4(out, (uint32_t)((ct * 32 + c) * 128 + wt * 32 + 8 * q + 4 * h), acc[4 * q], acc[4 * q + 1],
+                         acc[4 * q + 2], acc[4 * q + 3]);
+        }
+        // dW3: slot c = sum_j [first(j) = c] g_j h2[f][j]; B lane (c, h): g's parts of samples
+        // 16 u + 8 h + k where slot c is first(j), else 0
+        const bool live_slot = FST[c] == c && r0 + c < A.B;
+        const uint32_t slots = (uint32_t)__ballot(live_slot);  // lanes 0-31 = slots 0-31
+        float s3 = 0.0f;  // db3 of slot c over this lane half's 16 samples
+        bf16x8 bv[2][3], gv[2][3];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            tfrag(H2Ts, wt * 32 + c, u, bv[u]);
+            uint32_t keep[4];  // 16-bit lane masks of the 8 samples, two per word
+#pragma unroll
+            for (int k2 = 0; k2 < 4; ++k2) {
+                const int j = 16 * u + 8 * h + 2 * k2;
+                const bool m0 = FST[j] == c, m1 = FST[j + 1] == c;
+                keep[k2] = (m0 ? 0x0000ffffu : 0u) | (m1 ? 0xffff0000u : 0u);
+                s3 += m0 ? G[j] : 0.0f;
+                s3 += m1 ? G[j + 1] : 0.0f;
+            }
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                u32x4 w = __builtin_bit_cast(u32x4, *reinterpret_cast<const bf16x8*>(GS + p * 32 + 16 * u + 8 * h));
+#pragma unroll
+                for (int k2 = 0; k2 < 4; ++k2) w[k2] &= keep[k2];
+                gv[u][p] = __builtin_bit_cast(bf16x8, w);
+            }
+        }
+        const f32x16 acc = x3_k32(bv, gv);
+        float* o3 = A.W.part_w3 + (int64_t)blockIdx.x * 32 * 128;
+#if SHIPENV_QT_ABL & 2  // timing only: the dW3 partials computed, not stored
+        if (A.B < 0)
+#endif
+        if ((slots >> c) & 1u)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                st_part4(o3, (uint32_t)(c * 128 + wt * 32 + 8 * q + 4 * h), acc[4 * q], acc[4 * q + 1], acc[4 * q + 2],
+                         acc[4 * q + 3]);
+        if (wt == 0) {  // db3 of slot c: this lane half's 16 samples, then the other half's
             const float x3 = __shfl_xor(s3, 32);
             if (h == 0) {
                 st_part1(A.W.part_b3 + (int64_t)blockIdx.x * 32 + c, s3 + x3);
@@ -2021,7 +2193,7 @@ int qtrain_step(se_qtrain* q, se_qnet* qn, int64_t batch, const float* obs, cons
     DeviceGuard g(q->device);
     const hipStream_t s = (hipStream_t)stream;
     const int64_t tiles = (batch + kQT - 1) / kQT;
-    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 8 * 32) * 4 + (SHIPENV_QT_X3 ? 3 * 8 * 3 * 64 * 16 + 32 * 4 : 0);
+    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 8 * 32) * 4 + (SHIPENV_QT_X3 ? 3 * 8 * 3 * 64 * 16 + 32 * 4 + 256 : 0);
     static std::atomic<uint64_t> lds_set{0};
     rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(qtrain_tile_kernel), (int)lds, q->device);
     if (rc) return rc;
