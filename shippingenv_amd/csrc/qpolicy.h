@@ -923,6 +923,9 @@ struct Fc1Slot {
 // no bias is read from LDS (4 x 16-byte reads per row tile and env tile). Measured even or
 // slower (0.2776 vs 0.2751 ms per call, medians of 4 alternating runs,
 // profiles/r05/ab_policy_f32_bias_fold.jsonl): not kept.
+#ifndef SHIPENV_X3_PACK_VEC
+#define SHIPENV_X3_PACK_VEC 1  // pack_x3_items: fc2 / fc3 items with float4 loads and paired splits (0: per element)
+#endif
 #ifndef SHIPENV_X3_BFOLD
 #define SHIPENV_X3_BFOLD 0
 #endif
@@ -964,7 +967,43 @@ __device__ __forceinline__ void pack_x3_items(const PackX3Args& A, uint8_t* img,
     const int in1 = q.in1();
     const int n_w1 = SHIPENV_X3_FC1 ? 4 * 2 * 64 : 4 * 3 * 64, n_w2 = 32 * 64, n_w3 = q.mt3 * 8 * 64;
     const int total = n_w1 + n_w2 + n_w3 + 2 * kQHidden + q.mt3 * 32 + q.P + q.mt3;
+#if SHIPENV_X3_PACK_VEC
+    // fc2 / fc3 fragments first, in a loop of their own: an item's 8 weights are two float4
+    // loads (elements 0-3 and 4-7 are consecutive columns), split as pairs, and two items'
+    // loads go out together. Same bits as the per-element split3 below.
+#pragma unroll 2
+    for (int u0 = first; u0 < n_w2 + n_w3; u0 += stride) {
+        const bool second = u0 < n_w2;
+        const int u = second ? u0 : u0 - n_w2;
+        const int f = u >> 6, lane = u & 63, r = lane & 31, h = lane >> 5;
+        const int s = f & 1, kt = (f >> 1) & 3, mt = f >> 3;
+        const int row = mt * 32 + r;
+        const bool in = second || row < q.rows;
+        const float* W = second ? A.w2 : A.w3;
+        const int wrow = second ? row : (in ? q.action_of_row(row) : 0);
+        const float4* src = reinterpret_cast<const float4*>(W + wrow * kQHidden + kt * 32 + acc_row(s, 0, h));
+        float4 a = src[0], b = src[2];  // columns acc_row(s, 0..3, h) and acc_row(s, 4..7, h) = +8
+        if (!in) a = b = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        u32x4 w[3];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const f32x2 x{v[2 * k], v[2 * k + 1]};
+            const bf16x2 p0 = __builtin_convertvector(x, bf16x2);
+            const f32x2 r1 = x - __builtin_convertvector(p0, f32x2);
+            const bf16x2 p1 = __builtin_convertvector(r1, bf16x2);
+            const bf16x2 p2 = __builtin_convertvector(r1 - __builtin_convertvector(p1, f32x2), bf16x2);
+            w[0][k] = __builtin_bit_cast(uint32_t, p0);
+            w[1][k] = __builtin_bit_cast(uint32_t, p1);
+            w[2][k] = __builtin_bit_cast(uint32_t, p2);
+        }
+        uint8_t* dst = img + (second ? d.w2() : d.w3()) + f * 3 * 1024 + lane * 16;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) *reinterpret_cast<u32x4*>(dst + k * 1024) = w[k];
+    }
+#endif
     for (int t = first; t < total; t += stride) {
+        if (SHIPENV_X3_PACK_VEC && t >= n_w1 && t < n_w1 + n_w2 + n_w3) continue;  // packed above
         if (t < n_w1) {
             const int lane = t & 63;
             if (SHIPENV_X3_FC1) {  // fc1 fragment (mt, step, lane): element j = slot 16 step + 8h + j
@@ -1104,7 +1143,7 @@ __device__ __forceinline__ f32x16 kstep_x3(const bf16x8* Wf, int lane, const bf1
 #define SHIPENV_X3_STAGGER 0  // experiment: waves 4-7 sleep this many x 6400 cycles first
 #endif
 #ifndef SHIPENV_X3_PRIO
-#define SHIPENV_X3_PRIO 0  // experiment: waves 4-7 at issue priority 1
+#define SHIPENV_X3_PRIO 1  // waves 4-7 (each SIMD's second wave) at issue priority 1: 0.5-1.6 % faster in three alternating A/Bs (ab_policy_r05m/n, ab_policy_f32_pack_vec.jsonl); 0: off
 #endif
 #ifndef SHIPENV_X3_SCHED
 #define SHIPENV_X3_SCHED 1  // 0: the layers in plain order (the scheduler's own interleave)
@@ -1209,6 +1248,20 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
     extern __shared__ uint4 smem[];
     const PolicyArgs& A = F.p;
     const QnetDims q = D.q;
+    // the first tile's env state (an HBM round trip) is requested before the image is built,
+    // so the two overlap
+    const int lane = threadIdx.x & 63, h = lane >> 5;
+    const int64_t tiles = (A.n + 31) >> 5;
+    struct EnvIn {
+        double fuel;
+        uint32_t x8, y8, o8, d8;
+    };
+    auto load_env = [&](int64_t t) {
+        const int64_t ei = min(t * 32 + (lane & 31), A.n - 1);
+        return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei]};
+    };
+    int64_t tile = (int64_t)blockIdx.x * kPolicyX3Waves + (threadIdx.x >> 6);
+    EnvIn nxt = load_env(tile < tiles ? tile : 0);
     if constexpr (kW3Global) {  // fc3 stays in the packed global image: copy the rest
         const int staged = D.w3() / 16;
         for (int i = threadIdx.x; i < staged; i += kPolicyX3Block) smem[i] = A.qimg[i];
@@ -1230,22 +1283,11 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
     const uint64_t* SAME = reinterpret_cast<const uint64_t*>(qb + D.same());
     const uint32_t* REGM = reinterpret_cast<const uint32_t*>(qb + D.regm());
 
-    const int lane = threadIdx.x & 63, h = lane >> 5;
     const int P = q.P;
-    const int64_t tiles = (A.n + 31) >> 5;
     const int64_t stride = (int64_t)gridDim.x * kPolicyX3Waves;
     // the env state of the wave's next tile is loaded while this one computes (no HBM round
     // trip at the top of a tile), and its validity (the port on the ship's cell and that
     // port's stocks, two dependent L2 reads of the world image) resolved during fc3
-    struct EnvIn {
-        double fuel;
-        uint32_t x8, y8, o8, d8;
-    };
-    auto load_env = [&](int64_t t) {
-        const int64_t ei = min(t * 32 + (lane & 31), A.n - 1);
-        return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei]};
-    };
-    int64_t tile = (int64_t)blockIdx.x * kPolicyX3Waves + (threadIdx.x >> 6);
 #if SHIPENV_X3_PRIO
     if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
@@ -1257,7 +1299,6 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
         for (int i = 0; i < SHIPENV_X3_STAGGER; ++i) __builtin_amdgcn_s_sleep(100);
     }
 #endif
-    EnvIn nxt = load_env(tile < tiles ? tile : 0);
     EnvValid vnxt = env_valid(w, q, SAME, (int)nxt.x8, (int)nxt.y8, nxt.o8 == SE_NONE ? -1 : (int)nxt.o8);
     for (; tile < tiles; tile += stride) {
         const EnvIn in = nxt;
