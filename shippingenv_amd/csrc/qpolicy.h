@@ -1143,7 +1143,7 @@ __device__ __forceinline__ f32x16 kstep_x3(const bf16x8* Wf, int lane, const bf1
 #define SHIPENV_X3_STAGGER 0  // experiment: waves 4-7 sleep this many x 6400 cycles first
 #endif
 #ifndef SHIPENV_X3_PRIO
-#define SHIPENV_X3_PRIO 1  // waves 4-7 (each SIMD's second wave) at issue priority 1: 0.5-1.6 % faster in three alternating A/Bs (ab_policy_r05m/n, ab_policy_f32_pack_vec.jsonl); 0: off
+#define SHIPENV_X3_PRIO 1  // waves 4-7 (each SIMD's second wave) at issue priority 1: 0.3-1.6 % faster in three alternating A/Bs (profiles/r05/ab_policy_f32_fused_fc1.jsonl, _bias_fold.jsonl, _pack_vec.jsonl); even in round 5's first (ab_policy_r05m.jsonl); 0: off
 #endif
 #ifndef SHIPENV_X3_SCHED
 #define SHIPENV_X3_SCHED 1  // 0: the layers in plain order (the scheduler's own interleave)
