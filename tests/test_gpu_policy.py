@@ -353,3 +353,35 @@ def test_f32_sees_in_place_weight_updates(ports):
     np.testing.assert_array_equal(full, first_masked_argmax(q_out.cpu().numpy(), valid))
     np.testing.assert_array_equal(compact, full)
     assert (compact != before.cpu().numpy()).mean() > 0.1
+
+
+@pytest.mark.parametrize("ports", [None, "64"])
+def test_f32_unaligned_weights_choose_as_aligned(ports):
+    """The split image's fc2 / fc3 items load their weights as float4 when both matrices are
+    16-byte aligned (csrc/qpolicy.h pack_x3_items) and element by element otherwise: weights
+    bound 4 bytes past an aligned address choose the same actions and write the same Q rows."""
+    from conftest import golden_water
+    from shippingenv_amd import _native as N
+    from shippingenv_amd.policy import _ptr
+    from shippingenv_amd.vec import random_water_ports
+
+    if ports == "64":
+        ports = random_water_ports(golden_water(), 64, seed=3)
+    env, model, pol = make(4096 + 33, ports=ports, steps=5, scale=20.0)
+    q_a = torch.empty((env.n, env.action_space_size), dtype=torch.float32, device=env.device)
+    full_a = pol.act(0.0, 7, q_out=q_a, precision="f32").clone()
+    compact_a = pol.act(0.0, 7, precision="f32").clone()
+    shifted = []
+    for w in pol._w:
+        buf = torch.empty(w.numel() + 1, dtype=torch.float32, device=w.device)
+        v = buf[1:].view(w.shape)
+        v.copy_(w)
+        assert v.data_ptr() % 16 == 4
+        shifted.append(v)
+    pol._w = shifted  # keep them alive
+    N.check(N.lib().se_qnet_set_weights(pol._h, *[_ptr(t) for t in shifted], env._stream()))
+    q_b = torch.empty_like(q_a)
+    full_b = pol.act(0.0, 7, q_out=q_b, precision="f32")
+    compact_b = pol.act(0.0, 7, precision="f32")
+    assert torch.equal(full_a, full_b) and torch.equal(compact_a, compact_b)
+    assert torch.equal(q_a, q_b)
