@@ -427,6 +427,9 @@ __device__ __forceinline__ void finish_env(const QnetDims& q, const EnvValid& v,
     }
 }
 
+#ifndef SHIPENV_POLICY_EARLY_ENV
+#define SHIPENV_POLICY_EARLY_ENV 0  // 1: the first tile's env loads before the image / world staging: 64.9 vs 64.45 us (profiles/r05/ab_policy_bf16_early_env.jsonl), not kept
+#endif
 #ifndef SHIPENV_POLICY_MASKED
 #define SHIPENV_POLICY_MASKED 0  // 1: masked -inf fc3 bias + branch-free argmax (63.5 vs 63.4 us, profiles/r05/ab_policy_bf16_masked.jsonl: not kept); 0: the round-4 epilogue
 #endif
@@ -438,6 +441,24 @@ __attribute__((amdgpu_waves_per_eu(SHIPENV_POLICY_WAVES_PER_EU)))
 void policy_kernel(PolicyArgs A) {
     extern __shared__ uint4 smem[];
     const QnetDims q = A.q;
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+    const int64_t tiles = (A.n + 31) >> 5;
+    // env state of one tile (lane & 31 = env); the next tile's is loaded while this one
+    // computes, so the wave does not wait on HBM at the top of every tile. The first tile's
+    // loads go out before the network image and the world are staged, so they overlap.
+    struct EnvIn {
+        double fuel;
+        uint32_t x, y, o8, d8;
+    };
+    auto load_env = [&](int64_t tile) {
+        const int64_t e = tile * 32 + r;
+        const int64_t ei = e < A.n ? e : A.n - 1;
+        return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei]};
+    };
+    int64_t tile = (int64_t)blockIdx.x * kPolicyWaves + (threadIdx.x >> 6);
+#if SHIPENV_POLICY_EARLY_ENV
+    EnvIn nxt = load_env(tile < tiles ? tile : 0);
+#endif
     const int qwords = q.bytes() / 16;
     for (int i = threadIdx.x; i < qwords; i += kPolicyBlock) smem[i] = A.qimg[i];
     const LdsWorld w = stage_world(A.world, A.dims, reinterpret_cast<uint32_t*>(smem + qwords));
@@ -451,23 +472,11 @@ void policy_kernel(PolicyArgs A) {
     const uint64_t* SAME = reinterpret_cast<const uint64_t*>(qb + q.same());
     const uint32_t* REGM = reinterpret_cast<const uint32_t*>(qb + q.regm());
 
-    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
     const int P = q.P;
-    const int64_t tiles = (A.n + 31) >> 5;
     const int64_t stride = (int64_t)gridDim.x * kPolicyWaves;
-    // env state of one tile (lane & 31 = env); the next tile's is loaded while this
-    // one computes, so the wave does not wait on HBM at the top of every tile
-    struct EnvIn {
-        double fuel;
-        uint32_t x, y, o8, d8;
-    };
-    auto load_env = [&](int64_t tile) {
-        const int64_t e = tile * 32 + r;
-        const int64_t ei = e < A.n ? e : A.n - 1;
-        return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei]};
-    };
-    int64_t tile = (int64_t)blockIdx.x * kPolicyWaves + (threadIdx.x >> 6);
+#if !SHIPENV_POLICY_EARLY_ENV
     EnvIn nxt = load_env(tile < tiles ? tile : 0);
+#endif
     for (; tile < tiles; tile += stride) {
         const EnvIn cur_in = nxt;
         if (tile + stride < tiles) nxt = load_env(tile + stride);
