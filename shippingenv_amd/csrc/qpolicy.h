@@ -932,6 +932,9 @@ struct Fc1Slot {
 // no bias is read from LDS (4 x 16-byte reads per row tile and env tile). Measured even or
 // slower (0.2776 vs 0.2751 ms per call, medians of 4 alternating runs,
 // profiles/r05/ab_policy_f32_bias_fold.jsonl): not kept.
+#ifndef SHIPENV_X3_PTAB
+#define SHIPENV_X3_PTAB 1  // policy_x3_kernel stages the port table in LDS before its pack: 0.2652 -> 0.2629 ms per call (profiles/r05/ab_policy_f32_ptab.jsonl); 0: the pack reads L2
+#endif
 #ifndef SHIPENV_X3_PACK_VEC
 #define SHIPENV_X3_PACK_VEC 1  // pack_x3_items: fc2 / fc3 items with float4 loads and paired splits (0: per element)
 #endif
@@ -951,7 +954,21 @@ struct PackX3Args {
     WorldDims dims;
     QnetX3Dims d;
     uint8_t* img;
+    // policy_x3_kernel's own pack (SHIPENV_X3_PTAB): the port table (P positions, then P
+    // stock pairs) staged in LDS, so the b1 folds and the same-cell / register masks read it
+    // there instead of looping over L2 loads; null: the world image in place
+    const uint32_t* ptab = nullptr;
 };
+
+// the world view the pack reads the ports through
+__device__ __forceinline__ LdsWorld pack_world(const PackX3Args& A) {
+    LdsWorld wv = world_view(A.dims, A.world);
+    if (A.ptab) {
+        wv.pos = A.ptab;
+        wv.stock = reinterpret_cast<const int2*>(A.ptab + 64);
+    }
+    return wv;
+}
 
 // One thread per (fragment, lane) of fc2 / fc3 (its 8 elements' three parts), per fc1 float,
 // bias entry, same-cell mask and epilogue register mask (the latter as qnet_pack_f32_kernel).
@@ -959,7 +976,7 @@ struct PackX3Args {
 // qnet_pack_x3_kernel, the workgroup's LDS for policy_x3_kernel's own prologue)
 // b1[f] + W1[f, 6:] . the port block, in f64 then f32 (qnet_pack_kernel's fold)
 __device__ __forceinline__ float x3_fold_b1(const PackX3Args& A, int f) {
-    const LdsWorld wv = world_view(A.dims, A.world);
+    const LdsWorld wv = pack_world(A);
     const int in1 = A.d.q.in1();
     double acc = (double)A.b1[f];
     for (int p = 0; p < A.d.q.P; ++p) {
@@ -1060,7 +1077,7 @@ __device__ __forceinline__ void pack_x3_items(const PackX3Args& A, uint8_t* img,
             continue;
         }
         int u = t - (n_w1 + n_w2 + n_w3);
-        const LdsWorld wv = world_view(A.dims, A.world);
+        const LdsWorld wv = pack_world(A);
         const int P = q.P;
         if (u < kQHidden) {  // b1 + fc1 over the constant port block, in f64 then f32
             reinterpret_cast<float*>(img + d.b1())[u] = x3_fold_b1(A, u);
@@ -1278,7 +1295,21 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
         // the whole image fits: each workgroup splits the f32 weights into its own LDS copy
         // (about 93 KB of f32 reads per workgroup at P = 5 where the packed image is 152 KB),
         // so no pack kernel runs before the policy and in-place weight updates are seen
+#if SHIPENV_X3_PTAB
+        uint32_t* ptab = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(smem) + ((D.bytes() + 15) & ~15));
+        {
+            const LdsWorld wg = world_view(A.dims, A.world);
+            const int t = threadIdx.x, P0 = A.dims.P;
+            if (t < P0) ptab[t] = wg.pos[t];
+            else if (t >= 64 && t < 64 + 2 * P0) ptab[t] = reinterpret_cast<const uint32_t*>(wg.stock)[t - 64];
+        }
+        __syncthreads();
+        PackX3Args pk = PK;
+        pk.ptab = ptab;
+        pack_x3_items(pk, reinterpret_cast<uint8_t*>(smem), threadIdx.x, kPolicyX3Block);
+#else
         pack_x3_items(PK, reinterpret_cast<uint8_t*>(smem), threadIdx.x, kPolicyX3Block);
+#endif
     }
     __syncthreads();
     const LdsWorld w = world_view(A.dims, A.world);  // port_at / stocks read in place (L2)
@@ -1660,12 +1691,13 @@ int launch_policy_x3(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, 
     // the image from the current weights (in place updates by an optimizer or T2 included)
     PackX3Args pk{qn->w[0], qn->w[1], qn->w[2], qn->w[3], qn->w[4], qn->w[5], env->d_world, env->dims, d,
                   qn->d_img32};
-    const bool w3_global = d.bytes() > 160 * 1024;
+    constexpr int kPtabBytes = SHIPENV_X3_PTAB ? 3 * 64 * 4 + 16 : 0;  // the staged port table, past the image
+    const bool w3_global = d.bytes() + kPtabBytes > 160 * 1024;
     if (w3_global) {  // fc3's fragments are read from a packed global image
         qnet_pack_x3_kernel<<<128, 256, 0, s>>>(pk);
         HIP_TRY(hipGetLastError());
     }
-    const size_t lds = (size_t)(w3_global ? d.w3() : d.bytes());
+    const size_t lds = (size_t)(w3_global ? d.w3() : d.bytes() + kPtabBytes);
     if (lds > 160 * 1024) return fail(SE_EINVAL, "split-bf16 network exceeds the 160 KB LDS");
     static std::atomic<uint64_t> lds_set0{0}, lds_set1{0};
     static std::atomic<uint64_t> lds_set2{0};
