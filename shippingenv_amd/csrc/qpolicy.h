@@ -932,6 +932,9 @@ struct Fc1Slot {
 // no bias is read from LDS (4 x 16-byte reads per row tile and env tile). Measured even or
 // slower (0.2776 vs 0.2751 ms per call, medians of 4 alternating runs,
 // profiles/r05/ab_policy_f32_bias_fold.jsonl): not kept.
+#ifndef SHIPENV_X3_PACK_UNROLL
+#define SHIPENV_X3_PACK_UNROLL 6  // fc2 / fc3 pack items whose loads go out together (6 items a thread at P = 5): 0.2646 -> 0.2613 ms per call against 2 (profiles/r05/ab_policy_f32_pack_unroll.jsonl)
+#endif
 #ifndef SHIPENV_X3_PTAB
 #define SHIPENV_X3_PTAB 1  // policy_x3_kernel stages the port table in LDS before its pack: 0.2652 -> 0.2629 ms per call (profiles/r05/ab_policy_f32_ptab.jsonl); 0: the pack reads L2
 #endif
@@ -993,12 +996,16 @@ __device__ __forceinline__ void pack_x3_items(const PackX3Args& A, uint8_t* img,
     const int in1 = q.in1();
     const int n_w1 = SHIPENV_X3_FC1 ? 4 * 2 * 64 : 4 * 3 * 64, n_w2 = 32 * 64, n_w3 = q.mt3 * 8 * 64;
     const int total = n_w1 + n_w2 + n_w3 + 2 * kQHidden + q.mt3 * 32 + q.P + q.mt3;
+    // (SHIPENV_X3_PACK_VEC) fc2 / fc3 fragments first, in a loop of their own: an item's 8
+    // weights are two float4 loads (elements 0-3 and 4-7 are consecutive columns), split as
+    // pairs, and SHIPENV_X3_PACK_UNROLL items' loads go out together. Same bits as the
+    // per-element split3 below. Taken when both weight matrices are 16-byte aligned (torch's
+    // allocations are); otherwise the element-wise loop below packs them.
+    const bool vec = SHIPENV_X3_PACK_VEC &&
+                     ((reinterpret_cast<uintptr_t>(A.w2) | reinterpret_cast<uintptr_t>(A.w3)) & 15) == 0;
 #if SHIPENV_X3_PACK_VEC
-    // fc2 / fc3 fragments first, in a loop of their own: an item's 8 weights are two float4
-    // loads (elements 0-3 and 4-7 are consecutive columns), split as pairs, and two items'
-    // loads go out together. Same bits as the per-element split3 below.
-#pragma unroll 2
-    for (int u0 = first; u0 < n_w2 + n_w3; u0 += stride) {
+#pragma unroll SHIPENV_X3_PACK_UNROLL
+    for (int u0 = vec ? first : n_w2 + n_w3; u0 < n_w2 + n_w3; u0 += stride) {
         const bool second = u0 < n_w2;
         const int u = second ? u0 : u0 - n_w2;
         const int f = u >> 6, lane = u & 63, r = lane & 31, h = lane >> 5;
@@ -1029,7 +1036,7 @@ __device__ __forceinline__ void pack_x3_items(const PackX3Args& A, uint8_t* img,
     }
 #endif
     for (int t = first; t < total; t += stride) {
-        if (SHIPENV_X3_PACK_VEC && t >= n_w1 && t < n_w1 + n_w2 + n_w3) continue;  // packed above
+        if (vec && t >= n_w1 && t < n_w1 + n_w2 + n_w3) continue;  // packed above
         if (t < n_w1) {
             const int lane = t & 63;
             if (SHIPENV_X3_FC1) {  // fc1 fragment (mt, step, lane): element j = slot 16 step + 8h + j
