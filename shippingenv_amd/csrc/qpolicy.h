@@ -935,6 +935,9 @@ struct Fc1Slot {
 #ifndef SHIPENV_X3_PACK_UNROLL
 #define SHIPENV_X3_PACK_UNROLL 6  // fc2 / fc3 pack items whose loads go out together (6 items a thread at P = 5): 0.2646 -> 0.2613 ms per call against 2 (profiles/r05/ab_policy_f32_pack_unroll.jsonl)
 #endif
+#ifndef SHIPENV_X3_FOLD_UNROLL
+#define SHIPENV_X3_FOLD_UNROLL 1  // 8: 0.2699 vs 0.2687 ms per call (profiles/r05/ab_policy_f32_fold_unroll.jsonl), not kept
+#endif
 #ifndef SHIPENV_X3_PTAB
 #define SHIPENV_X3_PTAB 1  // policy_x3_kernel stages the port table in LDS before its pack: 0.2652 -> 0.2629 ms per call (profiles/r05/ab_policy_f32_ptab.jsonl); 0: the pack reads L2
 #endif
@@ -982,6 +985,9 @@ __device__ __forceinline__ float x3_fold_b1(const PackX3Args& A, int f) {
     const LdsWorld wv = pack_world(A);
     const int in1 = A.d.q.in1();
     double acc = (double)A.b1[f];
+    // unrolled so that several ports' weight loads go out before the adds wait on them (the
+    // adds stay in port order)
+#pragma unroll SHIPENV_X3_FOLD_UNROLL
     for (int p = 0; p < A.d.q.P; ++p) {
         const float* w = A.w1 + f * in1 + 6 + 4 * p;
         acc += (double)w[0] * (double)wv.px(p) + (double)w[1] * (double)wv.py(p) + (double)w[2] * (double)wv.pfuel(p) +
