@@ -230,6 +230,14 @@ struct PolicyArgs {
     int64_t rec_head, rec_cap;
 };
 
+// v = p0 + p1 + p2, each the bf16 rounding of the remainder (exact f32 subtractions)
+__device__ __forceinline__ void split3(float v, __bf16& p0, __bf16& p1, __bf16& p2) {
+    p0 = (__bf16)v;
+    const float r1 = v - (float)p0;
+    p1 = (__bf16)r1;
+    p2 = (__bf16)(r1 - (float)p1);
+}
+
 // accumulator initial value: bias rows (reg & 3) + 8 (reg >> 2) + 4h of a 32-row tile
 __device__ __forceinline__ f32x16 bias_frag(const float* b) {
     const float4 a = *reinterpret_cast<const float4*>(b), c = *reinterpret_cast<const float4*>(b + 8),
@@ -427,6 +435,19 @@ __device__ __forceinline__ void finish_env(const QnetDims& q, const EnvValid& v,
     }
 }
 
+#ifndef SHIPENV_POLICY_B1FOLD
+#define SHIPENV_POLICY_B1FOLD 1
+#endif
+// fc2 / fc3's biases by one extra MFMA per row tile against the fc1 input's ones, from
+// fragments staged past the world (1 LDS read instead of 4): 63.95 vs 62.45 us with the fc1
+// fold alone (profiles/r05/ab_policy_bf16_bias_fold.jsonl), not kept; the fc1 fold alone
+// 63.05 -> 62.45 (and 63.1 -> 61.75 in a first A/B), kept
+#ifndef SHIPENV_POLICY_BFOLD23
+#define SHIPENV_POLICY_BFOLD23 0
+#endif
+#if SHIPENV_POLICY_BFOLD23 && !SHIPENV_POLICY_B1FOLD
+#error "SHIPENV_POLICY_BFOLD23 needs SHIPENV_POLICY_B1FOLD (the input's k = 8..10 ones)"
+#endif
 #ifndef SHIPENV_POLICY_EARLY_ENV
 #define SHIPENV_POLICY_EARLY_ENV 0  // 1: the first tile's env loads before the image / world staging: 64.9 vs 64.45 us (profiles/r05/ab_policy_bf16_early_env.jsonl), not kept
 #endif
@@ -460,14 +481,62 @@ void policy_kernel(PolicyArgs A) {
     EnvIn nxt = load_env(tile < tiles ? tile : 0);
 #endif
     const int qwords = q.bytes() / 16;
+#if SHIPENV_POLICY_B1FOLD
+    // fc1's bias rides in the padding half of its single k-step: lanes 32-63 of each W1
+    // fragment (k = 8..15, zero in the packed image) get the three bf16 parts of their row's
+    // b1 at elements 0-2, and the input's k = 8..10 are 1.0, so the chain starts at 0 and the
+    // bias is not read per tile (4 x 16-byte LDS reads per row tile)
+    const int w1w = q.w1() / 16, b1f = q.b1() / 4;
+    for (int i = threadIdx.x; i < qwords; i += kPolicyBlock) {
+        const int k = i - w1w;  // W1 fragment (mt, lane) = k: mt = k >> 6, lane = k & 63
+        if ((unsigned)k < 4u * 64u && (k & 32)) {
+            const float b = reinterpret_cast<const float*>(A.qimg)[b1f + (k >> 6) * 32 + (k & 31)];
+            __bf16 p0, p1, p2;
+            split3(b, p0, p1, p2);
+            bf16x8 v{};
+            v[0] = p0;
+            v[1] = p1;
+            v[2] = p2;
+            smem[i] = __builtin_bit_cast(uint4, v);
+        } else {
+            smem[i] = A.qimg[i];
+        }
+    }
+#else
     for (int i = threadIdx.x; i < qwords; i += kPolicyBlock) smem[i] = A.qimg[i];
+#endif
+#if SHIPENV_POLICY_BFOLD23
+    // fc2 / fc3's bias fragments past the world image: (tile, lane) = the three bf16 parts of
+    // the tile row's bias at elements 0-2 of lanes 32-63 (k = 8..10), zero elsewhere. One
+    // MFMA of a fragment against the fc1 input (1.0 at k = 8..10, SHIPENV_POLICY_B1FOLD) starts
+    // a chain at its bias: one 16-byte LDS read per row tile instead of four.
+    uint4* BFw = smem + qwords + A.dims.padded() / 4;
+    {
+        const int nb = (4 + q.mt3) * 64, b2f = q.b2() / 4, b3f = q.b3() / 4;
+        for (int i = threadIdx.x; i < nb; i += kPolicyBlock) {
+            const int tl = i >> 6, l = i & 63;
+            bf16x8 v{};
+            if (l & 32) {
+                const int row = (tl < 4 ? tl : tl - 4) * 32 + (l & 31);
+                const float b = reinterpret_cast<const float*>(A.qimg)[(tl < 4 ? b2f : b3f) + row];
+                __bf16 p0, p1, p2;
+                split3(b, p0, p1, p2);
+                v[0] = p0;
+                v[1] = p1;
+                v[2] = p2;
+            }
+            BFw[i] = __builtin_bit_cast(uint4, v);
+        }
+    }
+    const bf16x8* BF = reinterpret_cast<const bf16x8*>(BFw);
+#endif
     const LdsWorld w = stage_world(A.world, A.dims, reinterpret_cast<uint32_t*>(smem + qwords));
     const uint8_t* qb = reinterpret_cast<const uint8_t*>(smem);
     const bf16x8* W1f = reinterpret_cast<const bf16x8*>(qb + q.w1());
     const bf16x8* W2f = reinterpret_cast<const bf16x8*>(qb + q.w2());
     const bf16x8* W3f = reinterpret_cast<const bf16x8*>(qb + q.w3());
-    const float* B1 = reinterpret_cast<const float*>(qb + q.b1());
-    const float* B2 = reinterpret_cast<const float*>(qb + q.b2());
+    [[maybe_unused]] const float* B1 = reinterpret_cast<const float*>(qb + q.b1());
+    [[maybe_unused]] const float* B2 = reinterpret_cast<const float*>(qb + q.b2());
     const float* B3 = reinterpret_cast<const float*>(qb + q.b3());
     const uint64_t* SAME = reinterpret_cast<const uint64_t*>(qb + q.same());
     const uint32_t* REGM = reinterpret_cast<const uint32_t*>(qb + q.regm());
@@ -498,12 +567,23 @@ void policy_kernel(PolicyArgs A) {
         ob[5] = fl;
         ob[6] = (__bf16)(float)origin;
         ob[7] = (__bf16)(float)dest;
+#if SHIPENV_POLICY_B1FOLD
+        if (h) {  // k = 8..10: 1.0 against the bias parts, 11..15 padding
+            ob = bf16x8{};
+            ob[0] = ob[1] = ob[2] = (__bf16)1.0f;
+        }
+#else
         if (h) ob = bf16x8{};  // k = 8..15 of the single fc1 step are padding
+#endif
 
         bf16x8 h1[4][2], h2[4][2];
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {  // fc1 + relu
+#if SHIPENV_POLICY_B1FOLD
+            f32x16 c = {};
+#else
             f32x16 c = PBIAS(B1 + mt * 32 + 4 * h);
+#endif
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(W1f[mt * 64 + lane], ob, c, 0, 0, 0);
             relu_pack(c, h1[mt]);
         }
@@ -522,7 +602,12 @@ void policy_kernel(PolicyArgs A) {
         for (int pass = 0; pass < SHIPENV_FC2_SPLIT; ++pass) {
             f32x16 c2[kFc2Tiles];
 #pragma unroll
-            for (int i = 0; i < kFc2Tiles; ++i) c2[i] = PBIAS(B2 + (pass * kFc2Tiles + i) * 32 + 4 * h);
+            for (int i = 0; i < kFc2Tiles; ++i)
+#if SHIPENV_POLICY_BFOLD23
+                c2[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(BF[(pass * kFc2Tiles + i) * 64 + lane], ob, f32x16{}, 0, 0, 0);
+#else
+                c2[i] = PBIAS(B2 + (pass * kFc2Tiles + i) * 32 + 4 * h);
+#endif
 #if SHIPENV_POLICY_LOOKAHEAD > 0
             static_assert(kFc2Tiles == 1, "the fragment lookahead is written for one tile per pass");
             // the tile's 8 fragments read SHIPENV_POLICY_LOOKAHEAD k-steps ahead of their MFMA,
@@ -600,7 +685,12 @@ void policy_kernel(PolicyArgs A) {
             // without q_out (round 5): rows this env cannot take start at -inf (masked_bias), so
             // the first maximum below needs no validity test and no per-register branch
             constexpr bool kMasked = !kQout && SHIPENV_POLICY_MASKED;
+#if SHIPENV_POLICY_BFOLD23
+            f32x16 c = kMasked ? masked_bias(B3 + mt * 32 + 4 * h, m >> (4 * h))
+                               : __builtin_amdgcn_mfma_f32_32x32x16_bf16(BF[(4 + mt) * 64 + lane], ob, f32x16{}, 0, 0, 0);
+#else
             f32x16 c = kMasked ? masked_bias(B3 + mt * 32 + 4 * h, m >> (4 * h)) : PBIAS(B3 + mt * 32 + 4 * h);
+#endif
 #pragma unroll
             for (int k = 0; k < 8; ++k)
                 c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k], h2[k >> 1][k & 1], c, 0, 0, 0);
@@ -910,13 +1000,6 @@ struct QnetX3Dims {
     __host__ __device__ int bytes() const { return w3() + q.mt3 * 24 * 1024; }
 };
 
-// v = p0 + p1 + p2, each the bf16 rounding of the remainder (exact f32 subtractions)
-__device__ __forceinline__ void split3(float v, __bf16& p0, __bf16& p1, __bf16& p2) {
-    p0 = (__bf16)v;
-    const float r1 = v - (float)p0;
-    p1 = (__bf16)r1;
-    p2 = (__bf16)(r1 - (float)p1);
-}
 
 // fc1 on bf16 MFMA (SHIPENV_X3_FC1): the six dynamic columns' products as 24 of the 32 k
 // slots of two v_mfma_f32_32x32x16_bf16 per row tile. Slot k (step k >> 4, lane half
@@ -1648,7 +1731,7 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
     DeviceGuard g(env->device);
     // the compact layout unless every row's Q is wanted
     const QnetDims& q = q_out ? qn->q : qn->qc;
-    const size_t lds = (size_t)q.bytes() + lds_bytes(env);
+    const size_t lds = (size_t)q.bytes() + lds_bytes(env) + (SHIPENV_POLICY_BFOLD23 ? (size_t)(4 + q.mt3) * 1024 : 0);
     static std::atomic<uint64_t> lds_set{0};
     static std::atomic<uint64_t> lds_set_q{0};
     rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(policy_kernel<false>), 160 * 1024, env->device);
