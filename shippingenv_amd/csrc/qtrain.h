@@ -1,4 +1,4 @@
-// qtrain.h — the DQN update fused on fp32 MFMA.
+// qtrain.h — the DQN update fused on MFMA in f32 arithmetic.
 //
 // Part of shipenv.hip's translation unit (included at its end, after replay.h).
 // Reference: agents/dqn.py DQNAgent.update (:206-245) on a sampled minibatch.
@@ -6,8 +6,10 @@
 // then nn.MSELoss and backward, then Adam (lr, betas (0.9, 0.999), eps 1e-8).
 //
 // The torch version is about 50 small kernels per update, launch-bound below B = 2^13.
-// Here it is two kernels, all in f32 (v_mfma_f32_32x32x2_f32 is an exact f32 fma chain,
-// and gfx950 has no xf32), deterministic (fixed summation orders, no atomics):
+// Here it is two kernels, all in f32 arithmetic, deterministic (fixed summation orders, no
+// atomics). The forward GEMMs (fc2 of both nets, the target's fc3) run on bf16 MFMA with
+// every f32 operand split into three bf16 parts (SHIPENV_QT_X3, below); fc1 and the
+// backward on v_mfma_f32_32x32x2_f32 (an exact f32 fma chain; gfx950 has no xf32):
 //
 // T1, qtrain_tile_kernel (one workgroup per 32 samples, 8 waves: the online and the
 // target net's four 32-row feature tiles side by side):
