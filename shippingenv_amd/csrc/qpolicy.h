@@ -448,6 +448,9 @@ __device__ __forceinline__ void finish_env(const QnetDims& q, const EnvValid& v,
 #if SHIPENV_POLICY_BFOLD23 && !SHIPENV_POLICY_B1FOLD
 #error "SHIPENV_POLICY_BFOLD23 needs SHIPENV_POLICY_B1FOLD (the input's k = 8..10 ones)"
 #endif
+#ifndef SHIPENV_POLICY_VALID64
+#define SHIPENV_POLICY_VALID64 1  // 63.1 -> 61.0 us (profiles/r05/ab_policy_bf16_valid64.jsonl, five alternating rounds); 0: per-tile masks
+#endif
 #ifndef SHIPENV_POLICY_EARLY_ENV
 #define SHIPENV_POLICY_EARLY_ENV 0  // 1: the first tile's env loads before the image / world staging: 64.9 vs 64.45 us (profiles/r05/ab_policy_bf16_early_env.jsonl), not kept
 #endif
@@ -656,6 +659,22 @@ void policy_kernel(PolicyArgs A) {
         const int c_lo = q.cargo_row1(), c_hi = c_lo + cst - 1, f_lo = q.fuel_row1(), f_hi = f_lo + fst - 1;
         // SELECT: bit p for each port on the ship's cell other than the origin (P <= 64)
         const uint64_t sel = cur >= 0 ? SAME[max(cur, 0)] & ~(origin >= 0 ? 1ull << origin : 0ull) : 0ull;
+#if SHIPENV_POLICY_VALID64
+        // (compact layouts of at most 64 rows, every greedy call of the bench) the env's valid
+        // rows as one 64-bit word, built once per env tile: a fc3 tile's mask is then a shift
+        // of it and "any row of this tile valid" its being nonzero, where the per-tile form
+        // rebuilt three ranges and the SELECT shift for each fc3 tile
+        const bool use64 = !kQout && q.mt3 <= 2;  // uniform
+        uint64_t v64 = 0;
+        if (use64) {
+            auto range64 = [](int lo, int hi) {  // bits lo..hi, 0 <= lo, hi <= 63; empty if hi < lo
+                const uint64_t top = hi >= 63 ? ~0ull : ((2ull << (hi & 63)) - 1ull);
+                const uint64_t low = (1ull << (lo & 63)) - 1ull;
+                return hi < lo ? 0ull : (top & ~low);
+            };
+            v64 = 0xfull | (sel << 4) | range64(c_lo, c_hi) | range64(f_lo, f_hi);
+        }
+#endif
         float best = -INFINITY;
         int bidx = 0x7fffffff;
 #if SHIPENV_POLICY_ABL == 2  // timing-only: no fc3
@@ -667,15 +686,24 @@ void policy_kernel(PolicyArgs A) {
             // a tile no env of the wave can choose from is skipped, MFMAs included
             // (exact: its rows are invalid for all 32 envs); with port stocks <= 20
             // (add_port's randint(5, 20)) the valid rows sit in the first few tiles
-            const bool maybe = (mt == 0) | ((cur >= 0) & (base < 4 + P)) |
-                               ((cst > 0) & (c_lo <= top) & (c_hi >= base)) |
-                               ((fst > 0) & (f_lo <= top) & (f_hi >= base));
-            if (!kQout && !__any(maybe)) continue;
-            uint32_t m = range_bits(-base, 3 - base) | range_bits(c_lo - base, c_hi - base) |
-                         range_bits(f_lo - base, f_hi - base);
-            if (base < 4 + P) {  // SELECT rows 4 + p live in this tile (uniform): sel shifted by 4 - base
-                const int sh = base - 4;
-                m |= (uint32_t)(sh < 0 ? sel << -sh : (sh < 64 ? sel >> sh : 0ull));
+            uint32_t m;
+#if SHIPENV_POLICY_VALID64
+            if (use64) {
+                m = (uint32_t)(v64 >> (base & 63));
+                if (!__any(m != 0u)) continue;
+            } else
+#endif
+            {
+                const bool maybe = (mt == 0) | ((cur >= 0) & (base < 4 + P)) |
+                                   ((cst > 0) & (c_lo <= top) & (c_hi >= base)) |
+                                   ((fst > 0) & (f_lo <= top) & (f_hi >= base));
+                if (!kQout && !__any(maybe)) continue;
+                m = range_bits(-base, 3 - base) | range_bits(c_lo - base, c_hi - base) |
+                    range_bits(f_lo - base, f_hi - base);
+                if (base < 4 + P) {  // SELECT rows 4 + p live in this tile (uniform): sel shifted by 4 - base
+                    const int sh = base - 4;
+                    m |= (uint32_t)(sh < 0 ? sel << -sh : (sh < 64 ? sel >> sh : 0ull));
+                }
             }
             // registers that hold no valid action for any env are skipped (wave-uniform)
             const uint32_t rm = __builtin_amdgcn_readfirstlane(REGM[mt]);
