@@ -339,6 +339,16 @@ __device__ __forceinline__ uint32_t tile_mask(const EnvValid& v, int mt, int P) 
     return m;
 }
 
+// all of an env's valid rows (layouts of at most 64 rows) as one word: bit r = row r
+__device__ __forceinline__ uint64_t valid_rows64(const EnvValid& v) {
+    auto range64 = [](int lo, int hi) {  // bits lo..hi, 0 <= lo, hi <= 63; empty if hi < lo
+        const uint64_t top = hi >= 63 ? ~0ull : ((2ull << (hi & 63)) - 1ull);
+        const uint64_t low = (1ull << (lo & 63)) - 1ull;
+        return hi < lo ? 0ull : (top & ~low);
+    };
+    return 0xfull | (v.sel << 4) | range64(v.c_lo, v.c_hi) | range64(v.f_lo, v.f_hi);
+}
+
 // the masked first maximum over one fc3 tile's accumulator (ascending rows), registers
 // outside the wave-uniform mask rm skipped
 __device__ __forceinline__ void tile_argmax(const f32x16& c, uint32_t m, uint32_t rm, int base, int h, float& best,
@@ -1049,6 +1059,12 @@ struct Fc1Slot {
 #ifndef SHIPENV_X3_FOLD_UNROLL
 #define SHIPENV_X3_FOLD_UNROLL 1  // 8: 0.2699 vs 0.2687 ms per call (profiles/r05/ab_policy_f32_fold_unroll.jsonl), not kept
 #endif
+// the bf16 kernel's 64-bit valid-row masks (SHIPENV_POLICY_VALID64) in this kernel: 0.2724 vs
+// 0.2630 ms per call (profiles/r05/ab_policy_f32_valid64.jsonl; 256 VGPRs and more SGPR
+// spills), not kept
+#ifndef SHIPENV_X3_VALID64
+#define SHIPENV_X3_VALID64 0
+#endif
 #ifndef SHIPENV_X3_PTAB
 #define SHIPENV_X3_PTAB 1  // policy_x3_kernel stages the port table in LDS before its pack: 0.2652 -> 0.2629 ms per call (profiles/r05/ab_policy_f32_ptab.jsonl); 0: the pack reads L2
 #endif
@@ -1575,7 +1591,12 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
         // beside its first 8 groups (done before k-step 6 reads it). Without q_out, a row
         // no action of this env can take starts at -inf (masked_bias), so the argmax needs
         // no validity test and never picks it.
-        f32x16 c = kQout ? bias_frag(B3 + 4 * h) : masked_bias(B3 + 4 * h, tile_mask(v, 0, P) >> (4 * h));
+        // (SHIPENV_POLICY_VALID64, compact layouts of at most 64 rows) the fc3 tiles' masks as
+        // shifts of one 64-bit word of the env's valid rows
+        const bool use64 = SHIPENV_X3_VALID64 && !kQout && q.mt3 <= 2;  // uniform
+        const uint64_t v64 = use64 ? valid_rows64(v) : 0ull;
+        auto mask_of = [&](int mt) { return use64 ? (uint32_t)(v64 >> ((32 * mt) & 63)) : tile_mask(v, mt, P); };
+        f32x16 c = kQout ? bias_frag(B3 + 4 * h) : masked_bias(B3 + 4 * h, mask_of(0) >> (4 * h));
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             if (32 + k + kLa < 40) frag_of(32 + k + kLa, wf[(32 + k + kLa) % (kLa + 1)]);
@@ -1591,15 +1612,15 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
         if (more) vnxt = env_valid_from(w, q, SAME, ncode, nstock, nxt.o8 == SE_NONE ? -1 : (int)nxt.o8);
         // fc3 tiles 1..: the previous tile's argmax beside each chain, 4 registers a group
         int pbase = 0;
-        uint32_t pm = tile_mask(v, 0, P), prm = __builtin_amdgcn_readfirstlane(REGM[0]);
+        uint32_t pm = kQout ? tile_mask(v, 0, P) : 0u, prm = __builtin_amdgcn_readfirstlane(REGM[0]);
         if (kQout && live) tile_q_out(A.q_out, A.ldq, q.rows, c, e, 0, h);
 #pragma nounroll
         for (int mt = 1; mt < ((SHIPENV_X3_ABL & 2) ? 1 : q.mt3); ++mt) {  // (ABL & 2: timing only, fc3 tile 0 alone)
             const int base = mt * 32;
-            if (!kQout && !__any(tile_maybe(v, mt, P))) continue;
+            const uint32_t m3 = kQout ? 0u : mask_of(mt);
+            if (!kQout && !__any(use64 ? m3 != 0u : tile_maybe(v, mt, P))) continue;
             const bf16x8* W3t = W3 + mt * 8 * 192;
-            f32x16 c3 = kQout ? bias_frag(B3 + mt * 32 + 4 * h)
-                              : masked_bias(B3 + mt * 32 + 4 * h, tile_mask(v, mt, P) >> (4 * h));
+            f32x16 c3 = kQout ? bias_frag(B3 + mt * 32 + 4 * h) : masked_bias(B3 + mt * 32 + 4 * h, m3 >> (4 * h));
 #pragma unroll
             for (int j = 0; j < kLa; ++j) x3_frags(W3t, j, lane, wf[j]);
             __builtin_amdgcn_sched_barrier(0);
@@ -1619,7 +1640,7 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
             }
             c = c3;
             pbase = base;
-            pm = tile_mask(v, mt, P);
+            if (kQout) pm = tile_mask(v, mt, P);
             prm = __builtin_amdgcn_readfirstlane(REGM[mt]);
             if (kQout && live) tile_q_out(A.q_out, A.ldq, q.rows, c, e, base, h);
         }
