@@ -388,6 +388,17 @@ __device__ __forceinline__ void argmax_masked_part(const f32x16& c, int base, fl
     }
 }
 
+// argmax_masked_part with the winner's tile-local row kept as an inline constant (bt); after
+// part 3 the caller adds the tile's base once if the tile raised the maximum (best != best0)
+__device__ __forceinline__ void argmax_local_part(const f32x16& c, float& best, int& bt, int j) {
+#pragma unroll
+    for (int reg = 4 * j; reg < 4 * j + 4; ++reg) {
+        const bool better = c[reg] > best;
+        best = better ? c[reg] : best;
+        bt = better ? (reg & 3) + 8 * (reg >> 2) : bt;
+    }
+}
+
 __device__ __forceinline__ void tile_q_out(float* q_out, int64_t ldq, int rows, const f32x16& c, int64_t e, int base,
                                            int h) {
 #pragma unroll
@@ -457,6 +468,9 @@ __device__ __forceinline__ void finish_env(const QnetDims& q, const EnvValid& v,
 #endif
 #if SHIPENV_POLICY_BFOLD23 && !SHIPENV_POLICY_B1FOLD
 #error "SHIPENV_POLICY_BFOLD23 needs SHIPENV_POLICY_B1FOLD (the input's k = 8..10 ones)"
+#endif
+#ifndef SHIPENV_POLICY_LOCAL_IDX
+#define SHIPENV_POLICY_LOCAL_IDX 1
 #endif
 #ifndef SHIPENV_POLICY_VALID64
 #define SHIPENV_POLICY_VALID64 1  // 63.1 -> 61.0 us (profiles/r05/ab_policy_bf16_valid64.jsonl, five alternating rounds); 0: per-tile masks
@@ -743,6 +757,21 @@ void policy_kernel(PolicyArgs A) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) argmax_masked_part(c, base, best, bidx, j);  // rows without 4h
             } else {
+#if SHIPENV_POLICY_LOCAL_IDX
+                // the winning register's tile-local row as an inline constant, the tile's base
+                // added once if the tile raised the maximum (strict >: the first maximum stays)
+                const float best0 = best;
+                int bt = 0;
+#pragma unroll
+                for (int reg = 0; reg < 16; ++reg) {
+                    if (!((rm >> reg) & 1u)) continue;
+                    const int i = (reg & 3) + 8 * (reg >> 2);
+                    const bool better = ((m >> i) & 1u) && c[reg] > best;  // ascending rows: first max
+                    best = better ? c[reg] : best;
+                    bt = better ? i : bt;
+                }
+                bidx = best != best0 ? base + 4 * h + bt : bidx;
+#else
 #pragma unroll
                 for (int reg = 0; reg < 16; ++reg) {
                     if (!((rm >> reg) & 1u)) continue;
@@ -751,6 +780,7 @@ void policy_kernel(PolicyArgs A) {
                     best = better ? c[reg] : best;
                     bidx = better ? base + 4 * h + i : bidx;
                 }
+#endif
             }
 #endif
             if (kQout && live) {
@@ -1612,6 +1642,8 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
         if (more) vnxt = env_valid_from(w, q, SAME, ncode, nstock, nxt.o8 == SE_NONE ? -1 : (int)nxt.o8);
         // fc3 tiles 1..: the previous tile's argmax beside each chain, 4 registers a group
         int pbase = 0;
+        [[maybe_unused]] float best0 = best;
+        [[maybe_unused]] int bt = 0;
         uint32_t pm = kQout ? tile_mask(v, 0, P) : 0u, prm = __builtin_amdgcn_readfirstlane(REGM[0]);
         if (kQout && live) tile_q_out(A.q_out, A.ldq, q.rows, c, e, 0, h);
 #pragma nounroll
@@ -1632,8 +1664,17 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
                     c3 = khalf_x3(wf[k % (kLa + 1)], X2[k >> 1][k & 1], c3, half);
                     const int g = 2 * k + half;
                     if (g < 4) {
-                        if (kQout) tile_argmax_part(c, pm, prm, pbase, h, best, bidx, g);
-                        else argmax_masked_part(c, pbase, best, bidx, g);
+                        if (kQout) {
+                            tile_argmax_part(c, pm, prm, pbase, h, best, bidx, g);
+                        } else {
+#if SHIPENV_POLICY_LOCAL_IDX
+                            if (g == 0) best0 = best;
+                            argmax_local_part(c, best, bt, g);
+                            if (g == 3) bidx = best != best0 ? pbase + bt : bidx;
+#else
+                            argmax_masked_part(c, pbase, best, bidx, g);
+#endif
+                        }
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
@@ -1647,8 +1688,15 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
         if (kQout) {
             tile_argmax(c, pm, prm, pbase, h, best, bidx);
         } else {
+#if SHIPENV_POLICY_LOCAL_IDX
+            best0 = best;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) argmax_local_part(c, best, bt, g);
+            bidx = best != best0 ? pbase + bt : bidx;
+#else
 #pragma unroll
             for (int g = 0; g < 4; ++g) argmax_masked_part(c, pbase, best, bidx, g);
+#endif
             bidx += bidx == 0x7fffffff ? 0 : 4 * h;  // the lane half's rows (argmax_masked_part omits 4h)
         }
 #else
