@@ -413,11 +413,46 @@ __device__ __forceinline__ void tile_q_out(float* q_out, int64_t ldq, int rows, 
 #define FINISH_ENV(v, e, live, h, best, bidx, x8, y8, o8, d8, ff)                                             \
     finish_env(q, v, e, live, h, best, bidx, x8, y8, o8, d8, ff, A.actions, A.eps, A.seed, A.env_base, A.t,       \
                A.rec_pos, A.rec_fuel, A.rec_act, A.rec_head, A.rec_cap)
+// the same with the env's epsilon draw words 0 and 1 already drawn (PairedDraws)
+#define FINISH_ENV_D(v, e, live, h, best, bidx, x8, y8, o8, d8, ff, dw)                                        \
+    finish_env(q, v, e, live, h, best, bidx, x8, y8, o8, d8, ff, A.actions, A.eps, A.seed, A.env_base, A.t,       \
+               A.rec_pos, A.rec_fuel, A.rec_act, A.rec_head, A.rec_cap, &(dw))
+
+// the epsilon draws of two tiles from one Philox pass: on even iterations lanes 0-31 draw
+// for this tile's envs and lanes 32-63 for the next tile's (tile + stride), whose words
+// move to lanes 0-31 and are kept for the odd iteration (a draw depends only on the env
+// id, t and the slot, so the words are the same as drawing them one tile at a time)
+// (the kept words wait in the wave's 32 x 8-byte LDS slot, not in registers)
+constexpr int kPairedDrawBytes = 32 * 8;  // per wave
+struct PairedDraws {
+    uint2* slot;  // this wave's
+    int it = 0;   // iteration parity (uniform)
+    __device__ __forceinline__ U4 next(bool on, int64_t e, int64_t stride, int h, int r, uint64_t seed,
+                                       int64_t env_base, uint32_t t) {
+        U4 d{{0u, 0u, 0u, 0u}};
+        if (on) {
+            if ((it & 1) == 0) {
+                const int64_t de = h ? e + stride * 32 : e;  // the env of this lane in tile + stride
+                const U4 w = draw(env_key(seed, env_base + de), t, kSlotPolicy);
+                d.v[0] = w.v[0];
+                d.v[1] = w.v[1];
+                if (h) slot[r] = make_uint2(w.v[0], w.v[1]);
+            } else if (!h) {
+                const uint2 w = slot[r];
+                d.v[0] = w.x;
+                d.v[1] = w.y;
+            }
+        }
+        ++it;
+        return d;
+    }
+};
+
 __device__ __forceinline__ void finish_env(const QnetDims& q, const EnvValid& v, int64_t e, bool live, int h, float best,
                                            int bidx, uint32_t x8, uint32_t y8, uint32_t o8, uint32_t d8, float ff,
                                            int32_t* actions, double eps, uint64_t seed, int64_t env_base, uint32_t t,
                                            uint32_t* rec_pos, float* rec_fuel, int32_t* rec_act, int64_t rec_head,
-                                           int64_t rec_cap) {
+                                           int64_t rec_cap, const U4* drawn = nullptr) {
     const float ob2 = __shfl_xor(best, 32);
     const int oi = __shfl_xor(bidx, 32);
     if (ob2 > best || (ob2 == best && oi < bidx)) {
@@ -428,7 +463,7 @@ __device__ __forceinline__ void finish_env(const QnetDims& q, const EnvValid& v,
         const int P = q.P;
         int act = bidx == 0x7fffffff ? 0 : q.action_of_row(bidx);  // no valid action: 0 (:188-189)
         if (eps > 0.0) {
-            const U4 d = draw(env_key(seed, env_base + e), t, kSlotPolicy);
+            const U4 d = drawn ? *drawn : draw(env_key(seed, env_base + e), t, kSlotPolicy);
             if (u32(d.v[0]) <= eps) {  // np.random.rand() <= epsilon (:191)
                 // random.choice(valid_actions) (:192): the k-th valid action, ascending
                 const int nsel = __popcll(v.sel);
@@ -478,6 +513,34 @@ __device__ __forceinline__ void finish_env(const QnetDims& q, const EnvValid& v,
 #ifndef SHIPENV_POLICY_EARLY_ENV
 #define SHIPENV_POLICY_EARLY_ENV 0  // 1: the first tile's env loads before the image / world staging: 64.9 vs 64.45 us (profiles/r05/ab_policy_bf16_early_env.jsonl), not kept
 #endif
+#ifndef SHIPENV_POLICY_DRAW_PAIR
+#define SHIPENV_POLICY_DRAW_PAIR 0  // 1: one Philox pass per two tiles' epsilon draws (PairedDraws): within noise in three alternating A/Bs (bf16 0.0602 -> 0.0595, 0.0597 -> 0.0599, 0.0604 -> 0.0602 ms; fp32 0.2668 -> 0.2641 and, words held in registers, 0.2591 -> 0.261; profiles/r05/ab_policy_*_drawpair*.jsonl), one or three VGPRs spilled: not kept
+#endif
+#ifndef SHIPENV_POLICY_STAGE_BATCH
+#define SHIPENV_POLICY_STAGE_BATCH 0  // 1: policy_kernel's image copy as four loads per thread before one wait: 0.0598 -> 0.0602 and 0.0593 -> 0.0600 ms (profiles/r05/ab_policy_bf16_stage.jsonl), not kept
+#endif
+// n 16-byte words global -> LDS by a block of `block` threads: four loads per thread issued
+// (past the end: the last word again), one wait, four guarded stores
+__device__ __forceinline__ void copy_to_lds(const uint4* __restrict__ g, uint4* l, int n, int block) {
+    for (int i0 = 0; i0 < n; i0 += 4 * block) {
+        uint4 r[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[k] = g[min(i0 + (int)threadIdx.x + k * block, n - 1)];
+        // the loads stay ahead of the guarded stores (not sunk into them, one wait each)
+        for (int k = 0; k < 4; ++k) asm volatile("" ::"v"(r[k].x), "v"(r[k].y), "v"(r[k].z), "v"(r[k].w));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = i0 + (int)threadIdx.x + k * block;
+            if (i < n) l[i] = r[k];
+        }
+    }
+}
+#ifndef SHIPENV_POLICY_NXT_WAIT
+#define SHIPENV_POLICY_NXT_WAIT 1  // the next tile's loads waited for before the stores (policy_kernel): 0.0598 -> 0.0593 ms (profiles/r05/ab_policy_bf16_stage.jsonl)
+#endif
+#ifndef SHIPENV_POLICY_PRIO
+#define SHIPENV_POLICY_PRIO 3  // static issue priorities of each SIMD's waves (see policy_kernel): 3 (the youngest wave at 1) 0.0602 -> 0.05955 ms (profiles/r05/ab_policy_bf16_prio.jsonl), 1 and 2 0.0599
+#endif
 #ifndef SHIPENV_POLICY_MASKED
 #define SHIPENV_POLICY_MASKED 0  // 1: masked -inf fc3 bias + branch-free argmax (63.5 vs 63.4 us, profiles/r05/ab_policy_bf16_masked.jsonl: not kept); 0: the round-4 epilogue
 #endif
@@ -504,6 +567,18 @@ void policy_kernel(PolicyArgs A) {
         return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei]};
     };
     int64_t tile = (int64_t)blockIdx.x * kPolicyWaves + (threadIdx.x >> 6);
+#if SHIPENV_POLICY_PRIO == 1  // each SIMD's waves at static issue priorities 0..3 (wave >> 2)
+    {
+        const int pw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >> 2;  // the immediate is a constant
+        if (pw == 1) __builtin_amdgcn_s_setprio(1);
+        else if (pw == 2) __builtin_amdgcn_s_setprio(2);
+        else if (pw == 3) __builtin_amdgcn_s_setprio(3);
+    }
+#elif SHIPENV_POLICY_PRIO == 2  // each SIMD's younger two waves at priority 1
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 8) __builtin_amdgcn_s_setprio(1);
+#elif SHIPENV_POLICY_PRIO == 3  // each SIMD's youngest wave at priority 1
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 12) __builtin_amdgcn_s_setprio(1);
+#endif
 #if SHIPENV_POLICY_EARLY_ENV
     EnvIn nxt = load_env(tile < tiles ? tile : 0);
 #endif
@@ -514,6 +589,26 @@ void policy_kernel(PolicyArgs A) {
     // b1 at elements 0-2, and the input's k = 8..10 are 1.0, so the chain starts at 0 and the
     // bias is not read per tile (4 x 16-byte LDS reads per row tile)
     const int w1w = q.w1() / 16, b1f = q.b1() / 4;
+#if SHIPENV_POLICY_STAGE_BATCH
+    // the image in batches of four 16-byte loads per thread, all issued before one wait
+    // (left to itself the compiler sank each load into its guarded store and waited on
+    // every one); then each patched W1 fragment lane by the thread that copied it
+    copy_to_lds(A.qimg, smem, qwords, kPolicyBlock);
+    {
+        int k = (int)threadIdx.x - w1w % kPolicyBlock;  // W1 fragment (mt, lane) = k: mt = k >> 6, lane = k & 63
+        k += k < 0 ? kPolicyBlock : 0;                  // w1w + k == threadIdx.x (mod the block)
+        if (k < 4 * 64 && (k & 32)) {
+            const float b = reinterpret_cast<const float*>(A.qimg)[b1f + (k >> 6) * 32 + (k & 31)];
+            __bf16 p0, p1, p2;
+            split3(b, p0, p1, p2);
+            bf16x8 v{};
+            v[0] = p0;
+            v[1] = p1;
+            v[2] = p2;
+            smem[w1w + k] = __builtin_bit_cast(uint4, v);
+        }
+    }
+#else
     for (int i = threadIdx.x; i < qwords; i += kPolicyBlock) {
         const int k = i - w1w;  // W1 fragment (mt, lane) = k: mt = k >> 6, lane = k & 63
         if ((unsigned)k < 4u * 64u && (k & 32)) {
@@ -529,6 +624,7 @@ void policy_kernel(PolicyArgs A) {
             smem[i] = A.qimg[i];
         }
     }
+#endif
 #else
     for (int i = threadIdx.x; i < qwords; i += kPolicyBlock) smem[i] = A.qimg[i];
 #endif
@@ -572,6 +668,12 @@ void policy_kernel(PolicyArgs A) {
     const int64_t stride = (int64_t)gridDim.x * kPolicyWaves;
 #if !SHIPENV_POLICY_EARLY_ENV
     EnvIn nxt = load_env(tile < tiles ? tile : 0);
+#endif
+#if SHIPENV_POLICY_DRAW_PAIR
+    // past the world image (and the bias fragments of SHIPENV_POLICY_BFOLD23)
+    PairedDraws pd{reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(smem + qwords + A.dims.padded() / 4) +
+                                            (SHIPENV_POLICY_BFOLD23 ? (4 + q.mt3) * 1024 : 0) +
+                                            __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kPairedDrawBytes)};
 #endif
     for (; tile < tiles; tile += stride) {
         const EnvIn cur_in = nxt;
@@ -792,6 +894,12 @@ void policy_kernel(PolicyArgs A) {
             }
         }
         if (!kQout && SHIPENV_POLICY_MASKED) bidx += bidx == 0x7fffffff ? 0 : 4 * h;  // the lane half's rows
+#if SHIPENV_POLICY_NXT_WAIT
+        // the next tile's env loads (issued a tile ago) are waited for here, before this
+        // tile's stores: stores count in vmcnt too, so a wait at the loop's back edge would
+        // wait out the action / record stores' round trip as well
+        asm volatile("" ::"v"(nxt.fuel), "v"(nxt.x), "v"(nxt.y), "v"(nxt.o8), "v"(nxt.d8));
+#endif
         // the two lane halves hold the same env: larger value, then lower index
         const float ob2 = __shfl_xor(best, 32);
         const int oi = __shfl_xor(bidx, 32);
@@ -799,10 +907,17 @@ void policy_kernel(PolicyArgs A) {
             best = ob2;
             bidx = oi;
         }
+#if SHIPENV_POLICY_DRAW_PAIR
+        const U4 dw = pd.next(A.eps > 0.0, e, stride, h, lane & 31, A.seed, A.env_base, A.t);
+#endif
         if (h == 0 && live) {
             int act = bidx == 0x7fffffff ? 0 : q.action_of_row(bidx);  // no valid action: 0 (:188-189)
             if (A.eps > 0.0) {
+#if SHIPENV_POLICY_DRAW_PAIR
+                const U4 d = dw;
+#else
                 const U4 d = draw(env_key(A.seed, A.env_base + e), A.t, kSlotPolicy);
+#endif
                 if (u32(d.v[0]) <= A.eps) {  // np.random.rand() <= epsilon (:191)
                     // random.choice(valid_actions) (:192): the k-th valid action, ascending
                     const int nsel = __popcll(sel);
@@ -1098,6 +1213,7 @@ struct Fc1Slot {
 #ifndef SHIPENV_X3_PTAB
 #define SHIPENV_X3_PTAB 1  // policy_x3_kernel stages the port table in LDS before its pack: 0.2652 -> 0.2629 ms per call (profiles/r05/ab_policy_f32_ptab.jsonl); 0: the pack reads L2
 #endif
+constexpr int kX3PtabBytes = SHIPENV_X3_PTAB ? 3 * 64 * 4 + 16 : 0;  // the staged port table, past the image
 #ifndef SHIPENV_X3_PACK_VEC
 #define SHIPENV_X3_PACK_VEC 1  // pack_x3_items: fc2 / fc3 items with float4 loads and paired splits (0: per element)
 #endif
@@ -1338,6 +1454,15 @@ __device__ __forceinline__ f32x16 kstep_x3(const bf16x8* Wf, int lane, const bf1
 #ifndef SHIPENV_X3_STAGGER
 #define SHIPENV_X3_STAGGER 0  // experiment: waves 4-7 sleep this many x 6400 cycles first
 #endif
+#ifndef SHIPENV_X3_WORLD_PIN
+#define SHIPENV_X3_WORLD_PIN 1  // the next tile's world reads waited for at their uses, not at their loads: 0.2573 (0) -> 0.2551 ms at k-step groups 8 / 24 (0.259 at 4 / 20, 0.2581 at 12 / 28; profiles/r05/ab_policy_f32_worldpin.jsonl, within the box's noise)
+#endif
+#ifndef SHIPENV_X3_CODE_AT
+#define SHIPENV_X3_CODE_AT 8  // fc2 k-step group at which the next tile's cell code is read (SHIPENV_X3_WORLD_PIN)
+#endif
+#ifndef SHIPENV_X3_STOCK_AT
+#define SHIPENV_X3_STOCK_AT 24  // ... and that port's stocks
+#endif
 #ifndef SHIPENV_X3_PRIO
 #define SHIPENV_X3_PRIO 1  // waves 4-7 (each SIMD's second wave) at issue priority 1: 0.3-1.6 % faster in three alternating A/Bs (profiles/r05/ab_policy_f32_fused_fc1.jsonl, _bias_fold.jsonl, _pack_vec.jsonl); even in round 5's first (ab_policy_r05m.jsonl); 0: off
 #endif
@@ -1510,6 +1635,12 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
     }
 #endif
     EnvValid vnxt = env_valid(w, q, SAME, (int)nxt.x8, (int)nxt.y8, nxt.o8 == SE_NONE ? -1 : (int)nxt.o8);
+#if SHIPENV_POLICY_DRAW_PAIR
+    // past the image (kW3Global: past the staged part) and the port table
+    PairedDraws pd{reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(smem) +
+                                            (kW3Global ? D.w3() : ((D.bytes() + 15) & ~15) + kX3PtabBytes) +
+                                            __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kPairedDrawBytes)};
+#endif
     for (; tile < tiles; tile += stride) {
         const EnvIn in = nxt;
         const EnvValid v = vnxt;
@@ -1601,8 +1732,18 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
 #pragma unroll
         for (int i = 0; i < 32; ++i) {
             const int kt = i >> 3, mt = (i >> 1) & 3, s2 = i & 1;
-            if (i == 4 && more) ncode = w.code((int)nxt.x8, (int)nxt.y8);
+            if (i == SHIPENV_X3_CODE_AT && (more || SHIPENV_X3_WORLD_PIN)) ncode = w.code((int)nxt.x8, (int)nxt.y8);
+#if SHIPENV_X3_WORLD_PIN
+            // unconditional (past the last tile nxt is tile 0's state, a valid address) and
+            // opaque until their uses: under `if (more)` the compiler merged the arithmetic on
+            // each into its load's block and waited out the round trip right there
+            if (i == SHIPENV_X3_STOCK_AT) {
+                asm volatile("" : "+v"(ncode));
+                nstock = w.stock[max(w.port_of_code(ncode), 0)];
+            }
+#else
             if (i == 20 && more) nstock = w.stock[max(w.port_of_code(ncode), 0)];
+#endif
             frag_of(i + kLa, wf[(i + kLa) % (kLa + 1)]);
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
@@ -1639,7 +1780,15 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
             }
         }
         // the next tile's validity from the world reads issued during fc2 (ncode, nstock)
+#if SHIPENV_X3_WORLD_PIN
+        // waited for here on every path: a wait only inside env_valid_from's port branch left
+        // the load outstanding into the next tile, whose first write of its registers then
+        // waited out the new env loads as well
+        asm volatile("" ::"v"(nstock.x), "v"(nstock.y));
+        vnxt = env_valid_from(w, q, SAME, ncode, nstock, nxt.o8 == SE_NONE ? -1 : (int)nxt.o8);
+#else
         if (more) vnxt = env_valid_from(w, q, SAME, ncode, nstock, nxt.o8 == SE_NONE ? -1 : (int)nxt.o8);
+#endif
         // fc3 tiles 1..: the previous tile's argmax beside each chain, 4 registers a group
         int pbase = 0;
         [[maybe_unused]] float best0 = best;
@@ -1731,6 +1880,9 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyF32Args
 #endif
 #if SHIPENV_X3_ABL & 1  // timing only: no epilogue (the chosen row stored as the action)
         if (h == 0 && live) A.actions[e] = bidx;
+#elif SHIPENV_POLICY_DRAW_PAIR
+        const U4 dw = pd.next(A.eps > 0.0, e, stride, h, lane & 31, A.seed, A.env_base, A.t);
+        FINISH_ENV_D(v, e, live, h, best, bidx, x8, y8, o8, d8, ff, dw);
 #else
         FINISH_ENV(v, e, live, h, best, bidx, x8, y8, o8, d8, ff);
 #endif
@@ -1828,7 +1980,8 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
     DeviceGuard g(env->device);
     // the compact layout unless every row's Q is wanted
     const QnetDims& q = q_out ? qn->q : qn->qc;
-    const size_t lds = (size_t)q.bytes() + lds_bytes(env) + (SHIPENV_POLICY_BFOLD23 ? (size_t)(4 + q.mt3) * 1024 : 0);
+    const size_t lds = (size_t)q.bytes() + lds_bytes(env) + (SHIPENV_POLICY_BFOLD23 ? (size_t)(4 + q.mt3) * 1024 : 0) +
+                       (SHIPENV_POLICY_DRAW_PAIR ? (size_t)kPolicyWaves * kPairedDrawBytes : 0);
     static std::atomic<uint64_t> lds_set{0};
     static std::atomic<uint64_t> lds_set_q{0};
     rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(policy_kernel<false>), 160 * 1024, env->device);
@@ -1884,13 +2037,14 @@ int launch_policy_x3(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, 
     // the image from the current weights (in place updates by an optimizer or T2 included)
     PackX3Args pk{qn->w[0], qn->w[1], qn->w[2], qn->w[3], qn->w[4], qn->w[5], env->d_world, env->dims, d,
                   qn->d_img32};
-    constexpr int kPtabBytes = SHIPENV_X3_PTAB ? 3 * 64 * 4 + 16 : 0;  // the staged port table, past the image
+    constexpr int kPtabBytes = kX3PtabBytes + (SHIPENV_POLICY_DRAW_PAIR ? kPolicyX3Waves * kPairedDrawBytes : 0);
     const bool w3_global = d.bytes() + kPtabBytes > 160 * 1024;
     if (w3_global) {  // fc3's fragments are read from a packed global image
         qnet_pack_x3_kernel<<<128, 256, 0, s>>>(pk);
         HIP_TRY(hipGetLastError());
     }
-    const size_t lds = (size_t)(w3_global ? d.w3() : d.bytes() + kPtabBytes);
+    const size_t lds = (size_t)(w3_global ? d.w3() + (SHIPENV_POLICY_DRAW_PAIR ? kPolicyX3Waves * kPairedDrawBytes : 0)
+                                          : ((d.bytes() + 15) & ~15) + kPtabBytes);
     if (lds > 160 * 1024) return fail(SE_EINVAL, "split-bf16 network exceeds the 160 KB LDS");
     static std::atomic<uint64_t> lds_set0{0}, lds_set1{0};
     static std::atomic<uint64_t> lds_set2{0};

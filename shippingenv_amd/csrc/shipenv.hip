@@ -246,6 +246,9 @@ __device__ __forceinline__ LdsWorld stage_finish(const uint32_t* __restrict__ g,
 
 // Any block size (the other kernels): every thread's 16-byte loads issued before any
 // store (the image is padded to whole 1024-dword rows).
+#ifndef SHIPENV_STAGE_PIN
+#define SHIPENV_STAGE_PIN 0  // 1: the loads pinned ahead of the guarded stores (one wait per four); with the policy image batched too, 0.0593 -> 0.0600 ms per policy call (profiles/r05/ab_policy_bf16_stage.jsonl), not kept
+#endif
 __device__ __forceinline__ LdsWorld stage_world(const uint32_t* __restrict__ g, WorldDims d,
                                                 uint32_t* lds) {
     const int total = (d.total() + 3) / 4;
@@ -258,6 +261,11 @@ __device__ __forceinline__ LdsWorld stage_world(const uint32_t* __restrict__ g, 
         uint4 r[kR];
 #pragma unroll
         for (int k = 0; k < kR; ++k) r[k] = g4[min(i0 + (int)threadIdx.x + k * (int)blockDim.x, total - 1)];
+#if SHIPENV_STAGE_PIN
+        // all four loads before one wait: without this use the compiler sank each load into
+        // its guarded store and waited on every one
+        for (int k = 0; k < 4; ++k) asm volatile("" ::"v"(r[k].x), "v"(r[k].y), "v"(r[k].z), "v"(r[k].w));
+#endif
 #pragma unroll
         for (int k = 0; k < kR; ++k) {
             const int i = i0 + (int)threadIdx.x + k * (int)blockDim.x;

@@ -168,6 +168,50 @@ def test_explore_is_uniform_over_valid_actions(steps, ports):
     assert 0.2 < (u <= 0.3).mean() < 0.4
 
 
+def philox_np(e, t, slot, seed):
+    """Philox4x32-10 of counters (e lo, e hi, t, slot) and key seed, vectorised over env ids e
+    (the RNG contract, philox.h); checked against the oracle's scalar form below."""
+    e = np.asarray(e, np.uint64)
+    c0, c1 = (e & 0xFFFFFFFF).astype(np.uint64), (e >> np.uint64(32)).astype(np.uint64)
+    c2 = np.full_like(c0, t)
+    c3 = np.full_like(c0, slot)
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    m32 = np.uint64(0xFFFFFFFF)
+    for _ in range(10):
+        p0 = np.uint64(0xD2511F53) * c0
+        p1 = np.uint64(0xCD9E8D57) * c2
+        c0, c1, c2, c3 = ((p1 >> np.uint64(32)) ^ c1 ^ np.uint64(k0), p1 & m32,
+                          (p0 >> np.uint64(32)) ^ c3 ^ np.uint64(k1), p0 & m32)
+        k0, k1 = (k0 + 0x9E3779B9) & 0xFFFFFFFF, (k1 + 0xBB67AE85) & 0xFFFFFFFF
+    return c0, c1
+
+
+@pytest.mark.parametrize("precision", ["bf16", "f32"])
+def test_explore_over_several_tiles_per_wave(precision):
+    """2^18 + 37 envs: 8194 tiles over the 4096 resident waves, so waves run two or three
+    tiles: the epsilon draws of a wave's later tiles (in a SHIPENV_POLICY_DRAW_PAIR=1 build,
+    one Philox pass for a tile and the next, used on odd iterations and drawn past the last
+    tile) against the RNG contract.
+    epsilon = 0.3: the Philox choice among the valid actions exactly where u <= 0.3, the
+    greedy action elsewhere (the same kernel at epsilon 0)."""
+    n = (1 << 18) + 37
+    env, model, pol = make(n, steps=3, scale=20.0)
+    for i in (0, 1, n // 2, n - 1):  # the vectorised Philox against the oracle's
+        w = O.philox([i & 0xFFFFFFFF, i >> 32, 11, 14], [env.seed & 0xFFFFFFFF, env.seed >> 32])
+        w0, w1 = philox_np([i], 11, 14, env.seed)
+        assert (int(w0[0]), int(w1[0])) == (int(w[0]), int(w[1]))
+    valid = valid_bool(env)
+    w0, w1 = philox_np(np.arange(n), 11, 14, env.seed)
+    u = w0.astype(np.float64) / 2**32
+    cnt = valid.sum(1).astype(np.uint64)
+    k = ((w1 * cnt) >> np.uint64(32)).astype(np.int64)
+    explore = (valid.cumsum(1, dtype=np.int16) > k[:, None].astype(np.int16)).argmax(1)
+    greedy = pol.act(0.0, 11, precision=precision).cpu().numpy()
+    act = pol.act(0.3, 11, precision=precision).cpu().numpy()
+    np.testing.assert_array_equal(act, np.where(u <= 0.3, explore, greedy))
+    assert 0.25 < (u <= 0.3).mean() < 0.35
+
+
 @pytest.mark.parametrize("n", [1, 5, 31, 33])
 def test_tiny_batches_choose_as_the_rule(n):
     """One partial 32-env tile (n < 32) or a full tile and a partial one (33): both policy
