@@ -535,6 +535,25 @@ __device__ __forceinline__ void copy_to_lds(const uint4* __restrict__ g, uint4* 
         }
     }
 }
+#ifndef SHIPENV_POLICY_RM_SKIP
+#define SHIPENV_POLICY_RM_SKIP 1  // 0: every register of an fc3 tile tested: 0.0591 -> 0.0603 ms (profiles/r05/ab_policy_bf16_rmskip.jsonl), not kept
+#endif
+#ifndef SHIPENV_POLICY_WAVE_SKIP
+#define SHIPENV_POLICY_WAVE_SKIP 0  // 1: fc3 tiles / registers also skipped by the wave's union of valid rows (DPP OR per env tile): 0.0592 -> 0.0615 ms, and 0.0595 -> 0.0618 in config 5's state (profiles/r05/ab_policy_bf16_waveskip*.jsonl; 99.9 % of waves hold an env at a port), not kept
+#endif
+// OR over the 64 lanes of a wave, wave-uniform: a prefix OR within each 16-lane row (DPP
+// row_shr 1, 2, 4, 8), then the four rows' last lanes
+__device__ __forceinline__ uint32_t wave_or32(uint32_t x) {
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+    return (uint32_t)(__builtin_amdgcn_readlane((int)x, 15) | __builtin_amdgcn_readlane((int)x, 31) |
+                      __builtin_amdgcn_readlane((int)x, 47) | __builtin_amdgcn_readlane((int)x, 63));
+}
+__device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
+    return (uint64_t)wave_or32((uint32_t)x) | (uint64_t)wave_or32((uint32_t)(x >> 32)) << 32;
+}
 #ifndef SHIPENV_POLICY_NXT_WAIT
 #define SHIPENV_POLICY_NXT_WAIT 1  // the next tile's loads waited for before the stores (policy_kernel): 0.0598 -> 0.0593 ms (profiles/r05/ab_policy_bf16_stage.jsonl)
 #endif
@@ -800,6 +819,11 @@ void policy_kernel(PolicyArgs A) {
             };
             v64 = 0xfull | (sel << 4) | range64(c_lo, c_hi) | range64(f_lo, f_hi);
         }
+#if SHIPENV_POLICY_WAVE_SKIP
+        // the rows any env of the wave can take (wave-uniform): an fc3 tile's registers that
+        // hold none of them are skipped, the moves-only registers of a wave at sea included
+        const uint64_t u64 = use64 ? wave_or64(v64) : ~0ull;
+#endif
 #endif
         float best = -INFINITY;
         int bidx = 0x7fffffff;
@@ -816,7 +840,11 @@ void policy_kernel(PolicyArgs A) {
 #if SHIPENV_POLICY_VALID64
             if (use64) {
                 m = (uint32_t)(v64 >> (base & 63));
+#if SHIPENV_POLICY_WAVE_SKIP
+                if ((uint32_t)(u64 >> (base & 63)) == 0u) continue;
+#else
                 if (!__any(m != 0u)) continue;
+#endif
             } else
 #endif
             {
@@ -832,7 +860,16 @@ void policy_kernel(PolicyArgs A) {
                 }
             }
             // registers that hold no valid action for any env are skipped (wave-uniform)
+#if SHIPENV_POLICY_VALID64 && SHIPENV_POLICY_WAVE_SKIP
+            uint32_t rm = __builtin_amdgcn_readfirstlane(REGM[mt]);
+            if (use64) {  // ... and those that hold none for this wave's envs
+                uint32_t u2 = (uint32_t)(u64 >> (base & 63));
+                u2 |= u2 >> 4;  // lane half h holds rows 4h + (reg & 3) + 8 (reg >> 2)
+                rm &= (u2 & 0xFu) | ((u2 >> 4) & 0xF0u) | ((u2 >> 8) & 0xF00u) | ((u2 >> 12) & 0xF000u);
+            }
+#else
             const uint32_t rm = __builtin_amdgcn_readfirstlane(REGM[mt]);
+#endif
             bf16x8 wf[8];  // the tile's 8 fragments, read before the chain consumes them
 #pragma unroll
             for (int k = 0; k < 8; ++k) wf[k] = W3f[(mt * 8 + k) * 64 + lane];
@@ -866,7 +903,10 @@ void policy_kernel(PolicyArgs A) {
                 int bt = 0;
 #pragma unroll
                 for (int reg = 0; reg < 16; ++reg) {
-                    if (!((rm >> reg) & 1u)) continue;
+                    // (SHIPENV_POLICY_RM_SKIP 0: no per-register skip; the row masks already
+                    // exclude every row no env can take, and the skip's branches were laid out
+                    // with the common case taken twice per register)
+                    if (SHIPENV_POLICY_RM_SKIP && !((rm >> reg) & 1u)) continue;
                     const int i = (reg & 3) + 8 * (reg >> 2);
                     const bool better = ((m >> i) & 1u) && c[reg] > best;  // ascending rows: first max
                     best = better ? c[reg] : best;

@@ -19,6 +19,9 @@ def main():
     p.add_argument("--n", type=int, default=1 << 20)
     p.add_argument("--launches", type=int, default=20)
     p.add_argument("--steps", type=int, default=20, help="policy+step iterations before timing")
+    p.add_argument("--preroll", type=int, default=0,
+                   help="bench.py config 5's state: auto-reset envs, this many steps at epsilon 1.0 "
+                        "(bench: 300) before the --steps ones")
     p.add_argument("--eps", type=float, default=0.1)
     p.add_argument("--lib", default=None)
     p.add_argument("--precision", default="bf16", choices=("bf16", "f32"))
@@ -30,10 +33,12 @@ def main():
     from shippingenv_amd.policy import DQNNetwork, QPolicy
     from shippingenv_amd.vec import VecEnv
 
-    env = VecEnv(a.n, seed=2026, device="cuda:0")
+    env = VecEnv(a.n, seed=2026, device="cuda:0", auto_reset=a.preroll > 0)
     env.reset()
     torch.manual_seed(2026)
     pol = QPolicy(env, DQNNetwork(env.obs_size, env.action_space_size))
+    for t in range(a.preroll):
+        env.step(pol.act(1.0, 200_000 + t))
     for t in range(a.steps):
         env.step(pol.act(a.eps, t))
     px = torch.as_tensor(env.port_x, device="cuda:0").long()
@@ -48,7 +53,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     print(json.dumps({"lib": os.path.basename(a.lib or "default"), "precision": a.precision,
-                      "f32_mode": os.environ.get("SHIPENV_POLICY_F32", "split-bf16"), "n": a.n, "ms_per_launch": round(e0.elapsed_time(e1) / a.launches, 4),
+                      "f32_mode": os.environ.get("SHIPENV_POLICY_F32", "split-bf16"), "n": a.n, "preroll": a.preroll, "ms_per_launch": round(e0.elapsed_time(e1) / a.launches, 4),
                       "at_port": float(at.float().mean()), "wave32_with_port": float(waves_any)}))
 
 
