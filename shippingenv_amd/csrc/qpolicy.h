@@ -535,6 +535,15 @@ __device__ __forceinline__ void copy_to_lds(const uint4* __restrict__ g, uint4* 
         }
     }
 }
+#ifndef SHIPENV_POLICY_EPS_INT
+#define SHIPENV_POLICY_EPS_INT 0  // 1: policy_kernel's explore test as an integer compare with eps_threshold: 0.05985 -> 0.0607 ms (profiles/r05/ab_policy_bf16_epsint.jsonl), not kept
+#endif
+// u32(w) <= eps (w * 2^-32 in double, exact) as an integer test w <= eps_threshold(eps), for
+// 0 < eps: w <= eps * 2^32 (exact: a power-of-two scaling) <=> w <= floor(eps * 2^32) for an
+// integer w, and every w passes once eps >= 1 (u32(w) < 1)
+__device__ __forceinline__ uint32_t eps_threshold(double eps) {
+    return eps >= 1.0 ? 0xFFFFFFFFu : (uint32_t)floor(eps * 4294967296.0);
+}
 #ifndef SHIPENV_POLICY_RM_SKIP
 #define SHIPENV_POLICY_RM_SKIP 1  // 0: every register of an fc3 tile tested: 0.0591 -> 0.0603 ms (profiles/r05/ab_policy_bf16_rmskip.jsonl), not kept
 #endif
@@ -687,6 +696,9 @@ void policy_kernel(PolicyArgs A) {
     const int64_t stride = (int64_t)gridDim.x * kPolicyWaves;
 #if !SHIPENV_POLICY_EARLY_ENV
     EnvIn nxt = load_env(tile < tiles ? tile : 0);
+#endif
+#if SHIPENV_POLICY_EPS_INT
+    const uint32_t eps_thr = eps_threshold(A.eps);
 #endif
 #if SHIPENV_POLICY_DRAW_PAIR
     // past the world image (and the bias fragments of SHIPENV_POLICY_BFOLD23)
@@ -958,7 +970,11 @@ void policy_kernel(PolicyArgs A) {
 #else
                 const U4 d = draw(env_key(A.seed, A.env_base + e), A.t, kSlotPolicy);
 #endif
+#if SHIPENV_POLICY_EPS_INT
+                if (d.v[0] <= eps_thr) {  // np.random.rand() <= epsilon (:191), as an integer compare
+#else
                 if (u32(d.v[0]) <= A.eps) {  // np.random.rand() <= epsilon (:191)
+#endif
                     // random.choice(valid_actions) (:192): the k-th valid action, ascending
                     const int nsel = __popcll(sel);
                     int k = uniform_int(d.v[1], (uint32_t)(4 + nsel + cst + fst));
