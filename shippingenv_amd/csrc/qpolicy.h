@@ -1003,6 +1003,177 @@ void policy_kernel(PolicyArgs A) {
     }
 }
 
+// ------------------------------------------------------------------ the paired-tile form
+// (SHIPENV_POLICY_PAIR, compact layouts of at most 64 rows, no q_out) The same step with two
+// 32-env tiles per wave iteration: every fragment read from LDS feeds two MFMAs (one per
+// tile), so a wave reads the network half as often per env and has two independent
+// accumulation chains in flight; 512-thread workgroups, two waves per SIMD at up to 256
+// VGPRs (the two tiles' activations). Results are those of policy_kernel<false>: the same
+// bf16 products in the same order per env, the same masked first maximum and draws.
+// Measured slower: 0.0603 -> 0.0723 ms per call in config 5's state (226 VGPRs, two waves per
+// SIMD; profiles/r05/ab_policy_bf16_pair.jsonl), so halving the fragment reads does not pay for
+// the halved occupancy; off by default (the policy tests pass on it: SHIPENV_POLICY_PAIR=1)
+#ifndef SHIPENV_POLICY_PAIR
+#define SHIPENV_POLICY_PAIR 0
+#endif
+constexpr int kPairBlock = 512;
+constexpr int kPairWaves = kPairBlock / 64;
+__global__ __launch_bounds__(kPairBlock) void policy_pair_kernel(PolicyArgs A) {
+    extern __shared__ uint4 smem[];
+    const QnetDims q = A.q;
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+    const int64_t tiles = (A.n + 31) >> 5, pairs = (tiles + 1) >> 1;
+    struct EnvIn {
+        double fuel;
+        uint32_t x, y, o8, d8;
+    };
+    auto load_env = [&](int64_t tile) {
+        const int64_t e = tile * 32 + r;
+        const int64_t ei = e < A.n ? e : A.n - 1;
+        return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei]};
+    };
+    int64_t pair = (int64_t)blockIdx.x * kPairWaves + (threadIdx.x >> 6);
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);  // each SIMD's second wave
+    const int qwords = q.bytes() / 16;
+    {  // the image, fc1's bias in the padding half of its k-step (policy_kernel, SHIPENV_POLICY_B1FOLD)
+        const int w1w = q.w1() / 16, b1f = q.b1() / 4;
+        for (int i = threadIdx.x; i < qwords; i += kPairBlock) {
+            const int k = i - w1w;
+            if ((unsigned)k < 4u * 64u && (k & 32)) {
+                const float b = reinterpret_cast<const float*>(A.qimg)[b1f + (k >> 6) * 32 + (k & 31)];
+                __bf16 p0, p1, p2;
+                split3(b, p0, p1, p2);
+                bf16x8 v{};
+                v[0] = p0;
+                v[1] = p1;
+                v[2] = p2;
+                smem[i] = __builtin_bit_cast(uint4, v);
+            } else {
+                smem[i] = A.qimg[i];
+            }
+        }
+    }
+    const LdsWorld w = stage_world(A.world, A.dims, reinterpret_cast<uint32_t*>(smem + qwords));
+    const uint8_t* qb = reinterpret_cast<const uint8_t*>(smem);
+    const bf16x8* W1f = reinterpret_cast<const bf16x8*>(qb + q.w1());
+    const bf16x8* W2f = reinterpret_cast<const bf16x8*>(qb + q.w2());
+    const bf16x8* W3f = reinterpret_cast<const bf16x8*>(qb + q.w3());
+    const float* B2 = reinterpret_cast<const float*>(qb + q.b2());
+    const float* B3 = reinterpret_cast<const float*>(qb + q.b3());
+    const uint64_t* SAME = reinterpret_cast<const uint64_t*>(qb + q.same());
+    const uint32_t* REGM = reinterpret_cast<const uint32_t*>(qb + q.regm());
+    const int64_t stride = (int64_t)gridDim.x * kPairWaves;
+    EnvIn nxt[2];
+    {
+        const int64_t p0 = pair < pairs ? pair : 0;
+        nxt[0] = load_env(2 * p0);
+        nxt[1] = load_env(2 * p0 + 1);
+    }
+    for (; pair < pairs; pair += stride) {
+        EnvIn cur[2] = {nxt[0], nxt[1]};
+        if (pair + stride < pairs) {
+            nxt[0] = load_env(2 * (pair + stride));
+            nxt[1] = load_env(2 * (pair + stride) + 1);
+        }
+        bf16x8 ob[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {  // the observation rows (policy_kernel)
+            const float ff = (float)cur[t].fuel;
+            const __bf16 fh = (__bf16)ff, fl = (__bf16)(ff - (float)fh);
+            const int origin = cur[t].o8 == SE_NONE ? -1 : (int)cur[t].o8;
+            const int dest = cur[t].d8 == SE_NONE ? -1 : (int)cur[t].d8;
+            bf16x8 o;
+            o[0] = (__bf16)(float)(int)cur[t].x;
+            o[1] = (__bf16)(float)(int)cur[t].y;
+            o[2] = fh;
+            o[3] = fl;
+            o[4] = fh;
+            o[5] = fl;
+            o[6] = (__bf16)(float)origin;
+            o[7] = (__bf16)(float)dest;
+            if (h) {  // k = 8..10: 1.0 against fc1's bias parts
+                o = bf16x8{};
+                o[0] = o[1] = o[2] = (__bf16)1.0f;
+            }
+            ob[t] = o;
+        }
+        bf16x8 h1[2][4][2], h2[2][4][2];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {  // fc1 + relu
+            const bf16x8 f = W1f[mt * 64 + lane];
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+                relu_pack(__builtin_amdgcn_mfma_f32_32x32x16_bf16(f, ob[t], f32x16{}, 0, 0, 0), h1[t][mt]);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {  // fc2 + relu, one row tile at a time, the two tiles' chains side by side
+            const f32x16 b = bias_frag(B2 + mt * 32 + 4 * h);
+            f32x16 c2[2] = {b, b};
+            bf16x8 wf[2];
+            wf[0] = W2f[(mt * 8) * 64 + lane];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (k + 1 < 8) wf[(k + 1) & 1] = W2f[(mt * 8 + k + 1) * 64 + lane];
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+                    c2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k & 1], h1[t][k >> 1][k & 1], c2[t], 0, 0, 0);
+            }
+#pragma unroll
+            for (int t = 0; t < 2; ++t) relu_pack(c2[t], h2[t][mt]);
+        }
+        EnvValid v[2];
+        uint64_t v64[2];
+        float best[2];
+        int bidx[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            v[t] = env_valid(w, q, SAME, (int)cur[t].x, (int)cur[t].y, cur[t].o8 == SE_NONE ? -1 : (int)cur[t].o8);
+            v64[t] = valid_rows64(v[t]);
+            best[t] = -INFINITY;
+            bidx[t] = 0x7fffffff;
+        }
+        for (int mt = 0; mt < q.mt3; ++mt) {  // fc3 + the masked first maximum (policy_kernel)
+            const int base = mt * 32;
+            const uint32_t m0 = (uint32_t)(v64[0] >> (base & 63)), m1 = (uint32_t)(v64[1] >> (base & 63));
+            if (!__any((m0 | m1) != 0u)) continue;
+            const uint32_t rm = __builtin_amdgcn_readfirstlane(REGM[mt]);
+            const f32x16 b = bias_frag(B3 + mt * 32 + 4 * h);
+            f32x16 c[2] = {b, b};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const bf16x8 f = W3f[(mt * 8 + k) * 64 + lane];
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+                    c[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, h2[t][k >> 1][k & 1], c[t], 0, 0, 0);
+            }
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const uint32_t m = (t ? m1 : m0) >> (4 * h);  // register reg holds row base + 4h + (reg & 3) + 8 (reg >> 2)
+                const float best0 = best[t];
+                int bt = 0;
+#pragma unroll
+                for (int reg = 0; reg < 16; ++reg) {
+                    if (!((rm >> reg) & 1u)) continue;
+                    const int i = (reg & 3) + 8 * (reg >> 2);
+                    const bool better = ((m >> i) & 1u) && c[t][reg] > best[t];  // ascending rows: first max
+                    best[t] = better ? c[t][reg] : best[t];
+                    bt = better ? i : bt;
+                }
+                bidx[t] = best[t] != best0 ? base + 4 * h + bt : bidx[t];
+            }
+        }
+        // the next pair's env loads waited for before the stores (policy_kernel, SHIPENV_POLICY_NXT_WAIT)
+        asm volatile("" ::"v"(nxt[0].fuel), "v"(nxt[0].x), "v"(nxt[0].y), "v"(nxt[0].o8), "v"(nxt[0].d8),
+                     "v"(nxt[1].fuel), "v"(nxt[1].x), "v"(nxt[1].y), "v"(nxt[1].o8), "v"(nxt[1].d8));
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int64_t e = (2 * pair + t) * 32 + r;
+            FINISH_ENV(v[t], e, e < A.n, h, best[t], bidx[t], cur[t].x, cur[t].y, cur[t].o8, cur[t].d8,
+                       (float)cur[t].fuel);
+        }
+    }
+}
+
 // ------------------------------------------------------------------ the f32 policy step
 // The fp32-faithful form of the same step (se_policy_f32): DQNNetwork evaluated in f32 as
 // agents/dqn.py:198-200 runs it (fp32 weights, fp32 activations), on
@@ -2072,8 +2243,18 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
         A.rec_head = rec->head;
         A.rec_cap = rec->cap;
     }
-    if (q_out) policy_kernel<true><<<grid, kPolicyBlock, lds, (hipStream_t)stream>>>(A);
-    else policy_kernel<false><<<grid, kPolicyBlock, lds, (hipStream_t)stream>>>(A);
+    if (SHIPENV_POLICY_PAIR && !q_out && q.mt3 <= 2 && !getenv("SHIPENV_POLICY_UNPAIRED")) {
+        static std::atomic<uint64_t> lds_set_p{0};
+        rc = allow_dynamic_lds(lds_set_p, reinterpret_cast<const void*>(policy_pair_kernel), 160 * 1024, env->device);
+        if (rc) return rc;
+        const int64_t pairs = (tiles + 1) / 2, wantp = (pairs + kPairWaves - 1) / kPairWaves;
+        const int gridp = (int)(wantp < dev_cus ? wantp : dev_cus);
+        policy_pair_kernel<<<gridp, kPairBlock, q.bytes() + lds_bytes(env), (hipStream_t)stream>>>(A);
+    } else if (q_out) {
+        policy_kernel<true><<<grid, kPolicyBlock, lds, (hipStream_t)stream>>>(A);
+    } else {
+        policy_kernel<false><<<grid, kPolicyBlock, lds, (hipStream_t)stream>>>(A);
+    }
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }
