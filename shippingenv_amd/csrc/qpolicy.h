@@ -2243,7 +2243,7 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
         A.rec_head = rec->head;
         A.rec_cap = rec->cap;
     }
-    if (SHIPENV_POLICY_PAIR && !q_out && q.mt3 <= 2 && !getenv("SHIPENV_POLICY_UNPAIRED")) {
+    if (SHIPENV_POLICY_PAIR && !q_out && q.mt3 <= 2) {
         static std::atomic<uint64_t> lds_set_p{0};
         rc = allow_dynamic_lds(lds_set_p, reinterpret_cast<const void*>(policy_pair_kernel), 160 * 1024, env->device);
         if (rc) return rc;
