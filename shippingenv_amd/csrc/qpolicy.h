@@ -253,6 +253,22 @@ __device__ __forceinline__ f32x16 bias_frag(const float* b) {
 // 32-row tile where an f32 max per register took 24.
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
+// a - b on two f32 lanes as two v_sub_f32 (SHIPENV_SCALAR_SUB): the vector form compiles to
+// v_pk_add_f32, whose issue beside MFMAs costs more than two scalar subtractions
+// (MI355X_MICROARCH.md, per-instruction constants). Exact either way.
+#ifndef SHIPENV_SCALAR_SUB
+#define SHIPENV_SCALAR_SUB 1  // fp32 policy 0.2617 -> 0.2605 ms, update 0.03685 -> 0.0368 ms (profiles/r05/ab_policy_f32_scalarsub.jsonl, ab_update_scalarsub.jsonl): about even
+#endif
+__device__ __forceinline__ f32x2 sub2(f32x2 a, f32x2 b) {
+#if SHIPENV_SCALAR_SUB
+    float r0, r1;
+    asm("v_sub_f32 %0, %1, %2" : "=v"(r0) : "v"(a[0]), "v"(b[0]));
+    asm("v_sub_f32 %0, %1, %2" : "=v"(r1) : "v"(a[1]), "v"(b[1]));
+    return f32x2{r0, r1};
+#else
+    return a - b;
+#endif
+}
 typedef __attribute__((ext_vector_type(2))) short i16x2;
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 __device__ __forceinline__ void relu_pack(const f32x16& c, bf16x8 (&out)[2]) {
@@ -1527,7 +1543,7 @@ __device__ __forceinline__ void pack_x3_items(const PackX3Args& A, uint8_t* img,
         u32x4 w[3];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const f32x2 x{v[2 * k], v[2 * k + 1]};
+            const f32x2 x{v[2 * k], v[2 * k + 1]};  // (the pack, not beside MFMAs: packed subtractions)
             const bf16x2 p0 = __builtin_convertvector(x, bf16x2);
             const f32x2 r1 = x - __builtin_convertvector(p0, f32x2);
             const bf16x2 p1 = __builtin_convertvector(r1, bf16x2);
@@ -1643,9 +1659,9 @@ __device__ __forceinline__ void relu_split3(const f32x16& c, bf16x8 (&out)[2][3]
         for (int p = 0; p < 4; ++p) {
             const f32x2 v{relu_bits(c[8 * s + 2 * p]), relu_bits(c[8 * s + 2 * p + 1])};
             const bf16x2 a = __builtin_convertvector(v, bf16x2);
-            const f32x2 r1 = v - __builtin_convertvector(a, f32x2);
+            const f32x2 r1 = sub2(v, __builtin_convertvector(a, f32x2));
             const bf16x2 b = __builtin_convertvector(r1, bf16x2);
-            const bf16x2 e = __builtin_convertvector(r1 - __builtin_convertvector(b, f32x2), bf16x2);
+            const bf16x2 e = __builtin_convertvector(sub2(r1, __builtin_convertvector(b, f32x2)), bf16x2);
             out[s][0][2 * p] = a[0];
             out[s][0][2 * p + 1] = a[1];
             out[s][1][2 * p] = b[0];
@@ -1716,10 +1732,10 @@ __device__ __forceinline__ void split_chunk(const f32x16& c, bf16x8 (&out)[2][3]
         const bf16x2 a = __builtin_convertvector(v, bf16x2);
         out[s][0][2 * p] = a[0];
         out[s][0][2 * p + 1] = a[1];
-        r[pr] = v - __builtin_convertvector(a, f32x2);
+        r[pr] = sub2(v, __builtin_convertvector(a, f32x2));
     } else {
         const bf16x2 b = __builtin_convertvector(r[pr], bf16x2);
-        const bf16x2 e = __builtin_convertvector(r[pr] - __builtin_convertvector(b, f32x2), bf16x2);
+        const bf16x2 e = __builtin_convertvector(sub2(r[pr], __builtin_convertvector(b, f32x2)), bf16x2);
         out[s][1][2 * p] = b[0];
         out[s][1][2 * p + 1] = b[1];
         out[s][2][2 * p] = e[0];
@@ -1739,9 +1755,9 @@ __device__ __forceinline__ void split_pair(const f32x16& c, bf16x8 (&out)[2][3],
 #endif
     const f32x2 v{relu_bits(c[8 * s + 2 * p]), relu_bits(c[8 * s + 2 * p + 1])};
     const bf16x2 a = __builtin_convertvector(v, bf16x2);
-    const f32x2 r1 = v - __builtin_convertvector(a, f32x2);
+    const f32x2 r1 = sub2(v, __builtin_convertvector(a, f32x2));
     const bf16x2 b = __builtin_convertvector(r1, bf16x2);
-    const bf16x2 e = __builtin_convertvector(r1 - __builtin_convertvector(b, f32x2), bf16x2);
+    const bf16x2 e = __builtin_convertvector(sub2(r1, __builtin_convertvector(b, f32x2)), bf16x2);
     out[s][0][2 * p] = a[0];
     out[s][0][2 * p + 1] = a[1];
     out[s][1][2 * p] = b[0];

@@ -336,9 +336,9 @@ __device__ __forceinline__ void split8_half(const float4& a, const float4& b, bf
     for (int q = 2 * half; q < 2 * half + 2; ++q) {
         const f32x2 x{v[2 * q], v[2 * q + 1]};
         const bf16x2 p0 = __builtin_convertvector(x, bf16x2);
-        const f32x2 r1 = x - __builtin_convertvector(p0, f32x2);
+        const f32x2 r1 = sub2(x, __builtin_convertvector(p0, f32x2));
         const bf16x2 p1 = __builtin_convertvector(r1, bf16x2);
-        const bf16x2 p2 = __builtin_convertvector(r1 - __builtin_convertvector(p1, f32x2), bf16x2);
+        const bf16x2 p2 = __builtin_convertvector(sub2(r1, __builtin_convertvector(p1, f32x2)), bf16x2);
         w[0][2 * q] = p0[0];
         w[0][2 * q + 1] = p0[1];
         w[1][2 * q] = p1[0];
