@@ -767,7 +767,7 @@ void policy_kernel(PolicyArgs A) {
 #define SHIPENV_FC2_SPLIT 4  // one pass per row tile: no spills at 128 VGPRs (2 passes spill 7, 1 spills 14)
 #endif
 #ifndef SHIPENV_POLICY_LOOKAHEAD
-#define SHIPENV_POLICY_LOOKAHEAD 1  // fc2 fragments read this many k-steps ahead (0: as needed; 3 no better, 2 spills)
+#define SHIPENV_POLICY_LOOKAHEAD 1  // fc2 fragments read this many k-steps ahead (0: as needed); 2 and 3 now fit 128 VGPRs and measure even (0.0603 / 0.0601 / 0.061 ms, profiles/r05/ab_policy_bf16_la.jsonl)
 #endif
         // fc2 + relu in SHIPENV_FC2_SPLIT passes over the 4 row tiles: the tiles of a pass
         // advance together (consecutive MFMAs independent, a k-step's fragments read in one
