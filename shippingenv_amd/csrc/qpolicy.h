@@ -1692,7 +1692,7 @@ __device__ __forceinline__ f32x16 kstep_x3(const bf16x8* Wf, int lane, const bf1
                           // 4 no fragment re-reads, 8 no splits
 #endif
 #ifndef SHIPENV_X3_LOOKAHEAD
-#define SHIPENV_X3_LOOKAHEAD 2  // k-steps ahead that fc2 / fc3's fragments are read
+#define SHIPENV_X3_LOOKAHEAD 2  // k-steps ahead that fc2 / fc3's fragments are read; 1 / 3: 0.2582 / 0.2569 vs 0.2549 ms (profiles/r05/ab_policy_f32_la.jsonl)
 #endif
 #ifndef SHIPENV_X3_STAGGER
 #define SHIPENV_X3_STAGGER 0  // experiment: waves 4-7 sleep this many x 6400 cycles first
