@@ -38,7 +38,7 @@ STAMP = OUT + ".cmd"  # the flags that built OUT: options, defines and arch (no 
 
 
 def _flags():
-    extra = os.environ.get("SHIPENV_HIPCC_DEFINES", "").split()  # e.g. -DSHIPENV_POLICY_BLOCK=768
+    extra = os.environ.get("SHIPENV_HIPCC_DEFINES", "").split()  # e.g. -DSHIPENV_TRACE=1 (the instrumentation builds)
     return FLAGS + extra
 
 

@@ -61,11 +61,8 @@ __device__ __forceinline__ U4 philox10(uint32_t c0, uint32_t c1, uint32_t c2, ui
     // instead of the compiler hoisting every block's schedule out of the step
     // loop: ~20 live SGPRs per block spilled to VGPR lanes (v_readlane + s_nop).
     asm volatile("" : "+s"(k0), "+s"(k1));
-#ifndef SHIPENV_PHILOX_ROUNDS
-#define SHIPENV_PHILOX_ROUNDS 10  // the contract; other values are timing-only ablations
-#endif
 #pragma unroll
-    for (int r = 0; r < SHIPENV_PHILOX_ROUNDS; ++r) {
+    for (int r = 0; r < 10; ++r) {
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
         // three-way xor in one v_bitop3_b32 (truth table 0x96, gfx950)

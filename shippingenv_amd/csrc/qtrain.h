@@ -8,7 +8,7 @@
 // The torch version is about 50 small kernels per update, launch-bound below B = 2^13.
 // Here it is two kernels, all in f32 arithmetic, deterministic (fixed summation orders, no
 // atomics). The forward GEMMs (fc2 of both nets, the target's fc3) run on bf16 MFMA with
-// every f32 operand split into three bf16 parts (SHIPENV_QT_X3, below); fc1 and the
+// every f32 operand split into three bf16 parts (x3_index, below); fc1 and the
 // backward on v_mfma_f32_32x32x2_f32 (an exact f32 fma chain; gfx950 has no xf32):
 //
 // T1, qtrain_tile_kernel (one workgroup per 32 samples, 8 waves: the online and the
@@ -86,68 +86,32 @@ struct QtWork {
     float* part_w3;  // [tiles][32][128]: only the rows of live slots are stored
     float* part_b3;  // [tiles][32]
     int32_t* part_map; // [tiles][32]
-    // SHIPENV_QT_SLOT_TABLE: part_slot[a][t] = the slot of action a in tile t (0..31), 0xff when
+    // part_slot[a][t] = the slot of action a in tile t (0..31), 0xff when
     // the tile has none; row stride slot_ld (the workspace's tile capacity)
     uint8_t* part_slot;
     int64_t slot_ld;
 };
 
-#ifndef SHIPENV_QT_NT
-#define SHIPENV_QT_NT 0  // 1 = T1's gradient partials leave with nontemporal stores (experiment)
-#endif
-__device__ __forceinline__ void st_part(float* p, float v) {
-    if constexpr (SHIPENV_QT_NT != 0) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
+__device__ __forceinline__ void st_part(float* p, float v) { *p = v; }
 // T1's dW2 / dW3 partials as 16-byte stores (4 consecutive f1 / feature columns of one
 // row: the MFMAs take H1 / H2 as their A operand, so a lane's accumulator registers 4q..4q+3
-// are 4 adjacent columns). SHIPENV_QT_WT = 1: write-through (sc1), so the 12.6-16.8 MB of
+// are 4 adjacent columns), write-through (buffer-store aux 16 = sc1), so the 12.6-16.8 MB of
 // partials are not left dirty in the XCDs' L2s for the kernel boundary to flush before T2
-// (MI355X_MICROARCH.md price list, "boundary" and "publish-large"); 2: the small partials
-// too; 0: plain stores. Update at B = 8192: 42.2 (4-byte plain stores) -> 41.3 (16-byte
-// plain) -> 39.65 us (16-byte write-through) (profiles/r04/ab_update_t1_wt.jsonl).
-#ifndef SHIPENV_QT_WT
-#define SHIPENV_QT_WT 1
-#endif
-// the 16-byte partial stores' cache bits (buffer-store aux): 16 = sc1, write-through. Per update
-// at B = 8192 (profiles/r04/ab_update_t1_aux.jsonl, medians of 12 alternating runs): 16 39.3 us,
-// 17 (sc0 + sc1) 39.25, 2 (nt) 40.8, 18 (sc1 + nt) 46.35
-#ifndef SHIPENV_QT_AUX
-#define SHIPENV_QT_AUX 16
-#endif
-// T1's second-dispatched half (waves 4-7, the target net's) at issue priority 1 for the whole
-// kernel: each SIMD holds one online and one target wave, and at equal priority the older
-// (online) wave wins every VALU arbitration, so the target waves finished fc2 2.3 us after the
-// online ones (profiles/r04/qtrace_t1_t2_r04.jsonl). MI355X_MICROARCH.md "Two waves per SIMD"
-// item 4, cdna_hip_programming.md T5 static form. 39.95 -> 39.6 us per update (median of 12,
-// alternating builds, profiles/r04/ab_prio.jsonl); 0 = off.
-#ifndef SHIPENV_QT_PRIO
-#define SHIPENV_QT_PRIO 1
-#endif
-#ifndef SHIPENV_QT_ABL
-#define SHIPENV_QT_ABL 0  // timing-only ablations of T1 (1: no dW2 partial stores, 2: no dW3 partial stores)
-#endif
-// the small per-tile partials (dW1's 6 columns, db1, db2, db3, the slot map, the loss and
-// weight sums; 4.4 KB per tile) as 4-byte stores: write-through too at SHIPENV_QT_WT = 2
+// (MI355X_MICROARCH.md price list, "boundary" and "publish-large"). Update at B = 8192: 42.2
+// (4-byte plain stores) -> 41.3 (16-byte plain) -> 39.65 us (16-byte write-through)
+// (profiles/r04/ab_update_t1_wt.jsonl); other aux bits 17 (sc0 + sc1) 39.25, 2 (nt) 40.8,
+// 18 (sc1 + nt) 46.35 against 16's 39.3 us (profiles/r04/ab_update_t1_aux.jsonl); the small
+// partials write-through too: +9.7 us (profiles/r04/ab_update_t1_wt_small.jsonl).
 template <typename T>
 __device__ __forceinline__ void st_part1(T* p, T v) {
     static_assert(sizeof(T) == 4, "4-byte partials");
-    if constexpr (SHIPENV_QT_WT >= 2) {
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, (short)0, 0x7fffffff, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, 0u, 0, 16);  // aux 16: sc1
-    } else {
-        *p = v;
-    }
+    *p = v;
 }
 __device__ __forceinline__ void st_part4(float* base, uint32_t idx, float a, float b, float c, float d) {
     const uint4 w = make_uint4(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b),
                                __builtin_bit_cast(uint32_t, c), __builtin_bit_cast(uint32_t, d));
-    if constexpr (SHIPENV_QT_WT != 0) {
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), r, 4u * idx, 0, SHIPENV_QT_AUX);
-    } else {
-        *reinterpret_cast<uint4*>(base + idx) = w;
-    }
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), r, 4u * idx, 0, 16);  // aux 16: sc1
 }
 
 __device__ __forceinline__ int acc_r(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
@@ -167,24 +131,16 @@ struct Frags {
     }
 };
 
-#ifndef SHIPENV_QT_LATE_ADAM
-#define SHIPENV_QT_LATE_ADAM 1  // T2: Adam's constants after the sums' loads are issued (0: at the start)
-#endif
-#ifndef SHIPENV_QT_W3U
-#define SHIPENV_QT_W3U 16  // T2: dW3 rows gathered per thread and round (8 x kU rows per round)
-#endif
-#ifndef SHIPENV_QT_LOOKAHEAD
-#define SHIPENV_QT_LOOKAHEAD 8  // B operands read this many k-steps ahead of their MFMA (0: as needed)
-#endif
 // acc += A (fragments in registers) x B (an LDS [k][kLS] tile), k-steps [S0, S1). The B
-// operands are read kLookahead k-steps ahead of the MFMA that uses them, pinned in that
+// operands are read kQtLookahead k-steps ahead of the MFMA that uses them, pinned in that
 // order by scheduling groups (one LDS read, one MFMA): left to itself the compiler read
 // each pair just before its two MFMAs, so every pair waited out an LDS round trip.
+constexpr int kQtLookahead = 8;
 template <int kSteps, int S0 = 0, int S1 = kSteps>
 __device__ __forceinline__ f32x16 gemm_lds(const Frags<kSteps>& a, const float* src, f32x16 acc, int lane) {
     const int h = lane >> 5, c = lane & 31;
     constexpr int N = S1 - S0;
-    constexpr int L = SHIPENV_QT_LOOKAHEAD < N ? SHIPENV_QT_LOOKAHEAD : N;
+    constexpr int L = kQtLookahead < N ? kQtLookahead : N;
     if constexpr (L == 0) {
 #pragma unroll
         for (int s = S0; s < S1; ++s) acc = mfma_f32(a.v[s], src[(2 * s + h) * kLS + c], acc);
@@ -230,65 +186,16 @@ __device__ __forceinline__ void store_relu(float* dst, int tile, const f32x16& a
 // every f32 operand split into three bf16 parts (split3 in qpolicy.h: round to nearest, exact
 // remainders) and the six part products of order <= 2, smallest first: the policy's
 // fp32-faithful datapath (§10), at 6 x 32 MFMA cycles per K = 16 where the f32 MFMA takes
-// 8 x 64. The weights stay f32 in global memory, in the order the bf16 A operand reads them
-// (x3_index; 32 B per lane and k-step, the f32 image's bytes), and are split in registers;
-// the activations are split once, by the wave that produced them, into LDS B fragments.
-// 0: the f32 MFMA forward of round 4.
-#ifndef SHIPENV_QT_X3
-#define SHIPENV_QT_X3 1
-#endif
-#ifndef SHIPENV_QT_X3B
-// 1: the backward's MFMAs too (dH1 on dZ2 fragments split by its producer; dW2 / dW3 with both
-// operands read from the f32 LDS tiles and split in registers). Measured slower: update 38.8 ->
-// 41.1 us, backward phase 6.8 -> 8.2 us (profiles/r05/ab_update_x3_backward.jsonl,
-// qtrace_x3_backward.jsonl): the splits of operands that are read once cost more than the MFMA
-// cycles they save. Needs SHIPENV_QT_X3.
-#define SHIPENV_QT_X3B 0
-#endif
-#if SHIPENV_QT_X3B && !SHIPENV_QT_X3
-#error "SHIPENV_QT_X3B needs SHIPENV_QT_X3 (its fragments reuse the forward's LDS)"
-#endif
-// 1: fc2 / fc3's weights pre-split in global memory (three bf16 parts, [tile][k-step][part][lane]
-// bf16x8, kstep_x3's layout; 6 B per weight instead of 4), so T1 runs no weight splits; 0: f32
-// weights split in registers
-#ifndef SHIPENV_QT_X3W
-#define SHIPENV_QT_X3W 1
-#endif
-#if SHIPENV_QT_X3W && !SHIPENV_QT_X3
-#error "SHIPENV_QT_X3W needs SHIPENV_QT_X3"
-#endif
-// 1: dW2 and dW3 (the target waves' part of the backward) on split-bf16 MFMA over K = 32
-// samples, with operands split once into sample-major LDS tiles by transposing passes in
-// phases that already exist (h1 and h2 in the q / g phase, dZ2 by the dZ2 phase itself, which
-// then takes one feature and 8 samples per thread): 12 MFMAs of 32 cycles per 32 x 32 tile
-// where the f32 MFMA ran 16 of 64. dH1 stays on f32 MFMA. Needs SHIPENV_QT_X3, not _X3B.
-// Measured slower: 34.0 -> 37.3 us per update back to back, the backward phase 6.9 -> 9.0 us
-// in the stamped build, and the untouched input / fc1 phases slower too
-// (profiles/r05/time_update_x3bt.jsonl, qtrace_x3bt.jsonl): not kept.
-#ifndef SHIPENV_QT_X3BT
-#define SHIPENV_QT_X3BT 0
-#endif
-#if SHIPENV_QT_X3BT && (!SHIPENV_QT_X3 || SHIPENV_QT_X3B)
-#error "SHIPENV_QT_X3BT needs SHIPENV_QT_X3 and excludes SHIPENV_QT_X3B"
-#endif
-#ifndef SHIPENV_QT_PICK_FIRST
-#define SHIPENV_QT_PICK_FIRST 1  // T1: the minibatch picks' first ring loads ahead of the weight loads (0: after)
-#endif
-#ifndef SHIPENV_QT_BIAS_LATE
-#define SHIPENV_QT_BIAS_LATE 1  // T1: fc1's operands loaded first, fc2 / fc3's bias added after the chain (0: as initial values)
-#endif
+// 8 x 64. fc2 / fc3's weights are stored pre-split in global memory (three bf16 parts,
+// [tile][k-step][part][lane] bf16x8, kstep_x3's layout; 6 B per weight instead of 4), so T1
+// runs no weight splits; the activations are split once, by the wave that produced them, into
+// LDS B fragments. The backward stays on f32 MFMA: split-bf16 backward forms measured slower
+// (dH1 / dW2 / dW3 split in registers: update 38.8 -> 41.1 us, profiles/r05/ab_update_x3_backward.jsonl;
+// dW2 / dW3 from sample-major split tiles: 34.0 -> 37.3 us, profiles/r05/time_update_x3bt.jsonl):
+// the splits of operands that are read once cost more than the MFMA cycles they save.
 // T1 also writes each tile's action -> slot table column, so a W3 block of T2 reads one
 // coalesced 256-byte row of it instead of scanning every tile's 32-entry slot map (9.4 MB of
 // map lines across the W3 blocks at B = 8192); 0: the scan
-#ifndef SHIPENV_QT_SLOT_TABLE
-#define SHIPENV_QT_SLOT_TABLE SHIPENV_QT_X3
-#endif
-#if SHIPENV_QT_SLOT_TABLE && !SHIPENV_QT_X3
-#error "SHIPENV_QT_SLOT_TABLE needs SHIPENV_QT_X3 (its LDS map lives past the split fragments)"
-#endif
-#ifndef SHIPENV_QT_X3_SCHED
-#define SHIPENV_QT_X3_SCHED 1  // the next k-step's splits between the MFMAs of this one, fenced (0: the compiler's order)
-#endif
 
 // f32 image index of W[row][k] (128 columns) for the split-bf16 A operand: [row tile][k-step
 // g][lane][8], element j of lane (r, h) = W[32 tile + r][32 (g >> 1) + acc_row(g & 1, j, h)],
@@ -299,7 +206,7 @@ __host__ __device__ __forceinline__ int x3_index(int row, int k) {
     return (((row >> 5) * 8 + g) * 64 + (row & 31) + 32 * h) * 8 + j;
 }
 
-// bf16 index of part 0 of W[row][k] in a pre-split image (SHIPENV_QT_X3W): [row tile][k-step g]
+// bf16 index of part 0 of W[row][k] in a pre-split image: [row tile][k-step g]
 // [part][lane][8], elements as x3_index; part p is 512 p further
 __host__ __device__ __forceinline__ int x3w_index(int row, int k) {
     const int kk = k & 31, g = 2 * (k >> 5) + (kk >> 4), h = (kk >> 2) & 1, j = 4 * ((kk >> 3) & 1) + (kk & 3);
@@ -374,7 +281,7 @@ __device__ __forceinline__ void t_split_row(const float* src, __bf16* T, int slo
 
 // acc + W X over k-steps [g0, g0 + G): W from f32 registers wa[2 (g - g0)], [2 (g - g0) + 1]
 // (split here), X the LDS B fragments S[g][part][lane]. Step g + 1's splits and LDS reads are
-// issued between step g's MFMAs (SHIPENV_QT_X3_SCHED fences: left alone the scheduler
+// issued between step g's MFMAs (sched_barrier fences: left alone the scheduler
 // clustered the VALU ahead of the chain, as in the policy's x3 kernel).
 template <int G>
 __device__ __forceinline__ f32x16 gemm_x3(const float4* wa, const bf16x8* S, int g0, f32x16 acc, int lane) {
@@ -392,15 +299,15 @@ __device__ __forceinline__ f32x16 gemm_x3(const float4* wa, const bf16x8* S, int
         acc = mfma_bf16(w[c][0], x[c][2], acc);
         acc = mfma_bf16(w[c][1], x[c][1], acc);
         acc = mfma_bf16(w[c][2], x[c][0], acc);
-        if (SHIPENV_QT_X3_SCHED) __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);
         if (i + 1 < G) split8_half(wa[2 * i + 2], wa[2 * i + 3], w[n], 0);
-        if (SHIPENV_QT_X3_SCHED) __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);
         acc = mfma_bf16(w[c][0], x[c][1], acc);
         acc = mfma_bf16(w[c][1], x[c][0], acc);
         acc = mfma_bf16(w[c][0], x[c][0], acc);
-        if (SHIPENV_QT_X3_SCHED) __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);
         if (i + 1 < G) split8_half(wa[2 * i + 2], wa[2 * i + 3], w[n], 1);
-        if (SHIPENV_QT_X3_SCHED) __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);
     }
     return acc;
 }
@@ -479,42 +386,15 @@ __global__ __launch_bounds__(kQABlock) void qtrain_pack_kernel(QtPackArgs A) {
             const int row = tile * 32 + (lane & 31), k = 2 * s + (lane >> 5);
             A.W.pw1[A.which][e] = A.net.w1[(int64_t)row * in + k];
         } else if (e < n1 + n2) {
-            if (SHIPENV_QT_X3W) continue;  // the split images: below
-            const int i = e - n1;
-#if SHIPENV_QT_X3  // [tile][g][lane][j] (x3_index)
-            const int j = i & 7, lane = (i >> 3) & 63, g = (i >> 9) & 7, tile = i >> 12;
-            A.W.pw2[A.which][i] = A.net.w2[(tile * 32 + (lane & 31)) * 128 + 32 * (g >> 1) + acc_row(g & 1, j, lane >> 5)];
-#else
-            const int lane = i & 63, s = (i >> 6) & 63, tile = i >> 12;
-            A.W.pw2[A.which][i] = A.net.w2[(tile * 32 + (lane & 31)) * 128 + 2 * s + (lane >> 5)];
-#endif
+            continue;  // fc2's split image: below
         } else if (e < n1 + 2 * n2) {
             if (A.which) continue;  // the transposed image is the online net's (backward)
             const int i = e - n1 - n2, lane = i & 63, s = (i >> 6) & 63, tile = i >> 12;
-#if SHIPENV_QT_X3B  // W2^T in x3_index order: element (f1, f2) = W2[f2][f1]
-            {
-                const int j = i & 7, ln = (i >> 3) & 63, g = (i >> 9) & 7, tl = i >> 12;
-                (void)lane; (void)s; (void)tile;
-                A.W.pw2t[i] = A.net.w2[(32 * (g >> 1) + acc_row(g & 1, j, ln >> 5)) * 128 + tl * 32 + (ln & 31)];
-            }
-#else
             A.W.pw2t[i] = A.net.w2[(2 * s + (lane >> 5)) * 128 + tile * 32 + (lane & 31)];
-#endif
         } else {
-            if (SHIPENV_QT_X3W) continue;
-            const int i = e - n1 - 2 * n2;
-#if SHIPENV_QT_X3
-            const int j = i & 7, lane = (i >> 3) & 63, g = (i >> 9) & 7, tile = i >> 12;
-            const int row = tile * 32 + (lane & 31);
-            A.W.pw3t[i] = row < A.d.A ? A.net.w3[row * 128 + 32 * (g >> 1) + acc_row(g & 1, j, lane >> 5)] : 0.0f;
-#else
-            const int lane = i & 63, s = (i >> 6) & 63, tile = i >> 12;
-            const int row = tile * 32 + (lane & 31);
-            A.W.pw3t[i] = row < A.d.A ? A.net.w3[row * 128 + 2 * s + (lane >> 5)] : 0.0f;
-#endif
+            continue;  // fc3's split image: below
         }
     }
-#if SHIPENV_QT_X3W
     // fc2 (and the target's fc3) pre-split: one item per (tile, k-step, lane), its 8 weights'
     // three parts
     const int m2 = 4 * 8 * 64, m3 = A.which ? A.d.mt3 * 8 * 64 : 0;
@@ -537,7 +417,6 @@ __global__ __launch_bounds__(kQABlock) void qtrain_pack_kernel(QtPackArgs A) {
 #pragma unroll
         for (int q = 0; q < 3; ++q) dst[q * 64] = p[q];
     }
-#endif
 }
 
 struct QtStepArgs {
@@ -600,49 +479,29 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     float* RW = WT + 64;            // [32] r_j
     float* DN = RW + 32;            // [32] done_j
     int* FST = reinterpret_cast<int*>(DN + 32);  // [32] first(j): the dW3 slot of sample j
-#if SHIPENV_QT_X3
     // split-bf16 B fragments [k-step][part][lane]: h1 of both nets, the target's h2; fc3's
     // partial accumulators of the tiles past the eighth ([tile - 8][wt][reg][lane] f32) reuse
     // the h1 fragments once fc2 is done
     bf16x8* SH1 = reinterpret_cast<bf16x8*>(FST + 32);  // [2][8][3][64]
     bf16x8* SH2 = SH1 + 2 * 8 * 3 * 64;                  // [8][3][64]
-#if SHIPENV_QT_X3BT
-    float* XP = TA;  // TA and TB (33.8 KB) are unused until dZ2 in this form; SH1 takes the transposes
-#else
     float* XP = reinterpret_cast<float*>(SH1);
-#endif
     int* MAPL = reinterpret_cast<int*>(SH2 + 8 * 3 * 64);  // [32] the tile's slot map
-#if SHIPENV_QT_X3BT
-    // sample-major split tiles [part][feature][32 samples] bf16 (64 B rows): h1 and h2 of the
-    // online net in the h1 fragments' space once fc2 and fc3 are done, dZ2 in the target h2
-    // fragments' space; g's parts [part][32]
-    __bf16* HTs = reinterpret_cast<__bf16*>(SH1);
-    __bf16* H2Ts = HTs + 3 * 128 * kTS;
-    __bf16* DZ2Ts = reinterpret_cast<__bf16*>(SH2);
-    __bf16* GS = reinterpret_cast<__bf16*>(MAPL + 32);
-#endif
-#endif
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wt = wave & 3;
     const bool tgt = wave >= 4;
     const int64_t r0 = (int64_t)blockIdx.x * kQT;
     const int in = A.d.in;
     QSTAMP(0);
-#if SHIPENV_QT_PRIO  // the younger half at issue priority 1 (a wave-uniform guard: s_setprio ignores EXEC)
     if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= kQTBlock / 2) __builtin_amdgcn_s_setprio(1);
-#endif
     if (A.bump && blockIdx.x == 0 && tid == 0)  // no return value: the wave does not wait on it
         __hip_atomic_fetch_add(A.bump, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
     // fc1's operands and fc2's fragments do not depend on the batch: their loads are in
     // flight while the inputs are staged
     const int net = tgt ? 1 : 0;
-#if SHIPENV_QT_BIAS_LATE
     // fc1's operands first: behind the fragment loads, fc1 waited for all of them
     Frags<3> f1;
     f1.load(A.W.pw1[net] + wt * 3 * 64, lane);
     f32x16 acc1 = bias_init(A.W.c1[net], wt, lane, 128);
-#endif
-#if SHIPENV_QT_PICK_FIRST
     // the first try of wave 0's minibatch picks: its ring loads go out ahead of the weights'
     // (the vector memory counter is in order: behind ~24 KB of fragments per wave they waited)
     PickFirst pf{{-1, 0u, 0u, 0.0f, 0.0f, 0.0f, 0, 0}, -1};
@@ -655,14 +514,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         pkey = draw(env_key(A.seed, kReplayKeyId), pt, kSlotReplay);
         if (r0 + tid < A.B) pf = pick_issue(A.ring, psize, pkey, feistel_half((uint32_t)psize), r0 + tid);
     }
-#endif
-#if SHIPENV_QT_X3
-#if SHIPENV_QT_X3B
-    float4 wd[16];  // W2^T (dH1) in x3_index order, loaded during fc3
-#else
     Frags<64> fb;   // W2^T (dH1), loaded during fc3
-#endif
-#if SHIPENV_QT_X3W
     bf16x8 wa[8][3];  // fc2's pre-split A operands
     {
         const bf16x8* p = reinterpret_cast<const bf16x8*>(A.W.pw2[net]) + wt * 8 * 3 * 64;
@@ -671,41 +523,14 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
 #pragma unroll
             for (int q = 0; q < 3; ++q) wa[g][q] = p[(g * 3 + q) * 64 + lane];
     }
-#else
-    float4 wa[16];  // fc2's f32 A operands in x3_index order, then fc3's
-    {
-        const float4* p = reinterpret_cast<const float4*>(A.W.pw2[net]) + wt * 8 * 64 * 2;
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            wa[2 * g] = p[(g * 64 + lane) * 2];
-            wa[2 * g + 1] = p[(g * 64 + lane) * 2 + 1];
-        }
-    }
-#endif
-#else
-    Frags<64> fa, fb;  // fc2, then fc3 / W2^T: each loaded one layer ahead
-    fa.load(A.W.pw2[net] + wt * 64 * 64, lane);
-#endif
-#if !SHIPENV_QT_BIAS_LATE
-    Frags<3> f1;
-    f1.load(A.W.pw1[net] + wt * 3 * 64, lane);
-    f32x16 acc1 = bias_init(A.W.c1[net], wt, lane, 128);
-#endif
 
     if (A.from_ring) {  // the sampler's pick of row r0 + tid, straight into the tiles
         if (tid < 32) {
             const Ring& ring = A.ring;
             const int64_t row = r0 + tid;
             Pick pk{-1, 0u, 0u, 0.0f, 0.0f, 0.0f, 0, 0};
-#if SHIPENV_QT_PICK_FIRST
             const uint32_t t = pt;
             if (row < A.B) pk = pick_resolve(pf, ring, psize, pkey, feistel_half((uint32_t)psize), row, A.B);
-#else
-            const int64_t size = A.size_host >= 0 ? A.size_host : *ring.d_size;
-            const uint32_t t = A.t_host >= 0 ? (uint32_t)A.t_host : (uint32_t)A.ctr[0];
-            const U4 key = draw(env_key(A.seed, kReplayKeyId), t, kSlotReplay);
-            if (row < A.B) pk = pick_transition(ring, size, key, feistel_half((uint32_t)size), row, A.B);
-#endif
             const bool ok = pk.slot >= 0;
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
@@ -746,19 +571,6 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     // this thread's slice of W3[a_j] (q_j and dZ2 below): sample j = tid >> 4, features
     // 8 (tid & 15) .. + 7
     const int qj = tid >> 4, qpart = tid & 15;
-#if SHIPENV_QT_X3B
-    // (SHIPENV_QT_X3B) features 16 g + 4 h + {0..3, 8..11} of slot (g, h) = (qpart >> 1,
-    // qpart & 1): the elements of lane (qj, h)'s split-bf16 B fragment of dZ2's k-step g
-    const int qf0 = 16 * (qpart >> 1) + 4 * (qpart & 1);
-    auto qfeat = [&](int k) { return qf0 + (k & 3) + 8 * (k >> 2); };
-    float w3s[8];
-    {
-        const float4* w3r = reinterpret_cast<const float4*>(A.on.w3 + (int64_t)ACT[qj] * 128 + qf0);
-        const float4 u = w3r[0], v = w3r[2];
-        w3s[0] = u.x; w3s[1] = u.y; w3s[2] = u.z; w3s[3] = u.w;
-        w3s[4] = v.x; w3s[5] = v.y; w3s[6] = v.z; w3s[7] = v.w;
-    }
-#else
     auto qfeat = [&](int k) { return qpart * 8 + k; };
     float w3s[8];
     {
@@ -766,16 +578,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) w3s[k] = w3r[k];
     }
-#endif
-#if SHIPENV_QT_X3BT
-    // the dZ2 phase's slice: feature tf = tid >> 2 of samples 8 tg .. 8 tg + 7
-    const int tf = tid >> 2, tg = tid & 3;
-    float w3g[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w3g[i] = A.on.w3[(int64_t)ACT[8 * tg + i] * 128 + tf];
-#endif
 
-#if SHIPENV_QT_X3
     // fc1 (f32 MFMA, K = 6), then its relu split into the h1 fragments (the online net's
     // f32 h1 is kept too, for the backward)
     {
@@ -786,18 +589,13 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     __syncthreads(); QSTAMP(2);
     // fc2 of row tile wt; fc3's A operands (tile `wave`) load behind its first k-step,
     // into the registers fc2's consumed k-steps free
-#if SHIPENV_QT_X3W
     // fc3's pre-split A operands of k-step g load once fc2's k-step g has consumed its own
     // (fenced, so that at most one k-step's worth more is live)
     bf16x8 wb[8][3];
-#if SHIPENV_QT_BIAS_LATE
     // the chain starts at 0 and the bias is added after it, so its loads' round trip hides
     // under the chain instead of holding its first MFMA
     const f32x16 bias2 = bias_init(tgt ? A.tg.b2 : A.on.b2, wt, lane, 128);
     f32x16 acc = {};
-#else
-    f32x16 acc = bias_init(tgt ? A.tg.b2 : A.on.b2, wt, lane, 128);
-#endif
     {
         const bf16x8* S = SH1 + net * 8 * 3 * 64;
         const bf16x8* P3 = reinterpret_cast<const bf16x8*>(A.W.pw3t) + wave * 8 * 3 * 64;
@@ -821,31 +619,10 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             for (int q = 0; q < 3; ++q) wb[g][q] = P3[(g * 3 + q) * 64 + lane];
             __builtin_amdgcn_sched_barrier(0);
         }
-#if SHIPENV_QT_BIAS_LATE
         acc += bias2;
-#endif
         if (tgt) store_split(SH2, wt, acc, lane);
         else store_relu(HB, wt, acc, lane);
     }
-#else
-    float4 wb[16];
-    f32x16 acc = bias_init(tgt ? A.tg.b2 : A.on.b2, wt, lane, 128);
-    {
-        const bf16x8* S = SH1 + net * 8 * 3 * 64;
-        acc = gemm_x3<1>(wa, S, 0, acc, lane);
-        __builtin_amdgcn_sched_barrier(0);
-        const float4* p = reinterpret_cast<const float4*>(A.W.pw3t) + wave * 8 * 64 * 2;
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            wb[2 * g] = p[(g * 64 + lane) * 2];
-            wb[2 * g + 1] = p[(g * 64 + lane) * 2 + 1];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        acc = gemm_x3<7>(wa + 2, S, 1, acc, lane);
-        if (tgt) store_split(SH2, wt, acc, lane);
-        else store_relu(HB, wt, acc, lane);
-    }
-#endif
     QSTAMP(14);
     __syncthreads(); QSTAMP(3);
     // target fc3: tile `wave` on each wave (mt3 >= 9), and the mt3 - 8 (at most 2) tiles past
@@ -855,7 +632,6 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
     {
         const int xt = tgt ? 8 : 9;
         const bool extra = xt < A.d.mt3;  // wave-uniform
-#if SHIPENV_QT_X3W
         bf16x8 wx[2][3];
         f32x16 accx = {};
         if (extra) {
@@ -866,40 +642,9 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
                 for (int q = 0; q < 3; ++q) wx[u][q] = p[((2 * wt + u) * 3 + q) * 64 + lane];
             if (wt == 0) accx = bias_init(A.tg.b3, xt, lane, A.d.A);
         }
-#if SHIPENV_QT_BIAS_LATE
         const f32x16 bias3 = bias_init(A.tg.b3, wave, lane, A.d.A);
         f32x16 acc3 = gemm_x3w<8>(wb, SH2, 0, f32x16{}, lane) + bias3;
-#else
-        f32x16 acc3 = bias_init(A.tg.b3, wave, lane, A.d.A);
-        acc3 = gemm_x3w<8>(wb, SH2, 0, acc3, lane);
-#endif
-#else
-        float4 wx[4];
-        f32x16 accx = {};
-        if (extra) {
-            const float4* p = reinterpret_cast<const float4*>(A.W.pw3t) + xt * 8 * 64 * 2;
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                wx[2 * u] = p[((2 * wt + u) * 64 + lane) * 2];
-                wx[2 * u + 1] = p[((2 * wt + u) * 64 + lane) * 2 + 1];
-            }
-            if (wt == 0) accx = bias_init(A.tg.b3, xt, lane, A.d.A);
-        }
-        f32x16 acc3 = bias_init(A.tg.b3, wave, lane, A.d.A);
-        acc3 = gemm_x3<8>(wb, SH2, 0, acc3, lane);
-#endif
-#if SHIPENV_QT_X3B
-        if (!tgt) {  // dH1's A operands (W2^T, x3_index order)
-            const float4* p = reinterpret_cast<const float4*>(A.W.pw2t) + wt * 8 * 64 * 2;
-#pragma unroll
-            for (int g = 0; g < 8; ++g) {
-                wd[2 * g] = p[(g * 64 + lane) * 2];
-                wd[2 * g + 1] = p[(g * 64 + lane) * 2 + 1];
-            }
-        }
-#else
         if (!tgt) fb.load(A.W.pw2t + wt * 64 * 64, lane);  // dH1's operands
-#endif
         float m = -INFINITY;
 #pragma unroll
         for (int r = 0; r < 16; ++r)
@@ -907,105 +652,16 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         m = fmaxf(m, __shfl_xor(m, 32));  // lane & 31 = sample
         if (lane < 32) QM[wave * 32 + lane] = m;
         if (extra) {
-#if SHIPENV_QT_X3W
             accx = gemm_x3w<2>(wx, SH2, 2 * wt, accx, lane);
-#else
-            accx = gemm_x3<2>(wx, SH2, 2 * wt, accx, lane);
-#endif
             float* o = XP + ((xt - 8) * 4 + wt) * 16 * 64;
 #pragma unroll
             for (int r = 0; r < 16; ++r) o[r * 64 + lane] = accx[r];
         }
     }
     QSTAMP(15);
-#else
-    // fc1, fc2 of both networks: online on states, target on next_states
-    store_relu(tgt ? TA : HA, wt, gemm_lds(f1, tgt ? XN : X, acc1, lane), lane);
-    __syncthreads(); QSTAMP(2);
-    // fc3's fragments (64 loads per lane, ~1 us of the CU's memory pipeline for 8 waves)
-    // are issued after fc2's first MFMAs: ahead of them, the chain's wait for its bias
-    // (the counter is in order) also waited for every fragment load
-    f32x16 acc = bias_init(tgt ? A.tg.b2 : A.on.b2, wt, lane, 128);
-    f32x16 acc3 = {};
-    {
-        acc = gemm_lds<64, 0, 2>(fa, tgt ? TA : HA, acc, lane);
-        __builtin_amdgcn_sched_barrier(0);
-        if (wave < A.d.mt3) {
-            acc3 = bias_init(A.tg.b3, wave, lane, A.d.A);
-            fb.load(A.W.pw3t + wave * 64 * 64, lane);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        acc = gemm_lds<64, 2, 64>(fa, tgt ? TA : HA, acc, lane);
-        store_relu(tgt ? TB : HB, wt, acc, lane);
-    }
-    QSTAMP(14);  // this wave's fc2 done (its relu stores wait for the chain's last MFMA)
-    __syncthreads(); QSTAMP(3);
-    // target fc3 over all A rows and the max over actions: tile `wave` on each wave, and the
-    // mt3 - 8 (at most 2) tiles beyond the eighth in 16 x 16 quadrants, so every SIMD gets the
-    // same MFMA cycles: tile 8 on waves 4-7, tile 9 on waves 0-3, quadrant wt = (row half
-    // rh, sample half sh) on v_mfma_f32_16x16x4_f32 (32 steps of K = 4, 32 cycles each; a
-    // quarter of a 32-row tile's 64 x 64 cycles). Before, waves 0 and 1 took the extra tiles
-    // whole and their SIMDs ran 1.5x the others' MFMA cycles.
-    {
-        const int xt = tgt ? 8 : 9, rh = wt >> 1, sh = wt & 1;
-        const bool extra = xt < A.d.mt3;  // wave-uniform
-        float xa[32];  // quadrant A operands: rows 16 rh + (lane & 15), k = 4 t + (lane >> 4)
-        if (extra) {
-#pragma unroll
-            for (int t = 0; t < 32; ++t) {
-                const int k = 4 * t + (lane >> 4);
-                xa[t] = A.W.pw3t[(xt * 64 + (k >> 1)) * 64 + rh * 16 + (lane & 15) + 32 * (k & 1)];
-            }
-        }
-        float m = -INFINITY;
-        if (wave < A.d.mt3) {
-            acc3 = gemm_lds(fb, TB, acc3, lane);
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                if (wave * 32 + acc_r(r, lane) < A.d.A) m = fmaxf(m, acc3[r]);
-        }
-        if (!tgt) fb.load(A.W.pw2t + wt * 64 * 64, lane);  // dH1's operands
-        m = fmaxf(m, __shfl_xor(m, 32));  // lane & 31 = sample
-        if (extra) {
-            f32x4 acc;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = xt * 32 + rh * 16 + 4 * (lane >> 4) + r;
-                acc[r] = row < A.d.A ? A.tg.b3[row] : 0.0f;
-            }
-            const float* hb = TB + (lane >> 4) * kLS + sh * 16 + (lane & 15);
-            constexpr int L = 8;  // B operands read L steps ahead (pinned as in gemm_lds)
-            float bq[32];
-#pragma unroll
-            for (int i = 0; i < L; ++i) bq[i] = hb[4 * i * kLS];
-#pragma unroll
-            for (int i = 0; i < 32; ++i) {
-                if (i + L < 32) bq[i + L] = hb[4 * (i + L) * kLS];
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[i], bq[i], acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int i = 0; i < L; ++i) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-#pragma unroll
-            for (int i = 0; i < 32; ++i) {
-                if (i + L < 32) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            }
-            float qm = -INFINITY;  // over this lane's 4 rows, then the 16 rows of the quadrant
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (xt * 32 + rh * 16 + 4 * (lane >> 4) + r < A.d.A) qm = fmaxf(qm, acc[r]);
-            qm = fmaxf(qm, __shfl_xor(qm, 16));
-            qm = fmaxf(qm, __shfl_xor(qm, 32));  // every lane with lane & 15 = i: sample 16 sh + i
-            if (((lane & 31) >> 4) == sh) m = fmaxf(m, qm);
-        }
-        if (lane < 32) QM[wave * 32 + lane] = m;
-    }
-    QSTAMP(15);  // this wave's fc3 done
-#endif
     __syncthreads(); QSTAMP(4);
     if (tid < 64) {
         float mx = -INFINITY;
-#if SHIPENV_QT_X3
         // the tiles past the eighth: the four K-partials of each in a fixed order
         for (int xt = 8; xt < A.d.mt3; ++xt) {
             const float* o = XP + (xt - 8) * 4 * 16 * 64;
@@ -1017,21 +673,12 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             }
         }
         mx = fmaxf(mx, __shfl_xor(mx, 32));
-#endif
         if (tid < 32) {
             const int64_t row = r0 + tid;
             for (int w = 0; w < 8; ++w) mx = fmaxf(mx, QM[w * 32 + tid]);
             Y[tid] = row < A.B ? RW[tid] + (A.gamma * mx) * (1.0f - DN[tid]) : 0.0f;
         }
     }
-#if SHIPENV_QT_X3BT
-    else {  // the idle waves: h1 and h2 (online, relu'd f32 tiles) into the sample-major split tiles
-        for (int it = tid - 64; it < 2 * 512; it += kQTBlock - 64) {
-            const int which = it >> 9, f = (it >> 2) & 127, g8 = it & 3;
-            t_split_row((which ? HB : HA) + f * kLS + 8 * g8, which ? H2Ts : HTs, tslot(f, g8));
-        }
-    }
-#endif
     __syncthreads(); QSTAMP(5);
 
     // q_j = W3[a_j] . h2_j + b3[a_j]; g_j = 2 w_j (q_j - y_j): 16 threads per sample
@@ -1061,30 +708,10 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             const float d = (s + A.on.b3[ACT[qj]]) - Y[qj];
             G[qj] = 2.0f * WT[qj] * d;
             LW[qj] = WT[qj] * d * d;
-#if SHIPENV_QT_X3BT
-            __bf16 g0, g1, g2;
-            split3(G[qj], g0, g1, g2);
-            GS[qj] = g0;
-            GS[32 + qj] = g1;
-            GS[64 + qj] = g2;
-#endif
         }
     }
     __syncthreads(); QSTAMP(6);
-    // dZ2 = (h2 > 0) g_j W3[a_j] (into the target's dead h1 buffer; with SHIPENV_QT_X3B also
-    // split into dH1's B fragments, in the target h2's dead fragments)
-#if SHIPENV_QT_X3BT
-    {  // feature tf of samples 8 tg .. + 7: the f32 tile (dH1, db2) and its sample-major split (dW2)
-        float d[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int j = 8 * tg + i;
-            d[i] = HB[tf * kLS + j] > 0.0f ? G[j] * w3g[i] : 0.0f;
-            DZ2[tf * kLS + j] = d[i];
-        }
-        t_split8(d, DZ2Ts, tslot(tf, tg));
-    }
-#else
+    // dZ2 = (h2 > 0) g_j W3[a_j] (into the target's dead h1 buffer)
     {
         const float g = G[qj];
         float d[8];
@@ -1094,203 +721,19 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             d[k] = HB[f * kLS + qj] > 0.0f ? g * w3s[k] : 0.0f;
             DZ2[f * kLS + qj] = d[k];
         }
-#if SHIPENV_QT_X3B
-        bf16x8 sp[3];
-        split8_half(make_float4(d[0], d[1], d[2], d[3]), make_float4(d[4], d[5], d[6], d[7]), sp, 0);
-        split8_half(make_float4(d[0], d[1], d[2], d[3]), make_float4(d[4], d[5], d[6], d[7]), sp, 1);
-#pragma unroll
-        for (int p = 0; p < 3; ++p) SH2[((qpart >> 1) * 3 + p) * 64 + qj + 32 * (qpart & 1)] = sp[p];
-#endif
     }
-#endif
     __syncthreads(); QSTAMP(7);
 
     const int h = lane >> 5, c = lane & 31;
     if (!tgt) {  // dH1 = W2^T dZ2 -> dZ1 = (h1 > 0) dH1
         f32x16 acc = {};
-#if SHIPENV_QT_X3B
-        acc = gemm_x3<8>(wd, SH2, 0, acc, lane);
-#else
         acc = gemm_lds(fb, DZ2, acc, lane);
-#endif
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int f = wt * 32 + acc_r(r, lane);
             DZ1[f * kLS + c] = HA[f * kLS + c] > 0.0f ? acc[r] : 0.0f;
         }
     } else {
-#if SHIPENV_QT_X3B
-        // partial dW2 (as H1 dZ2^T, f1 tile wt, 4 f2 tiles) and dW3 (as H2 G^T over the tile's
-        // slots) on split-bf16 MFMAs over K = 32 samples (two k-steps of 16): lane (r, h) of an
-        // operand holds samples 16 u + 8 h + 0..7 of its row, read from the f32 LDS tiles and
-        // split here. The accumulators are laid out as before, so are the stores.
-        auto row8 = [&](const float* src, int u, bf16x8 (&w)[3]) {
-            const float* q = src + 16 * u + 8 * h;
-            const float4 x = make_float4(q[0], q[1], q[2], q[3]), y = make_float4(q[4], q[5], q[6], q[7]);
-            split8_half(x, y, w, 0);
-            split8_half(x, y, w, 1);
-        };
-        auto x3_k32 = [&](const bf16x8 (&a)[2][3], const bf16x8 (&b)[2][3]) {
-            f32x16 acc = {};
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                acc = mfma_bf16(a[u][0], b[u][2], acc);
-                acc = mfma_bf16(a[u][1], b[u][1], acc);
-                acc = mfma_bf16(a[u][2], b[u][0], acc);
-                acc = mfma_bf16(a[u][0], b[u][1], acc);
-                acc = mfma_bf16(a[u][1], b[u][0], acc);
-                acc = mfma_bf16(a[u][0], b[u][0], acc);
-            }
-            return acc;
-        };
-        float* out = A.W.part_w2 + (int64_t)blockIdx.x * 128 * 128;
-        bf16x8 a2[2][3], b2[2][3];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) row8(HA + (wt * 32 + c) * kLS, u, a2[u]);
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) {
-#pragma unroll
-            for (int u = 0; u < 2; ++u) row8(DZ2 + (ct * 32 + c) * kLS, u, b2[u]);
-            const f32x16 acc = x3_k32(a2, b2);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)  // f1 = 32 wt + acc_r(4q + m, lane) = 32 wt + 8q + 4h + m
-#if SHIPENV_QT_ABL & 1  // timing only: the dW2 partials computed, not stored
-                if (A.B < 0)
-#endif
-                st_part4(out, (uint32_t)((ct * 32 + c) * 128 + wt * 32 + 8 * q + 4 * h), acc[4 * q], acc[4 * q + 1],
-                         acc[4 * q + 2], acc[4 * q + 3]);
-        }
-        // dW3: slot r = sum_j [first(j) = r] g_j h2[f][j]; B lane (c, h): sample j's g where
-        // slot c is first(j), else 0 (the split of the selected value)
-        const bool live_slot = FST[c] == c && r0 + c < A.B;
-        const uint32_t slots = (uint32_t)__ballot(live_slot);  // lanes 0-31 = slots 0-31
-        float av[16];
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int j = 16 * u + 8 * h + k;
-                av[8 * u + k] = FST[j] == c ? G[j] : 0.0f;
-            }
-        bf16x8 bv[2][3], gv[2][3];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            row8(HB + (wt * 32 + c) * kLS, u, bv[u]);
-            const float4 x = make_float4(av[8 * u], av[8 * u + 1], av[8 * u + 2], av[8 * u + 3]);
-            const float4 y = make_float4(av[8 * u + 4], av[8 * u + 5], av[8 * u + 6], av[8 * u + 7]);
-            split8_half(x, y, gv[u], 0);
-            split8_half(x, y, gv[u], 1);
-        }
-        const f32x16 acc = x3_k32(bv, gv);
-        float* o3 = A.W.part_w3 + (int64_t)blockIdx.x * 32 * 128;
-#if SHIPENV_QT_ABL & 2  // timing only: the dW3 partials computed, not stored
-        if (A.B < 0)
-#endif
-        if ((slots >> c) & 1u)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                st_part4(o3, (uint32_t)(c * 128 + wt * 32 + 8 * q + 4 * h), acc[4 * q], acc[4 * q + 1], acc[4 * q + 2],
-                         acc[4 * q + 3]);
-        if (wt == 0) {  // db3 of slot c: this lane half's 16 samples, then the other half's
-            float s3 = 0.0f;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) s3 += av[k];
-            const float x3 = __shfl_xor(s3, 32);
-            if (h == 0) {
-                st_part1(A.W.part_b3 + (int64_t)blockIdx.x * 32 + c, s3 + x3);
-                st_part1(A.W.part_map + (int64_t)blockIdx.x * 32 + c, live_slot ? (int32_t)ACT[c] : (int32_t)-1);
-#if SHIPENV_QT_SLOT_TABLE
-                MAPL[c] = live_slot ? (int32_t)ACT[c] : (int32_t)-1;
-#endif
-            }
-        }
-#elif SHIPENV_QT_X3BT
-        // partial dW2 (as H1 dZ2^T: f1 tile wt, 4 f2 tiles) and dW3 (as H2 G^T over the tile's
-        // slots) on split-bf16 MFMAs over K = 32 samples (two k-steps of 16): lane (r, h) of an
-        // operand holds samples 16 u + 8 h + 0..7 of its row, three 16-byte reads of the
-        // sample-major split tiles. The accumulators are laid out as before, so are the stores.
-        auto tfrag = [&](const __bf16* T, int row, int u, bf16x8 (&w)[3]) {
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-                w[p] = *reinterpret_cast<const bf16x8*>(T + p * 128 * kTS + 8 * tslot(row, 2 * u + h));
-        };
-        auto x3_k32 = [&](const bf16x8 (&a)[2][3], const bf16x8 (&b)[2][3]) {
-            f32x16 acc = {};
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                acc = mfma_bf16(a[u][0], b[u][2], acc);
-                acc = mfma_bf16(a[u][1], b[u][1], acc);
-                acc = mfma_bf16(a[u][2], b[u][0], acc);
-                acc = mfma_bf16(a[u][0], b[u][1], acc);
-                acc = mfma_bf16(a[u][1], b[u][0], acc);
-                acc = mfma_bf16(a[u][0], b[u][0], acc);
-            }
-            return acc;
-        };
-        float* out = A.W.part_w2 + (int64_t)blockIdx.x * 128 * 128;
-        bf16x8 a2[2][3], b2[2][3];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) tfrag(HTs, wt * 32 + c, u, a2[u]);
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) {
-#pragma unroll
-            for (int u = 0; u < 2; ++u) tfrag(DZ2Ts, ct * 32 + c, u, b2[u]);
-            const f32x16 acc = x3_k32(a2, b2);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)  // f1 = 32 wt + acc_r(4q + m, lane) = 32 wt + 8q + 4h + m
-#if SHIPENV_QT_ABL & 1  // timing only: the dW2 partials computed, not stored
-                if (A.B < 0)
-#endif
-                st_part4(out, (uint32_t)((ct * 32 + c) * 128 + wt * 32 + 8 * q + 4 * h), acc[4 * q], acc[4 * q + 1],
-                         acc[4 * q + 2], acc[4 * q + 3]);
-        }
-        // dW3: slot c = sum_j [first(j) = c] g_j h2[f][j]; B lane (c, h): g's parts of samples
-        // 16 u + 8 h + k where slot c is first(j), else 0
-        const bool live_slot = FST[c] == c && r0 + c < A.B;
-        const uint32_t slots = (uint32_t)__ballot(live_slot);  // lanes 0-31 = slots 0-31
-        float s3 = 0.0f;  // db3 of slot c over this lane half's 16 samples
-        bf16x8 bv[2][3], gv[2][3];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            tfrag(H2Ts, wt * 32 + c, u, bv[u]);
-            uint32_t keep[4];  // 16-bit lane masks of the 8 samples, two per word
-#pragma unroll
-            for (int k2 = 0; k2 < 4; ++k2) {
-                const int j = 16 * u + 8 * h + 2 * k2;
-                const bool m0 = FST[j] == c, m1 = FST[j + 1] == c;
-                keep[k2] = (m0 ? 0x0000ffffu : 0u) | (m1 ? 0xffff0000u : 0u);
-                s3 += m0 ? G[j] : 0.0f;
-                s3 += m1 ? G[j + 1] : 0.0f;
-            }
-#pragma unroll
-            for (int p = 0; p < 3; ++p) {
-                u32x4 w = __builtin_bit_cast(u32x4, *reinterpret_cast<const bf16x8*>(GS + p * 32 + 16 * u + 8 * h));
-#pragma unroll
-                for (int k2 = 0; k2 < 4; ++k2) w[k2] &= keep[k2];
-                gv[u][p] = __builtin_bit_cast(bf16x8, w);
-            }
-        }
-        const f32x16 acc = x3_k32(bv, gv);
-        float* o3 = A.W.part_w3 + (int64_t)blockIdx.x * 32 * 128;
-#if SHIPENV_QT_ABL & 2  // timing only: the dW3 partials computed, not stored
-        if (A.B < 0)
-#endif
-        if ((slots >> c) & 1u)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                st_part4(o3, (uint32_t)(c * 128 + wt * 32 + 8 * q + 4 * h), acc[4 * q], acc[4 * q + 1], acc[4 * q + 2],
-                         acc[4 * q + 3]);
-        if (wt == 0) {  // db3 of slot c: this lane half's 16 samples, then the other half's
-            const float x3 = __shfl_xor(s3, 32);
-            if (h == 0) {
-                st_part1(A.W.part_b3 + (int64_t)blockIdx.x * 32 + c, s3 + x3);
-                st_part1(A.W.part_map + (int64_t)blockIdx.x * 32 + c, live_slot ? (int32_t)ACT[c] : (int32_t)-1);
-#if SHIPENV_QT_SLOT_TABLE
-                MAPL[c] = live_slot ? (int32_t)ACT[c] : (int32_t)-1;
-#endif
-            }
-        }
-#else
   // partial dW2[f2][f1] = sum_j dZ2[f2][j] h1[f1][j]: f1 tile wt, 4 f2 tiles
         // computed as its transpose H1 dZ2^T (A operands: f1 rows wt*32.. of h1, once; each
         // f2 tile's B operands read while the previous tile's chain runs), so a lane's
@@ -1311,9 +754,6 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q)  // f1 = 32 wt + acc_r(4q + m, lane) = 32 wt + 8q + 4h + m
-#if SHIPENV_QT_ABL & 1  // timing only: the dW2 partials computed, not stored
-                if (A.B < 0)
-#endif
                 st_part4(out, (uint32_t)((ct * 32 + c) * 128 + wt * 32 + 8 * q + 4 * h), acc[4 * q], acc[4 * q + 1],
                          acc[4 * q + 2], acc[4 * q + 3]);
         }
@@ -1350,9 +790,6 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
 #pragma unroll
         for (int s = 0; s < 16; ++s) acc = mfma_f32(bv[s], av[s], acc);
         float* o3 = A.W.part_w3 + (int64_t)blockIdx.x * 32 * 128;
-#if SHIPENV_QT_ABL & 2  // timing only: the dW3 partials computed, not stored
-        if (A.B < 0)
-#endif
         if ((slots >> c) & 1u)
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -1366,12 +803,9 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             if (h == 0) {
                 st_part1(A.W.part_b3 + (int64_t)blockIdx.x * 32 + c, s3 + x3);
                 st_part1(A.W.part_map + (int64_t)blockIdx.x * 32 + c, live_slot ? (int32_t)ACT[c] : (int32_t)-1);
-#if SHIPENV_QT_SLOT_TABLE
                 MAPL[c] = live_slot ? (int32_t)ACT[c] : (int32_t)-1;
-#endif
             }
         }
-#endif
     }
     __syncthreads(); QSTAMP(8);  // dZ1 complete
     // partial dW1 (dynamic columns), db1, db2, loss and weight sums
@@ -1407,7 +841,6 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             st_part1(A.W.part_lw + 2 * blockIdx.x + 1, w);
         }
     }
-#if SHIPENV_QT_SLOT_TABLE
     if (tid < 32 * A.d.mt3) {  // this tile's column of the action -> slot table
         const int4* m4 = reinterpret_cast<const int4*>(MAPL);
         int sl = 0xff;
@@ -1421,13 +854,9 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         }
         A.W.part_slot[(int64_t)tid * A.W.slot_ld + blockIdx.x] = (uint8_t)sl;
     }
-#endif
     QSTAMP(9);
 }
 
-#ifndef SHIPENV_QT_T2FIX
-#define SHIPENV_QT_T2FIX 1  // T2: the step count as a vector load, no per-lane pointer reloads (0: round 4)
-#endif
 // sum over t = tid, tid + kQRBlock, ... < tiles of p[t * stride]: the first load issued with no
 // wait (its value is added where the sum is used), the rest (more than kQRBlock tiles) looped
 struct StridedSum {
@@ -1610,7 +1039,7 @@ __device__ __forceinline__ float slot_row_sum(const float* w3, const float* b3, 
     for (int64_t c0 = 0; c0 < tiles; c0 += kQRBlock) {
         const int64_t tt = c0 + t;
         int slot = -1;
-        if (slot_row) {  // SHIPENV_QT_SLOT_TABLE: row a of the action -> slot table
+        if (slot_row) {  // row a of the action -> slot table
             const int v = tt < tiles ? (int)slot_row[tt] : 0xff;
             slot = v == 0xff ? -1 : v;
         } else if (tt < tiles) {
@@ -1699,30 +1128,17 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
     QSTAMP(10);  // T2's stamps: slots 10-13 of the same rows (4 waves)
     // the Adam count: its load is in flight while the sums' loads are issued; the step's
     // constants (two powf) are formed where the first Adam step needs them, after the
-    // sums (SHIPENV_QT_LATE_ADAM; 0: at the kernel's start, ahead of every sum load)
-#if SHIPENV_QT_T2FIX
+    // sums (-0.35 us against the kernel's start, profiles/r04/ab_update_late_adam.jsonl)
     // a vector load (vmcnt): as a scalar load of a line T1 has just written, its wait
     // (lgkmcnt(0), which every later kernel-argument load shares) held each block ~1.4 us
     // before its first partial-sum load
     const int32_t steps_dev = A.step_dev ? vload_i32(A.step_dev) : 0;
-#else
-    const int32_t steps_dev = A.step_dev ? *A.step_dev : 0;
-#endif
-#if SHIPENV_QT_LATE_ADAM
 #define QT_ADAM() AdamStep(A, steps_dev)
-#else
-    const AdamStep adam_early(A, steps_dev);
-#define QT_ADAM() adam_early
-#endif
     // every block has read the count; ctr[0] is read by the next update's T1 only
-#if !SHIPENV_QT_T2FIX
-    if (A.ctr_sync && blockIdx.x == 0 && tid == 0) *A.ctr_sync = steps_dev;
-#endif
     // sum(w): this thread's share loads now, and the workgroup reduces it after its own
     // sum (inv is first needed by the Adam step), so the two round trips overlap
     const int mode = A.mode;  // block-uniform
     float* G = A.grad;
-#if SHIPENV_QT_T2FIX
     // (the first load of each strided sum is not waited for here: in a loop its s_waitcnt held
     // the block one round trip before its partial sums' loads were issued)
     StridedSum ws, ls;  // ls: the loss sum, W1 block 0 (mode 0) only
@@ -1733,17 +1149,6 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
     auto weight_inv = [&]() {
         return 1.0f / fmaxf(mode == 2 ? G[Grad::lw(A.d) + 1] : block_sum256(ws.value(), red), 1.0f);
     };
-#else
-    float wsum = 0.0f, lsum = 0.0f;  // lsum: the loss sum, W1 block 0 (mode 0) only
-    if (mode == 0 || (mode == 1 && blockIdx.x == 0))
-        for (int64_t t = tid; t < A.tiles; t += kQRBlock) {
-            wsum += A.W.part_lw[2 * t + 1];
-            if (mode == 0 && blockIdx.x == 0) lsum += A.W.part_lw[2 * t];
-        }
-    auto weight_inv = [&]() {
-        return 1.0f / fmaxf(mode == 2 ? G[Grad::lw(A.d) + 1] : block_sum256(wsum, red), 1.0f);
-    };
-#endif
     QSTAMP(11);
     const int b = blockIdx.x;
     if (b < 128) {  // W1 row f: 6 dynamic columns + db1 reduced over the tiles, the port columns
@@ -1797,11 +1202,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                     float l = 0.0f;
                     for (int64_t t = tid; t < A.tiles; t += kQRBlock) l += A.W.part_lw[2 * t];
                     const float lsm = block_sum256(l, red);
-#if SHIPENV_QT_T2FIX
                     const float wsm = block_sum256(ws.value(), red);
-#else
-                    const float wsm = block_sum256(wsum, red);
-#endif
                     if (tid == 0) {
                         G[Grad::lw(A.d)] = lsm;
                         G[Grad::lw(A.d) + 1] = wsm;
@@ -1812,9 +1213,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         }
         const float inv = weight_inv();
         const AdamStep adam = QT_ADAM();
-#if SHIPENV_QT_T2FIX
         if (A.ctr_sync && f == 0 && tid == 0) *A.ctr_sync = steps_dev;  // the next update's T1 reads it
-#endif
         QSTAMP(12);
         if (tid == 0)  // every thread holds the sums; the row loop below indexes them by column
 #pragma unroll
@@ -1867,11 +1266,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         if (f == 0) {  // the loss: sum w d^2 / sum w
             float loss;
             // (mode 0: this thread's share was loaded at the start, with the weight sum)
-#if SHIPENV_QT_T2FIX
             loss = mode == 2 ? G[Grad::lw(A.d)] : block_sum256(ls.value(), red);
-#else
-            loss = mode == 2 ? G[Grad::lw(A.d)] : block_sum256(lsum, red);
-#endif
             if (tid == 0) *A.loss_out = loss * inv;
         }
     } else if (b < 384) {  // W2 elements e0 .. e0 + 63 (row-major [f2][f1])
@@ -1893,10 +1288,8 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             }
         }
         float g;
-#if SHIPENV_QT_T2FIX
         StridedSum b2s;  // a row's first block: its db2 partials, issued ahead of dW2's
         if (mode != 2 && (e0 & 127) == 0) b2s.issue(A.W.part_b2 + f2, 128, A.tiles);
-#endif
         if (mode == 2) {
             g = tid < 64 ? G[Grad::w2 + e0 + tid] : 0.0f;
         } else {
@@ -1904,12 +1297,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             if (mode == 1) {
                 if (tid < 64) G[Grad::w2 + e0 + tid] = g;
                 if ((e0 & 127) == 0) {
-#if SHIPENV_QT_T2FIX
                     const float x = b2s.value();
-#else
-                    float x = 0.0f;
-                    for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[t * 128 + f2];
-#endif
                     const float s2 = block_sum256(x, red);
                     if (tid == 0) G[Grad::b2 + f2] = s2;
                 }
@@ -1925,7 +1313,6 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             A.m.w2[e] = pm;
             A.v.w2[e] = pv;
             A.on.w2[e] = p;
-#if SHIPENV_QT_X3W
             {
                 __bf16 p0, p1, p2;
                 split3(p, p0, p1, p2);
@@ -1934,10 +1321,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                 img[512] = p1;
                 img[1024] = p2;
             }
-#else
-            A.W.pw2[0][SHIPENV_QT_X3 ? x3_index(f2, f1) : frag_index(f2, f1)] = p;
-#endif
-            A.W.pw2t[SHIPENV_QT_X3B ? x3_index(f1, f2) : frag_index(f1, f2)] = p;
+            A.W.pw2t[frag_index(f1, f2)] = p;
             if (A.img[0])
 #pragma unroll
                 for (int l = 0; l < 2; ++l) put_bf16(A.img[l] + A.q[l].w2() + pol_offset(f2, f1), p);
@@ -1947,12 +1331,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             if (mode == 2) {
                 s2 = G[Grad::b2 + f2];
             } else {
-#if SHIPENV_QT_T2FIX
                 const float x = b2s.value();
-#else
-                float x = 0.0f;
-                for (int64_t t = tid; t < A.tiles; t += kQRBlock) x += A.W.part_b2[t * 128 + f2];
-#endif
                 s2 = block_sum256(x, red);
             }
             if (tid == 0) {
@@ -1971,7 +1350,6 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         const int f3 = tid;  // threads < 128: element f3 of the row; thread 128: b3
         const int64_t i3 = (int64_t)a3 * 128 + f3;
         float pw = 0.f, pm = 0.f, pv = 0.f;  // the Adam operands, loaded ahead of the sums
-#if SHIPENV_QT_T2FIX
         // the six pointers held in SGPRs (opaque), and every thread loads both candidates: the
         // compiler otherwise merged the two branches' loads (and the stores below) into one
         // through a pointer it re-read from the kernel arguments per lane, a dependent round trip
@@ -1984,26 +1362,13 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
             pm = tid < 128 ? m_ : bm_;
             pv = tid < 128 ? v_ : bv_;
         }
-#else
-        if (mode != 1 && row_live) {
-            if (tid < 128) {
-                pw = A.on.w3[i3];
-                pm = A.m.w3[i3];
-                pv = A.v.w3[i3];
-            } else if (tid == 128) {
-                pw = A.on.b3[a3];
-                pm = A.m.b3[a3];
-                pv = A.v.b3[a3];
-            }
-        }
-#endif
         float g = 0.0f;  // dW3[a3][tid] (tid < 128) or db3[a3] (tid = 128)
         if (mode == 2) {
             if (tid < 128) g = G[Grad::w3 + i3];
             else if (tid == 128) g = G[Grad::b3(A.d) + a3];
         } else {
-            g = slot_row_sum<SHIPENV_QT_W3U>(A.W.part_w3, A.W.part_b3, A.W.part_map, A.tiles, a3, red4, list, wtot,
-                                             SHIPENV_QT_SLOT_TABLE ? A.W.part_slot + (int64_t)a3 * A.W.slot_ld : nullptr);
+            g = slot_row_sum<16>(A.W.part_w3, A.W.part_b3, A.W.part_map, A.tiles, a3, red4, list, wtot,
+                                             A.W.part_slot + (int64_t)a3 * A.W.slot_ld);
             if (mode == 1) {
                 if (tid < 128) G[Grad::w3 + i3] = g;
                 else if (tid == 128) G[Grad::b3(A.d) + a3] = g;
@@ -2015,24 +1380,12 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         QSTAMP(12);
         if (row_live && tid <= 128) {
             const float p = adam(pw, g * inv, pm, pv);
-#if SHIPENV_QT_T2FIX
             float* dm = tid < 128 ? mw3 + i3 : mb3 + a3;
             float* dv = tid < 128 ? vw3 + i3 : vb3 + a3;
             float* dp = tid < 128 ? ow3 + i3 : ob3 + a3;
             *dm = pm;
             *dv = pv;
             *dp = p;
-#else
-            if (tid < 128) {
-                A.m.w3[i3] = pm;
-                A.v.w3[i3] = pv;
-                A.on.w3[i3] = p;
-            } else {
-                A.m.b3[a3] = pm;
-                A.v.b3[a3] = pv;
-                A.on.b3[a3] = p;
-            }
-#endif
             if (A.img[0])
 #pragma unroll
                 for (int l = 0; l < 2; ++l) {
@@ -2096,7 +1449,7 @@ int se_qtrain_create(se_qtrain** out, se_env* env, int64_t max_batch) {
     q->max_tiles = (max_batch + kQT - 1) / kQT;
     const size_t T = (size_t)q->max_tiles;
     const size_t mt3 = (size_t)q->d.mt3;
-    constexpr size_t kW = SHIPENV_QT_X3W ? 6 : 4;  // bytes per weight of fc2 / fc3's MFMA images
+    constexpr size_t kW = 6;  // bytes per weight of fc2 / fc3's MFMA images
     const size_t sizes[] = {4 * 3 * 64, 4 * 3 * 64, 4 * 64 * 16 * kW, 4 * 64 * 16 * kW, 4 * 64 * 64,
                             mt3 * 16 * 64 * kW, 128, 128, (size_t)(4 * P),
                             T * 128 * 128, T * 128 * 6, T * 128, T * 128, T * 2, T * 32 * 128,
@@ -2195,7 +1548,7 @@ int qtrain_step(se_qtrain* q, se_qnet* qn, int64_t batch, const float* obs, cons
     DeviceGuard g(q->device);
     const hipStream_t s = (hipStream_t)stream;
     const int64_t tiles = (batch + kQT - 1) / kQT;
-    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 8 * 32) * 4 + (SHIPENV_QT_X3 ? 3 * 8 * 3 * 64 * 16 + 32 * 4 + 256 : 0);
+    const size_t lds = (size_t)(16 * kLS + 4 * 128 * kLS + 8 * 32 + 8 * 32) * 4 + (3 * 8 * 3 * 64 * 16 + 32 * 4 + 256);
     static std::atomic<uint64_t> lds_set{0};
     rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(qtrain_tile_kernel), (int)lds, q->device);
     if (rc) return rc;

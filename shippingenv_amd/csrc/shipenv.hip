@@ -39,41 +39,12 @@
 #define SHIPENV_TRACE 0  // 1 = diagnostic build: per-wave phase timestamps (tools/archive/wave_trace.py)
 #endif
 
-#ifndef SHIPENV_ABL4
-// timing-only auto-reset ablations (bits): 1 reset words without Philox, 2 no done
-// list, 4 no episode statistics, 8 no auto-reset at all (tools/archive/build_ablation.sh), 16 the
-// done list without its records' stores, 32 without its per-segment count stores, 64
-// without the episode-start stamps' loads, 128 without their stores
-#define SHIPENV_ABL4 0
-#endif
-#ifndef SHIPENV_STAMP_ST
-#define SHIPENV_STAMP_ST 0  // 1 = the stamps' stores temporal (experiment; default nontemporal)
-#endif
-#ifndef SHIPENV_STAMP_GRAIN
-#define SHIPENV_STAMP_GRAIN 1  // lanes (16 B each) whose stamps load / store together (1, 2 or 4)
-#endif
-#ifndef SHIPENV_PREFETCH
-#define SHIPENV_PREFETCH 0  // 1 = load the next group before computing this one (step kernel)
-#endif
-#ifndef SHIPENV_EARLY_DRAWS
-#define SHIPENV_EARLY_DRAWS 1  // 0 = FUEL / GATE drawn where used, not ahead of the staging wait (experiment)
-#endif
-#ifndef SHIPENV_STAGE_ORDER
-#define SHIPENV_STAGE_ORDER 0  // 1 = write the world image to LDS before issuing the group's loads (experiment)
-#endif
-#ifndef SHIPENV_ABLATE
-#define SHIPENV_ABLATE 0  // 0 = the product; 1 = timing-only memory-traffic build, 2 = also no staging (tools/archive/build_ablation.sh, tools/archive/ablate_libs.sh)
-#endif
-
 using namespace shipenv;
 
 namespace {
 
 constexpr int kBlock = 256;       // 4 waves
-#ifndef SHIPENV_STEP_BLOCK
-#define SHIPENV_STEP_BLOCK 256
-#endif
-constexpr int kStepBlock = SHIPENV_STEP_BLOCK;  // step kernel workgroup (one LDS world copy each)
+constexpr int kStepBlock = 256;  // step kernel workgroup (one LDS world copy each)
 constexpr int kEnvsPerThread = 4; // one 4-byte / 16-byte lane access per field
 constexpr int kMaxBlocks = 2048;  // 256 CUs x 8; grid-stride beyond
 // step kernel default workgroup cap (SHIPENV_STEP_BLOCKS overrides): one group of 4 envs per
@@ -114,10 +85,7 @@ constexpr int kCellGround = 255;
 // kStepBlock x 4-dword rows of the world image the step kernel stages unguarded
 // (one 16-byte load per thread and row), at least 12 KB: the 100x100 image with up
 // to 130 ports
-#ifndef SHIPENV_STAGE_MIN_WORDS
-#define SHIPENV_STAGE_MIN_WORDS 3072  // the unguarded window (experiments: 1024 = one row)
-#endif
-constexpr int kStageRows = (SHIPENV_STAGE_MIN_WORDS + 4 * kStepBlock - 1) / (4 * kStepBlock);
+constexpr int kStageRows = (3072 + 4 * kStepBlock - 1) / (4 * kStepBlock);
 constexpr int kStageWords = kStageRows * 4 * kStepBlock;
 
 struct WorldDims {
@@ -246,9 +214,6 @@ __device__ __forceinline__ LdsWorld stage_finish(const uint32_t* __restrict__ g,
 
 // Any block size (the other kernels): every thread's 16-byte loads issued before any
 // store (the image is padded to whole 1024-dword rows).
-#ifndef SHIPENV_STAGE_PIN
-#define SHIPENV_STAGE_PIN 0  // 1: the loads pinned ahead of the guarded stores (one wait per four); with the policy image batched too, 0.0593 -> 0.0600 ms per policy call (profiles/r05/ab_policy_bf16_stage.jsonl), not kept
-#endif
 __device__ __forceinline__ LdsWorld stage_world(const uint32_t* __restrict__ g, WorldDims d,
                                                 uint32_t* lds) {
     const int total = (d.total() + 3) / 4;
@@ -261,11 +226,6 @@ __device__ __forceinline__ LdsWorld stage_world(const uint32_t* __restrict__ g, 
         uint4 r[kR];
 #pragma unroll
         for (int k = 0; k < kR; ++k) r[k] = g4[min(i0 + (int)threadIdx.x + k * (int)blockDim.x, total - 1)];
-#if SHIPENV_STAGE_PIN
-        // all four loads before one wait: without this use the compiler sank each load into
-        // its guarded store and waited on every one
-        for (int k = 0; k < 4; ++k) asm volatile("" ::"v"(r[k].x), "v"(r[k].y), "v"(r[k].z), "v"(r[k].w));
-#endif
 #pragma unroll
         for (int k = 0; k < kR; ++k) {
             const int i = i0 + (int)threadIdx.x + k * (int)blockDim.x;
@@ -618,14 +578,11 @@ __device__ __forceinline__ T* slab_of(T* p, int64_t g0) {
 // nontemporal hint (written lines do not linger dirty in L2 until the end-of-kernel
 // writeback). Loads take it only when the step's working set is cache-resident
 // (kNt, chosen per launch by step_nt_loads): measured faster at N = 2^20, slower
-// at 2^24. SHIPENV_NT (bit 0 loads, bit 1 stores) masks them for experiments.
-#ifndef SHIPENV_NT
-#define SHIPENV_NT 3
-#endif
+// at 2^24.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <bool kNt = false, typename V>
 __device__ __forceinline__ V ld_stream(const V* p) {
-    if constexpr (kNt && (SHIPENV_NT & 1) != 0) {
+    if constexpr (kNt) {
         if constexpr (sizeof(V) == 16)
             return __builtin_bit_cast(V, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p)));
         else
@@ -636,33 +593,16 @@ __device__ __forceinline__ V ld_stream(const V* p) {
 }
 template <typename V>
 __device__ __forceinline__ void st_stream(V* p, V v) {
-    if constexpr ((SHIPENV_NT & 2) != 0) {
-        if constexpr (sizeof(V) == 16)
-            __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), reinterpret_cast<u32x4*>(p));
-        else
-            __builtin_nontemporal_store(v, p);
-    } else {
-        *p = v;
-    }
+    if constexpr (sizeof(V) == 16)
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), reinterpret_cast<u32x4*>(p));
+    else
+        __builtin_nontemporal_store(v, p);
 }
 
-// Store cache policy of the full-group stores (experiments): 0 = st_stream above; else
-// the aux bits of a raw buffer store from a block-uniform base (16 = sc1, write-through
-// that drops the line from L2; 17 = sc0 sc1; 2 = nt).
-#ifndef SHIPENV_ST_POLICY
-#define SHIPENV_ST_POLICY 0
-#endif
+// the full-group stores: st_stream above at a byte offset
 template <typename V>
 __device__ __forceinline__ void st_at(void* base, uint32_t byte_off, V v) {
-#if SHIPENV_ST_POLICY
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
-    if constexpr (sizeof(V) == 16)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, byte_off, 0, SHIPENV_ST_POLICY);
-    else
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, byte_off, 0, SHIPENV_ST_POLICY);
-#else
     st_stream(reinterpret_cast<V*>(reinterpret_cast<char*>(base) + byte_off), v);
-#endif
 }
 
 template <bool kNt = false, typename T>
@@ -795,25 +735,15 @@ struct Group {
         ld4_full<kNt>(A.st.ep_return, at.g0, e);
 #pragma unroll
         for (int j = 0; j < 4; ++j) l[j] = 0u;
-        if ((SHIPENV_ABL4 & 64) == 0 && (kAll || any))
+        if (kAll || any)
             ld4_full<kNt>(reinterpret_cast<const uint32_t*>(A.st.ep_start), at.g0, l);
     }
     template <bool kAll = false>
     __device__ __forceinline__ void load_episode(const StepArgs&, At<false>, bool) {}  // loaded with the rest
 };
 
-// Whether this lane's stamps move: one of its envs finished, or (SHIPENV_STAMP_GRAIN > 1)
-// one of the lanes of its aligned run of GRAIN lanes, so the run's stores cover a whole
-// 32- or 64-byte span.
-__device__ __forceinline__ bool stamp_lane(uint32_t fin) {
-    if constexpr (SHIPENV_STAMP_GRAIN <= 1) {
-        return fin != 0;
-    } else {
-        const uint64_t b = __ballot(fin != 0);
-        const uint32_t g = (threadIdx.x & 63) & ~(uint32_t)(SHIPENV_STAMP_GRAIN - 1);
-        return ((b >> g) & ((1ull << SHIPENV_STAMP_GRAIN) - 1)) != 0;
-    }
-}
+// Whether this lane's stamps move: one of its envs finished.
+__device__ __forceinline__ bool stamp_lane(uint32_t fin) { return fin != 0; }
 
 // ep_start of a group after a step at counter t: t + 1 for the envs that finished (the
 // next step starts their new episode), unchanged for the others. A full group stores
@@ -826,13 +756,7 @@ __device__ __forceinline__ void store_stamps(const se_state& S, At<kFull> at, co
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = ((fin >> j) & 1u) ? t + 1u : l[j];
     if constexpr (kFull) {
-        if ((SHIPENV_ABL4 & 128) == 0 && any) {
-            if constexpr (SHIPENV_STAMP_ST == 0) {
-                st4_full(reinterpret_cast<uint32_t*>(S.ep_start), at.g0, v);
-            } else {  // experiment: temporal 16-byte store
-                reinterpret_cast<uint4*>(slab_of(S.ep_start, at.g0))[threadIdx.x] = make_uint4(v[0], v[1], v[2], v[3]);
-            }
-        }
+        if (any) st4_full(reinterpret_cast<uint32_t*>(S.ep_start), at.g0, v);
     } else {
         st4_tail(reinterpret_cast<uint32_t*>(S.ep_start), at.base, at.n, v);
     }
@@ -950,27 +874,6 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
     const uint32_t t = A.t;
     Pending p[4];
 
-#if SHIPENV_ABLATE  // timing-only build (tools/archive/build_ablation.sh, tools/archive/ablate_libs.sh): memory traffic, no logic or draws
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        s[j].x ^= ty[j] & 1;
-        s[j].fuel -= (double)va[j];
-        s[j].cargo += vb[j];
-        p[j] = Pending{(double)vb[j], er[j], false, false, false, false, false};
-    }
-    (void)qk;
-    (void)t;
-    (void)bs;
-    (void)F;
-    store_moved(S, at, s, p);
-    float rw[4], epr[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        rw[j] = (float)p[j].r;
-        epr[j] = kAuto ? G.e[j] + rw[j] : 0.0f;
-    }
-    store_rest<kAuto>(S, at, s, rw, epr);
-#else
     if constexpr (kReplay) {
         // one env at a time; a missing variate (NEED_DRAW) leaves its env untouched
 #pragma unroll
@@ -1008,9 +911,6 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
             arrive |= (uint32_t)p[j].arrive << j;
             fin |= (uint32_t)((kFull || base + j < n) & p[j].dead) << j;
         }
-#if SHIPENV_ABL4 & 8
-        fin = 0;
-#endif
         // The per-env flags travel as these VGPR bit masks from here on: opaque to
         // the compiler, so it does not keep 4 x 3 lane masks (SGPR pairs) live
         // across the draw blocks below, which spilled them to VGPR lanes.
@@ -1025,11 +925,7 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
                 uint32_t ow[4], dw[4];
                 {
                     const uint32_t rk[4] = {0u, fin & 1u, (uint32_t)__popc(fin & 3u), (uint32_t)__popc(fin & 7u)};
-#if SHIPENV_ABL4 & 1
-                    U4 r{{qk.e0 ^ t, qk.e0 + t, 0u, 0u}};
-#else
                     U4 r = draw(qk, t, reset_slot(0));
-#endif
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         ow[j] = r.v[0];
@@ -1038,11 +934,7 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
 #pragma unroll
                     for (uint32_t q = 1; q < 4; ++q) {
                         if (__popc(fin) > q) {
-#if SHIPENV_ABL4 & 1
-                            r = U4{{r.v[1], r.v[0] * 3u, 0u, 0u}};
-#else
                             r = draw(qk, t, reset_slot(q));
-#endif
 #pragma unroll
                             for (int j = (int)q; j < 4; ++j) {
                                 ow[j] = rk[j] >= q ? r.v[0] : ow[j];
@@ -1124,7 +1016,7 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
                 const bool f = (fin >> j) & 1u;
                 F.ret[j] = G.e[j] + rw[j];
                 F.len[j] = (int32_t)(t + 1u - G.l[j]);  // stamps are loaded where fin
-                if ((SHIPENV_ABL4 & 4) == 0 && f) {
+                if (f) {
                     bs.ret += (double)F.ret[j];
                     bs.eps += 1;
                     bs.len += F.len[j];
@@ -1139,7 +1031,6 @@ __device__ __forceinline__ void step_group(const StepArgs& A, const LdsWorld& w,
         store_rest<kAuto>(late_args().st, at, s, rw, epr);
         if constexpr (kAuto) store_stamps(late_args().st, at, G.l, fin, t, stamp_lane(fin));
     }
-#endif
 }
 
 // ------------------------------------------------------------------ agent-index path
@@ -1184,14 +1075,7 @@ __device__ __forceinline__ uint32_t cell_of(uint32_t p, uint32_t wh) {
 // group's loads are issued, so their VALU work overlaps the wait for the data
 // instead of following it.
 // LOSS_0 is drawn early with auto-reset (config 4 measured 12.71 -> 12.44 us at
-// 2^20) and on demand without (config 3: 8.48 vs 8.56 us); SHIPENV_SPEC_LOSS = 0 / 1
-// forces it off / on for both.
-#ifndef SHIPENV_SPEC_LOSS
-#define SHIPENV_SPEC_LOSS -1
-#endif
-#ifndef SHIPENV_SPEC_ARRIVE
-#define SHIPENV_SPEC_ARRIVE 0  // 1 = draw the ARRIVE block early too (experiment)
-#endif
+// 2^20) and on demand without (config 3: 8.48 vs 8.56 us).
 struct Draws {
     U4 fuel, gate, loss0, arrive;
 };
@@ -1202,12 +1086,12 @@ __device__ __forceinline__ Draws early_draws(const StepArgs& A, int64_t base) {
     d.fuel = draw(qk, A.t, kSlotFuel);
     d.gate = draw(qk, A.t, kSlotGate);
     d.loss0 = kSpecLoss ? draw(qk, A.t, loss_slot(0)) : U4{{0u, 0u, 0u, 0u}};
-    d.arrive = SHIPENV_SPEC_ARRIVE ? draw(qk, A.t, kSlotArrive) : U4{{0u, 0u, 0u, 0u}};
+    d.arrive = U4{{0u, 0u, 0u, 0u}};
     return d;
 }
 
 template <bool kAuto>
-constexpr bool spec_loss() { return SHIPENV_SPEC_LOSS < 0 ? kAuto : SHIPENV_SPEC_LOSS != 0; }
+constexpr bool spec_loss() { return kAuto; }
 
 // se_step_record, per group of 4 envs at env index base (a full group; head and cap
 // multiples of 4, so its ring slots are consecutive): the stores of replay_end4_kernel
@@ -1354,8 +1238,8 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
     }
     TRACE_STAMP(5);
     (void)gate_needed;  // drawn early (early_draws) whether or not an env needs it
-    const U4 fb = SHIPENV_EARLY_DRAWS ? D.fuel : draw(qk, t, kSlotFuel);
-    const U4 gb = SHIPENV_EARLY_DRAWS ? D.gate : draw(qk, t, kSlotGate);
+    const U4 fb = D.fuel;
+    const U4 gb = D.gate;
     uint32_t fire = 0, arrive = 0, fin = 0, dead = 0;
     double f[4], r[4];
     // kReplay: the group's tape records (the partial last group's missing envs read none)
@@ -1401,9 +1285,6 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
         dead |= (uint32_t)(do_move[j] & oof) << j;
         fin |= (uint32_t)((kFull || base + j < n) & do_move[j] & oof) << j;
     }
-#if SHIPENV_ABL4 & 8
-    fin = 0;
-#endif
     // the flags travel as opaque VGPR bit masks (no lane masks live in SGPR pairs
     // across the draw blocks below)
     asm volatile("" : "+v"(fire), "+v"(arrive), "+v"(fin), "+v"(dead));
@@ -1419,11 +1300,7 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
         if (fin) {
             uint32_t ow[4], dw[4];
             const uint32_t rk[4] = {0u, fin & 1u, (uint32_t)__popc(fin & 3u), (uint32_t)__popc(fin & 7u)};
-#if SHIPENV_ABL4 & 1
-            U4 rr{{qk.e0 ^ t, qk.e0 + t, 0u, 0u}};
-#else
             U4 rr = draw(qk, t, reset_slot(0));
-#endif
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 ow[j] = rr.v[0];
@@ -1432,11 +1309,7 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
 #pragma unroll
             for (uint32_t q = 1; q < 4; ++q) {
                 if (__popc(fin) > q) {
-#if SHIPENV_ABL4 & 1
-                    rr = U4{{rr.v[1], rr.v[0] * 3u, 0u, 0u}};
-#else
                     rr = draw(qk, t, reset_slot(q));
-#endif
 #pragma unroll
                     for (int j = (int)q; j < 4; ++j) {
                         ow[j] = rk[j] >= q ? rr.v[0] : ow[j];
@@ -1559,7 +1432,7 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
     // arrival (:325-337): +2 cargo, cargo 0, origin = dest, a new destination != origin
     if (arrive) {
         [[maybe_unused]] U4 ab{{0u, 0u, 0u, 0u}};
-        if constexpr (!kReplay) ab = SHIPENV_SPEC_ARRIVE ? D.arrive : draw(qk, t, kSlotArrive);
+        if constexpr (!kReplay) ab = draw(qk, t, kSlotArrive);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const bool aj = (arrive >> j) & 1u;
@@ -1589,7 +1462,7 @@ __device__ __forceinline__ void step_group_agent(const StepArgs& A, const LdsWor
             const bool fj = (fin >> j) & 1u;
             F.ret[j] = G.e[j] + rw[j];
             F.len[j] = (int32_t)(t + 1u - G.l[j]);  // stamps are loaded where fin (kRec: everywhere)
-            if ((SHIPENV_ABL4 & 4) == 0 && fj) {
+            if (fj) {
                 bs.ret += (double)F.ret[j];
                 bs.eps += 1;
                 bs.len += F.len[j];
@@ -1682,14 +1555,11 @@ __device__ __forceinline__ int wave_sum_int(int v) {
            (__builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48));
 }
 
-// Statistics slab update. SHIPENV_SLAB_ATOMIC = 0 (default): lanes 0-2 of each wave load the
+// Statistics slab update: lanes 0-2 of each wave load the
 // wave's entry at the kernel's start and store old + sum at its end (plain loads and stores;
 // the entry is this wave's alone during a launch). At N = 2^24 the three no-return f64
 // atomics per wave (memory-side 64-B requests) cost config 4 ~16 us of ~190
-// (SHIPENV_ABL4 = 4 ablation, profiles/r04/c4split.jsonl).
-#ifndef SHIPENV_SLAB_ATOMIC
-#define SHIPENV_SLAB_ATOMIC 0
-#endif
+// (a timing-only ablation, profiles/r04/c4split.jsonl).
 // slab[i] += v without reading it back into the wave: the add runs in L2 and the
 // wave does not wait for it. Only this wave's lane 0 adds to its own entry during
 // a launch (step_tail_kernel adds in a later launch), so the order of additions is
@@ -1707,7 +1577,7 @@ __device__ __forceinline__ void wave_compact(const StepArgs& A, const Finished& 
                                              int64_t segment) {
     const int nd = __popc(F.mask);
     const uint64_t b0 = __ballot(nd & 1), b1 = __ballot(nd & 2), b2 = __ballot(nd & 4);
-    if ((SHIPENV_ABL4 & 16) == 0 && nd) {
+    if (nd) {
         int64_t slot = segment * A.seg + (int32_t)(count_below(b0) + 2 * count_below(b1) + 4 * count_below(b2));
         const int32_t t = (int32_t)A.t;
 #pragma unroll
@@ -1715,17 +1585,17 @@ __device__ __forceinline__ void wave_compact(const StepArgs& A, const Finished& 
             if ((F.mask >> j) & 1u) A.done_recs[slot++] = se_done_rec{(int32_t)(base + j), F.ret[j], F.len[j], t};
     }
     const int32_t total = (int32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
-    if ((SHIPENV_ABL4 & 16) == 0 && A.done_pad > 1) {  // launch-uniform (done_pad_records)
+    if (A.done_pad > 1) {  // launch-uniform (done_pad_records)
         // the wave's records padded to whole lines with filler records (env -1) past the
         // count: a line of the list written in part by one wave leaves L2 as a partial-line
         // write, and at N = 2^24 the ~1 record per wave cost config 4 ~11 us of ~192
-        // (SHIPENV_ABL4 = 16 ablation, profiles/r04/ab_c4parts.jsonl). A segment holds 256
+        // (a timing-only ablation, profiles/r04/ab_c4parts.jsonl). A segment holds 256
         // records, a multiple of the pad, so the filler stays inside it.
         const int32_t pad = (-total) & (A.done_pad - 1), l = (int32_t)(threadIdx.x & 63);
         if (total != 0 && l < pad)
             A.done_recs[segment * A.seg + total + l] = se_done_rec{-1, 0.0f, 0, (int32_t)A.t};
     }
-    if ((SHIPENV_ABL4 & 32) == 0 && (threadIdx.x & 63) == 0) A.done_count[segment] = total;
+    if ((threadIdx.x & 63) == 0) A.done_count[segment] = total;
 }
 
 // Workgroup b owns the contiguous groups [b*iters*256, (b+1)*iters*256) (a group is
@@ -1737,31 +1607,20 @@ __device__ __forceinline__ void wave_compact(const StepArgs& A, const Finished& 
 // step_tail_kernel, so this loop carries no guarded scalar path. The world image's
 // loads, then the first group's, are all in flight before the LDS writes; each
 // iteration loads the next group after storing the current one.
-#ifndef SHIPENV_STEP_WPE
-#define SHIPENV_STEP_WPE 4  // minimum waves per SIMD the register allocation must allow
-#endif
 // kSeq: the same code, instantiated apart for se_step_seq's launches (the agent path without
 // auto-reset), so a kernel trace lists them under a name of their own: bench.py's headline leg
 // issues its timed steps that way, and its trace row then holds exactly those launches.
 template <bool kTyped, bool kReplay, bool kAuto, bool kNt = false, bool kRec = false, bool kSeq = false>
-__global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(SHIPENV_STEP_WPE))) void step_kernel(StepArgs A) {
+__global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4))) void step_kernel(StepArgs A) {
     static_assert(!kRec || (kAuto && !kTyped && !kReplay), "se_step_record: agent actions, auto-reset");
     extern __shared__ uint32_t lds[];
     const int64_t full = A.n >> 2;
     const int64_t first = (int64_t)blockIdx.x * A.iters * kStepBlock;  // block-uniform first group
 
     TRACE_STAMP(0);
-#if SHIPENV_ABLATE >= 2  // timing-only: no world staging either
-    (void)lds;
-#else
     const Staged st = stage_issue(A.world);
     // the image's loads first: the staging writes then wait for them alone
     __builtin_amdgcn_sched_barrier(0);
-#if SHIPENV_STAGE_ORDER == 1  // experiment: the image in LDS before the group's loads are issued
-    stage_write(A.world, A.dims, lds, st);
-    __builtin_amdgcn_sched_barrier(0);
-#endif
-#endif
     // first group: an unconditional load (lanes past the end re-read the last full
     // group; the host launches this kernel only when there is one), so the staging
     // writes below wait for exactly the image's loads
@@ -1773,9 +1632,9 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(SHIP
     }
     __builtin_amdgcn_sched_barrier(0);
     // auto-reset: this wave's statistics so far ({sum ret, episodes, sum len} on lanes 0-2),
-    // loaded now so the end of the wave adds to them without waiting (SHIPENV_SLAB_ATOMIC = 0)
+    // loaded now so the end of the wave adds to them without waiting
     // (kRec keeps the atomics: two more registers there spilled)
-    constexpr bool kSlabRmw = kAuto && !kRec && (SHIPENV_ABL4 & 4) == 0 && !SHIPENV_SLAB_ATOMIC;
+    constexpr bool kSlabRmw = kAuto && !kRec;
     [[maybe_unused]] double slab_prev = 0.0;
     if constexpr (kSlabRmw) {
         const uint32_t l = threadIdx.x & 63;
@@ -1783,22 +1642,15 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(SHIP
         slab_prev = sl[l < 3 ? l : 0];
     }
     // agent-index actions: the production step, or its replay-tape form (parity)
-    constexpr bool kAgent = !kTyped && !SHIPENV_ABLATE;
-    constexpr bool kDraws = kAgent && !kReplay && SHIPENV_EARLY_DRAWS;
+    constexpr bool kAgent = !kTyped;
+    constexpr bool kDraws = kAgent && !kReplay;
     Draws D{};
     if constexpr (kDraws) {
         D = early_draws<spec_loss<kAuto>()>(A, (first + threadIdx.x) * 4);
         // keep the draws ahead of the staging wait: they overlap the loads in flight
         asm volatile("" : "+v"(D.fuel.v[0]), "+v"(D.gate.v[0]), "+v"(D.loss0.v[0]), "+v"(D.arrive.v[0]));
     }
-#if SHIPENV_ABLATE >= 2
-    const LdsWorld w = world_view(A.dims, A.world);
-#elif SHIPENV_STAGE_ORDER == 1
-    __syncthreads();
-    const LdsWorld w = world_view(A.dims, lds);
-#else
     const LdsWorld w = stage_finish(A.world, A.dims, lds, st);
-#endif
     TRACE_STAMP(1);
 
     BlockStats bs;
@@ -1807,10 +1659,6 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(SHIP
         const int64_t g0 = first + k * kStepBlock, g = g0 + threadIdx.x;
         Finished F;
         const bool more = k + 1 < A.iters && g + kStepBlock < full;
-        // SHIPENV_PREFETCH: the next group's loads go out before this group's compute
-        // (software pipelining; pays only with several groups per thread)
-        Group<kTyped, kAuto, kNt> Gn;
-        if (SHIPENV_PREFETCH && more) Gn.template load<true>(A, At<true>{g0 + kStepBlock, 0, A.n});
         if (g < full) {
             if constexpr (kAgent) {
                 if constexpr (kDraws) {
@@ -1821,11 +1669,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(SHIP
             } else
                 step_group<kTyped, kReplay, kAuto, true, kNt>(A, w, G, At<true>{g0, g * 4, A.n}, bs, F);
             if (k == 0) TRACE_STAMP(2);
-            if (!SHIPENV_PREFETCH && more) G.template load<true>(A, At<true>{g0 + kStepBlock, 0, A.n});
+            if (more) G.template load<true>(A, At<true>{g0 + kStepBlock, 0, A.n});
         }
-        if (SHIPENV_PREFETCH) G = Gn;
         // done-list segment of this (iteration, wave): 64 groups, in env order
-        if constexpr (kAuto && (SHIPENV_ABL4 & 2) == 0) wave_compact(late_args(), F, g * 4, __builtin_amdgcn_readfirstlane((int32_t)(g >> 6)));
+        if constexpr (kAuto) wave_compact(late_args(), F, g * 4, __builtin_amdgcn_readfirstlane((int32_t)(g >> 6)));
     }
 
 #if SHIPENV_TRACE
@@ -1836,7 +1683,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(SHIP
         if (blockIdx.x == 0 && threadIdx.x == 0) *late_args().rec.d_size = late_args().rec.new_size;
         if (cuts) record_restart(late_args(), w, cuts);
     }
-    if (kAuto && (SHIPENV_ABL4 & 4) == 0) {
+    if (kAuto) {
         // per-wave statistics: a fixed-order tree (wave_sum), added to this wave's own
         // slab entry. With episodes ending about once per 240 steps, most waves have one
         // lane with a finished episode or none: then that lane's values are the sums
@@ -1894,9 +1741,9 @@ __global__ __launch_bounds__(64) void step_tail_kernel(StepArgs A) {
     G.template load<false>(A, at);
     BlockStats bs;
     Finished F;
-    if constexpr (!kTyped && !kReplay && !SHIPENV_ABLATE)
+    if constexpr (!kTyped && !kReplay)
         step_group_agent<kAuto, false, false>(A, w, G, at, bs, F, early_draws<spec_loss<kAuto>()>(A, at.base));
-    else if constexpr (!kTyped && kReplay && !SHIPENV_ABLATE)
+    else if constexpr (!kTyped && kReplay)
         step_group_agent<kAuto, false, false, false, true>(A, w, G, at, bs, F, Draws{});
     else
         step_group<kTyped, kReplay, kAuto, false>(A, w, G, at, bs, F);
@@ -1917,24 +1764,6 @@ __global__ __launch_bounds__(64) void step_tail_kernel(StepArgs A) {
         }
     }
 }
-
-#ifdef SHIPENV_ISA_PROBE  // inspection only: one env's two halves in isolation
-__global__ void probe_kernel(const uint32_t* world, WorldDims d, const int* in, double* out) {
-    extern __shared__ uint32_t lds[];
-    const LdsWorld w = stage_world(world, d, lds);
-    const int i = threadIdx.x;
-    int ty, va, vb;
-    const int er = decode_agent(w.P, in[i], ty, va, vb);
-    Ship s{in[i + 64], in[i + 128], (double)in[i + 192], in[i + 256], in[i + 320], in[i + 384]};
-    asm volatile("; probe: begin" ::: "memory");
-    Pending p = env_begin<true, false>(w, s, er, ty, va, vb, (double)(uint32_t)in[i + 448], 0.0,
-                                       (uint32_t)in[i + 512]);
-    asm volatile("; probe: finish" ::: "memory");
-    env_finish(s, p, in[i + 576], beta_part((uint32_t)in[i + 640], s.cargo), in[i + 704], p.fires, p.arrive);
-    asm volatile("; probe: end" ::: "memory");
-    out[i] = p.r + s.fuel + (double)(s.x + s.y + s.cargo + s.origin + s.dest + p.e + p.fires + p.arrive + p.dead);
-}
-#endif
 
 // Contiguous copy of the last step's done lists (se_done_compact), in two launches:
 // done_scan_kernel (one workgroup) turns the per-segment counts into exclusive
@@ -2443,18 +2272,10 @@ struct SampleArgs {
     int32_t* b;
 };
 
-#ifndef SHIPENV_SAMPLE_STAGE
-#define SHIPENV_SAMPLE_STAGE 0  // 1: stage the world image per workgroup (the round-1 form)
-#endif
 // One cell-code byte and one stock per env: read in place through L1 / L2 instead of
 // staging the 10.8 KB image into every one of up to 2048 workgroups.
 __global__ __launch_bounds__(kBlock) void sample_kernel(SampleArgs A) {
-#if SHIPENV_SAMPLE_STAGE
-    extern __shared__ uint32_t lds[];
-    const LdsWorld w = stage_world(A.world, A.dims, lds);
-#else
     const LdsWorld w = world_view(A.dims, A.world);
-#endif
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < A.n;
          i += (int64_t)gridDim.x * kBlock) {
         const Ship s{A.st.x[i], A.st.y[i], A.st.fuel[i], A.st.cargo[i], A.st.origin[i], A.st.dest[i]};
@@ -3118,7 +2939,7 @@ int se_sample_actions(se_env* env, int32_t* type, int32_t* a, int32_t* b, uint32
     if (!type || !a || !b) return fail(SE_EINVAL, "null output pointer");
     DeviceGuard g(env->device);
     SampleArgs A{env->d_world, env->dims, env->n, env->env_base, env->seed, t, env->st, type, a, b};
-    sample_kernel<<<grid_for(env->n), kBlock, SHIPENV_SAMPLE_STAGE ? lds_bytes(env) : 0, (hipStream_t)stream>>>(A);
+    sample_kernel<<<grid_for(env->n), kBlock, 0, (hipStream_t)stream>>>(A);
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }

@@ -89,8 +89,7 @@ class QPolicy:
         precision: "bf16" (se_policy: bf16 weights and activations on bf16 MFMA, f32
         accumulation) or "f32" (se_policy_f32: the network in fp32 as agents/dqn.py runs
         it; fc2 and fc3 on bf16 MFMA with every f32 operand split into three bf16 parts,
-        about 4x the bf16 policy's time; SHIPENV_POLICY_F32=mfma at QPolicy creation selects
-        the f32-MFMA kernel instead)."""
+        about 4x the bf16 policy's time)."""
         if precision not in ("bf16", "f32"):
             raise ValueError("precision must be 'bf16' or 'f32'")
         fn = N.lib().se_policy if precision == "bf16" else N.lib().se_policy_f32

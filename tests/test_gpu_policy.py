@@ -189,9 +189,7 @@ def philox_np(e, t, slot, seed):
 @pytest.mark.parametrize("precision", ["bf16", "f32"])
 def test_explore_over_several_tiles_per_wave(precision):
     """2^18 + 37 envs: 8194 tiles over the 4096 resident waves, so waves run two or three
-    tiles: the epsilon draws of a wave's later tiles (in a SHIPENV_POLICY_DRAW_PAIR=1 build,
-    one Philox pass for a tile and the next, used on odd iterations and drawn past the last
-    tile) against the RNG contract.
+    tiles: the epsilon draws of a wave's later tiles against the RNG contract.
     epsilon = 0.3: the Philox choice among the valid actions exactly where u <= 0.3, the
     greedy action elsewhere (the same kernel at epsilon 0)."""
     n = (1 << 18) + 37

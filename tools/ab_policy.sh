@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5: the f32 (split-bf16) policy over the library builds under shippingenv_amd/_lib/abl,
+# the bf16 or f32 (split-bf16) policy over the library builds under shippingenv_amd/_lib/abl,
 # ROUNDS rounds alternating (tools/time_policy.py, 2^20 envs); one JSON line per run
 set -u
 for rep in $(seq 1 ${ROUNDS:-3}); do

@@ -53,7 +53,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     print(json.dumps({"lib": os.path.basename(a.lib or "default"), "precision": a.precision,
-                      "f32_mode": os.environ.get("SHIPENV_POLICY_F32", "split-bf16"), "n": a.n, "preroll": a.preroll, "ms_per_launch": round(e0.elapsed_time(e1) / a.launches, 4),
+                      "n": a.n, "preroll": a.preroll, "ms_per_launch": round(e0.elapsed_time(e1) / a.launches, 4),
                       "at_port": float(at.float().mean()), "wave32_with_port": float(waves_any)}))
 
 
