@@ -308,7 +308,11 @@ def run_config(n, ports, auto, args, dist, label, preroll=0, step_seq=False):
     env.close()
     del acts
     torch.cuda.empty_cache()
-    info = {"preroll_steps": preroll, "allreduce_every": every, "allreduces_in_timed_region": count[0]}
+    # allreduces_in_timed_region counts the reduce_episode_stats calls; collectives_in_timed_region
+    # the RCCL all-reduces they issued (none at world size 1, dist.reduce_episode_stats)
+    info = {"preroll_steps": preroll, "allreduce_every": every, "allreduces_in_timed_region": count[0],
+            "collectives_in_timed_region": count[0] if dist.world > 1 else 0,
+            "collective_backend": dist.info.get("backend") if dist.world > 1 else None}
     return wall, k_ms, stats, info
 
 
@@ -441,7 +445,7 @@ def run_config5(n, args, dist):
     epsilon-greedy, fused in se_policy_f32 / se_policy) then se_step, and the RCCL SUM
     all-reduce of {sum of returns, episodes, sum of lengths} every min(100, K // 2) steps
     inside the timed region. `value` evaluates the network in fp32, the reference's own
-    precision (se_policy_f32, f32 MFMA); the bf16 policy's figure is beside it. Also: the
+    precision (se_policy_f32, split-bf16 MFMA); the bf16 policy's figure is beside it. Also: the
     env kernel alone (se_step over the same auto-reset shard) and the unfused torch policy."""
     from shippingenv_amd.policy import DQNNetwork, QPolicy
     from shippingenv_amd.vec import VecEnv
@@ -486,6 +490,7 @@ def run_config5(n, args, dist):
                       "e2e_kernel_ms": round(e2e_ms, 4),
                       "policy_ms": round(e0.elapsed_time(e1) / K, 4),
                       "allreduces_in_timed_region": count,
+                      "collectives_in_timed_region": count if dist.world > 1 else 0,
                       "episodes": st[1],
                       "mean_return": st[0] / st[1] if st[1] else None}
     # the env kernel alone: se_step over the same shard, the policy's last actions each step
@@ -541,7 +546,9 @@ def run_config5(n, args, dist):
     rows3 = 32 * ((4 + env.P + cmax + fmax + 31) // 32)
     flop_env = 2 * (6 * 128 + 128 * 128 + rows3 * 128)
     flop_ref = 2 * (env.obs_size * 128 + 128 * 128 + 128 * A)  # the reference network's MACs x 2
-    x3_flop_env = 6 * 2 * (128 * 128 + rows3 * 128) + 2 * 6 * 128
+    # the MFMA FLOPs se_policy_f32 executes per env: fc2 and fc3 six bf16 products each, fc1 two
+    # split-bf16 32x32x16 MFMAs per row tile (x3_fc1_slot: 24 of their 32 k slots used)
+    x3_flop_env = 6 * 2 * (128 * 128 + rows3 * 128) + 4 * 2 * (32 * 32 * 16 * 2) // 32
     pol32_ms, pol_ms = legs["f32"]["policy_ms"], legs["bf16"]["policy_ms"]
     achieved32 = flop_env * n / (pol32_ms * 1e-3) / 1e12
     achieved = flop_env * n / (pol_ms * 1e-3) / 1e12
@@ -571,6 +578,7 @@ def run_config5(n, args, dist):
         "preroll_steps": args.preroll5,
         "allreduce_every": every,
         "allreduces_in_timed_region": f32["allreduces_in_timed_region"],
+        "collectives_in_timed_region": f32["collectives_in_timed_region"],
         "episodes": f32["episodes"],
         "mean_return": f32["mean_return"],
         "env_kernel": {"value": round(n * dist.world / (step_ms * 1e-3), 1), "kernel_ms": round(step_ms, 5),
@@ -582,8 +590,8 @@ def run_config5(n, args, dist):
                                                       "masked argmax of the fp32 torch DQNNetwork"},
         "torch_unfused_policy_ms": round(torch_ms, 4),
         # se_policy_f32 (round 5) evaluates the fp32 network on bf16 MFMA with 3-way operand
-        # splits: six bf16 products per f32 product for fc2 and fc3 (fc1 stays on f32 MFMA,
-        # qpolicy.h policy_x3_kernel). Its roofline is the bf16 MFMA peak over the MFMA FLOPs
+        # splits: six bf16 products per f32 product for fc2 and fc3, fc1 as two split-bf16 MFMAs
+        # per row tile (qpolicy.h policy_x3_kernel, x3_fc1_slot). Its roofline is the bf16 MFMA peak over the MFMA FLOPs
         # the fp32-faithful algorithm executes; the f32-equivalent rate (the network's own
         # FLOPs) is beside it against the f32 MFMA peak, which the split datapath exceeds.
         "roofline": {"bound": "mfma (bf16, fp32 by 3-way operand splits)",
@@ -596,7 +604,7 @@ def run_config5(n, args, dist):
                                         "flop_per_env": flop_env},
                      "reference_network_flop_per_env": flop_ref,
                      "note": "se_policy_f32 (includes its per-call repack of the split image); flop_per_env = "
-                             "6 x (fc2 + fc3 over its 32-row tiles) bf16 MFMA FLOPs + fc1's on f32 MFMA; "
+                             "6 x (fc2 + fc3 over its 32-row tiles) bf16 MFMA FLOPs + fc1's 8 split-bf16 MFMAs per 32 envs; "
                              "f32_equivalent: the FLOPs the fused step evaluates (fc1's 6 dynamic inputs, fc2, "
                              "fc3's compact rows) against the f32 MFMA peak"},
         "roofline_bf16": {"bound": "mfma", "achieved": round(achieved, 1), "peak": BF16_DENSE_PEAK_TFLOPS,

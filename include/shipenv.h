@@ -206,6 +206,9 @@ int se_host_set_ports(se_host* h, int32_t P, const int32_t* port_x, const int32_
                       const int32_t* port_fuel, const int32_t* port_cargo);
 int se_host_step_replay(se_host* h, int64_t n, const se_state* st, const int32_t* type,
                         const int32_t* a, const int32_t* b, se_tape* tape);
+/* se_host_reset_to stamps ep_start = 0 (a host world keeps no step counter): lengths derived
+ * from a host world's stamps (counter - ep_start) are meaningless; the host stepper reports
+ * lengths through its own step records. */
 int se_host_reset_to(se_host* h, int64_t n, const se_state* st, const uint8_t* mask,
                      const int32_t* origin, const int32_t* dest);
 int se_host_destroy(se_host* h);

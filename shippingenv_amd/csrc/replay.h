@@ -436,7 +436,7 @@ int replay_end(se_replay* r, uint8_t* cut, int32_t max_steps, bool reset_cut, vo
     if (rc) return rc;
     if (!r->open) return fail(SE_ESTATE, "se_replay_end without se_replay_begin");
     se_env* env = r->env;
-    if (max_steps > 0 && (!cut || !env->st.ep_start))
+    if (max_steps > 0 && (!cut || !(env->flags & SE_FLAG_AUTO_RESET) || !env->st.ep_start))
         return fail(SE_EINVAL, "max_steps needs a cut buffer and an auto-reset env (ep_start)");
     if (reset_cut && !cut) return fail(SE_EINVAL, "se_replay_end_reset needs a cut buffer");
     if (reset_cut && env->dims.P < 2) return fail(SE_EINVAL, "reset needs at least two ports");

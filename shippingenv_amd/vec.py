@@ -145,7 +145,10 @@ class VecEnv:
     @property
     def ep_len(self):
         """Running episode lengths in step calls (auto-reset): (step counter - ep_start)
-        mod 2^32, as a new int32 device tensor computed on the current stream."""
+        mod 2^32, as a new int32 device tensor computed on the current stream. A snapshot:
+        a reference to it does not follow later steps (read the property again). Without
+        auto-reset the stamps are only written by reset (se_reset stamps the counter), so
+        the value is the steps since the last reset."""
         t = self.counters[0] & 0xFFFFFFFF
         d = (t - self.ep_start.to(torch.int64)) & 0xFFFFFFFF
         return torch.where(d >= 2**31, d - 2**32, d).to(torch.int32)

@@ -66,6 +66,29 @@ def rows(world, env):
     return O.observe(world, st)
 
 
+def test_max_steps_needs_auto_reset():
+    """se_replay_end refuses max_steps > 0 on an env without auto-reset, whose
+    episode-start stamps only reset writes (a length cut there would count from the last
+    reset, not from the episode's start); max_steps = 0 still records."""
+    from shippingenv_amd._native import ShipEnvError
+    from shippingenv_amd.dqn import ReplayBuffer
+    from shippingenv_amd.vec import VecEnv
+
+    env = VecEnv(256, seed=1)
+    _OPEN.append(env)
+    env.reset()
+    rb = ReplayBuffer(env, 1024)
+    _OPEN.append(rb)
+    cut = torch.zeros(256, dtype=torch.uint8, device=env.device)
+    a = env.gen_actions(0)
+    rb.begin(a)
+    env.step(a)
+    with pytest.raises(ShipEnvError, match="max_steps"):
+        rb.end(cut, 4)
+    rb.end(cut, 0)
+    assert rb.size == 256
+
+
 @pytest.mark.parametrize("n,cap,ports64", [(1000, 2500, False), (4099, 20000, True)])
 def test_replay_ring_and_minibatch_vs_oracle(n, cap, ports64):
     from conftest import golden_water

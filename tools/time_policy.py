@@ -25,6 +25,8 @@ def main():
     p.add_argument("--eps", type=float, default=0.1)
     p.add_argument("--lib", default=None)
     p.add_argument("--precision", default="bf16", choices=("bf16", "f32"))
+    p.add_argument("--trace", action="store_true",
+                   help="a SHIPENV_X3_TRACE=1 library: per-phase cycle medians of the fp32 policy's 4th tile")
     a = p.parse_args()
     if a.lib:
         from shippingenv_amd import _native
@@ -52,9 +54,37 @@ def main():
         pol.act(a.eps, 1000 + k, precision=a.precision)
     e1.record()
     torch.cuda.synchronize()
-    print(json.dumps({"lib": os.path.basename(a.lib or "default"), "precision": a.precision,
-                      "n": a.n, "preroll": a.preroll, "ms_per_launch": round(e0.elapsed_time(e1) / a.launches, 4),
-                      "at_port": float(at.float().mean()), "wave32_with_port": float(waves_any)}))
+    rec = {"lib": os.path.basename(a.lib or "default"), "precision": a.precision,
+           "n": a.n, "preroll": a.preroll, "ms_per_launch": round(e0.elapsed_time(e1) / a.launches, 4),
+           "at_port": float(at.float().mean()), "wave32_with_port": float(waves_any)}
+    if a.trace:
+        import ctypes
+        import numpy as np
+        from shippingenv_amd import _native as N
+
+        buf = np.zeros(4096 * 16, dtype=np.uint64)
+        N.lib().se_policy_trace_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        assert N.lib().se_policy_trace_read(buf.ctypes.data, buf.nbytes) == 0
+        st = buf.reshape(4096, 16).astype(np.int64)
+        ok = (st[:, 0] > 0) & (st[:, 8] > st[:, 0])
+        d = np.diff(st[ok][:, :9], axis=1)
+        rec["trace_waves"] = int(ok.sum())
+        rec["phase_cycles_median"] = [int(x) for x in np.median(d, axis=0)]
+        rec["tile_cycles_median"] = int(np.median(st[ok][:, 8] - st[ok][:, 0]))
+        live = st[:, 9] > 0  # stamps 9-11: s_memrealtime (100 MHz, chip-wide) at start, image staged, end
+        s9, s10, s11 = st[live, 9], st[live, 10], st[live, 11]
+        t0 = s9.min()
+        rec["us_image_median"] = float(np.median(s10 - s9)) / 100
+        rec["us_wave_median"] = float(np.median(s11 - s9)) / 100
+        rec["us_start_spread_max"] = float((s9 - t0).max()) / 100
+        rec["us_end_median"] = float(np.median(s11 - t0)) / 100
+        rec["us_end_max"] = float((s11 - t0).max()) / 100
+        # stamps 12-14: s_memtime (shader clock) beside 9-11: the wave's mean clock
+        rec["ghz_wave_median"] = float(np.median((st[live, 14] - st[live, 12]) / (s11 - s9) / 10))
+        wid = np.nonzero(live)[0] % 8
+        rec["us_wave_median_by_half"] = [float(np.median((s11 - s9)[wid < 4])) / 100,
+                                         float(np.median((s11 - s9)[wid >= 4])) / 100]
+    print(json.dumps(rec))
 
 
 if __name__ == "__main__":
