@@ -209,52 +209,6 @@ struct PolicyArgs {
     float* rec_fuel;
     int32_t* rec_act;
     int64_t rec_head, rec_cap;
-    // the fp32 policy's tile queue (TileQueue): this launch's kTileShards heads, zero at launch,
-    // and the other parity's, which this launch zeroes for the next one; null: static striding
-    uint32_t* queue;
-    uint32_t* queue_next;
-};
-
-// ------------------------------------------------------------------ tile queue
-// Dynamic tile assignment for the fp32 policy (round 6). With a static stride every wave steps
-// the same number of 32-env tiles, but the two waves of a SIMD do not progress alike (static
-// issue priority, XCD differences): at 2^20 envs the median wave of policy_x3_kernel finished
-// after 195 us and the last after 234 us (s_memrealtime stamps, SHIPENV_X3_TRACE), so the
-// launch ran a 17 % tail with half its SIMD partners idle. Here each wave's first tile is
-// static (wave w of the grid takes tile w) and the rest are handed out by kTileShards
-// per-shard heads (a returning device-scope atomic add by one lane: MI355X_MICROARCH.md
-// "dequeue"; one word saturates near 88 dequeues/us, 2048 waves at ~12 us per tile need ~170,
-// so the heads are sharded by blockIdx.x % kTileShards, ~the XCD under round-robin placement:
-// speed only). A tile's result does not depend on the wave that computes it. A wave claims its
-// next tile one tile ahead, so the atomic's ~1 us return is hidden. The heads are zeroed by the
-// launch before (parity), so no memset launch precedes the kernel.
-constexpr int kTileShards = 8;
-constexpr int kQueueStride = 32;  // u32 words per head: one 128-byte line each
-struct TileQueue {
-    uint32_t* head;  // this wave's shard head
-    int64_t lo, hi;  // the shard's dynamic tiles [lo, hi)
-    __device__ __forceinline__ static TileQueue of(const PolicyArgs& A, int64_t tiles, int64_t static_tiles) {
-        TileQueue Q;
-        const int shards = min((int)gridDim.x, kTileShards);
-        const int s = (int)(blockIdx.x % (unsigned)shards);
-        const int64_t dyn = tiles > static_tiles ? tiles - static_tiles : 0;
-        Q.head = A.queue + s * kQueueStride;
-        Q.lo = static_tiles + dyn * s / shards;
-        Q.hi = static_tiles + dyn * (s + 1) / shards;
-        if (blockIdx.x == 0 && threadIdx.x < kTileShards) A.queue_next[threadIdx.x * kQueueStride] = 0u;
-        return Q;
-    }
-    // one lane's claim, read a tile later with next()
-    __device__ __forceinline__ uint32_t issue() const {
-        uint32_t t = 0u;
-        if ((threadIdx.x & 63) == 0) t = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return t;
-    }
-    // the claimed tile, or hi (past the shard: the wave is done)
-    __device__ __forceinline__ int64_t next(uint32_t claim) const {
-        const int64_t t = lo + (int64_t)__builtin_amdgcn_readfirstlane(claim);
-        return t < hi ? t : hi;
-    }
 };
 
 // v = p0 + p1 + p2, each the bf16 rounding of the remainder (exact f32 subtractions)
@@ -478,10 +432,38 @@ __device__ __forceinline__ void finish_env(const QnetDims& q, const EnvValid& v,
     }
 }
 
+#ifndef SHIPENV_POLICY_FC3X
+#define SHIPENV_POLICY_FC3X 1  // round-6 A/B switch (removed once measured)
+#endif
+#ifndef SHIPENV_X3_TRACE
+#define SHIPENV_X3_TRACE 0  // 1 = diagnostic build: per-wave s_memtime phase stamps of the fp32 policy
+#endif                      // kernels' 4th tile (se_policy_trace_read, tools/time_policy.py --trace)
+#if SHIPENV_X3_TRACE
+__device__ uint64_t g_ptrace[4096 * 16];
+#define X3STAMP(k)                                                                                          \
+    do {                                                                                                    \
+        if (tile_iter == 3 && (threadIdx.x & 63) == 0)                                                      \
+            g_ptrace[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % 4096 * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#define X3STAMP_ANY(k)                                                                                      \
+    do {                                                                                                    \
+        if ((threadIdx.x & 63) == 0) {                                                                      \
+            uint64_t* p_ = g_ptrace + (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % 4096 * 16;       \
+            p_[(k)] = __builtin_amdgcn_s_memrealtime();                                                     \
+            p_[(k) + 3] = __builtin_amdgcn_s_memtime();                                                     \
+        }                                                                                                   \
+    } while (0)
+#else
+#define X3STAMP(k) \
+    do {           \
+    } while (0)
+#define X3STAMP_ANY(k) X3STAMP(k)
+#endif
 template <bool kQout>
 __global__ __launch_bounds__(kPolicyBlock)
 void policy_kernel(PolicyArgs A) {
     extern __shared__ uint4 smem[];
+    X3STAMP_ANY(9);
     const QnetDims q = A.q;
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
     const int64_t tiles = (A.n + 31) >> 5;
@@ -521,6 +503,8 @@ void policy_kernel(PolicyArgs A) {
         }
     }
     const LdsWorld w = stage_world(A.world, A.dims, reinterpret_cast<uint32_t*>(smem + qwords));
+    X3STAMP_ANY(10);
+    [[maybe_unused]] int tile_iter = 0;  // SHIPENV_X3_TRACE: the wave's 4th tile is stamped
     const uint8_t* qb = reinterpret_cast<const uint8_t*>(smem);
     const bf16x8* W1f = reinterpret_cast<const bf16x8*>(qb + q.w1());
     const bf16x8* W2f = reinterpret_cast<const bf16x8*>(qb + q.w2());
@@ -534,7 +518,8 @@ void policy_kernel(PolicyArgs A) {
     const int P = q.P;
     const int64_t stride = (int64_t)gridDim.x * kPolicyWaves;
     EnvIn nxt = load_env(tile < tiles ? tile : 0);
-    for (; tile < tiles; tile += stride) {
+    for (; tile < tiles; tile += stride, ++tile_iter) {
+        X3STAMP(0);
         const EnvIn cur_in = nxt;
         if (tile + stride < tiles) nxt = load_env(tile + stride);
         const int64_t e = tile * 32 + r;
@@ -567,6 +552,7 @@ void policy_kernel(PolicyArgs A) {
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(W1f[mt * 64 + lane], ob, c, 0, 0, 0);
             relu_pack(c, h1[mt]);
         }
+        X3STAMP(1);
         // fc2 + relu one row tile per pass: no spills at 128 VGPRs (2 tiles a pass spill 7
         // registers, 4 spill 14); a pass's relu issues in the shadow of the next pass's MFMAs
         constexpr int kFc2Passes = 4, kFc2Tiles = 4 / kFc2Passes;
@@ -601,6 +587,7 @@ void policy_kernel(PolicyArgs A) {
             for (int i = 0; i < kFc2Tiles; ++i) relu_pack(c2[i], h2[pass * kFc2Tiles + i]);
         }
 
+        X3STAMP(2);
         // is_valid_action (dqn.py:125-175): moves always; SELECT p at the ship's cell
         // and != origin; TAKE_CARGO / TAKE_FUEL at a port with 0 < amount <= stock
         const int cur = w.port_at(x, y);
@@ -626,7 +613,45 @@ void policy_kernel(PolicyArgs A) {
         }
         float best = -INFINITY;
         int bidx = 0x7fffffff;
-        for (int mt = 0; mt < q.mt3; ++mt) {  // fc3 + the masked first-maximum argmax
+        if (SHIPENV_POLICY_FC3X && use64) {
+            // compact layouts of at most 64 rows (the bench's greedy and epsilon calls): rows
+            // this env cannot take start at -inf (masked_bias, two VALU per register), so the
+            // first maximum is a compare and two selects per register with no validity test and
+            // no per-register branch, and fc3 tile 0's argmax runs beside tile 1's MFMAs
+            constexpr int L3 = 2;  // fragments read L3 k-steps ahead (a 3-slot ring: 12 VGPRs)
+            bf16x8 wf[L3 + 1];
+#pragma unroll
+            for (int k = 0; k < L3; ++k) wf[k] = W3f[k * 64 + lane];
+            f32x16 c = masked_bias(B3 + 4 * h, (uint32_t)v64 >> (4 * h));
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (k + L3 < 8) wf[(k + L3) % (L3 + 1)] = W3f[(k + L3) * 64 + lane];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k % (L3 + 1)], h2[k >> 1][k & 1], c, 0, 0, 0);
+            }
+            int bt = 0, pbase = 0;
+            if (q.mt3 > 1 && __any((uint32_t)(v64 >> 32) != 0u)) {  // fc3 tile 1 (uniform)
+#pragma unroll
+                for (int k = 0; k < L3; ++k) wf[k] = W3f[(8 + k) * 64 + lane];
+                f32x16 c1 = masked_bias(B3 + 32 + 4 * h, (uint32_t)(v64 >> 32) >> (4 * h));
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    if (k + L3 < 8) wf[(k + L3) % (L3 + 1)] = W3f[(8 + k + L3) * 64 + lane];
+                    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k % (L3 + 1)], h2[k >> 1][k & 1], c1, 0, 0, 0);
+                    if (k < 4) argmax_local_part(c, best, bt, k);  // tile 0's, beside tile 1's chain
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                bidx = best != -INFINITY ? bt : bidx;
+                c = c1;
+                pbase = 32;
+            }
+            const float best0 = best;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) argmax_local_part(c, best, bt, g);
+            bidx = best != best0 ? pbase + bt : bidx;
+            bidx += bidx == 0x7fffffff ? 0 : 4 * h;  // the lane half's rows (argmax_local_part omits 4h)
+        }
+        for (int mt = 0; mt < ((SHIPENV_POLICY_FC3X && use64) ? 0 : q.mt3); ++mt) {  // fc3 + the masked first-maximum argmax
             const int base = mt * 32, top = base + 31;
             // a tile no env of the wave can choose from is skipped, MFMAs included
             // (exact: its rows are invalid for all 32 envs); with port stocks <= 20
@@ -681,6 +706,7 @@ void policy_kernel(PolicyArgs A) {
                 }
             }
         }
+        X3STAMP(3);
         // the next tile's env loads (issued a tile ago) are waited for here, before this
         // tile's stores: stores count in vmcnt too, so a wait at the loop's back edge would
         // wait out the action / record stores' round trip as well
@@ -722,7 +748,9 @@ void policy_kernel(PolicyArgs A) {
             }
         }
         (void)dest;
+        X3STAMP(4);
     }
+    X3STAMP_ANY(11);
 }
 
 // ------------------------------------------------------------------ the split-bf16 f32 step
@@ -1060,42 +1088,7 @@ __device__ __forceinline__ void tile_argmax_part(const f32x16& c, uint32_t m, ui
 }
 
 constexpr int kPolicyX3Block = 512;
-#ifndef SHIPENV_X3_TRACE
-#define SHIPENV_X3_TRACE 0  // 1 = diagnostic build: per-wave s_memtime phase stamps of the fp32 policy
-#endif                      // kernels' 4th tile (se_policy_trace_read, tools/time_policy.py --trace)
-#if SHIPENV_X3_TRACE
-__device__ uint64_t g_ptrace[4096 * 16];
-#define X3STAMP(k)                                                                                          \
-    do {                                                                                                    \
-        if (tile_iter == 3 && (threadIdx.x & 63) == 0)                                                      \
-            g_ptrace[(blockIdx.x * kPolicyX3Waves + (threadIdx.x >> 6)) % 4096 * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
-#define X3STAMP_ANY(k)                                                                                      \
-    do {                                                                                                    \
-        if ((threadIdx.x & 63) == 0) {                                                                      \
-            uint64_t* p_ = g_ptrace + (blockIdx.x * kPolicyX3Waves + (threadIdx.x >> 6)) % 4096 * 16;       \
-            p_[(k)] = __builtin_amdgcn_s_memrealtime();                                                     \
-            p_[(k) + 3] = __builtin_amdgcn_s_memtime();                                                     \
-        }                                                                                                   \
-    } while (0)
-#else
-#define X3STAMP(k) \
-    do {           \
-    } while (0)
-#define X3STAMP_ANY(k) X3STAMP(k)
-#endif
-#ifndef SHIPENV_X3P
-#define SHIPENV_X3P 0  // round-6 A/B switch: 0 = policy_x3_kernel for every call (removed once measured)
-#endif
-#ifndef SHIPENV_X3_PRIO6
-#define SHIPENV_X3_PRIO6 1  // round-6 A/B switch (removed once measured)
-#endif
-#ifndef SHIPENV_X3_QUEUE
-#define SHIPENV_X3_QUEUE 1  // round-6 A/B switch (removed once measured)
-#endif
-#ifndef SHIPENV_X3P_LA
-#define SHIPENV_X3P_LA 2  // round-6 A/B switch (removed once measured)
-#endif
+
 constexpr int kPolicyX3Waves = kPolicyX3Block / 64;
 
 template <bool kW3Global, bool kQout = false>
@@ -1117,16 +1110,7 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
     };
     int64_t tile = (int64_t)blockIdx.x * kPolicyX3Waves + (threadIdx.x >> 6);
     EnvIn nxt = load_env(tile < tiles ? tile : 0);
-    // the wave's first tile is static (tile = its grid-wide wave index); the rest come from the
-    // tile queue (A.queue) or, without one, by striding over the grid
     const int64_t stride = (int64_t)gridDim.x * kPolicyX3Waves;
-    const bool queued = A.queue != nullptr;
-    TileQueue Q{};
-    uint32_t claim = 0u;
-    if (queued) {
-        Q = TileQueue::of(A, tiles, stride);
-        if (tile < tiles) claim = Q.issue();
-    }
     if constexpr (kW3Global) {  // fc3 stays in the packed global image: copy the rest
         const int staged = D.w3() / 16;
         for (int i = threadIdx.x; i < staged; i += kPolicyX3Block) smem[i] = A.qimg[i];
@@ -1163,20 +1147,16 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
     // the env state of the wave's next tile is loaded while this one computes (no HBM round
     // trip at the top of a tile), and its validity (the port on the ship's cell and that
     // port's stocks, two dependent L2 reads of the world image) resolved during fc3
-    if (SHIPENV_X3_PRIO6 && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
     EnvValid vnxt = env_valid(w, q, SAME, (int)nxt.x8, (int)nxt.y8, nxt.o8 == SE_NONE ? -1 : (int)nxt.o8);
     [[maybe_unused]] int tile_iter = 0;  // SHIPENV_X3_TRACE: the wave's 4th tile is stamped
     while (tile < tiles) {
         X3STAMP(0);
         const EnvIn in = nxt;
         const EnvValid v = vnxt;
-        // the wave's next tile: claimed a tile ago (the atomic's return has arrived), or strided
-        const int64_t tnext = queued ? Q.next(claim) : tile + stride;
-        const bool more = queued ? tnext < Q.hi : tnext < tiles;
-        if (more) {
-            nxt = load_env(tnext);
-            if (queued) claim = Q.issue();  // the tile after it
-        }
+        const int64_t tnext = tile + stride;
+        const bool more = tnext < tiles;
+        if (more) nxt = load_env(tnext);
         const int64_t e = tile * 32 + (lane & 31);
         const bool live = e < A.n;
         const double fuel = in.fuel;
@@ -1357,398 +1337,6 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
     X3STAMP_ANY(11);
 }
 
-// ------------------------------------------------------------------ the software-pipelined form
-// policy_x3_kernel without q_out, with a tile's VALU work beside MFMAs (round 6). Same Q rows
-// bit for bit (every accumulator sees the same MFMAs in the same order), same masks, first
-// maximum, draws and stores; only the placement of the work changes. In policy_x3_kernel a
-// tile ended in ~370 VALU with no MFMA beside them (the masked fc3 biases, the next tile's
-// validity, the last fc3 tile's argmax, the epsilon draw, the action decode and the stores),
-// and fc2's first k-tiles left most MFMA gaps empty. Here the MFMA stream of tile t is
-//   fc2 k-tiles 0..2 (a k-tile's 8 k-steps step-outer, row tile inner), each opened by the
-//     2 MFMAs of fc1's next row tile (fc1 is computed a row tile at a time, so only one f32
-//     fc1 tile is live),
-//   fc2 k-tile 3 (row tile outer), fc3 tile 0 (opened by the 2 MFMAs of fc1 row tile 0 of
-//     tile t + stride), fc3 tiles 1.. (the previous fc3 tile's argmax beside each),
-// and every other job sits beside it in a fixed group (3 MFMAs, half a k-step):
-//   k-tile 0: the argmax of the previous tile's last fc3 tile and that tile's finish (the two
-//     lane halves merged, its explore action, its action / record stores), fc1 row tile 1's
-//     split, this tile's Philox words;
-//   k-tile 1: fc1 row tile 2's split, the explore action (random.choice, branch-free);
-//   k-tile 2: fc1 row tile 3's split, the next tile's fc1 inputs;
-//   k-tile 3: fc3 tile 0's masked bias, fc2 row tiles 0-2's splits;
-//   fc3 tile 0: fc2 row tile 3's split, the next tile's validity, fc3 tile 1's masked bias;
-//   fc3 tile 1: fc3 tile 0's argmax, the next tile's fc1 row tile 0 split.
-// Stores go through buffer descriptors: a lane with nothing to store (the upper lane half, an
-// env past n, the first tile's empty predecessor) gets an offset past the buffer's end, which
-// the hardware drops, so the stream has no exec-mask branches. Needs n, rec_cap < 2^29.
-
-// f(std::integral_constant<int, I>) for I = B .. E - 1, unrolled at compile time (the
-// pipelined kernel's 80 MFMA groups: each group's job is chosen by `if constexpr`, so no
-// group carries the others' code into the unroller's size estimate)
-template <int B, int E, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (B < E) {
-        f(std::integral_constant<int, B>{});
-        static_for<B + 1, E>(f);
-    }
-}
-
-// Philox4x32-10 (philox10) a few rounds at a time, so its VALU can sit beside MFMAs
-struct PhiloxRun {
-    uint32_t c0, c1, c2, c3, k0, k1;
-    __device__ __forceinline__ void rounds(int n) {
-#pragma unroll
-        for (int r = 0; r < n; ++r) {
-            const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
-            const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-            const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
-            const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
-            c1 = (uint32_t)p1;
-            c3 = (uint32_t)p0;
-            c0 = n0;
-            c2 = n2;
-            k0 += 0x9E3779B9u;
-            k1 += 0xBB67AE85u;
-        }
-    }
-};
-
-// position of the k-th set bit (0-based) of b, for 0 <= k < popcount(b): a branch-free
-// binary search on popcounts (the explore path's `for (; k > 0; --k) b &= b - 1`)
-__device__ __forceinline__ int kth_bit64(uint64_t b, int k) {
-    const uint32_t lo = (uint32_t)b, hi = (uint32_t)(b >> 32);
-    int c = __popc(lo);
-    bool up = k >= c;
-    k -= up ? c : 0;
-    uint32_t x = up ? hi : lo;
-    int pos = up ? 32 : 0;
-#pragma unroll
-    for (int wd = 16; wd >= 1; wd >>= 1) {
-        const uint32_t m = (1u << wd) - 1u;
-        c = __popc(x & m);
-        up = k >= c;
-        k -= up ? c : 0;
-        x = up ? x >> wd : x & m;
-        pos += up ? wd : 0;
-    }
-    return pos;
-}
-
-template <bool kW3Global>
-__global__ __launch_bounds__(kPolicyX3Block) void policy_x3p_kernel(PolicyArgs A, QnetX3Dims D, PackX3Args PK) {
-    extern __shared__ uint4 smem[];
-    X3STAMP_ANY(9);
-    const QnetDims q = D.q;
-    const int lane = threadIdx.x & 63, h = lane >> 5;
-    const int64_t tiles = (A.n + 31) >> 5;
-    struct EnvIn {
-        double fuel;
-        uint32_t x8, y8, o8, d8;
-    };
-    auto load_env = [&](int64_t t) {
-        const int64_t ei = min(t * 32 + (lane & 31), A.n - 1);
-        return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei]};
-    };
-    int64_t tile = (int64_t)blockIdx.x * kPolicyX3Waves + (threadIdx.x >> 6);
-    EnvIn nxt = load_env(tile < tiles ? tile : 0);
-    if constexpr (kW3Global) {  // fc3 stays in the packed global image: copy the rest
-        const int staged = D.w3() / 16;
-        for (int i = threadIdx.x; i < staged; i += kPolicyX3Block) smem[i] = A.qimg[i];
-    } else {  // policy_x3_kernel's own split of the f32 weights into this workgroup's LDS
-        uint32_t* ptab = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(smem) + ((D.bytes() + 15) & ~15));
-        {
-            const LdsWorld wg = world_view(A.dims, A.world);
-            const int t = threadIdx.x, P0 = A.dims.P;
-            if (t < P0) ptab[t] = wg.pos[t];
-            else if (t >= 64 && t < 64 + 2 * P0) ptab[t] = reinterpret_cast<const uint32_t*>(wg.stock)[t - 64];
-        }
-        __syncthreads();
-        PackX3Args pk = PK;
-        pk.ptab = ptab;
-        pack_x3_items(pk, reinterpret_cast<uint8_t*>(smem), threadIdx.x, kPolicyX3Block);
-    }
-    __syncthreads();
-    X3STAMP_ANY(10);
-    if (tile >= tiles) return;  // wave-uniform, past the last barrier
-    const LdsWorld w = world_view(A.dims, A.world);  // port_at / stocks read in place (L2)
-    const uint8_t* qb = reinterpret_cast<const uint8_t*>(smem);
-    const bf16x8* W1b = reinterpret_cast<const bf16x8*>(qb + D.w1());
-    const bf16x8* W2 = reinterpret_cast<const bf16x8*>(qb + D.w2());
-    const bf16x8* W3 = reinterpret_cast<const bf16x8*>((kW3Global ? reinterpret_cast<const uint8_t*>(A.qimg) : qb) + D.w3());
-    const float* B1 = reinterpret_cast<const float*>(qb + D.b1());
-    const float* B2 = reinterpret_cast<const float*>(qb + D.b2());
-    const float* B3 = reinterpret_cast<const float*>(qb + D.b3());
-    const uint64_t* SAME = reinterpret_cast<const uint64_t*>(qb + D.same());
-    const int P = q.P;
-    const int64_t stride = (int64_t)gridDim.x * kPolicyX3Waves;
-    if (SHIPENV_X3_PRIO6 && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
-
-    // policy_x3_kernel's fc1 B operands from an env's packed (x, y, origin, dest) and f32 fuel
-    auto fc1_inputs = [&](uint32_t rec, float ff, bf16x8 (&xin)[2]) {
-        const uint32_t o8 = (rec >> 16) & 0xffu, d8 = rec >> 24;
-        const int origin = o8 == SE_NONE ? -1 : (int)o8, dest = d8 == SE_NONE ? -1 : (int)d8;
-        __bf16 f0, f1, f2;
-        split3(ff, f0, f1, f2);
-        const __bf16 fp[3] = {f0, f1, f2};
-        const __bf16 ex[6] = {(__bf16)(float)(rec & 0xffu), (__bf16)(float)((rec >> 8) & 0xffu), f0, f0, (__bf16)(float)origin,
-                              (__bf16)(float)dest};
-#pragma unroll
-        for (int st = 0; st < 2; ++st)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const Fc1Slot a = x3_fc1_slot(16 * st + j), b = x3_fc1_slot(16 * st + 8 + j);
-                const __bf16 va = a.col < 0 ? (__bf16)0.0f : (a.xp < 0 ? ex[a.col] : fp[a.xp]);
-                const __bf16 vb = b.col < 0 ? (__bf16)0.0f : (b.xp < 0 ? ex[b.col] : fp[b.xp]);
-                xin[st][j] = h ? vb : va;
-            }
-    };
-    auto fc1_mfma = [&](const bf16x8 (&xin)[2], int mt, f32x16 c) {  // c: the row tile's bias
-        c = mfma_bf16(W1b[(mt * 2 + 0) * 64 + lane], xin[0], c);
-        return mfma_bf16(W1b[(mt * 2 + 1) * 64 + lane], xin[1], c);
-    };
-    auto origin_of = [](uint32_t o8) { return o8 == SE_NONE ? -1 : (int)o8; };
-    auto pack_rec = [](const EnvIn& in) { return in.x8 | in.y8 << 8 | in.o8 << 16 | in.d8 << 24; };
-
-    // ---- the first tile's head (once per wave): its validity, fc1 inputs, fc1 row tile 0 split
-    // the current tile's env as the loop carries it: packed (x, y, origin, dest) and f32 fuel
-    uint32_t rec = pack_rec(nxt);
-    float ff = (float)nxt.fuel;
-    EnvValid v = env_valid(w, q, SAME, (int)nxt.x8, (int)nxt.y8, origin_of(nxt.o8));
-    bf16x8 X1[4][2][3];
-    {
-        bf16x8 xin[2];
-        fc1_inputs(rec, ff, xin);
-        relu_split3(fc1_mfma(xin, 0, bias_frag(B1 + 4 * h)), X1[0]);
-    }
-
-    // ---- the previous tile's pending epilogue (none before the first tile: its stores drop)
-    f32x16 cp;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) cp[r] = -INFINITY;
-    float bestp = -INFINITY;
-    int bidxp = 0x7fffffff, pbasep = 0, act_xp = -1;
-    uint32_t recp = 0;
-    float ffp = 0.0f;
-    int64_t tilep = 0;
-    bool havep = false;  // wave-uniform
-
-    // the argmax of the pending fc3 tile, part g (g = 3 finishes it: the tile base and the
-    // lane half's 4h added as policy_x3_kernel does)
-    float best0p = 0.0f;
-    int btp = 0;
-    auto pending_argmax = [&](int g) {
-        if (g == 0) best0p = bestp;
-        argmax_local_part(cp, bestp, btp, g);
-        if (g == 3) {
-            bidxp = bestp != best0p ? pbasep + btp : bidxp;
-            bidxp += bidxp == 0x7fffffff ? 0 : 4 * h;
-        }
-    };
-    // the pending tile's finish: lane halves merged (larger value, then lower index), greedy
-    // or explore action, and the action / record stores (finish_env's semantics)
-    auto pending_finish = [&]() {
-        const float ob2 = __shfl_xor(bestp, 32);
-        const int oi = __shfl_xor(bidxp, 32);
-        const bool take = ob2 > bestp || (ob2 == bestp && oi < bidxp);
-        const int bidx = take ? oi : bidxp;
-        const int greedy = bidx == 0x7fffffff ? 0 : q.action_of_row(bidx);
-        const int act = act_xp >= 0 ? act_xp : greedy;
-        const int64_t e = tilep * 32 + (lane & 31);
-        if (havep && h == 0 && e < A.n) {
-            A.actions[e] = act;
-            if (A.rec_pos) {  // replay_begin_kernel's record, from the state already in registers
-                int64_t slot = A.rec_head + e;
-                slot -= slot >= A.rec_cap ? A.rec_cap : 0;
-                A.rec_pos[slot] = recp;
-                A.rec_fuel[slot] = ffp;
-                A.rec_act[slot] = act;
-            }
-        }
-    };
-
-    constexpr int kLa = SHIPENV_X3P_LA;  // fragments read kLa k-steps ahead
-    [[maybe_unused]] int tile_iter = 0;  // SHIPENV_X3_TRACE: the wave's 4th tile is stamped
-    for (;;) {
-        X3STAMP(0);
-        const bool more = tile + stride < tiles;
-        if (more) nxt = load_env(tile + stride);
-        const int64_t e = tile * 32 + (lane & 31);
-        bf16x8 xin[2];  // this tile's fc1 inputs (row tiles 1..3 open k-tiles 0..2)
-        fc1_inputs(rec, ff, xin);
-        f32x16 acc[4];
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) acc[mt] = bias_frag(B2 + mt * 32 + 4 * h);
-        bf16x8 X2[4][2][3];
-        f32x16 c1n, c, c3, c1x;
-        bf16x8 xinx[2];  // the next tile's fc1 inputs
-        PhiloxRun ph;
-        int act_x = -1;
-        int ncode = 0;
-        int2 nstock = make_int2(0, 0);
-        EnvValid vnxt;
-        uint32_t m3 = 0;
-        // unit j (one k-step, 6 MFMAs): fc2 k-tiles 0..2 step-outer (j = 8 kt + 4 s + mt), k-tile
-        // 3 row-tile-outer (j = 24 + 2 mt + s), then fc3 tile 0's k-steps (j = 32 + k)
-        auto frag_of = [&](int j, bf16x8 (&dst)[3]) {
-            if (j < 24) x3_frags(W2, (((j & 3) * 4 + (j >> 3)) * 2 + ((j >> 2) & 1)), lane, dst);
-            else if (j < 32) x3_frags(W2, ((((j - 24) >> 1) * 4 + 3) * 2 + ((j - 24) & 1)), lane, dst);
-            else x3_frags(W3, j - 32, lane, dst);
-        };
-        // the job beside group g (half `g & 1` of unit g >> 1); constant-folded per group
-        auto job = [&](auto gc) {
-            constexpr int g = decltype(gc)::value;
-            // ---- k-tile 0: the previous tile's epilogue, fc1 row tile 1, this tile's draws
-            if constexpr (g == 0) c1n = bias_frag(B1 + 32 + 4 * h);
-            if constexpr (g < 4) pending_argmax(g);
-            if constexpr (g == 4) pending_finish();
-            if constexpr (g == 10) {
-                ph = PhiloxRun{(uint32_t)(uint64_t)(A.env_base + e), (uint32_t)((uint64_t)(A.env_base + e) >> 32),
-                               A.t, kSlotPolicy, (uint32_t)A.seed, (uint32_t)(A.seed >> 32)};
-                // the key opaque (philox10): its 20 round keys are added here, not hoisted out of the
-                // tile loop into 20 live SGPRs
-                asm volatile("" : "+s"(ph.k0), "+s"(ph.k1));
-            }
-            if constexpr (g >= 10 && g < 15) ph.rounds(2);
-            // ---- fc1 row tiles 1..3 split beside k-tiles 0..2 (their MFMAs open groups 1, 17, 33)
-            if constexpr (g >= 4 && g < 12) split_pair(c1n, X1[1], g - 4);
-            if constexpr (g == 16) c1n = bias_frag(B1 + 64 + 4 * h);
-            if constexpr (g >= 20 && g < 28) split_pair(c1n, X1[2], g - 20);
-            if constexpr (g == 32) c1n = bias_frag(B1 + 96 + 4 * h);
-            if constexpr (g >= 36 && g < 44) split_pair(c1n, X1[3], g - 36);
-            // ---- k-tile 1: the explore action (random.choice over the valid actions, :192)
-            if constexpr (g == 28) {
-                const bool explore = A.eps > 0.0 && u32(ph.c0) <= A.eps;  // np.random.rand() <= epsilon (:191)
-                const int nsel = __popcll(v.sel);
-                const int k = uniform_int(ph.c1, (uint32_t)(4 + nsel + v.cst + v.fst));
-                const int k2 = k - 4, k3 = k2 - nsel;
-                const int a_sel = 4 + kth_bit64(v.sel, k2 < 0 ? 0 : k2);
-                const int a_take = k3 < v.cst ? 5 + P + k3 : 55 + P + (k3 - v.cst);
-                act_x = !explore ? -1 : (k < 4 ? k : (k2 < nsel ? a_sel : a_take));
-            }
-            // ---- the next tile's world reads and fc1 inputs
-            if constexpr (g == 24) ncode = w.code((int)nxt.x8, (int)nxt.y8);
-            if constexpr (g == 40) {
-                asm volatile("" : "+v"(ncode));
-                nstock = w.stock[max(w.port_of_code(ncode), 0)];
-            }
-            // ---- k-tile 3: fc3 tile 0's masked bias, fc2 row tiles' splits
-            if constexpr (g == 48) m3 = tile_mask(v, 0, P) >> (4 * h);
-            if constexpr (g == 49) c = masked_bias(B3 + 4 * h, m3);
-            if constexpr (g >= 53 && g < 61) split_pair(acc[0], X2[0], g - 53);
-            if constexpr (g >= 57 && g < 65) split_pair(acc[1], X2[1], g - 57);
-            if constexpr (g >= 61 && g < 69) split_pair(acc[2], X2[2], g - 61);
-            if constexpr (g >= 65 && g < 73) split_pair(acc[3], X2[3], g - 65);
-            // ---- fc3 tile 0: the next tile's validity and fc1 row tile 0, fc3 tile 1's bias
-            if constexpr (g == 73) {
-                asm volatile("" ::"v"(nstock.x), "v"(nstock.y));
-                vnxt = env_valid_from(w, q, SAME, ncode, nstock, origin_of(nxt.o8));
-            }
-            if constexpr (g == 75) fc1_inputs(pack_rec(nxt), (float)nxt.fuel, xinx);
-        };
-
-        bf16x8 wf[kLa + 1][3];
-#pragma unroll
-        for (int j = 0; j < kLa; ++j) frag_of(j, wf[j]);
-        static_for<0, 80>([&](auto gc) {
-            constexpr int g = decltype(gc)::value, j = g >> 1, half = g & 1;
-            if constexpr (half == 0 && j + kLa < 40) frag_of(j + kLa, wf[(j + kLa) % (kLa + 1)]);
-            if constexpr (j < 24) {
-                constexpr int kt = j >> 3, s = (j >> 2) & 1, mt = j & 3;
-                acc[mt] = khalf_x3(wf[j % (kLa + 1)], X1[kt][s], acc[mt], half);
-            } else if constexpr (j < 32) {
-                constexpr int mt = (j - 24) >> 1, s = (j - 24) & 1;
-                acc[mt] = khalf_x3(wf[j % (kLa + 1)], X1[3][s], acc[mt], half);
-            } else {
-                constexpr int k = j - 32;
-                c = khalf_x3(wf[j % (kLa + 1)], X2[k >> 1][k & 1], c, half);
-            }
-            if constexpr (g == 8) X3STAMP(1);
-            if constexpr (g == 16) X3STAMP(2);
-            if constexpr (g == 32) X3STAMP(3);
-            if constexpr (g == 48) X3STAMP(4);
-            if constexpr (g == 64) X3STAMP(5);
-            if constexpr (g == 1) c1n = fc1_mfma(xin, 1, c1n);
-            if constexpr (g == 17) c1n = fc1_mfma(xin, 2, c1n);
-            if constexpr (g == 33) c1n = fc1_mfma(xin, 3, c1n);
-            job(gc);
-            __builtin_amdgcn_sched_barrier(0);
-        });
-
-        // ---- fc3 tiles 1.. (a tile no env of the wave can choose from is skipped, MFMAs
-        // included): the previous fc3 tile's argmax beside each; tile 1 also carries the next
-        // tile's fc1 row tile 0 split
-        X3STAMP(6);
-        float best = -INFINITY, best0 = -INFINITY;
-        int bidx = 0x7fffffff, bt = 0, pbase = 0;
-        bf16x8 X1x[2][3];
-        auto fc3_tile = [&](int mt, bool with_split) {
-            const bf16x8* W3t = W3 + mt * 8 * 192;
-            c3 = masked_bias(B3 + mt * 32 + 4 * h, tile_mask(v, mt, P) >> (4 * h));
-            if (with_split) c1x = bias_frag(B1 + 4 * h);
-#pragma unroll
-            for (int j = 0; j < kLa; ++j) x3_frags(W3t, j, lane, wf[j]);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                if (k + kLa < 8) x3_frags(W3t, k + kLa, lane, wf[(k + kLa) % (kLa + 1)]);
-#pragma unroll
-                for (int half = 0; half < 2; ++half) {
-                    c3 = khalf_x3(wf[k % (kLa + 1)], X2[k >> 1][k & 1], c3, half);
-                    const int g = 2 * k + half;
-                    if (with_split && g == 0) c1x = fc1_mfma(xinx, 0, c1x);
-                    if (g < 4) {
-                        if (g == 0) best0 = best;
-                        argmax_local_part(c, best, bt, g);
-                        if (g == 3) bidx = best != best0 ? pbase + bt : bidx;
-                    }
-                    if (with_split && g >= 4 && g < 12) split_pair(c1x, X1x, g - 4);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            c = c3;
-            pbase = mt * 32;
-        };
-        if (q.mt3 > 1 && __any(tile_maybe(v, 1, P))) {
-            fc3_tile(1, true);
-        } else {
-            relu_split3(fc1_mfma(xinx, 0, bias_frag(B1 + 4 * h)), X1x);
-        }
-#pragma nounroll
-        for (int mt = 2; mt < q.mt3; ++mt) {
-            if (!__any(tile_maybe(v, mt, P))) continue;
-            fc3_tile(mt, false);
-        }
-
-        X3STAMP(7);
-        // ---- hand over: this tile's last fc3 accumulator becomes the pending epilogue
-        cp = c;
-        bestp = best;
-        bidxp = bidx;
-        pbasep = pbase;
-        act_xp = act_x;
-        recp = rec;
-        ffp = ff;
-        tilep = tile;
-        havep = true;
-        X3STAMP(8);
-        ++tile_iter;
-        if (!more) break;
-        tile += stride;
-        rec = pack_rec(nxt);
-        ff = (float)nxt.fuel;
-        v = vnxt;
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int p = 0; p < 3; ++p) X1[0][s][p] = X1x[s][p];
-    }
-    // the last tile's epilogue
-#pragma unroll
-    for (int g = 0; g < 4; ++g) pending_argmax(g);
-    pending_finish();
-    X3STAMP_ANY(11);
-}
-
 }  // namespace
 
 struct se_qnet {
@@ -1763,8 +1351,6 @@ struct se_qnet {
     bool packed = false;
     uint8_t* d_img32 = nullptr;  // se_policy_f32's split image (the full layout's fc3, global)
     int img32_bytes = 0;
-    uint32_t* d_queue = nullptr;  // se_policy_f32's tile queue heads: 2 parities x kTileShards lines
-    uint32_t launches = 0;
 };
 
 extern "C" {
@@ -1911,9 +1497,6 @@ int launch_policy_x3(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, 
     int rc = allow_dynamic_lds(lds_set0, reinterpret_cast<const void*>(policy_x3_kernel<false>), 160 * 1024, env->device);
     if (!rc) rc = allow_dynamic_lds(lds_set1, reinterpret_cast<const void*>(policy_x3_kernel<true>), 160 * 1024, env->device);
     if (!rc) rc = allow_dynamic_lds(lds_set2, reinterpret_cast<const void*>(policy_x3_kernel<true, true>), 160 * 1024, env->device);
-    static std::atomic<uint64_t> lds_set3{0}, lds_set4{0};
-    if (!rc) rc = allow_dynamic_lds(lds_set3, reinterpret_cast<const void*>(policy_x3p_kernel<false>), 160 * 1024, env->device);
-    if (!rc) rc = allow_dynamic_lds(lds_set4, reinterpret_cast<const void*>(policy_x3p_kernel<true>), 160 * 1024, env->device);
     if (rc) return rc;
     int dev_cus = 256;
     if (hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, env->device) != hipSuccess)
@@ -1942,25 +1525,9 @@ int launch_policy_x3(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, 
         A.rec_head = rec->head;
         A.rec_cap = rec->cap;
     }
-    // the pipelined form's buffer stores take 32-bit byte offsets
-    const bool pipelined = SHIPENV_X3P && env->n < ((int64_t)1 << 29) && (!rec || rec->cap < ((int64_t)1 << 29));
-    if (SHIPENV_X3_QUEUE) {  // the tile queue (TileQueue): this launch's heads are zero
-        if (!qn->d_queue) {
-            const size_t qb = 2 * kTileShards * kQueueStride * sizeof(uint32_t);
-            HIP_TRY(hipMalloc(&qn->d_queue, qb));
-            HIP_TRY(hipMemsetAsync(qn->d_queue, 0, qb, s));
-        }
-        const uint32_t par = qn->launches++ & 1u;
-        A.queue = qn->d_queue + par * kTileShards * kQueueStride;
-        A.queue_next = qn->d_queue + (par ^ 1u) * kTileShards * kQueueStride;
-    }
     if (q_out) {  // the full layout (fc3 from global memory): unmasked Q rows for q_out
         if (!w3_global) return fail(SE_EINVAL, "q_out: the full fc3 layout is expected in global memory");
         policy_x3_kernel<true, true><<<grid, kPolicyX3Block, lds, s>>>(A, d, pk);
-    } else if (pipelined && w3_global) {
-        policy_x3p_kernel<true><<<grid, kPolicyX3Block, lds, s>>>(A, d, pk);
-    } else if (pipelined) {
-        policy_x3p_kernel<false><<<grid, kPolicyX3Block, lds, s>>>(A, d, pk);
     } else if (w3_global) {
         policy_x3_kernel<true><<<grid, kPolicyX3Block, lds, s>>>(A, d, pk);
     } else {
@@ -2024,12 +1591,11 @@ int se_qnet_repack(se_qnet* qn, int32_t* bump, void* stream) {
 
 int se_qnet_destroy(se_qnet* qn) {
     if (!qn) return SE_OK;
-    if (qn->d_img || qn->d_img32 || qn->d_queue) {  // does not touch the env, which may be gone already
+    if (qn->d_img || qn->d_img32) {  // does not touch the env, which may be gone already
         DeviceGuard g(qn->device);
         (void)hipDeviceSynchronize();
         if (qn->d_img) (void)hipFree(qn->d_img);
         if (qn->d_img32) (void)hipFree(qn->d_img32);
-        if (qn->d_queue) (void)hipFree(qn->d_queue);
     }
     delete qn;
     return SE_OK;

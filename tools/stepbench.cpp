@@ -1,7 +1,12 @@
 // stepbench.cpp — K back-to-back se_step calls driven from C++ (tuning tool): the
 // step rate without the Python host path, for one or more library builds.
 //   hipcc -O2 -std=c++17 -o tools/stepbench tools/stepbench.cpp -ldl
-//   tools/stepbench [--n N] [--config 3|4|5|6] [--steps K] [--rows R] lib.so [lib2.so ...]
+//   tools/stepbench [--n N] [--config 3|4|5|6] [--steps K] [--rows R] [--floor R] lib.so [lib2.so ...]
+// (--floor R: R alternating rounds of the product's K launches and K launches of streamfloor, a
+// bare kernel on the same buffers and action rows with the step kernel's grid (one group of 4
+// envs per thread, 256-thread workgroups) that moves exactly the step's bytes per env: 42 B, 50 B
+// with auto-reset (ep_return read and written), plain loads, nontemporal stores; VERDICT r05
+// item 6: how far config 4 sits from its streams alone)
 // (config 5: 64 ports without auto-reset; 6: the 5 ports with auto-reset)
 // (--rows R: step t reads action row t % R, so R small keeps the actions cache-resident)
 // Config 3: the bundled map, the reference's 5 default ports; config 4: 64 ports on
@@ -57,12 +62,63 @@ static void* dev(size_t bytes) {
     return p;
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <typename T>
+__device__ __forceinline__ void nt_store(T* p, T v) {
+    if constexpr (sizeof(T) == 16)
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), reinterpret_cast<u32x4*>(p));
+    else
+        __builtin_nontemporal_store(v, p);
+}
+// group g = 4 consecutive envs: x / y / origin / dest / done / err as one u32 each, cargo,
+// action, reward and ep_return as one 16-byte lane access, fuel as two
+template <bool kAuto>
+__global__ __launch_bounds__(256) void streamfloor(se_state st, const int32_t* act, int64_t groups) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= groups) return;
+    uint32_t* x = reinterpret_cast<uint32_t*>(st.x);
+    uint32_t* y = reinterpret_cast<uint32_t*>(st.y);
+    uint32_t* o = reinterpret_cast<uint32_t*>(st.origin);
+    uint32_t* d = reinterpret_cast<uint32_t*>(st.dest);
+    int4* c = reinterpret_cast<int4*>(st.cargo);
+    double2* f = reinterpret_cast<double2*>(st.fuel);
+    const int4 a = reinterpret_cast<const int4*>(act)[g];
+    uint32_t vx = x[g], vy = y[g], vo = o[g], vd = d[g];
+    int4 vc = c[g];
+    double2 f0 = f[2 * g], f1 = f[2 * g + 1];
+    float4 er = kAuto ? reinterpret_cast<float4*>(st.ep_return)[g] : make_float4(0.f, 0.f, 0.f, 0.f);
+    vx ^= (uint32_t)a.x & 0x01010101u;
+    vy ^= (uint32_t)a.y & 0x01010101u;
+    vc.x += a.z;
+    f0.x -= 1.0;
+    f1.y -= 1.0;
+    const float4 r = make_float4((float)a.x, (float)a.y, (float)a.z, (float)a.w);
+    nt_store(&x[g], vx);
+    nt_store(&y[g], vy);
+    nt_store(&o[g], vo);
+    nt_store(&d[g], vd);
+    nt_store(&c[g], vc);
+    nt_store(&f[2 * g], f0);
+    nt_store(&f[2 * g + 1], f1);
+    nt_store(&reinterpret_cast<float4*>(st.reward)[g], r);
+    nt_store(&reinterpret_cast<uint32_t*>(st.done)[g], (uint32_t)a.w & 0x01010101u);
+    nt_store(&reinterpret_cast<uint32_t*>(st.err)[g], 0u);
+    if (kAuto) {
+        er.x += r.x;
+        er.y += r.y;
+        er.z += r.z;
+        er.w += r.w;
+        nt_store(&reinterpret_cast<float4*>(st.ep_return)[g], er);
+    }
+}
+
 int main(int argc, char** argv) {
     int64_t n = 1 << 20;
     int config = 3, steps = 1000, rows = 0, warm = 20;  // rows > 0: cycle through that many action rows
     int preroll = 0;  // untimed steps from reset before the warm-up (the bench's steady state), one row each
     bool gen_late = false;  // generate the timed rows after the warm-up steps (right before timing)
     bool per_launch = false;  // also print every timed launch's own event-pair duration
+    int floor_rounds = 0;  // > 0: alternate the product's timed loop with streamfloor's
     std::vector<std::string> libs;
     for (int i = 1; i < argc; ++i) {
         if (!strcmp(argv[i], "--n")) n = atoll(argv[++i]);
@@ -73,6 +129,7 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--gen-late")) gen_late = true;
         else if (!strcmp(argv[i], "--preroll")) preroll = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--per-launch")) per_launch = true;
+        else if (!strcmp(argv[i], "--floor")) floor_rounds = atoi(argv[++i]);
         else libs.push_back(argv[i]);
     }
     FILE* f = fopen("shippingenv_amd/data/mapa_mundi_binario.jpg", "rb");
@@ -201,6 +258,29 @@ int main(int argc, char** argv) {
         float ms = 0.f;
         CK(hipEventElapsedTime(&ms, e0, e1));
         const char* base = strrchr(path.c_str(), '/');
+        for (int round = 0; round < floor_rounds; ++round) {  // product, then floor, alternating
+            float mp = 0.f, mf = 0.f;
+            CK(hipEventRecord(e0, s));
+            for (int t = 0; t < steps; ++t) SE(a.step(env, acts + (size_t)(warm + t % r) * n, s));
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            CK(hipEventElapsedTime(&mp, e0, e1));
+            const int64_t groups = n / 4;
+            const unsigned grid = (unsigned)((groups + 255) / 256);
+            CK(hipEventRecord(e0, s));
+            for (int t = 0; t < steps; ++t) {
+                if (aut) streamfloor<true><<<grid, 256, 0, s>>>(st, acts + (size_t)(warm + t % r) * n, groups);
+                else streamfloor<false><<<grid, 256, 0, s>>>(st, acts + (size_t)(warm + t % r) * n, groups);
+            }
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            CK(hipEventElapsedTime(&mf, e0, e1));
+            printf("{\"lib\": \"%s\", \"n\": %lld, \"config\": %d, \"round\": %d, \"us_per_step\": %.3f, "
+                   "\"floor_us_per_launch\": %.3f, \"floor_bytes_per_env\": %d}\n",
+                   base ? base + 1 : path.c_str(), (long long)n, config, round, 1000.0 * mp / steps,
+                   1000.0 * mf / steps, aut ? 50 : 42);
+            fflush(stdout);
+        }
         printf("{\"lib\": \"%s\", \"n\": %lld, \"config\": %d, \"steps\": %d, \"action_rows\": %d, "
                "\"warm\": %d, \"preroll\": %d, \"gen_late\": %d, \"step_blocks\": \"%s\", \"us_per_step\": %.3f}\n",
                base ? base + 1 : path.c_str(), (long long)n, config, steps, r, warm, preroll, (int)gen_late,

@@ -66,11 +66,12 @@ def main():
         N.lib().se_policy_trace_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
         assert N.lib().se_policy_trace_read(buf.ctypes.data, buf.nbytes) == 0
         st = buf.reshape(4096, 16).astype(np.int64)
-        ok = (st[:, 0] > 0) & (st[:, 8] > st[:, 0])
-        d = np.diff(st[ok][:, :9], axis=1)
+        last = max(k for k in range(9) if (st[:, k] > 0).any())  # the kernel's last phase stamp
+        ok = (st[:, 0] > 0) & (st[:, last] > st[:, 0])
+        d = np.diff(st[ok][:, :last + 1], axis=1)
         rec["trace_waves"] = int(ok.sum())
         rec["phase_cycles_median"] = [int(x) for x in np.median(d, axis=0)]
-        rec["tile_cycles_median"] = int(np.median(st[ok][:, 8] - st[ok][:, 0]))
+        rec["tile_cycles_median"] = int(np.median(st[ok][:, last] - st[ok][:, 0]))
         live = st[:, 9] > 0  # stamps 9-11: s_memrealtime (100 MHz, chip-wide) at start, image staged, end
         s9, s10, s11 = st[live, 9], st[live, 10], st[live, 11]
         t0 = s9.min()
@@ -81,9 +82,11 @@ def main():
         rec["us_end_max"] = float((s11 - t0).max()) / 100
         # stamps 12-14: s_memtime (shader clock) beside 9-11: the wave's mean clock
         rec["ghz_wave_median"] = float(np.median((st[live, 14] - st[live, 12]) / (s11 - s9) / 10))
-        wid = np.nonzero(live)[0] % 8
-        rec["us_wave_median_by_half"] = [float(np.median((s11 - s9)[wid < 4])) / 100,
-                                         float(np.median((s11 - s9)[wid >= 4])) / 100]
+        wpb = 8 if a.precision == "f32" else 16  # waves per workgroup; the last quarter / half at issue priority 1
+        wid = np.nonzero(live)[0] % wpb
+        hi = wid >= (4 if wpb == 8 else 12)
+        rec["us_wave_median_by_prio"] = [float(np.median((s11 - s9)[~hi])) / 100,
+                                         float(np.median((s11 - s9)[hi])) / 100]
     print(json.dumps(rec))
 
 
