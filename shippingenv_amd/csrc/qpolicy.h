@@ -209,7 +209,77 @@ struct PolicyArgs {
     float* rec_fuel;
     int32_t* rec_act;
     int64_t rec_head, rec_cap;
+    // the order the envs are visited in (policy_order_kernel): position p of the launch is
+    // env order[p]; null: position p is env p
+    const uint32_t* order;
 };
+
+// ------------------------------------------------------------------ visiting order
+// Only a ship on a port's cell can take anything but the 4 moves (is_valid_action,
+// agents/dqn.py:125-175): its valid rows reach fc3's second 32-row tile (the TAKE_FUEL
+// amounts), while a ship at sea needs rows 0-3 of tile 0. The policy kernels skip a
+// tile no env of the wave can use, but with ~1 ship in 5 in port hardly a 32-env tile
+// is all at sea (0.8^32). So the policy visits the envs in an order where they are:
+// each 1024-env chunk lists its ships at sea first, then those in port, each group in
+// ascending env order, and ~3 in 4 of the waves' tiles skip fc3's second tile. The
+// order changes only which lane computes which env: every output is keyed by the env
+// (actions, Philox draws, replay slots), so results are identical to position order.
+// A wave strides over the tiles (tile w + k * stride), and with a stride a multiple of 32 it
+// would meet every chunk at the same tile index, so the waves at the chunks' ends would get
+// every in-port tile (bf16 policy at 2^20: +5 us, the odd XCDs' SIMDs 10 us behind). So with
+// a visiting order, wave tile t is the order's tile (t mod c) * 32 + t / c over the c full
+// chunks (a transpose): a wave's tiles spread over the chunks' tile indices, and each meets
+// its share of in-port tiles. A relabelling of which wave computes which tile only.
+__device__ __forceinline__ int64_t order_tile(int64_t t, int64_t tiles) {
+    const uint32_t c = (uint32_t)(tiles >> 5), tt = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)t);
+    return tt < 32u * c ? (int64_t)((tt % c) * 32u + tt / c) : t;
+}
+constexpr int kOrderBlock = 256;
+constexpr int kOrderChunk = 4 * kOrderBlock;  // envs per workgroup: 4 consecutive per thread
+__global__ __launch_bounds__(kOrderBlock) void policy_order_kernel(const uint32_t* world, WorldDims dims,
+                                                                    const uint8_t* xs, const uint8_t* ys,
+                                                                    int64_t n, uint32_t* order) {
+    __shared__ uint32_t wsum[kOrderBlock / 64];
+    const LdsWorld w = world_view(dims, world);  // the cell codes, read in place (L2)
+    const int64_t base = (int64_t)blockIdx.x * kOrderChunk;
+    const int64_t e0 = base + 4 * (int64_t)threadIdx.x;
+    uint32_t live = 0u, port = 0u;  // bit j: env e0 + j exists / is on a port's cell
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (e0 + j < n) {
+            live |= 1u << j;
+            port |= (w.port_at(xs[e0 + j], ys[e0 + j]) >= 0 ? 1u : 0u) << j;
+        }
+    }
+    // exclusive prefix of (at sea, in port) counts over the chunk, packed as two 16-bit halves
+    const uint32_t mine = (uint32_t)__popc(live & ~port) | (uint32_t)__popc(port) << 16;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t inc = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_up(inc, d);
+        inc += lane >= d ? u : 0u;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t off = 0u, total = 0u;
+#pragma unroll
+    for (int i = 0; i < kOrderBlock / 64; ++i) {
+        off += i < wv ? wsum[i] : 0u;
+        total += wsum[i];
+    }
+    const uint32_t ex = inc - mine + off;
+    int64_t sea = base + (ex & 0xffffu), inport = base + (total & 0xffffu) + (ex >> 16);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if ((live >> j) & 1u) {
+            const bool p = (port >> j) & 1u;
+            order[p ? inport : sea] = (uint32_t)(e0 + j);
+            inport += p ? 1 : 0;
+            sea += p ? 0 : 1;
+        }
+    }
+}
 
 // v = p0 + p1 + p2, each the bf16 rounding of the remainder (exact f32 subtractions)
 __device__ __forceinline__ void split3(float v, __bf16& p0, __bf16& p1, __bf16& p2) {
@@ -311,8 +381,8 @@ __device__ __forceinline__ EnvValid env_valid_from(const LdsWorld& w, const Qnet
 // is skipped, MFMAs included)
 __device__ __forceinline__ bool tile_maybe(const EnvValid& v, int mt, int P) {
     const int base = mt * 32, top = base + 31;
-    return (mt == 0) | ((v.cur >= 0) & (base < 4 + P)) | ((v.cst > 0) & (v.c_lo <= top) & (v.c_hi() >= base)) |
-           ((v.fst > 0) & (v.f_lo <= top) & (v.f_hi() >= base));
+    return (int)(mt == 0) | (int)((v.cur >= 0) & (base < 4 + P)) |
+           (int)((v.cst > 0) & (v.c_lo <= top) & (v.c_hi() >= base)) | (int)((v.fst > 0) & (v.f_lo <= top) & (v.f_hi() >= base));
 }
 
 // valid rows of tile mt as bits of the tile
@@ -432,9 +502,6 @@ __device__ __forceinline__ void finish_env(const QnetDims& q, const EnvValid& v,
     }
 }
 
-#ifndef SHIPENV_POLICY_FC3X
-#define SHIPENV_POLICY_FC3X 1  // round-6 A/B switch (removed once measured)
-#endif
 #ifndef SHIPENV_X3_TRACE
 #define SHIPENV_X3_TRACE 0  // 1 = diagnostic build: per-wave s_memtime phase stamps of the fp32 policy
 #endif                      // kernels' 4th tile (se_policy_trace_read, tools/time_policy.py --trace)
@@ -473,11 +540,13 @@ void policy_kernel(PolicyArgs A) {
     struct EnvIn {
         double fuel;
         uint32_t x, y, o8, d8;
+        int64_t e;  // the env (A.order), past A.n for the last tile's idle lanes
     };
     auto load_env = [&](int64_t tile) {
-        const int64_t e = tile * 32 + r;
-        const int64_t ei = e < A.n ? e : A.n - 1;
-        return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei]};
+        const int64_t p = (A.order ? order_tile(tile, tiles) : tile) * 32 + r;
+        const int64_t pi = p < A.n ? p : A.n - 1;
+        const int64_t ei = A.order ? (int64_t)A.order[pi] : pi;
+        return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei], p < A.n ? ei : A.n};
     };
     int64_t tile = (int64_t)blockIdx.x * kPolicyWaves + (threadIdx.x >> 6);
     if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 12) __builtin_amdgcn_s_setprio(1);
@@ -522,7 +591,7 @@ void policy_kernel(PolicyArgs A) {
         X3STAMP(0);
         const EnvIn cur_in = nxt;
         if (tile + stride < tiles) nxt = load_env(tile + stride);
-        const int64_t e = tile * 32 + r;
+        const int64_t e = cur_in.e;
         const bool live = e < A.n;
         const int x = (int)cur_in.x, y = (int)cur_in.y;
         const int origin = cur_in.o8 == SE_NONE ? -1 : (int)cur_in.o8;
@@ -613,7 +682,7 @@ void policy_kernel(PolicyArgs A) {
         }
         float best = -INFINITY;
         int bidx = 0x7fffffff;
-        if (SHIPENV_POLICY_FC3X && use64) {
+        if (use64) {
             // compact layouts of at most 64 rows (the bench's greedy and epsilon calls): rows
             // this env cannot take start at -inf (masked_bias, two VALU per register), so the
             // first maximum is a compare and two selects per register with no validity test and
@@ -622,14 +691,21 @@ void policy_kernel(PolicyArgs A) {
             bf16x8 wf[L3 + 1];
 #pragma unroll
             for (int k = 0; k < L3; ++k) wf[k] = W3f[k * 64 + lane];
-            f32x16 c = masked_bias(B3 + 4 * h, (uint32_t)v64 >> (4 * h));
+            // a tile of ships at sea only (uniform; the visiting order makes them ~3 in 4):
+            // rows 0-3, the moves, are each env's valid rows, registers 0-3 of lane half 0
+            const bool sea = !__any(cur >= 0);
+            f32x16 c = sea ? bias_frag(B3 + 4 * h) : masked_bias(B3 + 4 * h, (uint32_t)v64 >> (4 * h));
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 if (k + L3 < 8) wf[(k + L3) % (L3 + 1)] = W3f[(k + L3) * 64 + lane];
                 c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k % (L3 + 1)], h2[k >> 1][k & 1], c, 0, 0, 0);
             }
             int bt = 0, pbase = 0;
-            if (q.mt3 > 1 && __any((uint32_t)(v64 >> 32) != 0u)) {  // fc3 tile 1 (uniform)
+            if (sea) {
+                argmax_local_part(c, best, bt, 0);
+                best = h ? -INFINITY : best;  // lane half 1 holds rows 4-7
+                bidx = best != -INFINITY ? bt : bidx;
+            } else if (q.mt3 > 1 && __any((uint32_t)(v64 >> 32) != 0u)) {  // fc3 tile 1 (uniform)
 #pragma unroll
                 for (int k = 0; k < L3; ++k) wf[k] = W3f[(8 + k) * 64 + lane];
                 f32x16 c1 = masked_bias(B3 + 32 + 4 * h, (uint32_t)(v64 >> 32) >> (4 * h));
@@ -645,33 +721,28 @@ void policy_kernel(PolicyArgs A) {
                 c = c1;
                 pbase = 32;
             }
-            const float best0 = best;
+            if (!sea) {
+                const float best0 = best;
 #pragma unroll
-            for (int g = 0; g < 4; ++g) argmax_local_part(c, best, bt, g);
-            bidx = best != best0 ? pbase + bt : bidx;
-            bidx += bidx == 0x7fffffff ? 0 : 4 * h;  // the lane half's rows (argmax_local_part omits 4h)
+                for (int g = 0; g < 4; ++g) argmax_local_part(c, best, bt, g);
+                bidx = best != best0 ? pbase + bt : bidx;
+                bidx += bidx == 0x7fffffff ? 0 : 4 * h;  // the lane half's rows (argmax_local_part omits 4h)
+            }
         }
-        for (int mt = 0; mt < ((SHIPENV_POLICY_FC3X && use64) ? 0 : q.mt3); ++mt) {  // fc3 + the masked first-maximum argmax
+        for (int mt = 0; mt < (use64 ? 0 : q.mt3); ++mt) {  // fc3 + the masked first-maximum argmax (other layouts)
             const int base = mt * 32, top = base + 31;
             // a tile no env of the wave can choose from is skipped, MFMAs included
             // (exact: its rows are invalid for all 32 envs); with port stocks <= 20
             // (add_port's randint(5, 20)) the valid rows sit in the first few tiles
-            uint32_t m;
-            if (use64) {
-                m = (uint32_t)(v64 >> (base & 63));
-                if (!__any(m != 0u)) continue;
-            } else
-            {
-                const bool maybe = (mt == 0) | ((cur >= 0) & (base < 4 + P)) |
-                                   ((cst > 0) & (c_lo <= top) & (c_hi >= base)) |
-                                   ((fst > 0) & (f_lo <= top) & (f_hi >= base));
-                if (!kQout && !__any(maybe)) continue;
-                m = range_bits(-base, 3 - base) | range_bits(c_lo - base, c_hi - base) |
-                    range_bits(f_lo - base, f_hi - base);
-                if (base < 4 + P) {  // SELECT rows 4 + p live in this tile (uniform): sel shifted by 4 - base
-                    const int sh = base - 4;
-                    m |= (uint32_t)(sh < 0 ? sel << -sh : (sh < 64 ? sel >> sh : 0ull));
-                }
+            const bool maybe = (mt == 0) | ((cur >= 0) & (base < 4 + P)) |
+                               ((cst > 0) & (c_lo <= top) & (c_hi >= base)) |
+                               ((fst > 0) & (f_lo <= top) & (f_hi >= base));
+            if (!kQout && !__any(maybe)) continue;
+            uint32_t m = range_bits(-base, 3 - base) | range_bits(c_lo - base, c_hi - base) |
+                         range_bits(f_lo - base, f_hi - base);
+            if (base < 4 + P) {  // SELECT rows 4 + p live in this tile (uniform): sel shifted by 4 - base
+                const int sh = base - 4;
+                m |= (uint32_t)(sh < 0 ? sel << -sh : (sh < 64 ? sel >> sh : 0ull));
             }
             // registers that hold no valid action for any env are skipped (wave-uniform)
             const uint32_t rm = __builtin_amdgcn_readfirstlane(REGM[mt]);
@@ -1100,13 +1171,22 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
     // so the two overlap
     const int lane = threadIdx.x & 63, h = lane >> 5;
     const int64_t tiles = (A.n + 31) >> 5;
-    struct EnvIn {
+    struct EnvIn {  // the four state bytes packed (x | y << 8 | origin << 16 | dest << 24): 2 VGPRs fewer
         double fuel;
-        uint32_t x8, y8, o8, d8;
+        uint32_t pk;
+        uint32_t e;  // the env (A.order), A.n for the last tile's idle lanes (n < 2^32: the order is u32)
+        __device__ uint32_t x8() const { return pk & 0xffu; }
+        __device__ uint32_t y8() const { return (pk >> 8) & 0xffu; }
+        __device__ uint32_t o8() const { return (pk >> 16) & 0xffu; }
+        __device__ uint32_t d8() const { return pk >> 24; }
     };
     auto load_env = [&](int64_t t) {
-        const int64_t ei = min(t * 32 + (lane & 31), A.n - 1);
-        return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei]};
+        const int64_t p = (A.order ? order_tile(t, tiles) : t) * 32 + (lane & 31);
+        const int64_t pi = min(p, A.n - 1);
+        const int64_t ei = A.order ? (int64_t)A.order[pi] : pi;
+        const uint32_t pk = (uint32_t)A.st.x[ei] | (uint32_t)A.st.y[ei] << 8 | (uint32_t)A.st.origin[ei] << 16 |
+                            (uint32_t)A.st.dest[ei] << 24;
+        return EnvIn{A.st.fuel[ei], pk, (uint32_t)(p < A.n ? ei : A.n)};
     };
     int64_t tile = (int64_t)blockIdx.x * kPolicyX3Waves + (threadIdx.x >> 6);
     EnvIn nxt = load_env(tile < tiles ? tile : 0);
@@ -1148,7 +1228,7 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
     // trip at the top of a tile), and its validity (the port on the ship's cell and that
     // port's stocks, two dependent L2 reads of the world image) resolved during fc3
     if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
-    EnvValid vnxt = env_valid(w, q, SAME, (int)nxt.x8, (int)nxt.y8, nxt.o8 == SE_NONE ? -1 : (int)nxt.o8);
+    EnvValid vnxt = env_valid(w, q, SAME, (int)nxt.x8(), (int)nxt.y8(), nxt.o8() == SE_NONE ? -1 : (int)nxt.o8());
     [[maybe_unused]] int tile_iter = 0;  // SHIPENV_X3_TRACE: the wave's 4th tile is stamped
     while (tile < tiles) {
         X3STAMP(0);
@@ -1157,10 +1237,10 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
         const int64_t tnext = tile + stride;
         const bool more = tnext < tiles;
         if (more) nxt = load_env(tnext);
-        const int64_t e = tile * 32 + (lane & 31);
+        const int64_t e = in.e;
         const bool live = e < A.n;
         const double fuel = in.fuel;
-        const uint32_t x8 = in.x8, y8 = in.y8, o8 = in.o8, d8 = in.d8;
+        const uint32_t x8 = in.x8(), y8 = in.y8(), o8 = in.o8(), d8 = in.d8();
         const int origin = o8 == SE_NONE ? -1 : (int)o8, dest = d8 == SE_NONE ? -1 : (int)d8;
         const float ff = (float)fuel;  // the preprocess_state row as torch's FloatTensor holds it
         bf16x8 X1[4][2][3], X2[4][2][3];
@@ -1228,7 +1308,7 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
 #pragma unroll
         for (int i = 0; i < 32; ++i) {
             const int kt = i >> 3, mt = (i >> 1) & 3, s2 = i & 1;
-            if (i == 8) ncode = w.code((int)nxt.x8, (int)nxt.y8);
+            if (i == 8) ncode = w.code((int)nxt.x8(), (int)nxt.y8());
             // unconditional (past the last tile nxt is tile 0's state, a valid address) and
             // opaque until their uses: under `if (more)` the compiler merged the arithmetic on
             // each into its load's block and waited out the round trip right there
@@ -1277,7 +1357,7 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
         // the load outstanding into the next tile, whose first write of its registers then
         // waited out the new env loads as well
         asm volatile("" ::"v"(nstock.x), "v"(nstock.y));
-        vnxt = env_valid_from(w, q, SAME, ncode, nstock, nxt.o8 == SE_NONE ? -1 : (int)nxt.o8);
+        vnxt = env_valid_from(w, q, SAME, ncode, nstock, nxt.o8() == SE_NONE ? -1 : (int)nxt.o8());
         // fc3 tiles 1..: the previous tile's argmax beside each chain, 4 registers a group
         int pbase = 0;
         [[maybe_unused]] float best0 = best;
@@ -1351,6 +1431,10 @@ struct se_qnet {
     bool packed = false;
     uint8_t* d_img32 = nullptr;  // se_policy_f32's split image (the full layout's fc3, global)
     int img32_bytes = 0;
+    // the visiting order (policy_order_kernel): used when n >= order_min_envs, resolved once
+    // by se_qnet_create (SHIPENV_POLICY_ORDER: 0 never, 1 always; unset: from 2^16 envs)
+    uint32_t* d_order = nullptr;
+    int64_t order_cap = 0, order_min_envs = (int64_t)1 << 16;
 };
 
 extern "C" {
@@ -1363,6 +1447,7 @@ int se_qnet_create(se_qnet** out, se_env* env) {
     se_qnet* qn = new se_qnet;
     qn->env = env;
     qn->device = env->device;
+    if (const char* v = getenv("SHIPENV_POLICY_ORDER")) qn->order_min_envs = atoi(v) != 0 ? 0 : INT64_MAX;
     *out = qn;
     return SE_OK;
 }
@@ -1401,6 +1486,26 @@ int se_qnet_set_weights(se_qnet* qn, const float* w1, const float* b1, const flo
 }  // extern "C"
 
 namespace {
+// this launch's visiting order, computed on the stream ahead of the policy kernel, or null
+// (position order: small launches, where the extra launch would cost more than it saves)
+int policy_order(se_qnet* qn, hipStream_t s, const uint32_t** out) {
+    se_env* env = qn->env;
+    *out = nullptr;
+    if (env->n < qn->order_min_envs) return SE_OK;
+    if (env->n > qn->order_cap) {
+        if (qn->d_order) HIP_TRY(hipFree(qn->d_order));
+        qn->d_order = nullptr;
+        HIP_TRY(hipMalloc(&qn->d_order, (size_t)env->n * sizeof(uint32_t)));
+        qn->order_cap = env->n;
+    }
+    const int64_t blocks = (env->n + kOrderChunk - 1) / kOrderChunk;
+    policy_order_kernel<<<(unsigned)blocks, kOrderBlock, 0, s>>>(env->d_world, env->dims, env->st.x, env->st.y,
+                                                                 env->n, qn->d_order);
+    HIP_TRY(hipGetLastError());
+    *out = qn->d_order;
+    return SE_OK;
+}
+
 struct PolicyRecord {
     uint32_t* pos;
     float* fuel;
@@ -1439,6 +1544,8 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
     const int64_t resident = (int64_t)dev_cus * kPolicyWgPerCu;  // workgroups resident at once
     const int grid = (int)(want < resident ? want : resident);
     PolicyArgs A{};
+    rc = policy_order(qn, (hipStream_t)stream, &A.order);
+    if (rc) return rc;
     A.world = env->d_world;
     A.dims = env->dims;
     A.qimg = reinterpret_cast<const uint4*>(qn->d_img + (q_out ? 0 : qn->c_off));
@@ -1505,6 +1612,8 @@ int launch_policy_x3(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, 
     const int64_t want = (tiles + kPolicyX3Waves - 1) / kPolicyX3Waves;
     const int grid = (int)(want < dev_cus ? want : dev_cus);
     PolicyArgs A{};
+    rc = policy_order(qn, s, &A.order);
+    if (rc) return rc;
     A.world = env->d_world;
     A.dims = env->dims;
     A.qimg = reinterpret_cast<const uint4*>(qn->d_img32);
@@ -1591,11 +1700,12 @@ int se_qnet_repack(se_qnet* qn, int32_t* bump, void* stream) {
 
 int se_qnet_destroy(se_qnet* qn) {
     if (!qn) return SE_OK;
-    if (qn->d_img || qn->d_img32) {  // does not touch the env, which may be gone already
+    if (qn->d_img || qn->d_img32 || qn->d_order) {  // does not touch the env, which may be gone already
         DeviceGuard g(qn->device);
         (void)hipDeviceSynchronize();
         if (qn->d_img) (void)hipFree(qn->d_img);
         if (qn->d_img32) (void)hipFree(qn->d_img32);
+        if (qn->d_order) (void)hipFree(qn->d_order);
     }
     delete qn;
     return SE_OK;

@@ -427,3 +427,66 @@ def test_f32_unaligned_weights_choose_as_aligned(ports):
     compact_b = pol.act(0.0, 7, precision="f32")
     assert torch.equal(full_a, full_b) and torch.equal(compact_a, compact_b)
     assert torch.equal(q_a, q_b)
+
+
+@pytest.mark.parametrize("precision", ["bf16", "f32"])
+@pytest.mark.parametrize("n,ports,steps", [(8192 + 7, None, 40), (2048 + 5, SHARED, 30), (4096 + 33, "64", 5)])
+def test_visiting_order_changes_nothing(monkeypatch, precision, n, ports, steps):
+    """policy_order_kernel (csrc/qpolicy.h): the policy visits each 1024-env chunk's ships at
+    sea first, then those in port, so most 32-env tiles skip fc3's second tile. It is on from
+    2^16 envs; SHIPENV_POLICY_ORDER=1 forces it (read when the policy is created), 0 turns it
+    off. The order only moves envs between lanes: greedy and exploring actions, the q_out rows
+    and the replay ring's records (se_policy_record) equal position order's, bit for bit."""
+    from conftest import golden_water
+    from shippingenv_amd.dqn import MiniBatch, ReplayBuffer
+    from shippingenv_amd.policy import QPolicy
+    from shippingenv_amd.vec import random_water_ports
+
+    if ports == "64":
+        ports = random_water_ports(golden_water(), 64, seed=3)
+    def setup():  # ships taken out of port by random valid actions (as bench.py's pre-roll)
+        e, m, p = make(n, ports=ports, steps=steps, scale=20.0)
+        for t in range(100):
+            e.step(p.act(1.0, 10_000 + t))
+        return e, m
+
+    env, model = setup()
+    in_port = valid_bool(env)[:, 4:].any(axis=1)
+    assert 0.02 < in_port.mean() < 0.98, in_port.mean()  # both kinds of tile
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("SHIPENV_POLICY_ORDER", mode)
+        pol = QPolicy(env, model)
+        _OPEN.append(pol)
+        q_out = torch.empty((n, env.action_space_size), dtype=torch.float32, device=env.device)
+        out[mode] = {"greedy": pol.act(0.0, 5, precision=precision).clone(),
+                     "explore": pol.act(0.3, 9, precision=precision).clone(),
+                     "q_greedy": pol.act(0.0, 5, q_out=q_out, precision=precision).clone(), "q": q_out}
+    for k in out["0"]:
+        assert torch.equal(out["0"][k], out["1"][k]), k
+    assert (out["1"]["greedy"] >= 4).any() and (out["1"]["greedy"] < 4).any()
+    # the replay record path: two envs stepped alike, one ring each, every transition compared
+    envs, rbs = [], []
+    for mode in ("0", "1"):
+        monkeypatch.delenv("SHIPENV_POLICY_ORDER")
+        e2, m2 = setup()
+        monkeypatch.setenv("SHIPENV_POLICY_ORDER", mode)
+        p2 = QPolicy(e2, m2)
+        _OPEN.append(p2)
+        rb = ReplayBuffer(e2, 3 * n)
+        _OPEN.append(rb)
+        for t in range(3):
+            p2.act_record(rb, 0.3, 100 + t, precision=precision)
+            e2.step(p2.actions)
+            rb.end()
+        envs.append(e2)
+        rbs.append(rb)
+    torch.cuda.synchronize()
+    assert rbs[0].size == rbs[1].size == 3 * n
+    outs = [MiniBatch(3 * n, envs[0].obs_size, envs[0].device) for _ in range(2)]
+    for rb, o in zip(rbs, outs):
+        rb.sample(o, t=1)
+    torch.cuda.synchronize()
+    for name in ("obs", "next_obs", "act", "rew", "done", "weight"):
+        assert torch.equal(getattr(outs[0], name), getattr(outs[1], name)), name
+    monkeypatch.delenv("SHIPENV_POLICY_ORDER")

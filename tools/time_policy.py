@@ -47,6 +47,12 @@ def main():
     py = torch.as_tensor(env.port_y, device="cuda:0").long()
     at = ((env.x.long()[:, None] == px[None]) & (env.y.long()[:, None] == py[None])).any(1)
     waves_any = at.view(-1, 32).any(1).float().mean() if a.n % 32 == 0 else float("nan")
+    # the same in the policy's visiting order (qpolicy.h policy_order_kernel: each 1024-env
+    # chunk's ships at sea first): the share of 32-env tiles that need fc3's second tile
+    ordered = float("nan")
+    if a.n % 1024 == 0:
+        c = at.view(-1, 1024).sort(dim=1, stable=True).values  # False (at sea) first
+        ordered = float(c.view(-1, 32).any(1).float().mean())
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -56,7 +62,8 @@ def main():
     torch.cuda.synchronize()
     rec = {"lib": os.path.basename(a.lib or "default"), "precision": a.precision,
            "n": a.n, "preroll": a.preroll, "ms_per_launch": round(e0.elapsed_time(e1) / a.launches, 4),
-           "at_port": float(at.float().mean()), "wave32_with_port": float(waves_any)}
+           "at_port": float(at.float().mean()), "wave32_with_port": float(waves_any),
+           "order": os.environ.get("SHIPENV_POLICY_ORDER", "auto"), "wave32_with_port_ordered": ordered}
     if a.trace:
         import ctypes
         import numpy as np
@@ -67,12 +74,14 @@ def main():
         assert N.lib().se_policy_trace_read(buf.ctypes.data, buf.nbytes) == 0
         st = buf.reshape(4096, 16).astype(np.int64)
         last = max(k for k in range(9) if (st[:, k] > 0).any())  # the kernel's last phase stamp
-        ok = (st[:, 0] > 0) & (st[:, last] > st[:, 0])
+        ok = (st[:, 0] > 0) & (st[:, last] > st[:, 0]) & (st[:, 9] >= st[:, 9].max() - 5000)
         d = np.diff(st[ok][:, :last + 1], axis=1)
         rec["trace_waves"] = int(ok.sum())
         rec["phase_cycles_median"] = [int(x) for x in np.median(d, axis=0)]
         rec["tile_cycles_median"] = int(np.median(st[ok][:, last] - st[ok][:, 0]))
-        live = st[:, 9] > 0  # stamps 9-11: s_memrealtime (100 MHz, chip-wide) at start, image staged, end
+        # stamps 9-11: s_memrealtime (100 MHz, chip-wide) at start, image staged, end; the last
+        # launch's waves only (a pre-roll's launches of the other kernel may have left more)
+        live = (st[:, 9] > 0) & (st[:, 9] >= st[:, 9].max() - 5000)
         s9, s10, s11 = st[live, 9], st[live, 10], st[live, 11]
         t0 = s9.min()
         rec["us_image_median"] = float(np.median(s10 - s9)) / 100
@@ -87,6 +96,20 @@ def main():
         hi = wid >= (4 if wpb == 8 else 12)
         rec["us_wave_median_by_prio"] = [float(np.median((s11 - s9)[~hi])) / 100,
                                          float(np.median((s11 - s9)[hi])) / 100]
+        # where the tail is: per XCD (workgroup b on XCD b % 8 under round-robin placement)
+        # and per SIMD (wave w of a workgroup on SIMD w % 4), the launch-relative end times
+        gw = np.nonzero(live)[0]
+        blk, end = gw // wpb, (s11 - t0) / 100
+        xcd = blk % 8
+        rec["us_end_by_xcd_median"] = [round(float(np.median(end[xcd == k])), 2) for k in range(8)]
+        rec["us_end_by_xcd_max"] = [round(float(end[xcd == k].max()), 2) for k in range(8)]
+        rec["us_start_by_xcd_median"] = [round(float(np.median((s9 - t0)[xcd == k])) / 100, 2) for k in range(8)]
+        simd = blk * 4 + (gw % wpb) % 4
+        last = np.zeros(simd.max() + 1)
+        np.maximum.at(last, simd, end)
+        last = last[np.unique(simd)]
+        rec["us_simd_last_end_q"] = [round(float(np.quantile(last, q)), 2) for q in (0.0, 0.1, 0.5, 0.9, 1.0)]
+        rec["us_wave_end_q"] = [round(float(np.quantile(end, q)), 2) for q in (0.0, 0.1, 0.5, 0.9, 1.0)]
     print(json.dumps(rec))
 
 
