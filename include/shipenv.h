@@ -188,6 +188,27 @@ int se_step_replay(se_env* env, const int32_t* type, const int32_t* a, const int
  * SE_ERR_NEED_DRAW with no effect. The step counter does not advance. */
 int se_step_agent_replay(se_env* env, const int32_t* actions, se_tape* tape, void* stream);
 
+/* The N = 1 GPU stepper as one resident wave (csrc/server.h): se_step_replay / se_reset_to
+ * on a 1-3 env handle without a launch or a stream synchronise per call. The handle's state
+ * (se_bind), the typed actions, the tape and the 16-byte mailbox live in coherent pinned host
+ * memory from se_host_alloc; the caller writes a call's inputs there, se_server_call posts
+ * the op and returns when the wave has answered (the outputs are then in the same memory).
+ *   SE_SERVER_STEP      se_step_replay(env, type, a, b, tape) (environment.py:359-376)
+ *   SE_SERVER_RESET_TO  se_reset_to(env, NULL, origin = type, dest = a) (:227-243)
+ * The wave ends after 20 ms without a call and is launched again by the next one.
+ * se_server_destroy ends it; destroy the server before its env. An extension: the reference
+ * steps in Python (Environment.step). */
+#define SE_SERVER_STEP 1
+#define SE_SERVER_RESET_TO 2
+typedef struct se_server se_server;
+int se_host_alloc(size_t bytes, void** out);  /* zeroed, coherent, device-mapped */
+int se_host_free(void* p);
+int se_server_create(se_server** out, se_env* env, const int32_t* type, const int32_t* a, const int32_t* b,
+                     se_tape* tape, uint32_t* mbox);
+int se_server_call(se_server* s, int32_t op);
+int se_server_launches(se_server* s, uint64_t* out);  /* kernel launches so far (idle restarts + 1) */
+int se_server_destroy(se_server* s);
+
 /* Host-resident environments (no device, no HIP call): the N = 1 drop-in
  * shipping.Environment steps here by default (shippingenv_amd/shipping/_host.py), with the
  * step kernels' own per-env code compiled for the host (replay_env in shipenv.hip), so a

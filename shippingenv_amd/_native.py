@@ -29,6 +29,9 @@ USED_FUEL_GATE, USED_LOSS_TYPE, USED_BETA, USED_ARRIVE, USED_MOVED = 1, 2, 4, 8,
 SAMPLE_RAISES, SAMPLE_NO_OTHER_PORT = -1, -2
 ROLL_DONE, ROLL_MAX_STEPS, ROLL_RAISED, ROLL_ATTEMPTS, ROLL_BAD_SRC = 0, 1, 2, 3, 4
 
+# se_server_call ops
+SERVER_STEP, SERVER_RESET_TO = 1, 2
+
 # every symbol include/shipenv.h declares
 EXPORTS = (
     "se_create", "se_set_ports", "se_bind", "se_reset", "se_reset_to", "se_step", "se_step_seq", "se_step_seq_mark",
@@ -44,6 +47,7 @@ EXPORTS = (
     "se_get_counters", "se_set_counters",
     "se_map_decode_luma", "se_map_area_threshold", "se_map_from_jpeg",
     "se_host_create", "se_host_set_ports", "se_host_step_replay", "se_host_reset_to", "se_host_destroy",
+    "se_host_alloc", "se_host_free", "se_server_create", "se_server_call", "se_server_launches", "se_server_destroy",
     "se_destroy", "se_last_error", "se_abi_version",
 )
 
@@ -130,6 +134,12 @@ def _declare(lib):
         "se_host_step_replay": [P, i64, P, P, P, P, P],
         "se_host_reset_to": [P, i64, P, P, P, P],
         "se_host_destroy": [P],
+        "se_host_alloc": [C.c_size_t, C.POINTER(P)],
+        "se_host_free": [P],
+        "se_server_create": [C.POINTER(P), P, P, P, P, P, P],
+        "se_server_call": [P, i32],
+        "se_server_launches": [P, C.POINTER(C.c_uint64)],
+        "se_server_destroy": [P],
         "se_destroy": [P],
         "se_last_error": [],
         "se_abi_version": [],

@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "shipenv.hip")
 MAPSRC = os.path.join(HERE, "csrc", "mapload.cpp")  # host-only: the JPEG map loader
-DEPS = [SRC, MAPSRC, os.path.join(HERE, "csrc", "philox.h"), os.path.join(HERE, "csrc", "qpolicy.h"), os.path.join(HERE, "csrc", "replay.h"),
+DEPS = [SRC, MAPSRC, os.path.join(HERE, "csrc", "philox.h"), os.path.join(HERE, "csrc", "qpolicy.h"), os.path.join(HERE, "csrc", "replay.h"), os.path.join(HERE, "csrc", "server.h"),
         os.path.join(HERE, "csrc", "qtrain.h"),
         os.path.join(ROOT, "include", "shipenv.h")]
 OUT = os.path.join(HERE, "_lib", "libshipenv_hip.so")

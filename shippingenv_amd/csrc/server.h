@@ -1,0 +1,224 @@
+// server.h — the N = 1 drop-in's GPU stepper as one persistent wave (VERDICT r05
+// item 8).
+//
+// Part of shipenv.hip's translation unit (included at its end). Reference callers: the agents
+// step one env at a time, once per decision (agents/dqn.py:287) and ~500 times per MCTS
+// decision (agents/mcts.py:228-236), each step() a few bytes in and out
+// (environment.py:359-376). As a kernel launch plus a stream synchronise per step that is
+// ~24 us, so the GPU stepper was 2.4x slower than the reference Python.
+//
+// Here one wave stays resident and steps on command: the host writes the step's inputs into a
+// block of coherent pinned host memory (se_host_alloc), then the command word; the wave sees it
+// with a system-scope acquire load, runs the same per-env code as se_step_replay's
+// step_tail_kernel (or se_reset_to's reset_env) on the state in that block, and answers with a
+// system-scope release store that the host spins on. No launch, no synchronise, no copy.
+//
+// Mailbox (4 u32, 16-byte aligned, in the same pinned memory):
+//   [0] command sequence   host: incremented per command (release store)
+//   [1] op                 host: SE_SERVER_STEP / SE_SERVER_RESET_TO / quit
+//   [2] answered sequence  device: the command it finished (release store)
+//   [3] running            host: 1 at launch; device: 0 when the kernel ends
+// The wave ends after kServerIdleTicks without a command (and on quit, se_server_destroy), so
+// no kernel outlives an idle or crashed host by more than that; the next se_server_call
+// launches it again, and a command that raced the exit is answered by the new kernel (it
+// starts from [2] and runs any command past it). Every access to the mailbox and the block is
+// a vector memory instruction (global loads / stores with sc0 sc1, buffer_inv / buffer_wbl2
+// from the acquire / release), which the ISA of server_kernel shows.
+
+#include <chrono>
+
+namespace {
+
+constexpr uint64_t kServerIdleTicks = 2000000;  // s_memrealtime ticks (100 MHz): 20 ms
+constexpr uint32_t kServerQuit = 0xffffffffu;
+
+struct ServerArgs {
+    StepArgs step;    // se_step_replay's arguments for the handle's envs (typed actions, tape)
+    ResetArgs reset;  // se_reset_to's: origin = type[i], dest = a[i]
+    uint32_t* mbox;
+};
+
+__global__ __launch_bounds__(64) void server_kernel(ServerArgs S) {
+    if (threadIdx.x != 0) return;
+    uint32_t* mb = S.mbox;
+    uint32_t last = __hip_atomic_load(mb + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const uint32_t c = __hip_atomic_load(mb, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (c != last) {
+            const uint32_t op = __hip_atomic_load(mb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (op == SE_SERVER_STEP) {
+                step_tail_envs<true, true, false>(S.step);
+            } else if (op == SE_SERVER_RESET_TO) {
+                const LdsWorld w = world_view(S.reset.dims, S.reset.world);
+                for (int64_t i = 0; i < S.reset.n; ++i) reset_env(S.reset, w, i);
+            }
+            __hip_atomic_store(mb + 2, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            last = c;
+            if (op == kServerQuit) break;
+            t0 = __builtin_amdgcn_s_memrealtime();
+        } else if (__builtin_amdgcn_s_memrealtime() - t0 > kServerIdleTicks) {
+            break;
+        } else {
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __hip_atomic_store(mb + 3, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+}  // namespace
+
+struct se_server {
+    se_env* env = nullptr;  // must outlive the server (destroy the server first)
+    int device = 0;
+    hipStream_t stream = nullptr;
+    ServerArgs args{};
+    uint32_t* mbox = nullptr;
+    uint32_t seq = 0;
+    bool launched = false;
+    uint64_t launches = 0;
+};
+
+namespace {
+
+uint32_t host_load(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+void host_store(uint32_t* p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+
+// (re)launch the wave once the previous one has ended
+int server_launch(se_server* s) {
+    if (s->launched) HIP_TRY(hipStreamSynchronize(s->stream));  // returns once it has ended
+    host_store(s->mbox + 3, 1u);
+    server_kernel<<<1, 64, 0, s->stream>>>(s->args);
+    HIP_TRY(hipGetLastError());
+    s->launched = true;
+    s->launches += 1;
+    return SE_OK;
+}
+
+bool host_pinned(const void* p) {
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) return false;
+    return at.type == hipMemoryTypeHost;
+}
+
+// post op and wait for its answer, relaunching the wave if it ended without answering
+int server_post(se_server* s, uint32_t op, double timeout_s) {
+    uint32_t* mb = s->mbox;
+    if (!s->launched || host_load(mb + 3) == 0u) {
+        int rc = server_launch(s);
+        if (rc) return rc;
+    }
+    const uint32_t seq = ++s->seq;
+    host_store(mb + 1, op);
+    host_store(mb, seq);
+    const auto t_start = std::chrono::steady_clock::now();
+    for (uint64_t spin = 0;; ++spin) {
+        if (host_load(mb + 2) == seq) return SE_OK;
+        if (host_load(mb + 3) == 0u) {  // the wave ended (idle) as the command arrived
+            if (op == kServerQuit) return SE_OK;
+            HIP_TRY(hipStreamSynchronize(s->stream));
+            if (host_load(mb + 2) == seq) return SE_OK;
+            int rc = server_launch(s);  // the new wave answers the pending command
+            if (rc) return rc;
+        }
+        if ((spin & 1023u) == 0 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() > timeout_s)
+            return fail(SE_ESTATE, "the stepper wave did not answer");
+        __builtin_ia32_pause();
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int se_host_alloc(size_t bytes, void** out) {
+    if (!out) return fail(SE_EINVAL, "null out");
+    *out = nullptr;
+    if (bytes == 0) return fail(SE_EINVAL, "zero bytes");
+    void* p = nullptr;
+    HIP_TRY(hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocMapped));
+    memset(p, 0, bytes);
+    *out = p;
+    return SE_OK;
+}
+
+int se_host_free(void* p) {
+    if (p) HIP_TRY(hipHostFree(p));
+    return SE_OK;
+}
+
+int se_server_create(se_server** out, se_env* env, const int32_t* type, const int32_t* a, const int32_t* b,
+                     se_tape* tape, uint32_t* mbox) {
+    if (!out) return fail(SE_EINVAL, "null out");
+    *out = nullptr;
+    int rc = check_ready(env);
+    if (rc) return rc;
+    if (env->n < 1 || env->n > 3) return fail(SE_EINVAL, "the stepper wave steps 1 to 3 envs");
+    if (env->flags & SE_FLAG_AUTO_RESET) return fail(SE_EINVAL, "the stepper wave replays tapes (no auto-reset)");
+    if (!type || !a || !b || !tape || !mbox) return fail(SE_EINVAL, "null action / tape / mailbox pointer");
+    if (!aligned16(type) || !aligned16(a) || !aligned16(b) || !aligned16(mbox))
+        return fail(SE_EINVAL, "action buffers and the mailbox must be 16-byte aligned");
+    if (!host_pinned(mbox)) return fail(SE_EINVAL, "the mailbox must be pinned host memory (se_host_alloc)");
+    DeviceGuard g(env->device);
+    se_server* s = new se_server;
+    s->env = env;
+    s->device = env->device;
+    StepArgs& A = s->args.step;
+    A.world = env->d_world;
+    A.dims = env->dims;
+    A.n = env->n;
+    A.env_base = env->env_base;
+    A.seed = env->seed;
+    A.t = (uint32_t)env->step_t;
+    A.st = env->st;
+    A.act = type;
+    A.act_a = a;
+    A.act_b = b;
+    A.tape = tape;
+    A.seg = env->seg;
+    A.done_pad = env->done_pad;
+    A.iters = env->iters;
+    A.slab = env->d_slab;
+    s->args.reset = ResetArgs{env->d_world, env->dims, env->n, env->env_base, env->seed, (uint32_t)env->epoch,
+                              (uint32_t)env->step_t, env->st, nullptr, type, a};
+    s->args.mbox = mbox;
+    s->mbox = mbox;
+    for (int i = 0; i < 4; ++i) host_store(mbox + i, 0u);
+    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete s;
+        return fail(SE_EHIP, "hipStreamCreateWithFlags failed");
+    }
+    *out = s;
+    return SE_OK;
+}
+
+int se_server_call(se_server* s, int32_t op) {
+    if (!s) return fail(SE_EINVAL, "null server");
+    if (op != SE_SERVER_STEP && op != SE_SERVER_RESET_TO) return fail(SE_EINVAL, "op must be SE_SERVER_STEP or SE_SERVER_RESET_TO");
+    DeviceGuard g(s->device);
+    return server_post(s, (uint32_t)op, 5.0);
+}
+
+int se_server_launches(se_server* s, uint64_t* out) {
+    if (!s || !out) return fail(SE_EINVAL, "null server / out");
+    *out = s->launches;
+    return SE_OK;
+}
+
+int se_server_destroy(se_server* s) {
+    if (!s) return SE_OK;
+    int rc = SE_OK;
+    {
+        DeviceGuard g(s->device);
+        if (s->launched) {
+            if (host_load(s->mbox + 3) != 0u) rc = server_post(s, kServerQuit, 1.0);
+            if (hipStreamSynchronize(s->stream) != hipSuccess && rc == SE_OK) rc = fail(SE_EHIP, "hipStreamSynchronize failed");
+        }
+        if (s->stream) (void)hipStreamDestroy(s->stream);
+    }
+    delete s;
+    return rc;
+}
+
+}  // extern "C"

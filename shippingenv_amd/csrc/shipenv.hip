@@ -1730,10 +1730,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
 // entry of the wave that owns that group (env order and a fixed summation order,
 // as in the main kernel).
 template <bool kTyped, bool kReplay, bool kAuto>
-__global__ __launch_bounds__(64) void step_tail_kernel(StepArgs A) {
+__device__ __forceinline__ void step_tail_envs(const StepArgs& A) {
     // at most 3 envs: the world is read in place (L2), not staged, so the step starts
-    // without the staging round trips (the N = 1 drop-in path is this kernel alone)
-    if (threadIdx.x != 0) return;
+    // without the staging round trips (the N = 1 drop-in path is this alone: step_tail_kernel,
+    // or a command to server_kernel, server.h)
     const LdsWorld w = world_view(A.dims, A.world);
     const int64_t g = A.n >> 2;
     const At<false> at{0, g * 4, A.n};
@@ -1763,6 +1763,12 @@ __global__ __launch_bounds__(64) void step_tail_kernel(StepArgs A) {
             sl[2] += (double)bs.len;
         }
     }
+}
+
+template <bool kTyped, bool kReplay, bool kAuto>
+__global__ __launch_bounds__(64) void step_tail_kernel(StepArgs A) {
+    if (threadIdx.x != 0) return;
+    step_tail_envs<kTyped, kReplay, kAuto>(A);
 }
 
 // Contiguous copy of the last step's done lists (se_done_compact), in two launches:
@@ -1820,11 +1826,8 @@ struct ResetArgs {
 // The world is read in place (only the port positions, for the envs being reset): staged
 // per workgroup as the other kernels do, it cost 2048 x 10.8 KB of L2 reads per launch,
 // the whole launch when a mask selects a few envs (the training loop's episode cuts).
-__global__ __launch_bounds__(kBlock) void reset_kernel(ResetArgs A) {
-    const LdsWorld w = world_view(A.dims, A.world);
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < A.n;
-         i += (int64_t)gridDim.x * kBlock) {
-        if (A.mask && !A.mask[i]) continue;
+__device__ __forceinline__ void reset_env(const ResetArgs& A, const LdsWorld& w, int64_t i) {
+    {
         Ship s;
         if (A.origin_in) {
             s.origin = A.origin_in[i];
@@ -1848,6 +1851,15 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(ResetArgs A) {
         A.st.done[i] = 0;
         A.st.err[i] = 0;
         A.st.reward[i] = 0.0f;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void reset_kernel(ResetArgs A) {
+    const LdsWorld w = world_view(A.dims, A.world);
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < A.n;
+         i += (int64_t)gridDim.x * kBlock) {
+        if (A.mask && !A.mask[i]) continue;
+        reset_env(A, w, i);
     }
 }
 
@@ -3144,3 +3156,4 @@ int se_host_destroy(se_host* h) {
 #include "qpolicy.h"
 #include "replay.h"
 #include "qtrain.h"
+#include "server.h"

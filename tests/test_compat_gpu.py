@@ -165,3 +165,45 @@ def test_default_stepper_is_host_and_gpu_is_selectable(monkeypatch):
     env.add_port([60, 22])
     env.reset()
     assert isinstance(env._stepper, HostStepper)
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_seeded_trace_on_the_launch_stepper(monkeypatch, seed):
+    """SHIPENV_GPU_SERVER=0: one se_step_replay launch and one synchronise per step instead of
+    the resident stepper wave; the same reference traces."""
+    monkeypatch.setenv("SHIPENV_GPU_SERVER", "0")
+    assert replay(load_script(seed)) > 600
+
+
+def test_stepper_wave_restarts_after_idle(monkeypatch):
+    """The resident stepper wave (csrc/server.h) ends after 20 ms without a command and the
+    next step launches it again: pauses of 50 ms inside a run give the same results as the
+    host stepper, step for step, and the wave was launched once per pause."""
+    import random
+
+    from shippingenv_amd.maps import BUILTIN_MAP
+    from shippingenv_amd.shipping import Environment
+    from shippingenv_amd.shipping._device import DeviceStepper
+
+    def run(kind, pause):
+        monkeypatch.setenv("SHIPENV_STEPPER", kind)
+        random.seed(7)
+        env = Environment(BUILTIN_MAP)
+        for p in ([41, 40], [60, 22], [78, 29]):
+            env.add_port(p)
+        env.reset()
+        out = []
+        for k in range(90):
+            if pause and k % 30 == 15:
+                time.sleep(0.05)
+            try:
+                out.append(repr(env.step([1, (0, 1) if k % 3 else (1, 0)])))
+            except Exception as e:  # noqa: BLE001 - the reference's exceptions are part of the trace
+                out.append(f"{type(e).__name__}: {e}")
+        launches = env._stepper.launches() if isinstance(env._stepper, DeviceStepper) else None
+        return out, launches
+
+    host, _ = run("host", False)
+    gpu, launches = run("gpu", True)
+    assert gpu == host
+    assert launches >= 4, launches
