@@ -203,8 +203,11 @@ int se_step_agent_replay(se_env* env, const int32_t* actions, se_tape* tape, voi
 typedef struct se_server se_server;
 int se_host_alloc(size_t bytes, void** out);  /* zeroed, coherent, device-mapped */
 int se_host_free(void* p);
-int se_server_create(se_server** out, se_env* env, const int32_t* type, const int32_t* a, const int32_t* b,
-                     se_tape* tape, uint32_t* mbox);
+/* block: the block of block_bytes (a multiple of 4, at most 1024) that holds the bound state,
+ * type, a, b and tape, which the wave copies to device memory and back per call; mbox: 16
+ * bytes outside it. */
+int se_server_create(se_server** out, se_env* env, void* block, int64_t block_bytes, const int32_t* type,
+                     const int32_t* a, const int32_t* b, se_tape* tape, uint32_t* mbox);
 int se_server_call(se_server* s, int32_t op);
 int se_server_launches(se_server* s, uint64_t* out);  /* kernel launches so far (idle restarts + 1) */
 int se_server_destroy(se_server* s);

@@ -11,7 +11,9 @@
 // block of coherent pinned host memory (se_host_alloc), then the command word; the wave sees it
 // with a system-scope acquire load, runs the same per-env code as se_step_replay's
 // step_tail_kernel (or se_reset_to's reset_env) on the state in that block, and answers with a
-// system-scope release store that the host spins on. No launch, no synchronise, no copy.
+// system-scope release store that the host spins on. No launch, no synchronise, no copy
+// call: the wave moves the block (at most 1 KB) over the host link itself, in one coalesced
+// load and one coalesced store per command, and steps on a device-memory mirror of it.
 //
 // Mailbox (4 u32, 16-byte aligned, in the same pinned memory):
 //   [0] command sequence   host: incremented per command (release store)
@@ -33,13 +35,20 @@ constexpr uint64_t kServerIdleTicks = 2000000;  // s_memrealtime ticks (100 MHz)
 constexpr uint32_t kServerQuit = 0xffffffffu;
 
 struct ServerArgs {
-    StepArgs step;    // se_step_replay's arguments for the handle's envs (typed actions, tape)
-    ResetArgs reset;  // se_reset_to's: origin = type[i], dest = a[i]
+    StepArgs step;    // se_step_replay's arguments for the handle's envs, on the device mirror
+    ResetArgs reset;  // se_reset_to's: origin = type[i], dest = a[i], on the mirror
     uint32_t* mbox;
+    uint32_t* block;   // the caller's pinned block (state, actions, tape)
+    uint32_t* mirror;  // its device-memory copy, which the step code reads and writes
+    int32_t words;     // block size in u32 (<= 64 * kServerWordsPerLane)
 };
+constexpr int kServerWordsPerLane = 4;
 
 __global__ __launch_bounds__(64) void server_kernel(ServerArgs S) {
-    if (threadIdx.x != 0) return;
+    // the block crosses the host link twice per command, as one coalesced load and one
+    // coalesced store of the whole wave: every access of the step itself (a few dozen,
+    // partly dependent) is to the device mirror, not a host-link round trip
+    const int lane = threadIdx.x;
     uint32_t* mb = S.mbox;
     uint32_t last = __hip_atomic_load(mb + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -47,13 +56,38 @@ __global__ __launch_bounds__(64) void server_kernel(ServerArgs S) {
         const uint32_t c = __hip_atomic_load(mb, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
         if (c != last) {
             const uint32_t op = __hip_atomic_load(mb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            if (op == SE_SERVER_STEP) {
-                step_tail_envs<true, true, false>(S.step);
-            } else if (op == SE_SERVER_RESET_TO) {
-                const LdsWorld w = world_view(S.reset.dims, S.reset.world);
-                for (int64_t i = 0; i < S.reset.n; ++i) reset_env(S.reset, w, i);
+            uint32_t v[kServerWordsPerLane];
+#pragma unroll
+            for (int k = 0; k < kServerWordsPerLane; ++k) {
+                const int i = k * 64 + lane;
+                v[k] = i < S.words ? S.block[i] : 0u;
             }
-            __hip_atomic_store(mb + 2, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+            for (int k = 0; k < kServerWordsPerLane; ++k) {
+                const int i = k * 64 + lane;
+                if (i < S.words) S.mirror[i] = v[k];
+            }
+            __threadfence_block();  // the mirror is complete before lane 0 reads it
+            if (lane == 0) {
+                if (op == SE_SERVER_STEP) {
+                    step_tail_envs<true, true, false>(S.step);
+                } else if (op == SE_SERVER_RESET_TO) {
+                    const LdsWorld w = world_view(S.reset.dims, S.reset.world);
+                    for (int64_t i = 0; i < S.reset.n; ++i) reset_env(S.reset, w, i);
+                }
+            }
+            __threadfence_block();  // lane 0's results are in the mirror before the copy back
+#pragma unroll
+            for (int k = 0; k < kServerWordsPerLane; ++k) {
+                const int i = k * 64 + lane;
+                if (i < S.words) v[k] = S.mirror[i];
+            }
+#pragma unroll
+            for (int k = 0; k < kServerWordsPerLane; ++k) {
+                const int i = k * 64 + lane;
+                if (i < S.words) S.block[i] = v[k];
+            }
+            if (lane == 0) __hip_atomic_store(mb + 2, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             last = c;
             if (op == kServerQuit) break;
             t0 = __builtin_amdgcn_s_memrealtime();
@@ -63,7 +97,7 @@ __global__ __launch_bounds__(64) void server_kernel(ServerArgs S) {
             __builtin_amdgcn_s_sleep(1);
         }
     }
-    __hip_atomic_store(mb + 3, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0) __hip_atomic_store(mb + 3, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace
@@ -71,6 +105,7 @@ __global__ __launch_bounds__(64) void server_kernel(ServerArgs S) {
 struct se_server {
     se_env* env = nullptr;  // must outlive the server (destroy the server first)
     int device = 0;
+    uint32_t* d_mirror = nullptr;
     hipStream_t stream = nullptr;
     ServerArgs args{};
     uint32_t* mbox = nullptr;
@@ -148,22 +183,65 @@ int se_host_free(void* p) {
     return SE_OK;
 }
 
-int se_server_create(se_server** out, se_env* env, const int32_t* type, const int32_t* a, const int32_t* b,
-                     se_tape* tape, uint32_t* mbox) {
+int se_server_create(se_server** out, se_env* env, void* block, int64_t block_bytes, const int32_t* type,
+                     const int32_t* a, const int32_t* b, se_tape* tape, uint32_t* mbox) {
     if (!out) return fail(SE_EINVAL, "null out");
     *out = nullptr;
     int rc = check_ready(env);
     if (rc) return rc;
     if (env->n < 1 || env->n > 3) return fail(SE_EINVAL, "the stepper wave steps 1 to 3 envs");
     if (env->flags & SE_FLAG_AUTO_RESET) return fail(SE_EINVAL, "the stepper wave replays tapes (no auto-reset)");
-    if (!type || !a || !b || !tape || !mbox) return fail(SE_EINVAL, "null action / tape / mailbox pointer");
-    if (!aligned16(type) || !aligned16(a) || !aligned16(b) || !aligned16(mbox))
-        return fail(SE_EINVAL, "action buffers and the mailbox must be 16-byte aligned");
-    if (!host_pinned(mbox)) return fail(SE_EINVAL, "the mailbox must be pinned host memory (se_host_alloc)");
+    if (!block || !type || !a || !b || !tape || !mbox) return fail(SE_EINVAL, "null block / action / tape / mailbox pointer");
+    if (!aligned16(block) || !aligned16(type) || !aligned16(a) || !aligned16(b) || !aligned16(mbox))
+        return fail(SE_EINVAL, "the block, the action buffers and the mailbox must be 16-byte aligned");
+    if (block_bytes <= 0 || (block_bytes & 3) || block_bytes > 64 * kServerWordsPerLane * 4)
+        return fail(SE_EINVAL, "block_bytes must be a multiple of 4 in (0, 1024]");
+    if (!host_pinned(block) || !host_pinned(mbox))
+        return fail(SE_EINVAL, "the block and the mailbox must be pinned host memory (se_host_alloc)");
+    // every buffer the step touches lies in the block; the mailbox does not
+    uint8_t* const lo = static_cast<uint8_t*>(block);
+    uint8_t* const hi = lo + block_bytes;
+    auto inside = [&](const void* p, int64_t bytes) {
+        const uint8_t* q = static_cast<const uint8_t*>(p);
+        return q >= lo && q + bytes <= hi;
+    };
+    const se_state& st = env->st;
+    const int64_t n = env->n;
+    if (!inside(st.x, n) || !inside(st.y, n) || !inside(st.fuel, 8 * n) || !inside(st.cargo, 4 * n) ||
+        !inside(st.origin, n) || !inside(st.dest, n) || !inside(st.reward, 4 * n) || !inside(st.done, n) ||
+        !inside(st.err, n) || (st.ep_return && !inside(st.ep_return, 4 * n)) ||
+        (st.ep_start && !inside(st.ep_start, 4 * n)) || (st.reward64 && !inside(st.reward64, 8 * n)) ||
+        !inside(type, 4 * n) || !inside(a, 4 * n) || !inside(b, 4 * n) || !inside(tape, (int64_t)sizeof(se_tape) * n))
+        return fail(SE_EINVAL, "the bound state, the actions and the tape must lie in the block");
+    if (static_cast<uint8_t*>(static_cast<void*>(mbox)) + 16 > lo && static_cast<uint8_t*>(static_cast<void*>(mbox)) < hi)
+        return fail(SE_EINVAL, "the mailbox must lie outside the block");
     DeviceGuard g(env->device);
     se_server* s = new se_server;
     s->env = env;
     s->device = env->device;
+    if (hipMalloc(&s->d_mirror, (size_t)block_bytes) != hipSuccess) {
+        delete s;
+        return fail(SE_EHIP, "hipMalloc of the block's mirror failed");
+    }
+    uint8_t* const m = reinterpret_cast<uint8_t*>(s->d_mirror);
+    auto mirror = [&](auto* p) { return p ? reinterpret_cast<decltype(p)>(m + (reinterpret_cast<const uint8_t*>(p) - lo)) : p; };
+    se_state ms = st;
+    ms.x = mirror(st.x);
+    ms.y = mirror(st.y);
+    ms.fuel = mirror(st.fuel);
+    ms.cargo = mirror(st.cargo);
+    ms.origin = mirror(st.origin);
+    ms.dest = mirror(st.dest);
+    ms.reward = mirror(st.reward);
+    ms.done = mirror(st.done);
+    ms.err = mirror(st.err);
+    ms.ep_return = mirror(st.ep_return);
+    ms.ep_start = mirror(st.ep_start);
+    ms.reward64 = mirror(st.reward64);
+    type = mirror(type);
+    a = mirror(a);
+    b = mirror(b);
+    tape = mirror(tape);
     StepArgs& A = s->args.step;
     A.world = env->d_world;
     A.dims = env->dims;
@@ -171,7 +249,7 @@ int se_server_create(se_server** out, se_env* env, const int32_t* type, const in
     A.env_base = env->env_base;
     A.seed = env->seed;
     A.t = (uint32_t)env->step_t;
-    A.st = env->st;
+    A.st = ms;
     A.act = type;
     A.act_a = a;
     A.act_b = b;
@@ -181,11 +259,15 @@ int se_server_create(se_server** out, se_env* env, const int32_t* type, const in
     A.iters = env->iters;
     A.slab = env->d_slab;
     s->args.reset = ResetArgs{env->d_world, env->dims, env->n, env->env_base, env->seed, (uint32_t)env->epoch,
-                              (uint32_t)env->step_t, env->st, nullptr, type, a};
+                              (uint32_t)env->step_t, ms, nullptr, type, a};
     s->args.mbox = mbox;
+    s->args.block = static_cast<uint32_t*>(block);
+    s->args.mirror = s->d_mirror;
+    s->args.words = (int32_t)(block_bytes / 4);
     s->mbox = mbox;
     for (int i = 0; i < 4; ++i) host_store(mbox + i, 0u);
     if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipFree(s->d_mirror);
         delete s;
         return fail(SE_EHIP, "hipStreamCreateWithFlags failed");
     }
@@ -216,6 +298,7 @@ int se_server_destroy(se_server* s) {
             if (hipStreamSynchronize(s->stream) != hipSuccess && rc == SE_OK) rc = fail(SE_EHIP, "hipStreamSynchronize failed");
         }
         if (s->stream) (void)hipStreamDestroy(s->stream);
+        if (s->d_mirror) (void)hipFree(s->d_mirror);
     }
     delete s;
     return rc;

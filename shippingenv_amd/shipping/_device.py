@@ -98,8 +98,8 @@ class DeviceStepper:
         self._base = b
         self._srv = C.c_void_p()
         if self.server:
-            N.check(lib.se_server_create(C.byref(self._srv), self._h, b + _TYPE, b + _A, b + _B, b + _TAPE,
-                                         b + _MBOX))
+            N.check(lib.se_server_create(C.byref(self._srv), self._h, b, _MBOX, b + _TYPE, b + _A, b + _B,
+                                         b + _TAPE, b + _MBOX))
         self._f64 = self.h.view(np.float64)
         self._i32 = self.h.view(np.int32)
 
