@@ -24,8 +24,8 @@
 // no kernel outlives an idle or crashed host by more than that; the next se_server_call
 // launches it again, and a command that raced the exit is answered by the new kernel (it
 // starts from [2] and runs any command past it). Every access to the mailbox and the block is
-// a vector memory instruction (global loads / stores with sc0 sc1, buffer_inv / buffer_wbl2
-// from the acquire / release), which the ISA of server_kernel shows.
+// a vector memory instruction (global loads / stores with sc0 sc1), which the ISA of
+// server_kernel shows.
 
 #include <chrono>
 
@@ -52,15 +52,21 @@ __global__ __launch_bounds__(64) void server_kernel(ServerArgs S) {
     uint32_t* mb = S.mbox;
     uint32_t last = __hip_atomic_load(mb + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    // No acquire / release fences: at system scope they invalidate and write back the L2
+    // (buffer_inv / buffer_wbl2 sc0 sc1), so every poll would evict the world image the step
+    // reads. The host-side words are read and written with system-scope relaxed accesses
+    // instead (sc0 sc1: to memory, past the caches), issued after the poll that saw the
+    // command returned; the host stored the block before the command word (x86 keeps its
+    // stores in order), and the answer is stored after the block's stores have completed.
     for (;;) {
-        const uint32_t c = __hip_atomic_load(mb, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t c = __hip_atomic_load(mb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (c != last) {
             const uint32_t op = __hip_atomic_load(mb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             uint32_t v[kServerWordsPerLane];
 #pragma unroll
             for (int k = 0; k < kServerWordsPerLane; ++k) {
                 const int i = k * 64 + lane;
-                v[k] = i < S.words ? S.block[i] : 0u;
+                v[k] = i < S.words ? __hip_atomic_load(S.block + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
             }
 #pragma unroll
             for (int k = 0; k < kServerWordsPerLane; ++k) {
@@ -85,9 +91,10 @@ __global__ __launch_bounds__(64) void server_kernel(ServerArgs S) {
 #pragma unroll
             for (int k = 0; k < kServerWordsPerLane; ++k) {
                 const int i = k * 64 + lane;
-                if (i < S.words) S.block[i] = v[k];
+                if (i < S.words) __hip_atomic_store(S.block + i, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
-            if (lane == 0) __hip_atomic_store(mb + 2, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the block's stores have completed
+            if (lane == 0) __hip_atomic_store(mb + 2, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             last = c;
             if (op == kServerQuit) break;
             t0 = __builtin_amdgcn_s_memrealtime();
@@ -97,7 +104,8 @@ __global__ __launch_bounds__(64) void server_kernel(ServerArgs S) {
             __builtin_amdgcn_s_sleep(1);
         }
     }
-    if (lane == 0) __hip_atomic_store(mb + 3, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(mb + 3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace
