@@ -10,7 +10,8 @@
 // Here one wave stays resident and steps on command: the host writes the step's inputs into a
 // block of coherent pinned host memory (se_host_alloc), then the command word; the wave sees it
 // with a system-scope acquire load, runs the same per-env code as se_step_replay's
-// step_tail_kernel (or se_reset_to's reset_env) on the state in that block, and answers with a
+// step_tail_kernel (or se_reset_to's reset_env) on the state in that block, with the world
+// image staged in LDS once per launch, and answers with a
 // system-scope release store that the host spins on. No launch, no synchronise, no copy
 // call: the wave moves the block (at most 1 KB) over the host link itself, in one coalesced
 // load and one coalesced store per command, and steps on a device-memory mirror of it.
@@ -48,6 +49,8 @@ __global__ __launch_bounds__(64) void server_kernel(ServerArgs S) {
     // the block crosses the host link twice per command, as one coalesced load and one
     // coalesced store of the whole wave: every access of the step itself (a few dozen,
     // partly dependent) is to the device mirror, not a host-link round trip
+    extern __shared__ uint32_t lds[];
+    const LdsWorld w = stage_world(S.step.world, S.step.dims, lds);  // once per launch
     const int lane = threadIdx.x;
     uint32_t* mb = S.mbox;
     uint32_t last = __hip_atomic_load(mb + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -76,9 +79,8 @@ __global__ __launch_bounds__(64) void server_kernel(ServerArgs S) {
             __threadfence_block();  // the mirror is complete before lane 0 reads it
             if (lane == 0) {
                 if (op == SE_SERVER_STEP) {
-                    step_tail_envs<true, true, false>(S.step);
+                    step_tail_envs<true, true, false>(S.step, w);
                 } else if (op == SE_SERVER_RESET_TO) {
-                    const LdsWorld w = world_view(S.reset.dims, S.reset.world);
                     for (int64_t i = 0; i < S.reset.n; ++i) reset_env(S.reset, w, i);
                 }
             }
@@ -130,8 +132,11 @@ void host_store(uint32_t* p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEA
 // (re)launch the wave once the previous one has ended
 int server_launch(se_server* s) {
     if (s->launched) HIP_TRY(hipStreamSynchronize(s->stream));  // returns once it has ended
+    static std::atomic<uint64_t> lds_set{0};
+    int rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(server_kernel), 160 * 1024, s->device);
+    if (rc) return rc;
     host_store(s->mbox + 3, 1u);
-    server_kernel<<<1, 64, 0, s->stream>>>(s->args);
+    server_kernel<<<1, 64, lds_bytes(s->env), s->stream>>>(s->args);
     HIP_TRY(hipGetLastError());
     s->launched = true;
     s->launches += 1;

@@ -1730,11 +1730,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
 // entry of the wave that owns that group (env order and a fixed summation order,
 // as in the main kernel).
 template <bool kTyped, bool kReplay, bool kAuto>
-__device__ __forceinline__ void step_tail_envs(const StepArgs& A) {
-    // at most 3 envs: the world is read in place (L2), not staged, so the step starts
-    // without the staging round trips (the N = 1 drop-in path is this alone: step_tail_kernel,
-    // or a command to server_kernel, server.h)
-    const LdsWorld w = world_view(A.dims, A.world);
+__device__ __forceinline__ void step_tail_envs(const StepArgs& A, const LdsWorld& w) {
+    // at most 3 envs: step_tail_kernel reads the world in place (L2), not staged, so the step
+    // starts without the staging round trips (the N = 1 drop-in path is this alone); the
+    // resident stepper wave (server.h) stages it in LDS once per launch
     const int64_t g = A.n >> 2;
     const At<false> at{0, g * 4, A.n};
     Group<kTyped, kAuto> G;
@@ -1768,7 +1767,7 @@ __device__ __forceinline__ void step_tail_envs(const StepArgs& A) {
 template <bool kTyped, bool kReplay, bool kAuto>
 __global__ __launch_bounds__(64) void step_tail_kernel(StepArgs A) {
     if (threadIdx.x != 0) return;
-    step_tail_envs<kTyped, kReplay, kAuto>(A);
+    step_tail_envs<kTyped, kReplay, kAuto>(A, world_view(A.dims, A.world));
 }
 
 // Contiguous copy of the last step's done lists (se_done_compact), in two launches:
