@@ -9,17 +9,16 @@
 //
 // Here one wave stays resident and steps on command: the host writes the step's inputs into a
 // block of coherent pinned host memory (se_host_alloc), then the command word; the wave sees it
-// with a system-scope acquire load, runs the same per-env code as se_step_replay's
-// step_tail_kernel (or se_reset_to's reset_env) on the state in that block, with the world
-// image staged in LDS once per launch, and answers with a
-// system-scope release store that the host spins on. No launch, no synchronise, no copy
-// call: the wave moves the block (at most 1 KB) over the host link itself, in one coalesced
-// load and one coalesced store per command, and steps on a device-memory mirror of it.
+// with a system-scope load, copies the block into LDS (one coalesced load of the wave), runs
+// replay_env, the per-env core of se_step_replay and se_host_step_replay (or se_reset_to's
+// explicit reset), on that copy with the world image staged in LDS once per launch, copies the
+// block back (one coalesced store) and answers with a system-scope store that the host spins on.
+// No launch, no synchronise, no copy call.
 //
 // Mailbox (4 u32, 16-byte aligned, in the same pinned memory):
-//   [0] command sequence   host: incremented per command (release store)
+//   [0] command sequence   host: incremented per command (stored after [1] and the block)
 //   [1] op                 host: SE_SERVER_STEP / SE_SERVER_RESET_TO / quit
-//   [2] answered sequence  device: the command it finished (release store)
+//   [2] answered sequence  device: the command it finished (stored after the block)
 //   [3] running            host: 1 at launch; device: 0 when the kernel ends
 // The wave ends after kServerIdleTicks without a command (and on quit, se_server_destroy), so
 // no kernel outlives an idle or crashed host by more than that; the next se_server_call
@@ -35,32 +34,48 @@ namespace {
 constexpr uint64_t kServerIdleTicks = 2000000;  // s_memrealtime ticks (100 MHz): 20 ms
 constexpr uint32_t kServerQuit = 0xffffffffu;
 
+// byte offsets in the block of each buffer the step touches (-1: absent)
+struct ServerLayout {
+    int32_t x, y, fuel, cargo, origin, dest, reward, done, err, ep_return, ep_start, reward64, type, a, b, tape;
+};
+
 struct ServerArgs {
-    StepArgs step;    // se_step_replay's arguments for the handle's envs, on the device mirror
-    ResetArgs reset;  // se_reset_to's: origin = type[i], dest = a[i], on the mirror
+    const uint32_t* world;
+    WorldDims dims;
+    int32_t n;
+    uint32_t step_t;  // se_reset_to's episode-start stamp (ep_start, if bound)
+    ServerLayout at;
     uint32_t* mbox;
-    uint32_t* block;   // the caller's pinned block (state, actions, tape)
-    uint32_t* mirror;  // its device-memory copy, which the step code reads and writes
-    int32_t words;     // block size in u32 (<= 64 * kServerWordsPerLane)
+    uint32_t* block;  // the caller's pinned block (state, actions, tape)
+    int32_t words;    // block size in u32 (<= 64 * kServerWordsPerLane)
 };
 constexpr int kServerWordsPerLane = 4;
 
+template <typename T>
+__device__ __forceinline__ T& lds_at(uint8_t* blk, int32_t off, int i) {
+    return reinterpret_cast<T*>(blk + off)[i];
+}
+
 __global__ __launch_bounds__(64) void server_kernel(ServerArgs S) {
-    // the block crosses the host link twice per command, as one coalesced load and one
-    // coalesced store of the whole wave: every access of the step itself (a few dozen,
-    // partly dependent) is to the device mirror, not a host-link round trip
+    // LDS: the world image (staged once per launch), then a copy of the block. The block
+    // crosses the host link twice per command, as one coalesced load and one coalesced store
+    // of the whole wave; lane 0 steps the envs in LDS with replay_env, the per-env core of
+    // se_step_replay (and of se_host_step_replay), so no step access is a memory round trip.
     extern __shared__ uint32_t lds[];
-    const LdsWorld w = stage_world(S.step.world, S.step.dims, lds);  // once per launch
+    const LdsWorld w = stage_world(S.world, S.dims, lds);
+    uint32_t* blk32 = lds + S.dims.padded();
+    uint8_t* blk = reinterpret_cast<uint8_t*>(blk32);
+    const ServerLayout& L = S.at;
     const int lane = threadIdx.x;
     uint32_t* mb = S.mbox;
     uint32_t last = __hip_atomic_load(mb + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     // No acquire / release fences: at system scope they invalidate and write back the L2
-    // (buffer_inv / buffer_wbl2 sc0 sc1), so every poll would evict the world image the step
-    // reads. The host-side words are read and written with system-scope relaxed accesses
-    // instead (sc0 sc1: to memory, past the caches), issued after the poll that saw the
-    // command returned; the host stored the block before the command word (x86 keeps its
-    // stores in order), and the answer is stored after the block's stores have completed.
+    // (buffer_inv / buffer_wbl2 sc0 sc1) on every poll. The host-side words are read and
+    // written with system-scope relaxed accesses instead (sc0 sc1: to memory, past the
+    // caches), issued after the poll that saw the command returned; the host stored the block
+    // before the command word (x86 keeps its stores in order), and the answer is stored after
+    // the block's stores have completed.
     for (;;) {
         const uint32_t c = __hip_atomic_load(mb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (c != last) {
@@ -74,26 +89,52 @@ __global__ __launch_bounds__(64) void server_kernel(ServerArgs S) {
 #pragma unroll
             for (int k = 0; k < kServerWordsPerLane; ++k) {
                 const int i = k * 64 + lane;
-                if (i < S.words) S.mirror[i] = v[k];
+                if (i < S.words) blk32[i] = v[k];
             }
-            __threadfence_block();  // the mirror is complete before lane 0 reads it
+            __syncthreads();
             if (lane == 0) {
-                if (op == SE_SERVER_STEP) {
-                    step_tail_envs<true, true, false>(S.step, w);
-                } else if (op == SE_SERVER_RESET_TO) {
-                    for (int64_t i = 0; i < S.reset.n; ++i) reset_env(S.reset, w, i);
+                for (int i = 0; i < S.n; ++i) {
+                    if (op == SE_SERVER_STEP) {  // se_host_step_replay's loop body, on LDS
+                        Ship sh{lds_at<uint8_t>(blk, L.x, i), lds_at<uint8_t>(blk, L.y, i), lds_at<double>(blk, L.fuel, i),
+                                lds_at<int32_t>(blk, L.cargo, i), lds_at<uint8_t>(blk, L.origin, i),
+                                lds_at<uint8_t>(blk, L.dest, i)};
+                        Pending p;
+                        se_tape& tp = lds_at<se_tape>(blk, L.tape, i);
+                        tp.used = (int32_t)replay_env(w, sh, p, SE_ERR_OK, lds_at<int32_t>(blk, L.type, i),
+                                                      lds_at<int32_t>(blk, L.a, i), lds_at<int32_t>(blk, L.b, i),
+                                                      tp.u_fuel, tp.u_gate, &tp);
+                        lds_at<uint8_t>(blk, L.x, i) = (uint8_t)sh.x;
+                        lds_at<uint8_t>(blk, L.y, i) = (uint8_t)sh.y;
+                        lds_at<double>(blk, L.fuel, i) = sh.fuel;
+                        lds_at<int32_t>(blk, L.cargo, i) = sh.cargo;
+                        lds_at<uint8_t>(blk, L.origin, i) = (uint8_t)sh.origin;
+                        lds_at<uint8_t>(blk, L.dest, i) = (uint8_t)sh.dest;
+                        lds_at<float>(blk, L.reward, i) = (float)p.r;  // one rounding of the f64 reward
+                        lds_at<uint8_t>(blk, L.done, i) = (uint8_t)p.dead;
+                        lds_at<int8_t>(blk, L.err, i) = (int8_t)p.e;
+                        if (L.reward64 >= 0) lds_at<double>(blk, L.reward64, i) = p.r;
+                    } else if (op == SE_SERVER_RESET_TO) {  // reset_kernel's explicit form
+                        const int o = lds_at<int32_t>(blk, L.type, i), d = lds_at<int32_t>(blk, L.a, i);
+                        if ((unsigned)o >= (unsigned)w.P || (unsigned)d >= (unsigned)w.P) continue;  // checked by the caller
+                        lds_at<uint8_t>(blk, L.x, i) = (uint8_t)w.px(o);
+                        lds_at<uint8_t>(blk, L.y, i) = (uint8_t)w.py(o);
+                        lds_at<double>(blk, L.fuel, i) = kFuelInit;
+                        lds_at<int32_t>(blk, L.cargo, i) = 0;
+                        lds_at<uint8_t>(blk, L.origin, i) = (uint8_t)o;
+                        lds_at<uint8_t>(blk, L.dest, i) = (uint8_t)d;
+                        if (L.ep_return >= 0) lds_at<float>(blk, L.ep_return, i) = 0.0f;
+                        if (L.ep_start >= 0) lds_at<int32_t>(blk, L.ep_start, i) = (int32_t)S.step_t;
+                        lds_at<uint8_t>(blk, L.done, i) = 0;
+                        lds_at<int8_t>(blk, L.err, i) = 0;
+                        lds_at<float>(blk, L.reward, i) = 0.0f;
+                    }
                 }
             }
-            __threadfence_block();  // lane 0's results are in the mirror before the copy back
+            __syncthreads();
 #pragma unroll
             for (int k = 0; k < kServerWordsPerLane; ++k) {
                 const int i = k * 64 + lane;
-                if (i < S.words) v[k] = S.mirror[i];
-            }
-#pragma unroll
-            for (int k = 0; k < kServerWordsPerLane; ++k) {
-                const int i = k * 64 + lane;
-                if (i < S.words) __hip_atomic_store(S.block + i, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (i < S.words) __hip_atomic_store(S.block + i, blk32[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the block's stores have completed
             if (lane == 0) __hip_atomic_store(mb + 2, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -115,7 +156,6 @@ __global__ __launch_bounds__(64) void server_kernel(ServerArgs S) {
 struct se_server {
     se_env* env = nullptr;  // must outlive the server (destroy the server first)
     int device = 0;
-    uint32_t* d_mirror = nullptr;
     hipStream_t stream = nullptr;
     ServerArgs args{};
     uint32_t* mbox = nullptr;
@@ -136,7 +176,7 @@ int server_launch(se_server* s) {
     int rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(server_kernel), 160 * 1024, s->device);
     if (rc) return rc;
     host_store(s->mbox + 3, 1u);
-    server_kernel<<<1, 64, lds_bytes(s->env), s->stream>>>(s->args);
+    server_kernel<<<1, 64, lds_bytes(s->env) + (size_t)s->args.words * 4, s->stream>>>(s->args);
     HIP_TRY(hipGetLastError());
     s->launched = true;
     s->launches += 1;
@@ -228,59 +268,43 @@ int se_server_create(se_server** out, se_env* env, void* block, int64_t block_by
         return fail(SE_EINVAL, "the bound state, the actions and the tape must lie in the block");
     if (static_cast<uint8_t*>(static_cast<void*>(mbox)) + 16 > lo && static_cast<uint8_t*>(static_cast<void*>(mbox)) < hi)
         return fail(SE_EINVAL, "the mailbox must lie outside the block");
+    auto mis = [&](const void* p, int align) { return p && ((static_cast<const uint8_t*>(p) - lo) & (align - 1)); };
+    if (mis(st.fuel, 8) || mis(st.reward64, 8) || mis(tape, 8) || mis(st.cargo, 4) || mis(st.reward, 4) ||
+        mis(st.ep_return, 4) || mis(st.ep_start, 4))
+        return fail(SE_EINVAL, "the block's f64 buffers and the tape must be 8-byte aligned, the 32-bit ones 4-byte aligned");
+    if (lds_bytes(env) + (size_t)block_bytes > 160 * 1024) return fail(SE_EINVAL, "world image + block exceed the LDS");
     DeviceGuard g(env->device);
     se_server* s = new se_server;
     s->env = env;
     s->device = env->device;
-    if (hipMalloc(&s->d_mirror, (size_t)block_bytes) != hipSuccess) {
-        delete s;
-        return fail(SE_EHIP, "hipMalloc of the block's mirror failed");
-    }
-    uint8_t* const m = reinterpret_cast<uint8_t*>(s->d_mirror);
-    auto mirror = [&](auto* p) { return p ? reinterpret_cast<decltype(p)>(m + (reinterpret_cast<const uint8_t*>(p) - lo)) : p; };
-    se_state ms = st;
-    ms.x = mirror(st.x);
-    ms.y = mirror(st.y);
-    ms.fuel = mirror(st.fuel);
-    ms.cargo = mirror(st.cargo);
-    ms.origin = mirror(st.origin);
-    ms.dest = mirror(st.dest);
-    ms.reward = mirror(st.reward);
-    ms.done = mirror(st.done);
-    ms.err = mirror(st.err);
-    ms.ep_return = mirror(st.ep_return);
-    ms.ep_start = mirror(st.ep_start);
-    ms.reward64 = mirror(st.reward64);
-    type = mirror(type);
-    a = mirror(a);
-    b = mirror(b);
-    tape = mirror(tape);
-    StepArgs& A = s->args.step;
-    A.world = env->d_world;
-    A.dims = env->dims;
-    A.n = env->n;
-    A.env_base = env->env_base;
-    A.seed = env->seed;
-    A.t = (uint32_t)env->step_t;
-    A.st = ms;
-    A.act = type;
-    A.act_a = a;
-    A.act_b = b;
-    A.tape = tape;
-    A.seg = env->seg;
-    A.done_pad = env->done_pad;
-    A.iters = env->iters;
-    A.slab = env->d_slab;
-    s->args.reset = ResetArgs{env->d_world, env->dims, env->n, env->env_base, env->seed, (uint32_t)env->epoch,
-                              (uint32_t)env->step_t, ms, nullptr, type, a};
+    auto off = [&](const void* p) { return p ? (int32_t)(static_cast<const uint8_t*>(p) - lo) : (int32_t)-1; };
+    ServerLayout& L = s->args.at;
+    L.x = off(st.x);
+    L.y = off(st.y);
+    L.fuel = off(st.fuel);
+    L.cargo = off(st.cargo);
+    L.origin = off(st.origin);
+    L.dest = off(st.dest);
+    L.reward = off(st.reward);
+    L.done = off(st.done);
+    L.err = off(st.err);
+    L.ep_return = off(st.ep_return);
+    L.ep_start = off(st.ep_start);
+    L.reward64 = off(st.reward64);
+    L.type = off(type);
+    L.a = off(a);
+    L.b = off(b);
+    L.tape = off(tape);
+    s->args.world = env->d_world;
+    s->args.dims = env->dims;
+    s->args.n = (int32_t)env->n;
+    s->args.step_t = (uint32_t)env->step_t;
     s->args.mbox = mbox;
     s->args.block = static_cast<uint32_t*>(block);
-    s->args.mirror = s->d_mirror;
     s->args.words = (int32_t)(block_bytes / 4);
     s->mbox = mbox;
     for (int i = 0; i < 4; ++i) host_store(mbox + i, 0u);
     if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
-        (void)hipFree(s->d_mirror);
         delete s;
         return fail(SE_EHIP, "hipStreamCreateWithFlags failed");
     }
@@ -311,7 +335,6 @@ int se_server_destroy(se_server* s) {
             if (hipStreamSynchronize(s->stream) != hipSuccess && rc == SE_OK) rc = fail(SE_EHIP, "hipStreamSynchronize failed");
         }
         if (s->stream) (void)hipStreamDestroy(s->stream);
-        if (s->d_mirror) (void)hipFree(s->d_mirror);
     }
     delete s;
     return rc;

@@ -1732,8 +1732,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(4)))
 template <bool kTyped, bool kReplay, bool kAuto>
 __device__ __forceinline__ void step_tail_envs(const StepArgs& A, const LdsWorld& w) {
     // at most 3 envs: step_tail_kernel reads the world in place (L2), not staged, so the step
-    // starts without the staging round trips (the N = 1 drop-in path is this alone); the
-    // resident stepper wave (server.h) stages it in LDS once per launch
+    // starts without the staging round trips (the N = 1 launch path is this kernel alone)
     const int64_t g = A.n >> 2;
     const At<false> at{0, g * 4, A.n};
     Group<kTyped, kAuto> G;
