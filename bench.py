@@ -321,8 +321,9 @@ def run_config1(args):
     the survey timed the reference: random.seed(0), the five DEFAULT_PORTS,
     moves uniform over N, E, S, W from random.Random(1), reset on done; median of 10 runs.
     Timed on the drop-in's default stepper (the step kernels' per-env code compiled for the
-    host: one C call per step) and on SHIPENV_STEPPER=gpu (one launch and one stream
-    synchronise per step)."""
+    host: one C call per step), on SHIPENV_STEPPER=gpu (the resident stepper wave: one mailbox
+    command per step, csrc/server.h) and on SHIPENV_STEPPER=gpu with SHIPENV_GPU_SERVER=0 (one
+    launch and one stream synchronise per step)."""
     import random
     import statistics
 
@@ -349,21 +350,26 @@ def run_config1(args):
         return (time.perf_counter() - t0) * 1e3
 
     ms = {}
-    prev = os.environ.get("SHIPENV_STEPPER")
+    prev = {k: os.environ.get(k) for k in ("SHIPENV_STEPPER", "SHIPENV_GPU_SERVER")}
     try:
-        for kind in ("host", "gpu"):
-            os.environ["SHIPENV_STEPPER"] = kind
+        for kind, server in (("host", "1"), ("gpu", "1"), ("gpu_launch", "0")):
+            os.environ["SHIPENV_STEPPER"] = kind.split("_")[0]
+            os.environ["SHIPENV_GPU_SERVER"] = server
             once()
             ms[kind] = statistics.median(once() for _ in range(10))
     finally:
-        if prev is None:
-            os.environ.pop("SHIPENV_STEPPER", None)
-        else:
-            os.environ["SHIPENV_STEPPER"] = prev
+        for k, v in prev.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     return {"workload": "BASELINE configs[0]: 1 env x 100 steps through shipping.Environment "
                         "(the reference's API) on its default host stepper",
             "ms_per_100_steps": round(ms["host"], 4),
             "ms_per_100_steps_gpu_stepper": round(ms["gpu"], 4),
+            "ms_per_100_steps_gpu_launch_per_step": round(ms["gpu_launch"], 4),
+            "gpu_stepper_note": "SHIPENV_STEPPER=gpu: the resident stepper wave (se_server_call, csrc/server.h); "
+                                "gpu_launch_per_step: SHIPENV_GPU_SERVER=0, one se_step_replay launch + synchronise",
             "reference_python_ms_per_100_steps": 0.98,
             "reference_note": "survey container, 1 core (BASELINE.md); the reference cannot run on the GPU box. "
                               "Same-host comparison in the build container: profiles/r03/config1_vs_reference.json"}

@@ -189,25 +189,41 @@ int se_step_replay(se_env* env, const int32_t* type, const int32_t* a, const int
 int se_step_agent_replay(se_env* env, const int32_t* actions, se_tape* tape, void* stream);
 
 /* The N = 1 GPU stepper as one resident wave (csrc/server.h): se_step_replay / se_reset_to
- * on a 1-3 env handle without a launch or a stream synchronise per call. The handle's state
- * (se_bind), the typed actions, the tape and the 16-byte mailbox live in coherent pinned host
- * memory from se_host_alloc; the caller writes a call's inputs there, se_server_call posts
- * the op and returns when the wave has answered (the outputs are then in the same memory).
- *   SE_SERVER_STEP      se_step_replay(env, type, a, b, tape) (environment.py:359-376)
- *   SE_SERVER_RESET_TO  se_reset_to(env, NULL, origin = type, dest = a) (:227-243)
- * The wave ends after 20 ms without a call and is launched again by the next one.
- * se_server_destroy ends it; destroy the server before its env. An extension: the reference
- * steps in Python (Environment.step). */
+ * on a one-env handle without a launch or a stream synchronise per call. The env's state,
+ * typed action and tape and the mailbox are one se_server_block in coherent pinned host memory
+ * (se_host_alloc, 64-byte aligned); the caller writes a call's inputs there, se_server_call
+ * posts the op and returns when the wave has answered, the outputs then in the same block:
+ *   SE_SERVER_STEP      se_step_replay (environment.py:359-376): x .. b and tape in, state,
+ *                       reward, reward64, done, err and tape.used out
+ *   SE_SERVER_RESET_TO  se_reset_to with origin = type, dest = a (:227-243); they must name
+ *                       ports (not checked on the device)
+ * The wave ends after 20 ms without a call and is launched again by the next one;
+ * se_server_destroy ends it (destroy the server before its env). The handle may also be
+ * bound (se_bind) to the block's fields for the launch path (se_step_replay). An extension:
+ * the reference steps in Python (Environment.step). */
 #define SE_SERVER_STEP 1
 #define SE_SERVER_RESET_TO 2
+typedef struct se_server_block {
+    uint8_t x, y, origin, dest, done;  /* 0 (origin / dest SE_NONE = None) */
+    int8_t err;
+    uint8_t pad0[2];
+    double fuel;                       /* 8 */
+    int32_t cargo;                     /* 16 */
+    float reward;                      /* 20 */
+    double reward64;                   /* 24 */
+    int32_t type, a, b;                /* 32 */
+    uint32_t seq0;                     /* 44: se_server_call: the call's number, line 0's copy */
+    se_tape tape;                      /* 48 */
+    uint32_t seq1;                     /* 88: the call's number again, stored last */
+    uint32_t op;                       /* 92 */
+    uint32_t answer;                   /* 96: the wave: the number of the call it answered */
+    uint32_t running;                  /* 100: the wave: 0 once it has ended */
+    uint8_t pad1[24];
+} se_server_block;                     /* 128 bytes: two 64-byte lines */
 typedef struct se_server se_server;
-int se_host_alloc(size_t bytes, void** out);  /* zeroed, coherent, device-mapped */
+int se_host_alloc(size_t bytes, void** out);  /* zeroed, coherent, device-mapped, 64-byte aligned */
 int se_host_free(void* p);
-/* block: the block of block_bytes (a multiple of 4, at most 1024) that holds the bound state,
- * type, a, b and tape, which the wave copies to device memory and back per call; mbox: 16
- * bytes outside it. */
-int se_server_create(se_server** out, se_env* env, void* block, int64_t block_bytes, const int32_t* type,
-                     const int32_t* a, const int32_t* b, se_tape* tape, uint32_t* mbox);
+int se_server_create(se_server** out, se_env* env, se_server_block* block);
 int se_server_call(se_server* s, int32_t op);
 int se_server_launches(se_server* s, uint64_t* out);  /* kernel launches so far (idle restarts + 1) */
 int se_server_destroy(se_server* s);

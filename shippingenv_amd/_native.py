@@ -136,7 +136,7 @@ def _declare(lib):
         "se_host_destroy": [P],
         "se_host_alloc": [C.c_size_t, C.POINTER(P)],
         "se_host_free": [P],
-        "se_server_create": [C.POINTER(P), P, P, i64, P, P, P, P, P],
+        "se_server_create": [C.POINTER(P), P, P],
         "se_server_call": [P, i32],
         "se_server_launches": [P, C.POINTER(C.c_uint64)],
         "se_server_destroy": [P],

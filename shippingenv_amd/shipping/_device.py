@@ -1,22 +1,24 @@
 """One environment on the GPU behind shipping.Environment.
 
 The compat class keeps the reference's attributes on the host (agents read and
-assign them directly) and runs every state transition through the step kernel's
-per-env code: se_step_replay's work on a one-env handle whose SoA buffers, action
-and tape all live in one 256-byte block of coherent pinned host memory
-(se_host_alloc), which the GPU reads and writes in place (ROCm maps pinned host
-memory into the GPU's address space). No copies: an H2D and a D2H copy per step
-measured 38.8 us per step for config 1, BASELINE configs[0].
+assign them directly) and runs every state transition through the step kernels'
+per-env code on the GPU. The env's state, its typed action and its tape are one
+se_server_block (include/shipenv.h) in coherent pinned host memory (se_host_alloc),
+which the GPU reads and writes in place (ROCm maps pinned host memory into the GPU's
+address space); the inputs go in with one struct.pack_into and the results come out
+with one unpack_from, as in the host stepper. No copies: an H2D and a D2H copy per
+step measured 38.8 us per step for config 1, BASELINE configs[0].
 
 By default a step is one call to the resident stepper wave (se_server_call,
-csrc/server.h): the wave polls a mailbox after the block and answers each command,
-so a step costs no launch and no stream synchronise. SHIPENV_GPU_SERVER=0 (or
-server=False) steps with one se_step_replay launch and one synchronise instead.
+csrc/server.h): the wave polls the block and answers each command, so a step costs
+no launch and no stream synchronise. SHIPENV_GPU_SERVER=0 (or server=False) steps
+with one se_step_replay launch and one synchronise instead.
 """
 from __future__ import annotations
 
 import ctypes as C
 import os
+import struct
 from dataclasses import dataclass
 
 import numpy as np
@@ -40,13 +42,22 @@ def _hip_sync(stream):
     if rc != 0:
         raise N.NativeLibraryError(f"hipStreamSynchronize failed ({rc})")
 
-# byte offsets inside the I/O block (each field 16-byte aligned for se_bind)
-_X, _Y, _ORG, _DST, _DONE, _ERR = 0, 16, 32, 48, 64, 80
-_FUEL, _CARGO, _REW, _REW64 = 96, 112, 128, 144
-_TYPE, _A, _B, _TAPE = 160, 176, 192, 208
-_MBOX = 256  # the stepper wave's mailbox: 4 u32 (csrc/server.h)
-_SIZE = 272
+# the block: se_server_block (include/shipenv.h), 128 bytes in coherent pinned host memory;
+# bytes 0-87 are also shipping/_host.py's block layout:
+#   0 x u8, 1 y u8, 2 origin u8, 3 dest u8, 4 done u8, 5 err i8, 8 fuel f64, 16 cargo i32,
+#   20 reward f32, 24 reward64 f64, 32 type i32, 36 a i32, 40 b i32, 44 seq0 (the wave's),
+#   48 tape {u_fuel, u_gate, u_type, beta f64; arrive_dest, used i32}, 88.. the mailbox
+# The launch path (se_step_replay wants 16-byte aligned action buffers) copies a and b to
+# 128 and 144.
+_IN = struct.Struct("<4B4xdi12xiii4xddddi")          # x y org dst | fuel cargo | type a b | tape
+_OUT = struct.Struct("<4BBb2xdifd52xi")               # x y org dst done err | fuel cargo rew rew64 | used
+_RESET_OUT = struct.Struct("<4B4xdi")
+_RESET_IN = struct.Struct("<ii")                      # origin, dest into type, a
+_AB = struct.Struct("<i12xi")                         # the launch path's a (128), b (144)
+_TYPE, _A, _B, _TAPE, _A16, _B16 = 32, 36, 40, 48, 128, 144
+_SIZE = 256
 _I32_MIN, _I32_MAX = -(2 ** 31), 2 ** 31 - 1
+_NONE = N.SE_NONE
 
 
 @dataclass
@@ -72,6 +83,7 @@ class DeviceStepper:
         if not torch.cuda.is_available():
             raise N.NativeLibraryError("shipping.Environment steps on a ROCm GPU; none is visible")
         lib = N.lib()
+        self._lib = lib
         self.dev = torch.device("cuda", torch.cuda.current_device()) if device is None \
             else torch.device(device)
         if server is None:
@@ -81,7 +93,7 @@ class DeviceStepper:
         with torch.cuda.device(self.dev):  # pinned for (mapped into) this GPU
             N.check(lib.se_host_alloc(_SIZE, C.byref(blk)))
         self._blk = blk
-        self.h = np.ctypeslib.as_array((C.c_uint8 * _SIZE).from_address(blk.value))
+        self._mv = memoryview((C.c_uint8 * _SIZE).from_address(blk.value)).cast("B")
         water = np.ascontiguousarray(water, np.uint8)
         H, W = water.shape
         self._h = C.c_void_p()
@@ -92,32 +104,14 @@ class DeviceStepper:
                                   px.ctypes.data_as(C.c_void_p), py.ctypes.data_as(C.c_void_p),
                                   pf.ctypes.data_as(C.c_void_p), pc.ctypes.data_as(C.c_void_p), 0, 0))
         b = blk.value
-        self._state = N.SeState(b + _X, b + _Y, b + _FUEL, b + _CARGO, b + _ORG, b + _DST,
-                                b + _REW, b + _DONE, b + _ERR, None, None, None, None, b + _REW64)
+        self._state = N.SeState(b + 0, b + 1, b + 8, b + 16, b + 2, b + 3, b + 20, b + 4, b + 5,
+                                None, None, None, None, b + 24)
         N.check(lib.se_bind(self._h, C.byref(self._state)))
         self._base = b
         self._srv = C.c_void_p()
         if self.server:
-            N.check(lib.se_server_create(C.byref(self._srv), self._h, b, _MBOX, b + _TYPE, b + _A, b + _B,
-                                         b + _TAPE, b + _MBOX))
-        self._f64 = self.h.view(np.float64)
-        self._i32 = self.h.view(np.int32)
-
-    def _put_state(self, x, y, fuel, cargo, origin, dest):
-        h = self.h
-        h[_X], h[_Y] = x, y
-        h[_ORG] = N.SE_NONE if origin is None else origin
-        h[_DST] = N.SE_NONE if dest is None else dest
-        self._f64[_FUEL // 8] = fuel
-        self._i32[_CARGO // 4] = cargo
-
-    def _get(self, err, used):
-        h = self.h
-        org, dst = int(h[_ORG]), int(h[_DST])
-        return StepResult(int(h[_X]), int(h[_Y]), float(self._f64[_FUEL // 8]),
-                          int(self._i32[_CARGO // 4]), -1 if org == N.SE_NONE else org,
-                          -1 if dst == N.SE_NONE else dst, float(self._f64[_REW64 // 8]),
-                          bool(h[_DONE]), err, used)
+            N.check(lib.se_server_create(C.byref(self._srv), self._h, b))
+        self._sv = self._srv.value
 
     def set_world(self, water, port_x, port_y, port_fuel, port_cargo):
         """Replace map and ports (a new handle: the map size may change)."""
@@ -126,39 +120,39 @@ class DeviceStepper:
 
     def step(self, x, y, fuel, cargo, origin, dest, act_type, a, b, tape):
         """tape: (u_fuel, u_gate, u_type, beta, arrive_dest), NaN / -1 where not drawn."""
-        self._put_state(x, y, fuel, cargo, origin, dest)
-        i32 = self._i32
-        i32[_TYPE // 4], i32[_A // 4], i32[_B // 4] = act_type, _clamp32(a), _clamp32(b)
-        f = self._f64
-        t0 = _TAPE // 8
-        f[t0], f[t0 + 1], f[t0 + 2], f[t0 + 3] = tape[0], tape[1], tape[2], tape[3]
-        i32[_TAPE // 4 + 8], i32[_TAPE // 4 + 9] = tape[4], 0
-        self._f64[_REW64 // 8] = 0.0
-        if self._srv.value:
-            N.check(N.lib().se_server_call(self._srv, N.SERVER_STEP))  # answered: results in the block
+        a, b = _clamp32(a), _clamp32(b)
+        _IN.pack_into(self._mv, 0, x, y, _NONE if origin is None else origin, _NONE if dest is None else dest,
+                      fuel, cargo, act_type, a, b, tape[0], tape[1], tape[2], tape[3], tape[4])
+        if self._sv:
+            rc = self._lib.se_server_call(self._sv, N.SERVER_STEP)  # answered: results in the block
+            if rc:
+                N.check(rc)
         else:
+            _AB.pack_into(self._mv, _A16, a, b)
             b_ = self._base
             stream = _raw_stream(self.dev.index)
-            N.check(N.lib().se_step_replay(self._h, b_ + _TYPE, b_ + _A, b_ + _B, b_ + _TAPE, stream))
+            N.check(self._lib.se_step_replay(self._h, b_ + _TYPE, b_ + _A16, b_ + _B16, b_ + _TAPE, stream))
             _hip_sync(stream)  # the kernel wrote its results into the pinned block
-        return self._get(int(self.h[_ERR].astype(np.int8)), int(i32[_TAPE // 4 + 9]))
+        x, y, org, dst, done, err, fuel, cargo, _, r64, used = _OUT.unpack_from(self._mv, 0)
+        return StepResult(x, y, fuel, cargo, -1 if org == _NONE else org, -1 if dst == _NONE else dst,
+                          r64, bool(done), err, used)
 
     def reset_to(self, origin, dest):
-        i32 = self._i32
-        i32[_TYPE // 4], i32[_A // 4] = origin, dest
-        if self._srv.value:
-            N.check(N.lib().se_server_call(self._srv, N.SERVER_RESET_TO))
+        _RESET_IN.pack_into(self._mv, _TYPE, origin, dest)
+        if self._sv:
+            N.check(self._lib.se_server_call(self._sv, N.SERVER_RESET_TO))
         else:
             b_ = self._base
             stream = _raw_stream(self.dev.index)
-            N.check(N.lib().se_reset_to(self._h, None, b_ + _TYPE, b_ + _A, stream))
+            N.check(self._lib.se_reset_to(self._h, None, b_ + _TYPE, b_ + _A, stream))
             _hip_sync(stream)
-        return self._get(0, 0)
+        x, y, org, dst, fuel, cargo = _RESET_OUT.unpack_from(self._mv, 0)
+        return StepResult(x, y, fuel, cargo, org, dst, 0.0, False, 0, 0)
 
     def launches(self):
         """Kernel launches of the stepper wave so far (1 + restarts after idle exits)."""
         n = C.c_uint64()
-        N.check(N.lib().se_server_launches(self._srv, C.byref(n)))
+        N.check(self._lib.se_server_launches(self._srv, C.byref(n)))
         return int(n.value)
 
     def close(self):
@@ -166,11 +160,13 @@ class DeviceStepper:
         if getattr(self, "_srv", None) is not None and self._srv.value:
             lib.se_server_destroy(self._srv)  # ends the wave
             self._srv = C.c_void_p()
+            self._sv = None
         if getattr(self, "_h", None) is not None and self._h.value:
             torch.cuda.synchronize(self.dev)
             lib.se_destroy(self._h)
             self._h = C.c_void_p()
         if getattr(self, "_blk", None) is not None and self._blk.value:
+            self._mv = None
             lib.se_host_free(self._blk)
             self._blk = C.c_void_p()
 

@@ -13,21 +13,17 @@ and seeded reference trace.
 from __future__ import annotations
 
 import ctypes as C
-import struct
 
 import numpy as np
 
 from .. import _native as N
-from ._device import StepResult
+from ._device import _IN, _OUT, _RESET_OUT, StepResult
 
 # the block: one env's SoA fields (se_state pointers), its typed action and its tape
 #   0 x u8, 1 y u8, 2 origin u8, 3 dest u8, 4 done u8, 5 err i8, 8 fuel f64, 16 cargo i32,
 #   20 reward f32, 24 reward64 f64, 32 type i32, 36 a i32, 40 b i32,
 #   48 tape {u_fuel, u_gate, u_type, beta f64; arrive_dest, used i32}
-_SIZE = 88
-_IN = struct.Struct("<4B4xdi12xiii4xddddi")          # x y org dst | fuel cargo | type a b | tape
-_OUT = struct.Struct("<4BBb2xdifd52xi")               # x y org dst done err | fuel cargo rew rew64 | used
-_RESET_OUT = struct.Struct("<4B4xdi")
+_SIZE = 88  # the structs (shared with the GPU stepper's se_server_block, whose first 88 bytes this is)
 _I32_MIN, _I32_MAX = -(2 ** 31), 2 ** 31 - 1
 _NONE = N.SE_NONE
 
