@@ -47,15 +47,16 @@ def _hip_sync(stream):
 #   0 x u8, 1 y u8, 2 origin u8, 3 dest u8, 4 done u8, 5 err i8, 8 fuel f64, 16 cargo i32,
 #   20 reward f32, 24 reward64 f64, 32 type i32, 36 a i32, 40 b i32, 44 seq0 (the wave's),
 #   48 tape {u_fuel, u_gate, u_type, beta f64; arrive_dest, used i32}, 88.. the mailbox
-# The launch path (se_step_replay wants 16-byte aligned action buffers) copies a and b to
-# 128 and 144.
+# The launch path (se_bind and se_step_replay want 16-byte aligned buffers) binds the handle
+# to a layout of 16-byte aligned fields from byte 256 (_L) and copies through it.
 _IN = struct.Struct("<4B4xdi12xiii4xddddi")          # x y org dst | fuel cargo | type a b | tape
 _OUT = struct.Struct("<4BBb2xdifd52xi")               # x y org dst done err | fuel cargo rew rew64 | used
 _RESET_OUT = struct.Struct("<4B4xdi")
 _RESET_IN = struct.Struct("<ii")                      # origin, dest into type, a
-_AB = struct.Struct("<i12xi")                         # the launch path's a (128), b (144)
-_TYPE, _A, _B, _TAPE, _A16, _B16 = 32, 36, 40, 48, 128, 144
-_SIZE = 256
+_TYPE = 32
+_L = dict(x=256, y=272, org=288, dst=304, done=320, err=336, fuel=352, cargo=368, rew=384, rew64=400,
+          type=416, a=432, b=448, tape=464)
+_SIZE = 512
 _I32_MIN, _I32_MAX = -(2 ** 31), 2 ** 31 - 1
 _NONE = N.SE_NONE
 
@@ -104,8 +105,9 @@ class DeviceStepper:
                                   px.ctypes.data_as(C.c_void_p), py.ctypes.data_as(C.c_void_p),
                                   pf.ctypes.data_as(C.c_void_p), pc.ctypes.data_as(C.c_void_p), 0, 0))
         b = blk.value
-        self._state = N.SeState(b + 0, b + 1, b + 8, b + 16, b + 2, b + 3, b + 20, b + 4, b + 5,
-                                None, None, None, None, b + 24)
+        L = {k: b + v for k, v in _L.items()}
+        self._state = N.SeState(L["x"], L["y"], L["fuel"], L["cargo"], L["org"], L["dst"], L["rew"], L["done"],
+                                L["err"], None, None, None, None, L["rew64"])
         N.check(lib.se_bind(self._h, C.byref(self._state)))
         self._base = b
         self._srv = C.c_void_p()
@@ -128,11 +130,7 @@ class DeviceStepper:
             if rc:
                 N.check(rc)
         else:
-            _AB.pack_into(self._mv, _A16, a, b)
-            b_ = self._base
-            stream = _raw_stream(self.dev.index)
-            N.check(self._lib.se_step_replay(self._h, b_ + _TYPE, b_ + _A16, b_ + _B16, b_ + _TAPE, stream))
-            _hip_sync(stream)  # the kernel wrote its results into the pinned block
+            self._launch_step()
         x, y, org, dst, done, err, fuel, cargo, _, r64, used = _OUT.unpack_from(self._mv, 0)
         return StepResult(x, y, fuel, cargo, -1 if org == _NONE else org, -1 if dst == _NONE else dst,
                           r64, bool(done), err, used)
@@ -142,12 +140,42 @@ class DeviceStepper:
         if self._sv:
             N.check(self._lib.se_server_call(self._sv, N.SERVER_RESET_TO))
         else:
-            b_ = self._base
-            stream = _raw_stream(self.dev.index)
-            N.check(self._lib.se_reset_to(self._h, None, b_ + _TYPE, b_ + _A, stream))
-            _hip_sync(stream)
+            self._launch_reset_to()
         x, y, org, dst, fuel, cargo = _RESET_OUT.unpack_from(self._mv, 0)
         return StepResult(x, y, fuel, cargo, org, dst, 0.0, False, 0, 0)
+
+    # the launch path: the block's fields through the aligned layout, one launch, one synchronise
+    def _copy(self, names, to_aligned):
+        mv = self._mv
+        src = {"x": 0, "y": 1, "org": 2, "dst": 3, "done": 4, "err": 5, "fuel": 8, "cargo": 16, "rew": 20,
+               "rew64": 24, "type": 32, "a": 36, "b": 40}
+        size = {"fuel": 8, "rew64": 8, "cargo": 4, "rew": 4, "type": 4, "a": 4, "b": 4}
+        for k in names:
+            o, n = src[k], size.get(k, 1)
+            if to_aligned:
+                mv[_L[k]:_L[k] + n] = mv[o:o + n]
+            else:
+                mv[o:o + n] = mv[_L[k]:_L[k] + n]
+
+    def _launch_step(self):
+        mv = self._mv
+        self._copy(("x", "y", "org", "dst", "fuel", "cargo", "type", "a", "b"), True)
+        mv[_L["tape"]:_L["tape"] + 40] = mv[48:88]
+        b_ = self._base
+        stream = _raw_stream(self.dev.index)
+        N.check(self._lib.se_step_replay(self._h, b_ + _L["type"], b_ + _L["a"], b_ + _L["b"], b_ + _L["tape"],
+                                         stream))
+        _hip_sync(stream)  # the kernel wrote its results into the pinned memory
+        self._copy(("x", "y", "org", "dst", "done", "err", "fuel", "cargo", "rew", "rew64"), False)
+        mv[48:88] = mv[_L["tape"]:_L["tape"] + 40]
+
+    def _launch_reset_to(self):
+        self._copy(("type", "a"), True)
+        b_ = self._base
+        stream = _raw_stream(self.dev.index)
+        N.check(self._lib.se_reset_to(self._h, None, b_ + _L["type"], b_ + _L["a"], stream))
+        _hip_sync(stream)
+        self._copy(("x", "y", "org", "dst", "done", "err", "fuel", "cargo", "rew"), False)
 
     def launches(self):
         """Kernel launches of the stepper wave so far (1 + restarts after idle exits)."""
