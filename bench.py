@@ -405,6 +405,9 @@ def run_rollouts(n, args, dist):
     wall = dist.max(time.perf_counter() - t0)
     total = float(sum(int(s.sum().item()) for s in kept))
     env.close()
+    k_ms = e0.elapsed_time(e1) / args.rollouts
+    steps_launch = total / args.rollouts
+    achieved = ROLLOUT_VALU_PER_STEP * steps_launch / (k_ms * 1e-3) / 1e9
     return {
         "workload": "se_rollout: 2^20 rollouts/GPU from config-3 states, max 100 counted steps "
                     "(sample_action + step, retries uncounted), Philox per rollout",
@@ -412,11 +415,22 @@ def run_rollouts(n, args, dist):
         "value": round(total * dist.world / wall, 1),
         "unit": "rollout env-steps/s",
         "ms_per_launch": round(wall / args.rollouts * 1e3, 4),
-        "kernel_ms": round(e0.elapsed_time(e1) / args.rollouts, 4),
+        "kernel_ms": round(k_ms, 4),
         "mean_steps_per_rollout": round(total / (args.rollouts * n), 2),
+        # rollout_kernel is bound by instruction issue (one rollout per lane: Philox draws,
+        # sample_action and the step's select chain; 20 VGPRs, no HBM stream to speak of):
+        # achieved = the VALU wave instructions per counted step of the committed PMC pass
+        # (profiles/r06/rollout/summary.json, SQ_INSTS_VALU / counted steps) x this launch's
+        # counted steps / its time, against one wave64 VALU instruction per 2 cycles per SIMD
+        "roofline": {"bound": "valu-issue", "achieved": round(achieved, 1), "peak": VALU_ISSUE_PEAK_G,
+                     "unit": "G wave-instr/s", "frac": round(achieved / VALU_ISSUE_PEAK_G, 4), "traffic": None,
+                     "valu_wave_instr_per_step": ROLLOUT_VALU_PER_STEP,
+                     "source": "profiles/r06/rollout/summary.json (SQ counters, kernel trace)"},
     }
 
 
+ROLLOUT_VALU_PER_STEP = 2.9451  # SQ_INSTS_VALU per counted env-step, profiles/r06/rollout/summary.json
+VALU_ISSUE_PEAK_G = 1024 * 2.4 / 2  # 1024 SIMDs x 2.4 GHz, one wave64 VALU per 2 cycles (MI355X_MICROARCH.md)
 F32_MFMA_PEAK_TFLOPS = 157.3  # v_mfma_f32_32x32x2_f32, MI355X_MICROARCH.md
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, no sparsity)
 
