@@ -19,12 +19,12 @@ bash tools/pmc_update.sh $TAG || exit $?
 R=$(pwd)
 (export TMPDIR=/tmp && cd /tmp &&
  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_SALU \
-   --output-format csv -d "$R/$OUT" -o pmc_pol -- python3 "$R/tools/time_policy.py" --launches 3 > "$R/$OUT/pmc_pol.log" 2>&1) || exit $?
+   --output-format csv -d "$R/$OUT" -o pmc_pol -- python3 "$R/tools/time_policy.py" --preroll 300 --launches 3 > "$R/$OUT/pmc_pol.log" 2>&1) || exit $?
 (export TMPDIR=/tmp && cd /tmp &&
  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_SALU \
-   --output-format csv -d "$R/$OUT" -o pmc_pol32a -- python3 "$R/tools/time_policy.py" --precision f32 --launches 3 > "$R/$OUT/pmc_pol32a.log" 2>&1 &&
+   --output-format csv -d "$R/$OUT" -o pmc_pol32a -- python3 "$R/tools/time_policy.py" --precision f32 --preroll 300 --launches 3 > "$R/$OUT/pmc_pol32a.log" 2>&1 &&
  timeout -s KILL 120 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_COEXEC_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE \
-   --output-format csv -d "$R/$OUT" -o pmc_pol32b -- python3 "$R/tools/time_policy.py" --precision f32 --launches 3 > "$R/$OUT/pmc_pol32b.log" 2>&1) || exit $?
+   --output-format csv -d "$R/$OUT" -o pmc_pol32b -- python3 "$R/tools/time_policy.py" --precision f32 --preroll 300 --launches 3 > "$R/$OUT/pmc_pol32b.log" 2>&1) || exit $?
 # round 6: the bf16 policy's wait counters, the rollout kernel's SQ counters, config 3 / 4 against
 # bare streaming kernels of their bytes (stepbench --floor), the N = 1 stepper wave
 bash tools/pmc_policy_bf16.sh $TAG || exit $?
