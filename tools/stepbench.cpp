@@ -1,6 +1,6 @@
 // stepbench.cpp — K back-to-back se_step calls driven from C++ (tuning tool): the
 // step rate without the Python host path, for one or more library builds.
-//   hipcc -O2 -std=c++17 -o tools/stepbench tools/stepbench.cpp -ldl
+//   hipcc --offload-arch=gfx950 -O2 -std=c++17 -o tools/stepbench tools/stepbench.cpp -ldl
 //   tools/stepbench [--n N] [--config 3|4|5|6] [--steps K] [--rows R] [--floor R] lib.so [lib2.so ...]
 // (--floor R: R alternating rounds of the product's K launches and K launches of streamfloor, a
 // bare kernel on the same buffers and action rows with the step kernel's grid (one group of 4
