@@ -209,9 +209,10 @@ struct PolicyArgs {
     float* rec_fuel;
     int32_t* rec_act;
     int64_t rec_head, rec_cap;
-    // the order the envs are visited in (policy_order_kernel): position p of the launch is
-    // env order[p]; null: position p is env p
-    const uint32_t* order;
+    // the visiting order (order_chunk): null = position order; else workgroup b visits the
+    // envs [b * chunk, (b + 1) * chunk) in the order it writes to order[b * chunk ...]
+    uint32_t* order;
+    int64_t chunk;
 };
 
 // ------------------------------------------------------------------ visiting order
@@ -219,66 +220,50 @@ struct PolicyArgs {
 // agents/dqn.py:125-175): its valid rows reach fc3's second 32-row tile (the TAKE_FUEL
 // amounts), while a ship at sea needs rows 0-3 of tile 0. The policy kernels skip a
 // tile no env of the wave can use, but with ~1 ship in 5 in port hardly a 32-env tile
-// is all at sea (0.8^32). So the policy visits the envs in an order where they are:
-// each 1024-env chunk lists its ships at sea first, then those in port, each group in
-// ascending env order, and ~3 in 4 of the waves' tiles skip fc3's second tile. The
-// order changes only which lane computes which env: every output is keyed by the env
-// (actions, Philox draws, replay slots), so results are identical to position order.
-// A wave strides over the tiles (tile w + k * stride), and with a stride a multiple of 32 it
-// would meet every chunk at the same tile index, so the waves at the chunks' ends would get
-// every in-port tile (bf16 policy at 2^20: +5 us, the odd XCDs' SIMDs 10 us behind). So with
-// a visiting order, wave tile t is the order's tile (t mod c) * 32 + t / c over the c full
-// chunks (a transpose): a wave's tiles spread over the chunks' tile indices, and each meets
-// its share of in-port tiles. A relabelling of which wave computes which tile only.
-__device__ __forceinline__ int64_t order_tile(int64_t t, int64_t tiles) {
-    const uint32_t c = (uint32_t)(tiles >> 5), tt = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)t);
-    return tt < 32u * c ? (int64_t)((tt % c) * 32u + tt / c) : t;
-}
-constexpr int kOrderBlock = 256;
-constexpr int kOrderChunk = 4 * kOrderBlock;  // envs per workgroup: 4 consecutive per thread
-__global__ __launch_bounds__(kOrderBlock) void policy_order_kernel(const uint32_t* world, WorldDims dims,
-                                                                    const uint8_t* xs, const uint8_t* ys,
-                                                                    int64_t n, uint32_t* order) {
-    __shared__ uint32_t wsum[kOrderBlock / 64];
-    const LdsWorld w = world_view(dims, world);  // the cell codes, read in place (L2)
-    const int64_t base = (int64_t)blockIdx.x * kOrderChunk;
-    const int64_t e0 = base + 4 * (int64_t)threadIdx.x;
-    uint32_t live = 0u, port = 0u;  // bit j: env e0 + j exists / is on a port's cell
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if (e0 + j < n) {
-            live |= 1u << j;
-            port |= (w.port_at(xs[e0 + j], ys[e0 + j]) >= 0 ? 1u : 0u) << j;
-        }
-    }
-    // exclusive prefix of (at sea, in port) counts over the chunk, packed as two 16-bit halves
-    const uint32_t mine = (uint32_t)__popc(live & ~port) | (uint32_t)__popc(port) << 16;
+// is all at sea (0.8^32). So from 2^16 envs each workgroup takes a contiguous chunk of envs
+// and first lists them in an order where they are: its ships at sea first, then those in
+// port, each group in ascending env order (order_chunk, written to a scratch list the
+// workgroup alone reads); its waves then take the chunk's 32-env tiles round robin, so
+// ~3 in 4 of the tiles skip fc3's second tile and every wave meets its share of in-port
+// tiles. The order changes only which lane computes which env: every output is keyed by the
+// env (actions, Philox draws, replay slots), so results are identical to position order.
+// (Round 6 first built the order in a kernel of its own: 5.6 us per call in the trace.)
+// wsum: kBlock / 64 u64 of LDS (the start of the policy's LDS, before the image is staged)
+template <int kBlock>
+__device__ void order_chunk(const LdsWorld& w, const uint8_t* xs, const uint8_t* ys, int64_t c0, int len,
+                            uint32_t* out, uint64_t* wsum) {
+    // thread t walks its own run [b, e) of the chunk twice: count, then place
+    const int per = (len + kBlock - 1) / kBlock, b = (int)threadIdx.x * per, e = min(b + per, len);
+    uint32_t port = 0u;
+    for (int i = b; i < e; ++i) port += w.port_at(xs[c0 + i], ys[c0 + i]) >= 0 ? 1u : 0u;
+    const uint32_t sea = (uint32_t)max(e - b, 0) - port;
+    // exclusive prefix of (at sea, in port) over the threads, as two 32-bit halves
+    const uint64_t mine = (uint64_t)sea | (uint64_t)port << 32;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t inc = mine;
+    uint64_t inc = mine;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t u = __shfl_up(inc, d);
-        inc += lane >= d ? u : 0u;
+        const uint64_t u = __shfl_up(inc, d);
+        inc += lane >= d ? u : 0ull;
     }
     if (lane == 63) wsum[wv] = inc;
     __syncthreads();
-    uint32_t off = 0u, total = 0u;
+    uint64_t off = 0ull, total = 0ull;
 #pragma unroll
-    for (int i = 0; i < kOrderBlock / 64; ++i) {
-        off += i < wv ? wsum[i] : 0u;
+    for (int i = 0; i < kBlock / 64; ++i) {
+        off += i < wv ? wsum[i] : 0ull;
         total += wsum[i];
     }
-    const uint32_t ex = inc - mine + off;
-    int64_t sea = base + (ex & 0xffffu), inport = base + (total & 0xffffu) + (ex >> 16);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if ((live >> j) & 1u) {
-            const bool p = (port >> j) & 1u;
-            order[p ? inport : sea] = (uint32_t)(e0 + j);
-            inport += p ? 1 : 0;
-            sea += p ? 0 : 1;
-        }
+    const uint64_t ex = inc - mine + off;
+    uint32_t at_sea = (uint32_t)ex, in_port = (uint32_t)total + (uint32_t)(ex >> 32);
+    for (int i = b; i < e; ++i) {
+        const bool p = w.port_at(xs[c0 + i], ys[c0 + i]) >= 0;
+        out[p ? in_port : at_sea] = (uint32_t)(c0 + i);
+        in_port += p ? 1u : 0u;
+        at_sea += p ? 0u : 1u;
     }
+    __threadfence_block();  // the list is complete before any wave of the workgroup reads it
+    __syncthreads();
 }
 
 // v = p0 + p1 + p2, each the bf16 rounding of the remainder (exact f32 subtractions)
@@ -542,13 +527,34 @@ void policy_kernel(PolicyArgs A) {
         uint32_t x, y, o8, d8;
         int64_t e;  // the env (A.order), past A.n for the last tile's idle lanes
     };
+    // the visiting order: this workgroup's chunk and its list (null: position order)
+    const uint32_t* ord = nullptr;
+    int64_t c0 = 0;
+    int len = 0;
+    if (A.order) {
+        c0 = (int64_t)blockIdx.x * A.chunk;
+        len = (int)min(A.chunk, A.n - c0);
+        uint32_t* list = A.order + c0;
+        order_chunk<kPolicyBlock>(world_view(A.dims, A.world), A.st.x, A.st.y, c0, len, list,
+                                  reinterpret_cast<uint64_t*>(smem));
+        ord = list;
+    }
     auto load_env = [&](int64_t tile) {
-        const int64_t p = (A.order ? order_tile(tile, tiles) : tile) * 32 + r;
-        const int64_t pi = p < A.n ? p : A.n - 1;
-        const int64_t ei = A.order ? (int64_t)A.order[pi] : pi;
-        return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei], p < A.n ? ei : A.n};
+        const int64_t p = tile * 32 + r;
+        int64_t ei;
+        bool live;
+        if (ord) {
+            live = p < len;
+            ei = (int64_t)ord[live ? p : len - 1];
+        } else {
+            live = p < A.n;
+            ei = live ? p : A.n - 1;
+        }
+        return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei], live ? ei : A.n};
     };
-    int64_t tile = (int64_t)blockIdx.x * kPolicyWaves + (threadIdx.x >> 6);
+    // tiles: the chunk's (waves round robin) or all of them (striding over the grid)
+    const int64_t my_tiles = ord ? (len + 31) >> 5 : tiles;
+    int64_t tile = ord ? (threadIdx.x >> 6) : (int64_t)blockIdx.x * kPolicyWaves + (threadIdx.x >> 6);
     if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 12) __builtin_amdgcn_s_setprio(1);
     const int qwords = q.bytes() / 16;
     // fc1's bias rides in the padding half of its single k-step: lanes 32-63 of each W1
@@ -585,12 +591,12 @@ void policy_kernel(PolicyArgs A) {
     const uint32_t* REGM = reinterpret_cast<const uint32_t*>(qb + q.regm());
 
     const int P = q.P;
-    const int64_t stride = (int64_t)gridDim.x * kPolicyWaves;
-    EnvIn nxt = load_env(tile < tiles ? tile : 0);
-    for (; tile < tiles; tile += stride, ++tile_iter) {
+    const int64_t stride = ord ? kPolicyWaves : (int64_t)gridDim.x * kPolicyWaves;
+    EnvIn nxt = load_env(tile < my_tiles ? tile : 0);
+    for (; tile < my_tiles; tile += stride, ++tile_iter) {
         X3STAMP(0);
         const EnvIn cur_in = nxt;
-        if (tile + stride < tiles) nxt = load_env(tile + stride);
+        if (tile + stride < my_tiles) nxt = load_env(tile + stride);
         const int64_t e = cur_in.e;
         const bool live = e < A.n;
         const int x = (int)cur_in.x, y = (int)cur_in.y;
@@ -1180,17 +1186,38 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
         __device__ uint32_t o8() const { return (pk >> 16) & 0xffu; }
         __device__ uint32_t d8() const { return pk >> 24; }
     };
+    // the visiting order: this workgroup's chunk and its list (null: position order)
+    const uint32_t* ord = nullptr;
+    int64_t c0 = 0;
+    int len = 0;
+    if (A.order) {
+        c0 = (int64_t)blockIdx.x * A.chunk;
+        len = (int)min(A.chunk, A.n - c0);
+        uint32_t* list = A.order + c0;
+        order_chunk<kPolicyX3Block>(world_view(A.dims, A.world), A.st.x, A.st.y, c0, len, list,
+                                    reinterpret_cast<uint64_t*>(smem));
+        ord = list;
+    }
     auto load_env = [&](int64_t t) {
-        const int64_t p = (A.order ? order_tile(t, tiles) : t) * 32 + (lane & 31);
-        const int64_t pi = min(p, A.n - 1);
-        const int64_t ei = A.order ? (int64_t)A.order[pi] : pi;
+        const int64_t p = t * 32 + (lane & 31);
+        int64_t ei;
+        bool live;
+        if (ord) {
+            live = p < len;
+            ei = (int64_t)ord[live ? p : len - 1];
+        } else {
+            live = p < A.n;
+            ei = live ? p : A.n - 1;
+        }
         const uint32_t pk = (uint32_t)A.st.x[ei] | (uint32_t)A.st.y[ei] << 8 | (uint32_t)A.st.origin[ei] << 16 |
                             (uint32_t)A.st.dest[ei] << 24;
-        return EnvIn{A.st.fuel[ei], pk, (uint32_t)(p < A.n ? ei : A.n)};
+        return EnvIn{A.st.fuel[ei], pk, (uint32_t)(live ? ei : A.n)};
     };
-    int64_t tile = (int64_t)blockIdx.x * kPolicyX3Waves + (threadIdx.x >> 6);
-    EnvIn nxt = load_env(tile < tiles ? tile : 0);
-    const int64_t stride = (int64_t)gridDim.x * kPolicyX3Waves;
+    // tiles: the chunk's (waves round robin) or all of them (striding over the grid)
+    const int64_t my_tiles = ord ? (len + 31) >> 5 : tiles;
+    int64_t tile = ord ? (threadIdx.x >> 6) : (int64_t)blockIdx.x * kPolicyX3Waves + (threadIdx.x >> 6);
+    EnvIn nxt = load_env(tile < my_tiles ? tile : 0);
+    const int64_t stride = ord ? kPolicyX3Waves : (int64_t)gridDim.x * kPolicyX3Waves;
     if constexpr (kW3Global) {  // fc3 stays in the packed global image: copy the rest
         const int staged = D.w3() / 16;
         for (int i = threadIdx.x; i < staged; i += kPolicyX3Block) smem[i] = A.qimg[i];
@@ -1230,12 +1257,12 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
     if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
     EnvValid vnxt = env_valid(w, q, SAME, (int)nxt.x8(), (int)nxt.y8(), nxt.o8() == SE_NONE ? -1 : (int)nxt.o8());
     [[maybe_unused]] int tile_iter = 0;  // SHIPENV_X3_TRACE: the wave's 4th tile is stamped
-    while (tile < tiles) {
+    while (tile < my_tiles) {
         X3STAMP(0);
         const EnvIn in = nxt;
         const EnvValid v = vnxt;
         const int64_t tnext = tile + stride;
-        const bool more = tnext < tiles;
+        const bool more = tnext < my_tiles;
         if (more) nxt = load_env(tnext);
         const int64_t e = in.e;
         const bool live = e < A.n;
@@ -1411,7 +1438,7 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
         }
         FINISH_ENV(v, e, live, h, best, bidx, x8, y8, o8, d8, ff);
         X3STAMP(8);
-        tile = more ? tnext : tiles;
+        tile = more ? tnext : my_tiles;
         ++tile_iter;
     }
     X3STAMP_ANY(11);
@@ -1431,7 +1458,7 @@ struct se_qnet {
     bool packed = false;
     uint8_t* d_img32 = nullptr;  // se_policy_f32's split image (the full layout's fc3, global)
     int img32_bytes = 0;
-    // the visiting order (policy_order_kernel): used when n >= order_min_envs, resolved once
+    // the visiting order's scratch list (order_chunk): used when n >= order_min_envs, resolved once
     // by se_qnet_create (SHIPENV_POLICY_ORDER: 0 never, 1 always; unset: from 2^16 envs)
     uint32_t* d_order = nullptr;
     int64_t order_cap = 0, order_min_envs = (int64_t)1 << 16;
@@ -1486,23 +1513,25 @@ int se_qnet_set_weights(se_qnet* qn, const float* w1, const float* b1, const flo
 }  // extern "C"
 
 namespace {
-// this launch's visiting order, computed on the stream ahead of the policy kernel, or null
-// (position order: small launches, where the extra launch would cost more than it saves)
-int policy_order(se_qnet* qn, hipStream_t s, const uint32_t** out) {
+// the visiting order's chunk per workgroup (a multiple of 32) and the grid that covers n with
+// it, and the scratch list (A.order, A.chunk); position order below order_min_envs
+int policy_order(se_qnet* qn, int* grid, PolicyArgs& A) {
     se_env* env = qn->env;
-    *out = nullptr;
+    A.order = nullptr;
+    A.chunk = 0;
     if (env->n < qn->order_min_envs) return SE_OK;
-    if (env->n > qn->order_cap) {
+    const int64_t per = (env->n + *grid - 1) / *grid;
+    const int64_t chunk = (per + 31) & ~(int64_t)31;
+    const int64_t g = (env->n + chunk - 1) / chunk;
+    if (g * chunk > qn->order_cap) {
         if (qn->d_order) HIP_TRY(hipFree(qn->d_order));
         qn->d_order = nullptr;
-        HIP_TRY(hipMalloc(&qn->d_order, (size_t)env->n * sizeof(uint32_t)));
-        qn->order_cap = env->n;
+        HIP_TRY(hipMalloc(&qn->d_order, (size_t)(g * chunk) * sizeof(uint32_t)));
+        qn->order_cap = g * chunk;
     }
-    const int64_t blocks = (env->n + kOrderChunk - 1) / kOrderChunk;
-    policy_order_kernel<<<(unsigned)blocks, kOrderBlock, 0, s>>>(env->d_world, env->dims, env->st.x, env->st.y,
-                                                                 env->n, qn->d_order);
-    HIP_TRY(hipGetLastError());
-    *out = qn->d_order;
+    *grid = (int)g;
+    A.order = qn->d_order;
+    A.chunk = chunk;
     return SE_OK;
 }
 
@@ -1542,9 +1571,9 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
     const int64_t tiles = (env->n + 31) / 32;
     const int64_t want = (tiles + kPolicyWaves - 1) / kPolicyWaves;
     const int64_t resident = (int64_t)dev_cus * kPolicyWgPerCu;  // workgroups resident at once
-    const int grid = (int)(want < resident ? want : resident);
+    int grid = (int)(want < resident ? want : resident);
     PolicyArgs A{};
-    rc = policy_order(qn, (hipStream_t)stream, &A.order);
+    rc = policy_order(qn, &grid, A);
     if (rc) return rc;
     A.world = env->d_world;
     A.dims = env->dims;
@@ -1610,9 +1639,9 @@ int launch_policy_x3(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, 
         dev_cus = 256;
     const int64_t tiles = (env->n + 31) / 32;
     const int64_t want = (tiles + kPolicyX3Waves - 1) / kPolicyX3Waves;
-    const int grid = (int)(want < dev_cus ? want : dev_cus);
+    int grid = (int)(want < dev_cus ? want : dev_cus);
     PolicyArgs A{};
-    rc = policy_order(qn, s, &A.order);
+    rc = policy_order(qn, &grid, A);
     if (rc) return rc;
     A.world = env->d_world;
     A.dims = env->dims;
