@@ -228,43 +228,64 @@ struct PolicyArgs {
 // tiles. The order changes only which lane computes which env: every output is keyed by the
 // env (actions, Philox draws, replay slots), so results are identical to position order.
 // (Round 6 first built the order in a kernel of its own: 5.6 us per call in the trace.)
-// wsum: kBlock / 64 u64 of LDS (the start of the policy's LDS, before the image is staged)
-template <int kBlock>
-__device__ void order_chunk(const LdsWorld& w, const uint8_t* xs, const uint8_t* ys, int64_t c0, int len,
-                            uint32_t* out, uint64_t* wsum) {
-    // thread t walks its own run [b, e) of the chunk twice: count, then place
-    const int per = (len + kBlock - 1) / kBlock, b = (int)threadIdx.x * per, e = min(b + per, len);
-    uint32_t port = 0u;
-    for (int i = b; i < e; ++i) port += w.port_at(xs[c0 + i], ys[c0 + i]) >= 0 ? 1u : 0u;
-    const uint32_t sea = (uint32_t)max(e - b, 0) - port;
-    // exclusive prefix of (at sea, in port) over the threads, as two 32-bit halves
-    const uint64_t mine = (uint64_t)sea | (uint64_t)port << 32;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint64_t inc = mine;
+// In two halves, so that a kernel can stage its image between them (the counting half's
+// loads then overlap the staging): count() walks thread t's own run [b, e) of the chunk and
+// counts its ships in port; place() scans the counts over the workgroup (wsum: kBlock / 64 u64
+// of LDS) and writes the list. place() ends with a barrier.
+constexpr uint32_t kOrderNone = 0xffffffffu;
+struct OrderRun {
+    int b = 0, e = 0;
+    uint32_t port = 0u, bits = 0u;  // bits: the first 32 envs' in-port flags, for place()
+
+    template <int kBlock>
+    __device__ __forceinline__ void count(const LdsWorld& w, const uint8_t* xs, const uint8_t* ys, int64_t c0,
+                                          int len) {
+        const int per = (len + kBlock - 1) / kBlock;
+        b = (int)threadIdx.x * per;
+        e = min(b + per, len);
+        for (int i = b; i < e; ++i) {
+            const uint32_t f = w.port_at(xs[c0 + i], ys[c0 + i]) >= 0 ? 1u : 0u;
+            port += f;
+            bits |= i - b < 32 ? f << (i - b) : 0u;
+        }
+    }
+
+    // the list's tail up to a whole tile reads kOrderNone (an idle lane)
+    template <int kBlock>
+    __device__ __forceinline__ void place(const LdsWorld& w, const uint8_t* xs, const uint8_t* ys, int64_t c0,
+                                          int len, uint32_t* out, uint64_t* wsum) const {
+        if ((int)threadIdx.x < ((-len) & 31)) out[len + threadIdx.x] = kOrderNone;
+        const uint32_t sea = (uint32_t)max(e - b, 0) - port;
+        // exclusive prefix of (at sea, in port) over the threads, as two 32-bit halves
+        const uint64_t mine = (uint64_t)sea | (uint64_t)port << 32;
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        uint64_t inc = mine;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t u = __shfl_up(inc, d);
-        inc += lane >= d ? u : 0ull;
-    }
-    if (lane == 63) wsum[wv] = inc;
-    __syncthreads();
-    uint64_t off = 0ull, total = 0ull;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t u = __shfl_up(inc, d);
+            inc += lane >= d ? u : 0ull;
+        }
+        if (lane == 63) wsum[wv] = inc;
+        __syncthreads();
+        uint64_t off = 0ull, total = 0ull;
 #pragma unroll
-    for (int i = 0; i < kBlock / 64; ++i) {
-        off += i < wv ? wsum[i] : 0ull;
-        total += wsum[i];
+        for (int i = 0; i < kBlock / 64; ++i) {
+            off += i < wv ? wsum[i] : 0ull;
+            total += wsum[i];
+        }
+        const uint64_t ex = inc - mine + off;
+        uint32_t at_sea = (uint32_t)ex, in_port = (uint32_t)total + (uint32_t)(ex >> 32);
+        for (int i = b; i < e; ++i) {
+            const bool p = i - b < 32 ? ((bits >> (i - b)) & 1u) != 0u : w.port_at(xs[c0 + i], ys[c0 + i]) >= 0;
+            out[p ? in_port : at_sea] = (uint32_t)(c0 + i);
+            in_port += p ? 1u : 0u;
+            at_sea += p ? 0u : 1u;
+        }
+        __threadfence_block();  // the list is complete before any wave of the workgroup reads it
+        __syncthreads();
     }
-    const uint64_t ex = inc - mine + off;
-    uint32_t at_sea = (uint32_t)ex, in_port = (uint32_t)total + (uint32_t)(ex >> 32);
-    for (int i = b; i < e; ++i) {
-        const bool p = w.port_at(xs[c0 + i], ys[c0 + i]) >= 0;
-        out[p ? in_port : at_sea] = (uint32_t)(c0 + i);
-        in_port += p ? 1u : 0u;
-        at_sea += p ? 0u : 1u;
-    }
-    __threadfence_block();  // the list is complete before any wave of the workgroup reads it
-    __syncthreads();
-}
+};
+constexpr int kOrderScanBytes = 16 * 8;  // place()'s wsum, past the policy's LDS (<= 16 waves)
 
 // v = p0 + p1 + p2, each the bf16 rounding of the remainder (exact f32 subtractions)
 __device__ __forceinline__ void split3(float v, __bf16& p0, __bf16& p1, __bf16& p2) {
@@ -531,30 +552,26 @@ void policy_kernel(PolicyArgs A) {
     const uint32_t* ord = nullptr;
     int64_t c0 = 0;
     int len = 0;
-    if (A.order) {
+    OrderRun orun;
+    if (A.order) {  // counted here, placed once the image is staged (the loads overlap it)
         c0 = (int64_t)blockIdx.x * A.chunk;
-        len = (int)min(A.chunk, A.n - c0);
-        uint32_t* list = A.order + c0;
-        order_chunk<kPolicyBlock>(world_view(A.dims, A.world), A.st.x, A.st.y, c0, len, list,
-                                  reinterpret_cast<uint64_t*>(smem));
-        ord = list;
+        len = __builtin_amdgcn_readfirstlane((int)min(A.chunk, A.n - c0));  // uniform: an SGPR
+        orun.count<kPolicyBlock>(world_view(A.dims, A.world), A.st.x, A.st.y, c0, len);
     }
     auto load_env = [&](int64_t tile) {
         const int64_t p = tile * 32 + r;
         int64_t ei;
         bool live;
-        if (ord) {
-            live = p < len;
-            ei = (int64_t)ord[live ? p : len - 1];
+        if (ord) {  // p < the chunk's whole tiles: its tail reads kOrderNone
+            const uint32_t v = ord[p];
+            live = v != kOrderNone;
+            ei = live ? (int64_t)v : A.n - 1;
         } else {
             live = p < A.n;
             ei = live ? p : A.n - 1;
         }
         return EnvIn{A.st.fuel[ei], A.st.x[ei], A.st.y[ei], A.st.origin[ei], A.st.dest[ei], live ? ei : A.n};
     };
-    // tiles: the chunk's (waves round robin) or all of them (striding over the grid)
-    const int64_t my_tiles = ord ? (len + 31) >> 5 : tiles;
-    int64_t tile = ord ? (threadIdx.x >> 6) : (int64_t)blockIdx.x * kPolicyWaves + (threadIdx.x >> 6);
     if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 12) __builtin_amdgcn_s_setprio(1);
     const int qwords = q.bytes() / 16;
     // fc1's bias rides in the padding half of its single k-step: lanes 32-63 of each W1
@@ -578,6 +595,13 @@ void policy_kernel(PolicyArgs A) {
         }
     }
     const LdsWorld w = stage_world(A.world, A.dims, reinterpret_cast<uint32_t*>(smem + qwords));
+    if (A.order) {
+        uint32_t* list = A.order + c0;
+        uint64_t* wsum = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(smem) +
+                                                     ((q.bytes() + 4 * A.dims.padded() + 7) & ~7));
+        orun.place<kPolicyBlock>(w, A.st.x, A.st.y, c0, len, list, wsum);
+        ord = list;
+    }
     X3STAMP_ANY(10);
     [[maybe_unused]] int tile_iter = 0;  // SHIPENV_X3_TRACE: the wave's 4th tile is stamped
     const uint8_t* qb = reinterpret_cast<const uint8_t*>(smem);
@@ -591,7 +615,12 @@ void policy_kernel(PolicyArgs A) {
     const uint32_t* REGM = reinterpret_cast<const uint32_t*>(qb + q.regm());
 
     const int P = q.P;
-    const int64_t stride = ord ? kPolicyWaves : (int64_t)gridDim.x * kPolicyWaves;
+    // tiles: the chunk's (waves round robin) or all of them (striding over the grid); after
+    // the order is placed (A.order: the tile loop reads the list)
+    const bool ordered = A.order != nullptr;
+    const int64_t my_tiles = ordered ? (len + 31) >> 5 : tiles;
+    int64_t tile = ordered ? (threadIdx.x >> 6) : (int64_t)blockIdx.x * kPolicyWaves + (threadIdx.x >> 6);
+    const int64_t stride = ordered ? kPolicyWaves : (int64_t)gridDim.x * kPolicyWaves;
     EnvIn nxt = load_env(tile < my_tiles ? tile : 0);
     for (; tile < my_tiles; tile += stride, ++tile_iter) {
         X3STAMP(0);
@@ -1192,19 +1221,22 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
     int len = 0;
     if (A.order) {
         c0 = (int64_t)blockIdx.x * A.chunk;
-        len = (int)min(A.chunk, A.n - c0);
+        len = __builtin_amdgcn_readfirstlane((int)min(A.chunk, A.n - c0));  // uniform: an SGPR
         uint32_t* list = A.order + c0;
-        order_chunk<kPolicyX3Block>(world_view(A.dims, A.world), A.st.x, A.st.y, c0, len, list,
-                                    reinterpret_cast<uint64_t*>(smem));
+        const LdsWorld wg = world_view(A.dims, A.world);
+        OrderRun orun;
+        orun.count<kPolicyX3Block>(wg, A.st.x, A.st.y, c0, len);
+        orun.place<kPolicyX3Block>(wg, A.st.x, A.st.y, c0, len, list, reinterpret_cast<uint64_t*>(smem));
         ord = list;
     }
     auto load_env = [&](int64_t t) {
         const int64_t p = t * 32 + (lane & 31);
         int64_t ei;
         bool live;
-        if (ord) {
-            live = p < len;
-            ei = (int64_t)ord[live ? p : len - 1];
+        if (ord) {  // p < the chunk's whole tiles: its tail reads kOrderNone
+            const uint32_t v = ord[p];
+            live = v != kOrderNone;
+            ei = live ? (int64_t)v : A.n - 1;
         } else {
             live = p < A.n;
             ei = live ? p : A.n - 1;
@@ -1558,7 +1590,7 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
     DeviceGuard g(env->device);
     // the compact layout unless every row's Q is wanted
     const QnetDims& q = q_out ? qn->q : qn->qc;
-    const size_t lds = (size_t)q.bytes() + lds_bytes(env);
+    const size_t lds = (((size_t)q.bytes() + lds_bytes(env) + 7) & ~(size_t)7) + kOrderScanBytes;
     static std::atomic<uint64_t> lds_set{0};
     static std::atomic<uint64_t> lds_set_q{0};
     rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(policy_kernel<false>), 160 * 1024, env->device);
