@@ -432,8 +432,8 @@ def test_f32_unaligned_weights_choose_as_aligned(ports):
 @pytest.mark.parametrize("precision", ["bf16", "f32"])
 @pytest.mark.parametrize("n,ports,steps", [(8192 + 7, None, 40), (2048 + 5, SHARED, 30), (4096 + 33, "64", 5)])
 def test_visiting_order_changes_nothing(monkeypatch, precision, n, ports, steps):
-    """policy_order_kernel (csrc/qpolicy.h): the policy visits each 1024-env chunk's ships at
-    sea first, then those in port, so most 32-env tiles skip fc3's second tile. It is on from
+    """The visiting order (csrc/qpolicy.h OrderRun): each policy workgroup visits its chunk's
+    ships at sea first, then those in port, so most 32-env tiles skip fc3's second tile. It is on from
     2^16 envs; SHIPENV_POLICY_ORDER=1 forces it (read when the policy is created), 0 turns it
     off. The order only moves envs between lanes: greedy and exploring actions, the q_out rows
     and the replay ring's records (se_policy_record) equal position order's, bit for bit."""

@@ -47,11 +47,11 @@ def main():
     py = torch.as_tensor(env.port_y, device="cuda:0").long()
     at = ((env.x.long()[:, None] == px[None]) & (env.y.long()[:, None] == py[None])).any(1)
     waves_any = at.view(-1, 32).any(1).float().mean() if a.n % 32 == 0 else float("nan")
-    # the same in the policy's visiting order (qpolicy.h policy_order_kernel: each 1024-env
-    # chunk's ships at sea first): the share of 32-env tiles that need fc3's second tile
+    # the same in the policy's visiting order (qpolicy.h OrderRun: each workgroup's chunk of
+    # 4096 envs at 2^20, ships at sea first): the share of 32-env tiles that need fc3's second tile
     ordered = float("nan")
-    if a.n % 1024 == 0:
-        c = at.view(-1, 1024).sort(dim=1, stable=True).values  # False (at sea) first
+    if a.n % 4096 == 0:
+        c = at.view(-1, 4096).sort(dim=1, stable=True).values  # False (at sea) first
         ordered = float(c.view(-1, 32).any(1).float().mean())
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
