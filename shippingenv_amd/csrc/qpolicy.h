@@ -880,6 +880,7 @@ void policy_kernel(PolicyArgs A) {
 // (the full layout). One 32-env tile per wave; 512-thread workgroups, one per CU.
 struct QnetX3Dims {
     QnetDims q;
+    int32_t zrow;  // bf16x8 index, at k-step 0 and part 0, of a zero row of fc3's last tile (lane 31 of it), or -1
     __host__ __device__ int w1() const { return 0; }  // fc1: bf16 fragments [mt][2 steps][lane] (8 KB)
     __host__ __device__ int w2() const { return 8192; }                 // [mt][kt][s][part] bf16 fragments: 96 KB
     __host__ __device__ int b1() const { return w2() + 96 * 1024; }
@@ -1398,16 +1399,52 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
         // no validity test and never picks it.
         X3STAMP(5);
         auto mask_of = [&](int mt) { return tile_mask(v, mt, P); };
-        f32x16 c = kQout ? bias_frag(B3 + 4 * h) : masked_bias(B3 + 4 * h, mask_of(0) >> (4 * h));
+        // a tile of ships at sea only (uniform; ~3 in 4 under the visiting order) needs rows 0-3
+        // (the moves) of fc3 tile 0: its six part products go as three chains, one per
+        // activation part x_j, each over the weight parts w_p with p + j <= 2 stacked in the
+        // MFMA's rows (x0: w0, w1, w2 in rows 0-3, 4-7, 8-11; x1: w0, w1; x2: w0; the other
+        // rows read a zero row of the image), 24 MFMAs where the tile takes 48. Q(row r) = rows
+        // r + (4 + r) + (8 + r): the same six products per k-step, summed by chain (an fp32
+        // rounding per MFMA as before, in another order: not the same bits as the full tile).
+        // 0.2409 -> 0.2275 ms per call at 2^20 (profiles/r06/order/ab_x3_stack.jsonl); the LDS
+        // image only (the global-image variant would spill).
+        const bool stack = !kW3Global && !kQout && D.zrow >= 0 && !__any(v.cur >= 0);
+        f32x16 c;
+        if (stack) {
+            c = f32x16{};
+            if (h == 0) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            if (32 + k + kLa < 40) frag_of(32 + k + kLa, wf[(32 + k + kLa) % (kLa + 1)]);
+                for (int i = 0; i < 4; ++i) c[i] = B3[i];
+            }
+            const int r = lane & 31;
+            // bf16x8 index of k-step 0's operand for chain j (k-step k adds 192)
+            const int zero = D.zrow + 32 * h;
+            const int src = (r >> 2) * 64 + (r & 3) + 32 * h;
+            const int o0 = r < 12 ? src : zero, o1 = r < 8 ? src : zero, o2 = r < 4 ? src : zero;
 #pragma unroll
-            for (int half = 0; half < 2; ++half) {
-                c = khalf_x3(wf[(32 + k) % (kLa + 1)], X2[k >> 1][k & 1], c, half);
-                const int g = 2 * k + half;
-                if (g < 8) split_pair(acc[3], X2[3], g);
+            for (int k = 0; k < 8; ++k) {
+                const bf16x8 a2 = W3[k * 192 + o2], a1 = W3[k * 192 + o1], a0 = W3[k * 192 + o0];
+                c = mfma_bf16(a2, X2[k >> 1][k & 1][2], c);
+                c = mfma_bf16(a1, X2[k >> 1][k & 1][1], c);
+                c = mfma_bf16(a0, X2[k >> 1][k & 1][0], c);
+                if (k < 4) {  // X2[3] complete before k-step 6 reads it
+                    split_pair(acc[3], X2[3], 2 * k);
+                    split_pair(acc[3], X2[3], 2 * k + 1);
+                }
                 __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+            c = kQout ? bias_frag(B3 + 4 * h) : masked_bias(B3 + 4 * h, mask_of(0) >> (4 * h));
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (32 + k + kLa < 40) frag_of(32 + k + kLa, wf[(32 + k + kLa) % (kLa + 1)]);
+#pragma unroll
+                for (int half = 0; half < 2; ++half) {
+                    c = khalf_x3(wf[(32 + k) % (kLa + 1)], X2[k >> 1][k & 1], c, half);
+                    const int g = 2 * k + half;
+                    if (g < 8) split_pair(acc[3], X2[3], g);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             }
         }
         X3STAMP(6);
@@ -1461,6 +1498,16 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
         X3STAMP(7);
         if (kQout) {
             tile_argmax(c, pm, prm, pbase, h, best, bidx);
+        } else if (stack) {  // rows 0-3 from the three chains' partial rows
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float qi = (c[i] + __shfl_xor(c[i], 32)) + c[4 + i];
+                const bool better = qi > best;  // ascending rows: the first maximum
+                best = better ? qi : best;
+                bidx = better ? i : bidx;
+            }
+            best = h ? -INFINITY : best;  // lane half 1 holds no row of its own
+            bidx = h ? 0x7fffffff : bidx;
         } else {
             best0 = best;
 #pragma unroll
@@ -1641,6 +1688,8 @@ int launch_policy_x3(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, 
     se_env* env = qn->env;
     QnetX3Dims d;
     d.q = q_out ? qn->q : qn->qc;  // the compact rows unless every row's Q is wanted
+    // a zero row of fc3's last tile (row 32 mt3 - 1, past the layout's rows), or none
+    d.zrow = d.q.rows < 32 * d.q.mt3 ? (d.q.mt3 - 1) * 8 * 192 + 31 : -1;
     if (d.bytes() > qn->img32_bytes) {
         if (qn->d_img32) HIP_TRY(hipFree(qn->d_img32));
         qn->d_img32 = nullptr;

@@ -436,7 +436,10 @@ def test_visiting_order_changes_nothing(monkeypatch, precision, n, ports, steps)
     ships at sea first, then those in port, so most 32-env tiles skip fc3's second tile. It is on from
     2^16 envs; SHIPENV_POLICY_ORDER=1 forces it (read when the policy is created), 0 turns it
     off. The order only moves envs between lanes: greedy and exploring actions, the q_out rows
-    and the replay ring's records (se_policy_record) equal position order's, bit for bit."""
+    and the replay ring's records (se_policy_record) equal position order's, bit for bit. (The
+    fp32 policy sums a sea tile's rows 0-3 by activation part, so there its Q bits may differ
+    from a mixed tile's in the last place: a near-tie could flip a greedy action; these states
+    have none, and q_out takes the full tiles in both orders.)"""
     from conftest import golden_water
     from shippingenv_amd.dqn import MiniBatch, ReplayBuffer
     from shippingenv_amd.policy import QPolicy
