@@ -236,13 +236,49 @@ constexpr uint32_t kOrderNone = 0xffffffffu;
 struct OrderRun {
     int b = 0, e = 0;
     uint32_t port = 0u, bits = 0u;  // bits: the first 32 envs' in-port flags, for place()
+    // load(): a run of 4, 8, 12 or 16 envs on a 4-byte boundary (2^20 envs: 4 per thread in the
+    // bf16 kernel, 8 in the fp32 one) is loaded as whole words, issued before the image is
+    // staged and used after it, so the loads overlap the staging; other runs go byte by byte
+    // in count() (the first form issued a dependent load chain per env: +3.3 / +8.6 us on the
+    // two kernels' prologues, profiles/r06/order/trace_prologue.jsonl)
+    static constexpr int kWords = 4;
+    uint32_t xw[kWords] = {}, yw[kWords] = {};
+    bool words = false;
 
     template <int kBlock>
-    __device__ __forceinline__ void count(const LdsWorld& w, const uint8_t* xs, const uint8_t* ys, int64_t c0,
-                                          int len) {
+    __device__ __forceinline__ void load(const uint8_t* xs, const uint8_t* ys, int64_t c0, int len) {
         const int per = (len + kBlock - 1) / kBlock;
         b = (int)threadIdx.x * per;
         e = min(b + per, len);
+        // uniform; with len a multiple of 4 every run is whole words, none reads past the chunk
+        words = (per & 3) == 0 && per <= 4 * kWords && (c0 & 3) == 0 && (len & 3) == 0;
+        if (words) {
+            const uint32_t* x4 = reinterpret_cast<const uint32_t*>(xs + c0 + b);
+            const uint32_t* y4 = reinterpret_cast<const uint32_t*>(ys + c0 + b);
+#pragma unroll
+            for (int k = 0; k < kWords; ++k) {
+                if (4 * k < e - b) {  // e - b: per, or a shorter multiple of 4 for the chunk's last runs
+                    xw[k] = x4[k];
+                    yw[k] = y4[k];
+                }
+            }
+        }
+    }
+
+    template <int kBlock>
+    __device__ __forceinline__ void count(const LdsWorld& w, const uint8_t* xs, const uint8_t* ys, int64_t c0) {
+        if (words) {
+#pragma unroll
+            for (int k = 0; k < 4 * kWords; ++k) {
+                if (k < e - b) {
+                    const int x = (int)((xw[k >> 2] >> (8 * (k & 3))) & 0xffu), y = (int)((yw[k >> 2] >> (8 * (k & 3))) & 0xffu);
+                    const uint32_t f = w.port_at(x, y) >= 0 ? 1u : 0u;
+                    port += f;
+                    bits |= f << k;
+                }
+            }
+            return;
+        }
         for (int i = b; i < e; ++i) {
             const uint32_t f = w.port_at(xs[c0 + i], ys[c0 + i]) >= 0 ? 1u : 0u;
             port += f;
@@ -553,10 +589,10 @@ void policy_kernel(PolicyArgs A) {
     int64_t c0 = 0;
     int len = 0;
     OrderRun orun;
-    if (A.order) {  // counted here, placed once the image is staged (the loads overlap it)
+    if (A.order) {  // loaded here, counted and placed once the image and the world are staged
         c0 = (int64_t)blockIdx.x * A.chunk;
         len = __builtin_amdgcn_readfirstlane((int)min(A.chunk, A.n - c0));  // uniform: an SGPR
-        orun.count<kPolicyBlock>(world_view(A.dims, A.world), A.st.x, A.st.y, c0, len);
+        orun.load<kPolicyBlock>(A.st.x, A.st.y, c0, len);
     }
     auto load_env = [&](int64_t tile) {
         const int64_t p = tile * 32 + r;
@@ -599,6 +635,7 @@ void policy_kernel(PolicyArgs A) {
         uint32_t* list = A.order + c0;
         uint64_t* wsum = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(smem) +
                                                      ((q.bytes() + 4 * A.dims.padded() + 7) & ~7));
+        orun.count<kPolicyBlock>(w, A.st.x, A.st.y, c0);  // the cell codes from LDS
         orun.place<kPolicyBlock>(w, A.st.x, A.st.y, c0, len, list, wsum);
         ord = list;
     }
@@ -1220,15 +1257,11 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
     const uint32_t* ord = nullptr;
     int64_t c0 = 0;
     int len = 0;
-    if (A.order) {
+    OrderRun orun;
+    if (A.order) {  // loaded here, counted and placed once the image is built (the loads overlap it)
         c0 = (int64_t)blockIdx.x * A.chunk;
         len = __builtin_amdgcn_readfirstlane((int)min(A.chunk, A.n - c0));  // uniform: an SGPR
-        uint32_t* list = A.order + c0;
-        const LdsWorld wg = world_view(A.dims, A.world);
-        OrderRun orun;
-        orun.count<kPolicyX3Block>(wg, A.st.x, A.st.y, c0, len);
-        orun.place<kPolicyX3Block>(wg, A.st.x, A.st.y, c0, len, list, reinterpret_cast<uint64_t*>(smem));
-        ord = list;
+        orun.load<kPolicyX3Block>(A.st.x, A.st.y, c0, len);
     }
     auto load_env = [&](int64_t t) {
         const int64_t p = t * 32 + (lane & 31);
@@ -1246,11 +1279,14 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
                             (uint32_t)A.st.dest[ei] << 24;
         return EnvIn{A.st.fuel[ei], pk, (uint32_t)(live ? ei : A.n)};
     };
-    // tiles: the chunk's (waves round robin) or all of them (striding over the grid)
-    const int64_t my_tiles = ord ? (len + 31) >> 5 : tiles;
-    int64_t tile = ord ? (threadIdx.x >> 6) : (int64_t)blockIdx.x * kPolicyX3Waves + (threadIdx.x >> 6);
-    EnvIn nxt = load_env(tile < my_tiles ? tile : 0);
-    const int64_t stride = ord ? kPolicyX3Waves : (int64_t)gridDim.x * kPolicyX3Waves;
+    // tiles: the chunk's (waves round robin) or all of them (striding over the grid); in
+    // position order the first tile's env state is requested before the image is built
+    const bool ordered = A.order != nullptr;
+    const int64_t my_tiles = ordered ? (len + 31) >> 5 : tiles;
+    int64_t tile = ordered ? (threadIdx.x >> 6) : (int64_t)blockIdx.x * kPolicyX3Waves + (threadIdx.x >> 6);
+    const int64_t stride = ordered ? kPolicyX3Waves : (int64_t)gridDim.x * kPolicyX3Waves;
+    EnvIn nxt{};
+    if (!ordered) nxt = load_env(tile < my_tiles ? tile : 0);
     if constexpr (kW3Global) {  // fc3 stays in the packed global image: copy the rest
         const int staged = D.w3() / 16;
         for (int i = threadIdx.x; i < staged; i += kPolicyX3Block) smem[i] = A.qimg[i];
@@ -1271,6 +1307,16 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
         pack_x3_items(pk, reinterpret_cast<uint8_t*>(smem), threadIdx.x, kPolicyX3Block);
     }
     __syncthreads();
+    if (ordered) {
+        uint32_t* list = A.order + c0;
+        const int wo = kW3Global ? ((D.w3() + 7) & ~7) : (((D.bytes() + 15) & ~15) + kX3PtabBytes);
+        const LdsWorld wg = world_view(A.dims, A.world);
+        orun.count<kPolicyX3Block>(wg, A.st.x, A.st.y, c0);
+        orun.place<kPolicyX3Block>(wg, A.st.x, A.st.y, c0, len, list,
+                                   reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(smem) + wo));
+        ord = list;
+        nxt = load_env(tile < my_tiles ? tile : 0);
+    }
     X3STAMP_ANY(10);
     const LdsWorld w = world_view(A.dims, A.world);  // port_at / stocks read in place (L2)
     const uint8_t* qb = reinterpret_cast<const uint8_t*>(smem);
@@ -1701,13 +1747,13 @@ int launch_policy_x3(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, 
     PackX3Args pk{qn->w[0], qn->w[1], qn->w[2], qn->w[3], qn->w[4], qn->w[5], env->d_world, env->dims, d,
                   qn->d_img32};
     constexpr int kPtabBytes = kX3PtabBytes;
-    const bool w3_global = d.bytes() + kPtabBytes > 160 * 1024;
+    const bool w3_global = d.bytes() + kPtabBytes + kOrderScanBytes > 160 * 1024;
     if (w3_global) {  // fc3's fragments are read from a packed global image
         qnet_pack_x3_kernel<<<128, 256, 0, s>>>(pk);
         HIP_TRY(hipGetLastError());
     }
-    const size_t lds = (size_t)(w3_global ? d.w3()
-                                          : ((d.bytes() + 15) & ~15) + kPtabBytes);
+    const size_t lds = (size_t)(w3_global ? ((d.w3() + 7) & ~7) : ((d.bytes() + 15) & ~15) + kPtabBytes) +
+                       kOrderScanBytes;
     if (lds > 160 * 1024) return fail(SE_EINVAL, "split-bf16 network exceeds the 160 KB LDS");
     static std::atomic<uint64_t> lds_set0{0}, lds_set1{0};
     static std::atomic<uint64_t> lds_set2{0};
