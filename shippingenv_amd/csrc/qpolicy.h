@@ -982,7 +982,8 @@ __device__ __forceinline__ float x3_fold_b1(const PackX3Args& A, int f) {
     const int in1 = A.d.q.in1();
     double acc = (double)A.b1[f];
     // unrolled so that several ports' weight loads go out before the adds wait on them (the
-    // adds stay in port order; unroll 8 measured even, profiles/r05/ab_policy_f32_fold_unroll.jsonl)
+    // adds stay in port order; unroll 8 measured even, profiles/r05/ab_policy_f32_fold_unroll.jsonl;
+    // all 8 ports' loads issued before the adds measured even too, profiles/r06/order/ab_x3_fold.jsonl)
 #pragma unroll 1
     for (int p = 0; p < A.d.q.P; ++p) {
         const float* w = A.w1 + f * in1 + 6 + 4 * p;
@@ -1306,6 +1307,10 @@ __global__ __launch_bounds__(kPolicyX3Block) void policy_x3_kernel(PolicyArgs A,
         pk.ptab = ptab;
         pack_x3_items(pk, reinterpret_cast<uint8_t*>(smem), threadIdx.x, kPolicyX3Block);
     }
+#if SHIPENV_X3_TRACE
+    if ((threadIdx.x & 63) == 0)  // slot 15: the wave's part of the image built
+        g_ptrace[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % 4096 * 16 + 15] = __builtin_amdgcn_s_memrealtime();
+#endif
     __syncthreads();
     if (ordered) {
         uint32_t* list = A.order + c0;

@@ -85,6 +85,8 @@ def main():
         s9, s10, s11 = st[live, 9], st[live, 10], st[live, 11]
         t0 = s9.min()
         rec["us_image_median"] = float(np.median(s10 - s9)) / 100
+        if (st[live, 15] > 0).all():  # the fp32 kernel's slot 15: its part of the image built
+            rec["us_pack_median"] = float(np.median(st[live, 15] - s9)) / 100
         rec["us_wave_median"] = float(np.median(s11 - s9)) / 100
         rec["us_start_spread_max"] = float((s9 - t0).max()) / 100
         rec["us_end_median"] = float(np.median(s11 - t0)) / 100
