@@ -213,6 +213,7 @@ struct PolicyArgs {
     // envs [b * chunk, (b + 1) * chunk) in the order it writes to order[b * chunk ...]
     uint32_t* order;
     int64_t chunk;
+    int32_t lds_list;  // >= 0: the bf16 kernel keeps the list in LDS at this byte offset (u16 per env)
 };
 
 // ------------------------------------------------------------------ visiting order
@@ -286,11 +287,13 @@ struct OrderRun {
         }
     }
 
-    // the list's tail up to a whole tile reads kOrderNone (an idle lane)
-    template <int kBlock>
+    // the list's tail up to a whole tile reads all ones (an idle lane). T = uint32_t: the envs
+    // (a global scratch list); T = uint16_t: their indices in the chunk (an LDS list)
+    template <int kBlock, typename T>
     __device__ __forceinline__ void place(const LdsWorld& w, const uint8_t* xs, const uint8_t* ys, int64_t c0,
-                                          int len, uint32_t* out, uint64_t* wsum) const {
-        if ((int)threadIdx.x < ((-len) & 31)) out[len + threadIdx.x] = kOrderNone;
+                                          int len, T* out, uint64_t* wsum) const {
+        constexpr bool kLocal = sizeof(T) == 2;
+        if ((int)threadIdx.x < ((-len) & 31)) out[len + threadIdx.x] = (T)~(T)0;
         const uint32_t sea = (uint32_t)max(e - b, 0) - port;
         // exclusive prefix of (at sea, in port) over the threads, as two 32-bit halves
         const uint64_t mine = (uint64_t)sea | (uint64_t)port << 32;
@@ -313,7 +316,7 @@ struct OrderRun {
         uint32_t at_sea = (uint32_t)ex, in_port = (uint32_t)total + (uint32_t)(ex >> 32);
         for (int i = b; i < e; ++i) {
             const bool p = i - b < 32 ? ((bits >> (i - b)) & 1u) != 0u : w.port_at(xs[c0 + i], ys[c0 + i]) >= 0;
-            out[p ? in_port : at_sea] = (uint32_t)(c0 + i);
+            out[p ? in_port : at_sea] = kLocal ? (T)i : (T)(c0 + i);
             in_port += p ? 1u : 0u;
             at_sea += p ? 0u : 1u;
         }
@@ -585,6 +588,7 @@ void policy_kernel(PolicyArgs A) {
         int64_t e;  // the env (A.order), past A.n for the last tile's idle lanes
     };
     // the visiting order: this workgroup's chunk and its list (null: position order)
+    const uint16_t* ord16 = nullptr;  // or in LDS (chunk indices)
     const uint32_t* ord = nullptr;
     int64_t c0 = 0;
     int len = 0;
@@ -598,7 +602,11 @@ void policy_kernel(PolicyArgs A) {
         const int64_t p = tile * 32 + r;
         int64_t ei;
         bool live;
-        if (ord) {  // p < the chunk's whole tiles: its tail reads kOrderNone
+        if (ord16) {  // p < the chunk's whole tiles: its tail reads 0xffff
+            const uint32_t v = ord16[p];
+            live = v != 0xffffu;
+            ei = live ? c0 + (int64_t)v : A.n - 1;
+        } else if (ord) {  // the same in global memory, kOrderNone
             const uint32_t v = ord[p];
             live = v != kOrderNone;
             ei = live ? (int64_t)v : A.n - 1;
@@ -636,8 +644,14 @@ void policy_kernel(PolicyArgs A) {
         uint64_t* wsum = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(smem) +
                                                      ((q.bytes() + 4 * A.dims.padded() + 7) & ~7));
         orun.count<kPolicyBlock>(w, A.st.x, A.st.y, c0);  // the cell codes from LDS
-        orun.place<kPolicyBlock>(w, A.st.x, A.st.y, c0, len, list, wsum);
-        ord = list;
+        if (A.lds_list >= 0) {  // the list in LDS: no global stores, fence or list reads from L2
+            uint16_t* list16 = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(smem) + A.lds_list);
+            orun.place<kPolicyBlock>(w, A.st.x, A.st.y, c0, len, list16, wsum);
+            ord16 = list16;
+        } else {
+            orun.place<kPolicyBlock>(w, A.st.x, A.st.y, c0, len, list, wsum);
+            ord = list;
+        }
     }
     X3STAMP_ANY(10);
     [[maybe_unused]] int tile_iter = 0;  // SHIPENV_X3_TRACE: the wave's 4th tile is stamped
@@ -1688,7 +1702,7 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
     DeviceGuard g(env->device);
     // the compact layout unless every row's Q is wanted
     const QnetDims& q = q_out ? qn->q : qn->qc;
-    const size_t lds = (((size_t)q.bytes() + lds_bytes(env) + 7) & ~(size_t)7) + kOrderScanBytes;
+    size_t lds = (((size_t)q.bytes() + lds_bytes(env) + 7) & ~(size_t)7) + kOrderScanBytes;
     static std::atomic<uint64_t> lds_set{0};
     static std::atomic<uint64_t> lds_set_q{0};
     rc = allow_dynamic_lds(lds_set, reinterpret_cast<const void*>(policy_kernel<false>), 160 * 1024, env->device);
@@ -1705,6 +1719,11 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
     PolicyArgs A{};
     rc = policy_order(qn, &grid, A);
     if (rc) return rc;
+    A.lds_list = -1;
+    if (A.order && A.chunk <= 0xffff && lds + (size_t)A.chunk * 2 <= 160 * 1024) {  // the list in LDS
+        A.lds_list = (int32_t)lds;
+        lds += (size_t)A.chunk * 2;
+    }
     A.world = env->d_world;
     A.dims = env->dims;
     A.qimg = reinterpret_cast<const uint4*>(qn->d_img + (q_out ? 0 : qn->c_off));
