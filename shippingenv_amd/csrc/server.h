@@ -148,7 +148,10 @@ int server_launch(se_server* s) {
 
 bool host_pinned(const void* p) {
     hipPointerAttribute_t at{};
-    if (hipPointerGetAttributes(&at, p) != hipSuccess) return false;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory: clear the error, or the next launch check reports it
+        return false;
+    }
     return at.type == hipMemoryTypeHost;
 }
 

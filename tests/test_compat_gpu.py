@@ -207,3 +207,63 @@ def test_stepper_wave_restarts_after_idle(monkeypatch):
     gpu, launches = run("gpu", True)
     assert gpu == host
     assert launches >= 4, launches
+
+
+def test_stepper_wave_refuses_misuse():
+    """se_server_create checks its block (pinned host memory from se_host_alloc, 64-byte
+    aligned) and takes a one-env handle only; se_server_call takes the two ops only; destroy
+    of NULL is a no-op. A refused block leaves no HIP error behind: the next step launches."""
+    import ctypes as C
+
+    import numpy as np
+
+    from shippingenv_amd import _native as N
+    from shippingenv_amd.maps import BUILTIN_MAP, builtin_water
+    from shippingenv_amd.shipping import Environment
+
+    lib = N.lib()
+    water = np.ascontiguousarray(builtin_water(), np.uint8)
+    H, W = water.shape
+    px, py, pf, pc = (np.ascontiguousarray(v, np.int32) for v in ([41, 60], [40, 22], [100, 100], [10, 10]))
+
+    def env_of(n):
+        h = C.c_void_p()
+        N.check(lib.se_create(C.byref(h), torch.cuda.current_device(), n, 0, H, W,
+                              water.ctypes.data_as(C.c_void_p), 2, px.ctypes.data_as(C.c_void_p),
+                              py.ctypes.data_as(C.c_void_p), pf.ctypes.data_as(C.c_void_p),
+                              pc.ctypes.data_as(C.c_void_p), 0, 0))
+        return h
+
+    blk = C.c_void_p()
+    N.check(lib.se_host_alloc(256, C.byref(blk)))
+    env1, env2 = env_of(1), env_of(2)
+    srv = C.c_void_p()
+    try:
+        pageable = np.zeros(512, np.uint8)
+        aligned = pageable.ctypes.data + (-pageable.ctypes.data) % 64
+        assert lib.se_server_create(C.byref(srv), env1, aligned) < 0 and not srv.value
+        assert lib.se_server_create(C.byref(srv), env1, blk.value + 16) < 0  # not 64-byte aligned
+        assert lib.se_server_create(C.byref(srv), env2, blk.value) < 0  # two envs
+        assert lib.se_server_create(C.byref(srv), env1, None) < 0
+        assert lib.se_server_create(C.byref(srv), None, blk.value) < 0
+        N.check(lib.se_server_create(C.byref(srv), env1, blk.value))
+        assert lib.se_server_call(srv, 0) < 0 and lib.se_server_call(srv, 3) < 0
+        assert lib.se_server_call(None, N.SERVER_STEP) < 0
+        n = C.c_uint64()
+        N.check(lib.se_server_launches(srv, C.byref(n)))
+        assert n.value == 0  # the wave starts with the first step
+        N.check(lib.se_server_destroy(srv))
+        srv = C.c_void_p()
+        assert lib.se_server_destroy(None) == 0
+    finally:
+        if srv.value:
+            lib.se_server_destroy(srv)
+        lib.se_destroy(env1)
+        lib.se_destroy(env2)
+        lib.se_host_free(blk)
+    env = Environment(BUILTIN_MAP)  # same thread, after the refused pageable block
+    env.add_port([41, 40])
+    env.add_port([60, 22])
+    env.reset()
+    env.step([1, (0, 1)]) if env.np_game[41, 41] != 0 else env.step([1, (0, -1)])
+    assert env._stepper.launches() >= 1
