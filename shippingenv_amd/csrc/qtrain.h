@@ -1023,17 +1023,20 @@ __device__ __forceinline__ float tile_sum64(const float* src, int64_t stride, in
     return r;
 }
 
-// dW3 row a and db3[a] summed over the tiles in tile order. A tile holds action a in at
-// most one slot (its slot map, T1). Chunk by chunk of 256 tiles, thread t scans tile
-// c0 + t's 32 map entries (8 int4 loads) for a; the tiles that hold it are listed in tile
-// order (wave ballot prefix, then the four wave offsets); thread (grp, q) then adds
-// float4 q of the rows of list entries grp, grp + 8, ... with kU independent loads per
-// round, and the 8 groups combine in a fixed tree. However the actions are spread, a row
-// sums at most one partial per tile. Thread t < 128 returns dW3[a][t], thread 128 db3[a].
-template <int kU>
+// dW3 row a (or its half: the columns from w3's offset) and db3[a] summed over the tiles in
+// tile order. A tile holds action a in at most one slot (its slot map, T1). Chunk by chunk of
+// 256 tiles, thread t reads row a of the action -> slot table for tile c0 + t (or scans that
+// tile's 32 map entries, 8 int4 loads, for a); the tiles that hold it are listed in tile order
+// (wave ballot prefix, then the four wave offsets); thread (grp, q) then adds float4 q (of kQ
+// per row part) of the rows of list entries grp, grp + 256 / kQ, ... with kU independent loads
+// per round, and the groups combine in a fixed pairwise tree. However the actions are spread,
+// a row sums at most one partial per tile. Thread t < 4 kQ returns column t of the part,
+// thread 4 kQ db3[a].
+template <int kU, int kQ>
 __device__ __forceinline__ float slot_row_sum(const float* w3, const float* b3, const int32_t* map, int64_t tiles,
                                               int a, float4* red, int* list, int* wtot, const uint8_t* slot_row) {
-    const int t = threadIdx.x, q = t & 31, grp = t >> 5, lane = t & 63, w = t >> 6;
+    constexpr int kG = kQRBlock / kQ;  // groups
+    const int t = threadIdx.x, q = t % kQ, grp = t / kQ, lane = t & 63, w = t >> 6;
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     float accb = 0.0f;
     for (int64_t c0 = 0; c0 < tiles; c0 += kQRBlock) {
@@ -1067,12 +1070,12 @@ __device__ __forceinline__ float slot_row_sum(const float* w3, const float* b3, 
         }
         if (slot >= 0) list[off + pre] = t * 32 + slot;  // the row within the chunk
         __syncthreads();
-        for (int i0 = grp; i0 < total; i0 += 8 * kU) {
+        for (int i0 = grp; i0 < total; i0 += kG * kU) {
             float4 v[kU];
             float vb[kU];
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
-                const int i = i0 + 8 * u;
+                const int i = i0 + kG * u;
                 const bool ok = i < total;
                 const int64_t row = c0 * 32 + (ok ? list[i] : 0);
                 v[u] = *reinterpret_cast<const float4*>(w3 + row * 128 + 4 * q);
@@ -1093,20 +1096,27 @@ __device__ __forceinline__ float slot_row_sum(const float* w3, const float* b3, 
         }
         __syncthreads();  // list and wtot are rewritten by the next chunk
     }
-    red[grp * 32 + q] = acc;
+    red[grp * kQ + q] = acc;
     float* rb = reinterpret_cast<float*>(list);  // free after the last chunk's barrier
     if (q == 0) rb[grp] = accb;
     __syncthreads();
     float r = 0.0f;
-    if (t < 128) {
-        const int qq = t >> 2, c = t & 3;
-        const float* f = reinterpret_cast<const float*>(red);
-        float e[8];
+    if (t <= 4 * kQ) {
+        float e[kG];
+        if (t < 4 * kQ) {
+            const int qq = t >> 2, c = t & 3;
+            const float* f = reinterpret_cast<const float*>(red);
 #pragma unroll
-        for (int g = 0; g < 8; ++g) e[g] = f[4 * (g * 32 + qq) + c];
-        r = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
-    } else if (t == 128) {
-        r = ((rb[0] + rb[1]) + (rb[2] + rb[3])) + ((rb[4] + rb[5]) + (rb[6] + rb[7]));
+            for (int g = 0; g < kG; ++g) e[g] = f[4 * (g * kQ + qq) + c];
+        } else {
+#pragma unroll
+            for (int g = 0; g < kG; ++g) e[g] = rb[g];
+        }
+#pragma unroll
+        for (int n = kG; n > 1; n >>= 1)  // ((e0 + e1) + (e2 + e3)) + ...
+#pragma unroll
+            for (int g = 0; g < n / 2; ++g) e[g] = e[2 * g] + e[2 * g + 1];
+        r = e[0];
     }
     __syncthreads();  // red and list may be reused
     return r;
@@ -1115,7 +1125,7 @@ __device__ __forceinline__ float slot_row_sum(const float* w3, const float* b3, 
 __device__ __forceinline__ float comp(const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
 
 // Workgroups: [0, 128) W1 row f (+ b1, the fold, the loss at f = 0); [128, 384) W2 64-element
-// blocks (+ b2 on a row's first block); then mt3 x 32 W3 rows (+ b3 of the row).
+// blocks (+ b2 on a row's first block); then mt3 x 32 W3 rows in two halves (+ b3 of the row).
 __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
     __shared__ float red[kQRBlock];
     __shared__ float4 red4[kQRBlock];
@@ -1152,7 +1162,10 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
     QSTAMP(11);
     const int b = blockIdx.x;
     if (b < 128) {  // W1 row f: 6 dynamic columns + db1 reduced over the tiles, the port columns
-        const int f = b;
+        // row f = 16 (b % 8) + b / 8: workgroups go round robin over the 8 XCDs, so each XCD
+        // sums 16 adjacent rows and the lines of [tiles][128][6] / [tiles][128] that they share
+        // (24 and 4 bytes per row and tile) are fetched into its L2 once, not by every block
+        const int f = ((b & 7) << 4) | (b >> 3);
         float* w1row = A.on.w1 + (int64_t)f * in;
         // the Adam operands of this thread's columns (tid, tid + 256: in <= 262) and of b1, loaded
         // now so their round trip overlaps the sums
@@ -1344,10 +1357,11 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                     for (int l = 0; l < 2; ++l) reinterpret_cast<float*>(A.img[l] + A.q[l].b2())[f2] = p;
             }
         }
-    } else {  // W3 row a3 and b3[a3] (rows up to mt3 x 32: the padding rows' sums are 0)
-        const int a3 = b - 384;
+    } else {  // W3 row a3's half h (64 columns) and, in half 0, b3[a3] (rows up to mt3 x 32: the padding rows' sums are 0)
+        const int a3 = (b - 384) >> 1, h = (b - 384) & 1;
         const bool row_live = a3 < A.d.A;
-        const int f3 = tid;  // threads < 128: element f3 of the row; thread 128: b3
+        const bool mine = tid < 64 || (tid == 64 && h == 0);  // thread 64 of half 0: b3
+        const int f3 = 64 * h + (tid & 63);
         const int64_t i3 = (int64_t)a3 * 128 + f3;
         float pw = 0.f, pm = 0.f, pv = 0.f;  // the Adam operands, loaded ahead of the sums
         // the six pointers held in SGPRs (opaque), and every thread loads both candidates: the
@@ -1356,33 +1370,32 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
         float *ow3 = sgpr_ptr(A.on.w3), *ob3 = sgpr_ptr(A.on.b3), *mw3 = sgpr_ptr(A.m.w3), *mb3 = sgpr_ptr(A.m.b3),
               *vw3 = sgpr_ptr(A.v.w3), *vb3 = sgpr_ptr(A.v.b3);
         if (mode != 1 && row_live) {
-            const int64_t iw = (int64_t)a3 * 128 + (tid & 127);
-            const float w_ = ow3[iw], m_ = mw3[iw], v_ = vw3[iw], bw_ = ob3[a3], bm_ = mb3[a3], bv_ = vb3[a3];
-            pw = tid < 128 ? w_ : bw_;
-            pm = tid < 128 ? m_ : bm_;
-            pv = tid < 128 ? v_ : bv_;
+            const float w_ = ow3[i3], m_ = mw3[i3], v_ = vw3[i3], bw_ = ob3[a3], bm_ = mb3[a3], bv_ = vb3[a3];
+            pw = tid < 64 ? w_ : bw_;
+            pm = tid < 64 ? m_ : bm_;
+            pv = tid < 64 ? v_ : bv_;
         }
-        float g = 0.0f;  // dW3[a3][tid] (tid < 128) or db3[a3] (tid = 128)
+        float g = 0.0f;  // dW3[a3][f3] (tid < 64) or db3[a3] (tid = 64)
         if (mode == 2) {
-            if (tid < 128) g = G[Grad::w3 + i3];
-            else if (tid == 128) g = G[Grad::b3(A.d) + a3];
+            if (tid < 64) g = G[Grad::w3 + i3];
+            else if (tid == 64) g = G[Grad::b3(A.d) + a3];
         } else {
-            g = slot_row_sum<16>(A.W.part_w3, A.W.part_b3, A.W.part_map, A.tiles, a3, red4, list, wtot,
-                                             A.W.part_slot + (int64_t)a3 * A.W.slot_ld);
+            g = slot_row_sum<16, 16>(A.W.part_w3 + 64 * h, A.W.part_b3, A.W.part_map, A.tiles, a3, red4, list, wtot,
+                                     A.W.part_slot + (int64_t)a3 * A.W.slot_ld);
             if (mode == 1) {
-                if (tid < 128) G[Grad::w3 + i3] = g;
-                else if (tid == 128) G[Grad::b3(A.d) + a3] = g;
+                if (tid < 64) G[Grad::w3 + i3] = g;
+                else if (tid == 64 && h == 0) G[Grad::b3(A.d) + a3] = g;
                 return;
             }
         }
         const float inv = weight_inv();
         const AdamStep adam = QT_ADAM();
         QSTAMP(12);
-        if (row_live && tid <= 128) {
+        if (row_live && mine) {
             const float p = adam(pw, g * inv, pm, pv);
-            float* dm = tid < 128 ? mw3 + i3 : mb3 + a3;
-            float* dv = tid < 128 ? vw3 + i3 : vb3 + a3;
-            float* dp = tid < 128 ? ow3 + i3 : ob3 + a3;
+            float* dm = tid < 64 ? mw3 + i3 : mb3 + a3;
+            float* dv = tid < 64 ? vw3 + i3 : vb3 + a3;
+            float* dp = tid < 64 ? ow3 + i3 : ob3 + a3;
             *dm = pm;
             *dv = pv;
             *dp = p;
@@ -1391,7 +1404,7 @@ __global__ __launch_bounds__(kQRBlock) void qtrain_adam_kernel(QtAdamArgs A) {
                 for (int l = 0; l < 2; ++l) {
                     const int row = row_of_action(A.q[l], a3);
                     if (row < 0) continue;
-                    if (tid < 128) put_bf16(A.img[l] + A.q[l].w3() + pol_offset(row, f3), p);
+                    if (tid < 64) put_bf16(A.img[l] + A.q[l].w3() + pol_offset(row, f3), p);
                     else reinterpret_cast<float*>(A.img[l] + A.q[l].b3())[row] = p;
                 }
         }
@@ -1561,7 +1574,7 @@ int qtrain_step(se_qtrain* q, se_qnet* qn, int64_t batch, const float* obs, cons
     // T2 counts Adam steps from ctr[1] (set by T1) when T1 drew the batch, and syncs ctr[0]
     const QtAdamArgs B = adam_args(q, qn, batch, act, lr, beta1, beta2, eps, ring ? step_dev + 1 : step_dev,
                                    loss_out, qn || ring ? 1 : 0, grad ? 1 : 0, grad, ring ? step_dev : nullptr);
-    qtrain_adam_kernel<<<384 + 32 * q->d.mt3, kQRBlock, 0, s>>>(B);
+    qtrain_adam_kernel<<<384 + 64 * q->d.mt3, kQRBlock, 0, s>>>(B);
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }
@@ -1614,7 +1627,7 @@ int se_qtrain_apply(se_qtrain* q, se_qnet* qn, const float* grad, float lr, floa
     DeviceGuard g(q->device);
     const QtAdamArgs B = adam_args(q, qn, 0, nullptr, lr, beta1, beta2, eps, step_dev, loss_out, 0, 2,
                                    const_cast<float*>(grad));
-    qtrain_adam_kernel<<<384 + 32 * q->d.mt3, kQRBlock, 0, (hipStream_t)stream>>>(B);
+    qtrain_adam_kernel<<<384 + 64 * q->d.mt3, kQRBlock, 0, (hipStream_t)stream>>>(B);
     HIP_TRY(hipGetLastError());
     return SE_OK;
 }

@@ -57,7 +57,7 @@ def main():
     out["start_spread_us"] = float(np.percentile(rel[:, :, 0].min(axis=1), 99))
     # T2 (slots 10-13, 4 waves): W1 rows [0, 128), W2 blocks [128, 384), then one block per
     # W3 row (mt3 x 32 rows, b3 with its row)
-    nb = 384 + 32 * ((4 + int(env.P) + 250 + 31) // 32)
+    nb = 384 + int(os.environ.get("QT_W3_BLOCKS_PER_ROW", "2")) * 32 * ((4 + int(env.P) + 250 + 31) // 32)
     t2 = buf.reshape(wg, 8, stamps)[:nb, :4, 10:14].astype(np.int64)
     t20 = t2[:, :, 0].min()
     r2 = (t2 - t20) / 100.0
