@@ -76,6 +76,18 @@ def main():
     }
     with open(os.path.join(dst, "sq_update_policy.json"), "w") as f:
         json.dump(sq, f, indent=1)
+    # round 6: the bf16 policy's wait counters (tools/pmc_policy_bf16.sh), the rollout kernel's
+    # SQ counters and trace (tools/pmc_rollout.sh), the stepper wave's timing
+    for sub, names, key in (("pmc_bf16", ("pmc_polb", "pmc_polc"), "policy_kernel<"),
+                            ("rollout", ("pmc_roll_a", "pmc_roll_b"), "rollout_kernel")):
+        if os.path.exists(c(names[0])):
+            os.makedirs(os.path.join(dst, sub), exist_ok=True)
+            with open(os.path.join(dst, sub, "summary.json"), "w") as f:
+                json.dump(pmc([c(n) for n in names], key), f, indent=1)
+    if os.path.exists(os.path.join(src, "kt_roll_kernel_stats.csv")):
+        shutil.copy(os.path.join(src, "kt_roll_kernel_stats.csv"), os.path.join(dst, "rollout", "kt_roll_kernel_stats.csv"))
+    if os.path.exists(os.path.join(src, "time_server.jsonl")):
+        shutil.copy(os.path.join(src, "time_server.jsonl"), os.path.join(dst, "time_server.jsonl"))
     rel = os.path.relpath(dst, os.path.join(ROOT, "profiles"))
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "summarize_profiles.py"),
                     os.path.join(ROOT, "gpurun_out", "prof_" + a.tag), os.path.join(rel, "pmc")], check=True)
