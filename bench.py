@@ -626,13 +626,16 @@ def run_config5(n, args, dist):
                      "note": "se_policy_f32 (includes its per-call repack of the split image); flop_per_env = "
                              "6 x (fc2 + fc3 over its 32-row tiles) bf16 MFMA FLOPs + fc1's 8 split-bf16 MFMAs per 32 envs; "
                              "f32_equivalent: the FLOPs the fused step evaluates (fc1's 6 dynamic inputs, fc2, "
-                             "fc3's compact rows) against the f32 MFMA peak"},
+                             "fc3's compact rows) against the f32 MFMA peak",
+                     # the policy-alone launches (policy_ms's basis) in the committed kernel trace
+                     "committed_trace": committed_trace("config5_policy_f32_alone")},
         "roofline_bf16": {"bound": "mfma", "achieved": round(achieved, 1), "peak": BF16_DENSE_PEAK_TFLOPS,
                           "unit": "TFLOP/s", "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4),
                           "flop_per_env": flop_env, "traffic": None,
                           "executed_mfma_per_32_envs": mfma_tile,
                           "note": "at most executed_mfma_per_32_envs v_mfma_f32_32x32x16_bf16 per 32 envs "
-                                  "(fc1 pads K to 16)"},
+                                  "(fc1 pads K to 16)",
+                          "committed_trace": committed_trace("config5_policy_bf16_alone")},
     }
 
 
@@ -759,7 +762,7 @@ def committed_trace(key):
     leg = d.get(key)
     if not leg:
         return None
-    return {"avg_us": leg["avg_us_timed"], "frac": leg["frac_from_trace"], "source": TRACE_SUMMARY,
+    return {"avg_us": leg["avg_us_timed"], "frac": leg.get("frac_from_trace"), "source": TRACE_SUMMARY,
             "traced_code": d.get("traced_code"), "trace": d.get("trace")}
 
 

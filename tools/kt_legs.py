@@ -17,6 +17,11 @@ next dispatches of that leg's kernel instantiation in the trace:
              105 launches, then the steady leg's P3 pre-roll steps and its 105 (the last)
   large_n config 4: the auto-reset kernel's last 105 launches (2^24, after its pre-roll); since
              round 5 that is the nontemporal-load instantiation (C4NT)
+  config 5   policy_x3_kernel<false, false> (the fp32 policy): its first dispatches are config 5's
+             W warm-up, K timed loop steps, then K policy-alone launches (bench.py run_config5);
+             policy_kernel<false> (bf16): the --preroll5 pre-roll steps (eps 1.0 from reset, bench.py's
+             default 300), then the bf16 leg's W + K + K in the same order. Both legs report the timed
+             loop's launches; *_alone the policy-alone launches (the basis of config5's policy_ms)
 For each leg this prints the average kernel duration (end - start of the dispatch, as
 rocprofv3 records it) over the K timed launches, over the timed launches after the
 first, the per-launch list, the idle gaps between consecutive timed launches and
@@ -28,6 +33,7 @@ from __future__ import annotations
 
 import argparse
 import csv
+import gzip
 import json
 
 C3 = "step_kernel<false, false, false, true, false, false>"
@@ -35,12 +41,14 @@ C3S = "step_kernel<false, false, false, true, false, true>"
 C4 = "step_kernel<false, false, true, false, false, false>"
 C4NT = "step_kernel<false, false, true, true, false, false>"  # auto-reset with nontemporal loads (N > 2^21, round 5)
 BIG = "step_kernel<false, false, false, false, false, false>"
+X3 = "policy_x3_kernel<false, false>"  # se_policy_f32, config 5
+PB = "policy_kernel<false>"  # se_policy (bf16)
 PEAK = 8000.0
 
 
 def load(path):
     rows = []
-    with open(path) as f:
+    with (gzip.open(path, "rt") if path.endswith(".gz") else open(path)) as f:
         for r in csv.DictReader(f):
             name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
             s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
@@ -79,6 +87,7 @@ def main():
     p.add_argument("--n", type=int, default=1 << 20)
     p.add_argument("--preroll3", type=int, default=1000)
     p.add_argument("--preroll4", type=int, default=1000)
+    p.add_argument("--preroll5", type=int, default=300)
     a = p.parse_args()
     rows = load(a.trace)
     K, W = a.steps, a.warmup
@@ -90,7 +99,11 @@ def main():
            "large_n_from_reset": leg(rows, BIG, 0, 2 * 105 + a.preroll3, 100, from_end=True, head=105),
            "large_n": leg(rows, BIG, 0, 105, 100, from_end=True),
            "config3_literal": leg(rows, C3S, W + K, 10 + 1000, 1000),
-           "large_n_config4": leg(rows, C4NT, 0, 105, 100, from_end=True)}
+           "large_n_config4": leg(rows, C4NT, 0, 105, 100, from_end=True),
+           "config5_policy_f32": leg(rows, X3, 0, W + K, K),
+           "config5_policy_f32_alone": leg(rows, X3, W + K, K, K),
+           "config5_policy_bf16": leg(rows, PB, a.preroll5, W + K, K),
+           "config5_policy_bf16_alone": leg(rows, PB, a.preroll5 + W + K, K, K)}
     for key, b in (("config3", 42), ("config3_from_reset", 42), ("config3_step_py", 42), ("config4", 50),
                    ("config3_literal", 42)):
         if out[key]:
