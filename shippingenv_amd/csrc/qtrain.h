@@ -441,7 +441,20 @@ struct QtStepArgs {
 };
 
 #ifndef SHIPENV_QTRACE
-#define SHIPENV_QTRACE 0  // 1 = diagnostic build: per-wave phase stamps of T1 (tools/archive/qtrain_trace.py)
+#define SHIPENV_QTRACE 0  // 1 = diagnostic build: per-wave phase stamps of T1 (tools/qtrain_trace.py);
+                          // 2 = the same, slots 14 / 15 inside the input staging instead (wave 0:
+                          // picks issued, picks in LDS; tools/qtrain_trace.py --inputs)
+#endif
+#if SHIPENV_QTRACE == 2
+#define QSTAMP_IN(k) QSTAMP(k)
+#define QSTAMP_MFMA(k) \
+    do {               \
+    } while (0)
+#else
+#define QSTAMP_IN(k) \
+    do {             \
+    } while (0)
+#define QSTAMP_MFMA(k) QSTAMP(k)
 #endif
 #if SHIPENV_QTRACE
 constexpr int kQTraceWg = 1024, kQTraceStamps = 16;
@@ -514,6 +527,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         pkey = draw(env_key(A.seed, kReplayKeyId), pt, kSlotReplay);
         if (r0 + tid < A.B) pf = pick_issue(A.ring, psize, pkey, feistel_half((uint32_t)psize), r0 + tid);
     }
+    QSTAMP_IN(14);  // (wave 0: the picks' loads issued)
     Frags<64> fb;   // W2^T (dH1), loaded during fc3
     bf16x8 wa[8][3];  // fc2's pre-split A operands
     {
@@ -545,6 +559,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             RW[tid] = ok ? pk.rw : 0.0f;
             DN[tid] = ok && (pk.fl & kRecDone) ? 1.0f : 0.0f;
             if (blockIdx.x == 0 && tid == 0) A.ctr[1] = (int32_t)(t + 1u);  // T2's Adam count
+            QSTAMP_IN(15);  // (the picked transitions arrived and are in LDS)
         }
     } else {
         for (int e = tid; e < 2 * 8 * 32; e += kQTBlock) {
@@ -623,7 +638,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
         if (tgt) store_split(SH2, wt, acc, lane);
         else store_relu(HB, wt, acc, lane);
     }
-    QSTAMP(14);
+    QSTAMP_MFMA(14);
     __syncthreads(); QSTAMP(3);
     // target fc3: tile `wave` on each wave (mt3 >= 9), and the mt3 - 8 (at most 2) tiles past
     // the eighth split over K: tile 8 on waves 4-7, tile 9 on waves 0-3, two k-steps each, so
@@ -658,7 +673,7 @@ __global__ __launch_bounds__(kQTBlock) void qtrain_tile_kernel(QtStepArgs A) {
             for (int r = 0; r < 16; ++r) o[r * 64 + lane] = accx[r];
         }
     }
-    QSTAMP(15);
+    QSTAMP_MFMA(15);
     __syncthreads(); QSTAMP(4);
     if (tid < 64) {
         float mx = -INFINITY;

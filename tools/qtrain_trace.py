@@ -26,6 +26,8 @@ def main():
     p.add_argument("--lib", required=True)
     p.add_argument("--n", type=int, default=1 << 20)
     p.add_argument("--batch", type=int, default=8192)
+    p.add_argument("--inputs", action="store_true",
+                   help="a SHIPENV_QTRACE=2 build: slots 14 / 15 are wave 0's picks issued / in LDS")
     a = p.parse_args()
     from shippingenv_amd import _native
 
@@ -69,6 +71,16 @@ def main():
         out["t2_" + name] = {"start_p50": float(np.median(w2[lo:hi, 0])), "start_max": float(w2[lo:hi, 0].max()),
                              "wsum": float(np.median(d2[:, 0])), "sum": float(np.median(d2[:, 1])),
                              "adam": float(np.median(d2[:, 2])), "end_max": float(w2[lo:hi, 3].max())}
+    if a.inputs:  # wave 0 of each T1 workgroup, from its own start (slot 0)
+        w0 = buf.reshape(wg, 8, stamps)[:tiles, 0, :].astype(np.int64)
+        rel0 = (w0 - w0[:, :1]) / 100.0
+        out["inputs_wave0_median_us"] = {"picks_issued": float(np.median(rel0[:, 14])),
+                                         "picks_in_lds": float(np.median(rel0[:, 15])),
+                                         "barrier_passed": float(np.median(rel0[:, 1]))}
+        print(json.dumps(out))
+        agent.close()
+        env.close()
+        return
     # slots 14 / 15: each wave's fc2 / fc3 chain done (before the phase's barrier), from the
     # phase start (the slowest wave's stamp after the previous barrier), per wave of a workgroup
     raw = buf.reshape(wg, 8, stamps)[:tiles].astype(np.int64)
