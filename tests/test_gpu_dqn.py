@@ -245,12 +245,14 @@ class _Ref64:
             assert bool((dv <= vb).all()), (what, name, "exp_avg_sq")
 
 
-@pytest.mark.parametrize("n,ports64,batch", [(2048, False, 256), (4099, True, 300), (4, False, 3), (64, False, 33)])
+@pytest.mark.parametrize("n,ports64,batch", [(2048, False, 256), (4099, True, 300), (4, False, 3), (64, False, 33),
+                                             (16384, True, 9000)])
 def test_fused_update_matches_reference_update(n, ports64, batch):
     """Per update k: from our parameters and Adam moments before it, the reference's update
     (agents/dqn.py:226-242: nn.MSELoss, torch.optim.Adam) in float64 on the minibatch the
     agent drew gives our loss (rtol 1e-4), parameters and moments within the per-element
-    bounds of _Ref64."""
+    bounds of _Ref64. Batch 9000: 282 tiles, past the bench's 8192, so T2's sums loop over
+    more than one 256-tile chunk (the action -> slot table, the W1 / W2 partials)."""
     import copy
 
     from conftest import golden_water
@@ -647,19 +649,20 @@ def _one_rank_dp():
     return OneRank
 
 
-def test_grad_then_apply_is_the_fused_step_bit_for_bit():
+@pytest.mark.parametrize("n,batch", [(4096, 512), (16384, 9000)])
+def test_grad_then_apply_is_the_fused_step_bit_for_bit(n, batch):
     """se_qtrain_grad + se_qtrain_apply (the update split at the all-reduce) against
     se_qtrain_step_policy, one rank: the same sums reach the same Adam step, so losses,
     weights, Adam moments, the update counter and both policy images agree bit for bit,
-    eager and from the two captured graphs."""
+    eager and from the two captured graphs (batch 9000: T2's sums over two 256-tile chunks)."""
     from shippingenv_amd.dqn import VecDQNAgent
 
     agents, envs = [], []
     for cls in (VecDQNAgent, _one_rank_dp()):
-        env = make_env(4096, seed=13)
+        env = make_env(n, seed=13)
         torch.manual_seed(2)
         kw = dict(data_parallel=True) if cls is not VecDQNAgent else {}
-        agent = cls(env, graph=True, graph_warmup=3, batch_size=512, epsilon=0.4, target_update_every=4,
+        agent = cls(env, graph=True, graph_warmup=3, batch_size=batch, epsilon=0.4, target_update_every=4,
                     max_steps=9, **kw)
         _OPEN.append(agent)
         agents.append(agent)
