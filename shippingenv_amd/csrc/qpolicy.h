@@ -1603,9 +1603,12 @@ struct se_qnet {
     uint8_t* d_img32 = nullptr;  // se_policy_f32's split image (the full layout's fc3, global)
     int img32_bytes = 0;
     // the visiting order's scratch list (order_chunk): used when n >= order_min_envs, resolved once
-    // by se_qnet_create (SHIPENV_POLICY_ORDER: 0 never, 1 always; unset: from 2^16 envs)
+    // by se_qnet_create (SHIPENV_POLICY_ORDER: 0 never, 1 always; unset: from 2^16 envs; 2 always,
+    // with the bf16 kernel's list in this global scratch as when it does not fit the LDS, which
+    // otherwise happens only past ~10M envs)
     uint32_t* d_order = nullptr;
     int64_t order_cap = 0, order_min_envs = (int64_t)1 << 16;
+    bool order_lds = true;
 };
 
 extern "C" {
@@ -1618,7 +1621,10 @@ int se_qnet_create(se_qnet** out, se_env* env) {
     se_qnet* qn = new se_qnet;
     qn->env = env;
     qn->device = env->device;
-    if (const char* v = getenv("SHIPENV_POLICY_ORDER")) qn->order_min_envs = atoi(v) != 0 ? 0 : INT64_MAX;
+    if (const char* v = getenv("SHIPENV_POLICY_ORDER")) {
+        qn->order_min_envs = atoi(v) != 0 ? 0 : INT64_MAX;
+        qn->order_lds = atoi(v) != 2;
+    }
     *out = qn;
     return SE_OK;
 }
@@ -1720,7 +1726,7 @@ int launch_policy(se_qnet* qn, int32_t* actions, double epsilon, uint32_t t, flo
     rc = policy_order(qn, &grid, A);
     if (rc) return rc;
     A.lds_list = -1;
-    if (A.order && A.chunk <= 0xffff && lds + (size_t)A.chunk * 2 <= 160 * 1024) {  // the list in LDS
+    if (A.order && qn->order_lds && A.chunk <= 0xffff && lds + (size_t)A.chunk * 2 <= 160 * 1024) {  // the list in LDS
         A.lds_list = (int32_t)lds;
         lds += (size_t)A.chunk * 2;
     }

@@ -435,7 +435,8 @@ def test_visiting_order_changes_nothing(monkeypatch, precision, n, ports, steps)
     """The visiting order (csrc/qpolicy.h OrderRun): each policy workgroup visits its chunk's
     ships at sea first, then those in port, so most 32-env tiles skip fc3's second tile. It is on from
     2^16 envs; SHIPENV_POLICY_ORDER=1 forces it (read when the policy is created), 0 turns it
-    off. The order only moves envs between lanes: greedy and exploring actions, the q_out rows
+    off, 2 forces it with the bf16 kernel's list in global memory (its path past ~10M envs,
+    where the list no longer fits the LDS). The order only moves envs between lanes: greedy and exploring actions, the q_out rows
     and the replay ring's records (se_policy_record) equal position order's, bit for bit. (The
     fp32 policy sums a sea tile's rows 0-3 by activation part, so there its Q bits may differ
     from a mixed tile's in the last place: a near-tie could flip a greedy action; these states
@@ -457,7 +458,7 @@ def test_visiting_order_changes_nothing(monkeypatch, precision, n, ports, steps)
     in_port = valid_bool(env)[:, 4:].any(axis=1)
     assert 0.02 < in_port.mean() < 0.98, in_port.mean()  # both kinds of tile
     out = {}
-    for mode in ("0", "1"):
+    for mode in ("0", "1", "2"):
         monkeypatch.setenv("SHIPENV_POLICY_ORDER", mode)
         pol = QPolicy(env, model)
         _OPEN.append(pol)
@@ -467,10 +468,11 @@ def test_visiting_order_changes_nothing(monkeypatch, precision, n, ports, steps)
                      "q_greedy": pol.act(0.0, 5, q_out=q_out, precision=precision).clone(), "q": q_out}
     for k in out["0"]:
         assert torch.equal(out["0"][k], out["1"][k]), k
+        assert torch.equal(out["0"][k], out["2"][k]), k
     assert (out["1"]["greedy"] >= 4).any() and (out["1"]["greedy"] < 4).any()
     # the replay record path: two envs stepped alike, one ring each, every transition compared
     envs, rbs = [], []
-    for mode in ("0", "1"):
+    for mode in ("0", "1", "2"):
         monkeypatch.delenv("SHIPENV_POLICY_ORDER")
         e2, m2 = setup()
         monkeypatch.setenv("SHIPENV_POLICY_ORDER", mode)
@@ -485,11 +487,12 @@ def test_visiting_order_changes_nothing(monkeypatch, precision, n, ports, steps)
         envs.append(e2)
         rbs.append(rb)
     torch.cuda.synchronize()
-    assert rbs[0].size == rbs[1].size == 3 * n
-    outs = [MiniBatch(3 * n, envs[0].obs_size, envs[0].device) for _ in range(2)]
+    assert rbs[0].size == rbs[1].size == rbs[2].size == 3 * n
+    outs = [MiniBatch(3 * n, envs[0].obs_size, envs[0].device) for _ in range(3)]
     for rb, o in zip(rbs, outs):
         rb.sample(o, t=1)
     torch.cuda.synchronize()
     for name in ("obs", "next_obs", "act", "rew", "done", "weight"):
         assert torch.equal(getattr(outs[0], name), getattr(outs[1], name)), name
+        assert torch.equal(getattr(outs[0], name), getattr(outs[2], name)), name
     monkeypatch.delenv("SHIPENV_POLICY_ORDER")
